@@ -1,0 +1,161 @@
+"""Generate golden fixtures by running the *reference* RenderFormer on CPU fp32.
+
+Run in the build container only (``/root/reference`` does not exist on the GPU
+box):  ``python tests/golden/make_golden.py``.  It imports the reference
+package read-only from /root/reference with the ``roma`` stand-in in
+``tests/golden/shim`` and ``ATTN_IMPL=sdpa`` (flash_attn is absent; the
+reference falls back to SDPA itself, attention.py:29-32), loads the
+build-defined synthetic weights with ``load_state_dict(strict=True)`` and
+writes small ``.npz`` files next to this script:
+
+* inputs in the HDF5 tensor format (per-triangle texture channels; the 32x32
+  patches are re-expanded deterministically by ``scenes.expand_texture``),
+* the weight seed plus per-tensor checksums (guards generator drift),
+* intermediate taps (stage-1 input/output, decoder layer outputs, DPT logits,
+  rays, camera-frame triangles) for the small cases, and
+* the final HDR output ``[B, V, res, res, 3]``.
+
+Only data is written; no reference source is copied.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import warnings
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("RF_REFERENCE", "/root/reference")
+
+os.environ["ATTN_IMPL"] = "sdpa"
+sys.path[:0] = [os.path.join(HERE, "shim"), REF, REPO]
+warnings.filterwarnings("ignore")
+
+import torch  # noqa: E402
+
+from renderformer_amd.config import RenderFormerConfig  # noqa: E402
+from renderformer_amd.scenes import batch_scenes, synthetic_scene  # noqa: E402
+from renderformer_amd.weights import synthetic_state_dict  # noqa: E402
+
+TINY = dict(latent_dim=256, num_layers=2, num_heads=2, dim_feedforward=512, view_transformer_latent_dim=256,
+            view_transformer_ffn_hidden_dim=512, view_transformer_n_heads=2, view_transformer_n_layers=4,
+            dpt_features=32, dpt_out_channels=[16, 32, 64, 128])
+
+CASES = {
+    # name: (config overrides, [n_tris per scene], padding_length, n_views, res, weight seed, scene seed, taps)
+    "tiny_swin": (dict(TINY, view_transformer_use_swin_attn=True), [61, 45], 64, 2, 64, 0, 11, True),
+    "tiny_swin_r128": (dict(TINY, view_transformer_use_swin_attn=True), [70], None, 1, 128, 1, 12, True),
+    "tiny_full": (dict(TINY, view_transformer_use_swin_attn=False), [53], None, 2, 64, 2, 13, True),
+    "tiny_large": (dict(latent_dim=1024, num_layers=1, num_heads=8, dim_feedforward=4096,
+                        view_transformer_latent_dim=1024, view_transformer_ffn_hidden_dim=4096,
+                        view_transformer_n_heads=8, view_transformer_n_layers=4,
+                        view_transformer_use_swin_attn=True, dpt_features=256,
+                        dpt_out_channels=[128, 256, 512, 1024]), [100], None, 1, 64, 3, 14, False),
+    "cbox_base": (dict(num_layers=2, view_transformer_n_layers=4, view_transformer_use_swin_attn=True),
+                  [5633], None, 1, 64, 4, 15, False),
+}
+
+
+def weight_checksums(sd):
+    names = sorted(sd)
+    return names, np.array([[float(sd[n].double().sum()), float(sd[n].double().abs().sum())] for n in names])
+
+
+def run_case(name, over, ntris, pad, nv, res, wseed, sseed, taps):
+    from renderformer.models.config import RenderFormerConfig as RefConfig
+    from renderformer.models.renderformer import RenderFormer as RefModel
+    from renderformer.pipelines.rendering_pipeline import RenderFormerRenderingPipeline as RefPipeline
+
+    cfg = RenderFormerConfig(**over)
+    sd = synthetic_state_dict(cfg, seed=wseed)
+    model = RefModel(RefConfig(**over))
+    model.load_state_dict(sd, strict=True)
+    model.eval()
+    pipe = RefPipeline(model)
+
+    scenes = [synthetic_scene(n, nv, seed=sseed + i) for i, n in enumerate(ntris)]
+    batch = batch_scenes(scenes, padding_length=pad)
+    tex = batch["texture"].clone()
+
+    got = {}
+    hooks = []
+    if taps:
+        hooks.append(model.transformer.register_forward_pre_hook(lambda m, a: got.__setitem__("seq0", a[0].clone())))
+        hooks.append(model.transformer.register_forward_hook(lambda m, a, o: got.__setitem__("enc_out", o.clone())))
+        for i, layer in enumerate(model.view_transformer.transformer.layers):
+            hooks.append(layer.register_forward_hook(
+                lambda m, a, o, i=i: got.__setitem__(f"dec{i}", o.clone())))
+        hooks.append(model.view_transformer.out_dpt.register_forward_hook(
+            lambda m, a, o: got.__setitem__("dpt", o.clone())))
+    with torch.no_grad():
+        out = pipe.render(batch["triangles"], tex, batch["mask"], batch["vn"], batch["c2w"], batch["fov"],
+                          resolution=res, torch_dtype=torch.float32)
+    for h in hooks:
+        h.remove()
+
+    names, sums = weight_checksums(sd)
+    rec = dict(
+        cfg=json.dumps(cfg.to_dict()), weight_seed=np.int64(wseed), weight_names=np.array(names),
+        weight_sums=sums, res=np.int64(res),
+        triangles=batch["triangles"].numpy(), vn=batch["vn"].numpy(), tex_channels=batch["tex_channels"].numpy(),
+        mask=batch["mask"].numpy(), c2w=batch["c2w"].numpy(), fov=batch["fov"].numpy(),
+        texture_after_ch10=tex[:, :, 10, 0, 0].numpy(),
+        hdr=out.numpy().astype(np.float32),
+    )
+    for k, v in got.items():
+        rec["tap_" + k] = v.numpy().astype(np.float32)
+    if not taps:
+        # size-independent signature of stage 1 at production sequence length
+        with torch.no_grad():
+            enc = {}
+            h = model.transformer.register_forward_hook(lambda m, a, o: enc.__setitem__("o", o))
+            pipe.render(batch["triangles"], batch["texture"].clone(), batch["mask"], batch["vn"], batch["c2w"],
+                        batch["fov"], resolution=res, torch_dtype=torch.float32)
+            h.remove()
+            rec["enc_rownorm"] = enc["o"].norm(dim=-1).numpy().astype(np.float32)
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, **rec)
+    print(f"{name}: hdr {tuple(out.shape)} range [{out.min():.3g}, {out.max():.3g}] -> {os.path.getsize(path)/1e6:.2f} MB")
+
+
+def op_level():
+    """Op-level known answers: triangle RoPE tables, NeRF encoding, Swin mask, rays, camera transform."""
+    from renderformer.encodings.nerf_encoding import NeRFEncoding
+    from renderformer.encodings.rope import TriangleRotaryEmbedding, freqs_to_cos_sin
+    from renderformer.layers.attention import get_swin_attn_mask
+    from renderformer.utils.ray_generator import RayGenerator
+    from renderformer.utils.transform import trans_to_cam_coord
+
+    g = torch.Generator().manual_seed(5)
+    pos = torch.rand(2, 37, 9, generator=g) * 2 - 1
+    rope = TriangleRotaryEmbedding(dim=12)
+    cos, sin = freqs_to_cos_sin(rope.get_triangle_freqs(pos), head_dim=128)
+    vn = torch.randn(3, 5, 9, generator=g)
+    nerf = NeRFEncoding(in_dim=9, num_frequencies=6, include_input=True)(vn)
+    m16 = get_swin_attn_mask(16, 16, 8, 4, "cpu")
+    m8 = get_swin_attn_mask(8, 8, 8, 4, "cpu")
+    c2w = torch.randn(2, 4, 4, generator=g)
+    c2w[:, 3] = torch.tensor([0.0, 0, 0, 1])
+    q, _ = torch.linalg.qr(torch.randn(2, 3, 3, generator=g))
+    c2w[:, :3, :3] = q
+    fov = torch.full((2, 1), 0.6)
+    ro, rd = RayGenerator()(c2w, fov, 32)
+    tris = torch.randn(2, 7, 3, 3, generator=g)
+    tcam, _, _ = trans_to_cam_coord(c2w, tris)
+    np.savez_compressed(os.path.join(HERE, "ops.npz"), rope_pos=pos.numpy(), rope_freqs=rope.freqs.detach().numpy(),
+                        rope_cos=cos.numpy(), rope_sin=sin.numpy(), nerf_in=vn.numpy(), nerf_out=nerf.numpy(),
+                        swin_mask16=m16.numpy(), swin_mask8=m8.numpy(), c2w=c2w.numpy(), fov=fov.numpy(),
+                        rays_o=ro.numpy(), rays_d=rd.numpy(), tris=tris.numpy(), tris_cam=tcam.numpy())
+    print("ops.npz written")
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(os.cpu_count() or 8)
+    only = sys.argv[1:]
+    op_level()
+    for name, args in CASES.items():
+        if not only or name in only:
+            run_case(name, *args)

@@ -1,0 +1,43 @@
+"""Pin the CPU oracle (oracle/rf_ref.py) against fixtures produced by the reference itself."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import rf_ref
+from golden_util import CASES, GOLDEN, load_case, rel_l2
+
+TOL = 1e-5  # restatement vs reference on identical CPU fp32 kernels
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_matches_reference(name):
+    cfg, sd, inp, res, z = load_case(name)
+    taps = {}
+    tex = inp["texture"].clone()
+    out = rf_ref.render(sd, cfg, inp["triangles"], tex, inp["mask"], inp["vn"], inp["c2w"], inp["fov"], res, taps)
+    assert out.shape == z["hdr"].shape
+    assert rel_l2(out, z["hdr"]) < TOL
+    # in-place log encoding of the emission channels (rendering_pipeline.py:67-68)
+    np.testing.assert_allclose(tex[:, :, 10, 0, 0].numpy(), z["texture_after_ch10"], rtol=1e-6, atol=1e-7)
+    for k in z.files:
+        if not k.startswith("tap_"):
+            continue
+        key = k[4:]
+        mine = {"enc_out": taps.get(f"enc{cfg.num_layers - 1}")}.get(key, taps.get(key))
+        assert mine is not None, key
+        assert rel_l2(mine, z[k]) < TOL, key
+
+
+def test_oracle_ops():
+    z = np.load(f"{GOLDEN}/ops.npz")
+    cos, sin = rf_ref.rope_cos_sin(torch.from_numpy(z["rope_pos"]), torch.from_numpy(z["rope_freqs"]), 128)
+    np.testing.assert_allclose(cos.numpy(), z["rope_cos"], atol=1e-6)
+    np.testing.assert_allclose(sin.numpy(), z["rope_sin"], atol=1e-6)
+    np.testing.assert_allclose(rf_ref.nerf_encode(torch.from_numpy(z["nerf_in"]), 6).numpy(), z["nerf_out"], atol=1e-6)
+    assert np.array_equal(rf_ref.swin_mask(16, 16, 8, 4).numpy(), z["swin_mask16"])
+    assert np.array_equal(rf_ref.swin_mask(8, 8, 8, 4).numpy(), z["swin_mask8"])
+    ro, rd = rf_ref.ray_gen(torch.from_numpy(z["c2w"]), torch.from_numpy(z["fov"]), 32)
+    np.testing.assert_allclose(ro.numpy(), z["rays_o"], atol=1e-6)
+    np.testing.assert_allclose(rd.numpy(), z["rays_d"], atol=1e-6)
+    tc = rf_ref.cam_transform(torch.from_numpy(z["c2w"]), torch.from_numpy(z["tris"]))
+    np.testing.assert_allclose(tc.numpy(), z["tris_cam"], atol=1e-5)
