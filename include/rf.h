@@ -1,0 +1,124 @@
+/*
+ * librfhip — C ABI of the MI355X-native RenderFormer inference path.
+ *
+ * Every entry point is stream-ordered and asynchronous (no device sync, no
+ * allocation), takes plain device pointers, explicit sizes/strides (in
+ * elements) and a hipStream_t passed as `void*`, and returns RF_OK or an
+ * error code; rf_last_error() returns a thread-local message.  The caller
+ * owns every buffer.  Tensors are row-major; "bf16" buffers hold raw
+ * bfloat16 bits, "f32" buffers IEEE float.
+ *
+ * Reference interfaces replaced (paths relative to the reference checkout):
+ *   rf_gemm_bf16       nn.Linear / aten mm+addmm in attention.py:51-57,95-100,121-125,202,342,361;
+ *                      renderformer.py:49,63 (encoders); view_transformer.py:45 (ray encoder)
+ *   rf_rmsnorm         nn.RMSNorm pre-norms attention.py:436-439,463,482 (+ kv_norm :508)
+ *   rf_qk_norm_rope    q/k RMSNorm over full width (attention.py:127-133) fused with the
+ *                      triangle RoPE (rope.py:106-149 apply_rotary_emb_*cossin, :78-103, :315-333)
+ *   rf_attn_fwd        flash_attn_varlen_qkvpacked_func / flash_attn_varlen_kvpacked_func
+ *                      (attention.py:164-198) and the masked SDPA branch (attention.py:143-161)
+ *   rf_swin_attn_fwd   SwinSelfAttention roll + window_partition + masked SDPA + window_reverse
+ *                      (attention.py:205-271, 316-370), with the roll done as index math
+ *   rf_texture_pack    rendering_pipeline.py:67-68 (in-place log10 encode) + renderformer.py:145-147
+ *                      flatten, with flash_attn.bert_padding.unpad_input-style compaction
+ *   rf_vn_encode       NeRFEncoding (nerf_encoding.py:63-84) on vertex normals, renderformer.py:139
+ *   rf_ray_tokens      RayGenerator (ray_generator.py:13-50) + patchify rearrange (view_transformer.py:104-105)
+ *   rf_patchify_rays   the patchify rearrange alone, for RenderFormer.forward callers (renderformer.py:171)
+ *   rf_scene_pos       trans_to_cam_coord (transform.py:7-27) + process_tri_vpos_list (renderformer.py:103-124)
+ *   rf_embed           token assembly renderformer.py:139-163, view_transformer.py:108 (RMSNorm eps=None)
+ *   rf_hdr_output      ELU(1e-3) (view_transformer.py:86,122) + 10^x - 1 + permute (rendering_pipeline.py:119-123)
+ */
+#ifndef RF_H
+#define RF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RF_OK 0
+#define RF_ERR_INVALID 1
+#define RF_ERR_LAUNCH 2
+#define RF_ERR_UNSUPPORTED 3
+
+#define RF_ABI_VERSION 1
+
+/* GEMM epilogues */
+#define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
+#define RF_EPI_F32 1        /* C(f32)   = A W^T + bias                                   */
+#define RF_EPI_ADD_F32 2    /* C(f32)  += A W^T + bias   (residual stream update)         */
+#define RF_EPI_SWIGLU 3     /* C(bf16)[M, N/2] = silu(A W1^T) * (A W3^T); W rows interleaved
+                               in 16-row groups [w1[16g:16g+16]; w3[16g:16g+16]]            */
+
+const char* rf_last_error(void);
+int rf_abi_version(void);
+
+/* C[M,N] (epilogue) A[M,K] * W[N,K]^T ; A, W bf16; K % 64 == 0, N % 128 == 0, 16-B aligned rows. */
+int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
+                 const float* bias, int m, int n, int k, int epilogue, void* stream);
+
+/* out(bf16)[r, :] = x[r, :] * rsqrt(mean(x^2) + eps) * weight ; x f32. */
+int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, float eps, void* out, int64_t ldo,
+               int rows, int dim, void* stream);
+
+/* dst[r] = rope(rmsnorm(src[src_rows ? src_rows[r] : r]))  (bf16 -> bf16, may alias when src_rows == NULL)
+ * norm_w may be NULL (no norm); pos may be NULL (no rope).  RoPE: head_dim 128, per head the half-split
+ * rotation with angle[i] = pos[r / pos_div][i / n_freqs] * freqs[i % n_freqs] for i < 9*n_freqs, else 0. */
+int rf_qk_norm_rope(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, const int32_t* src_rows,
+                    int rows, int dim, int n_heads, const float* norm_w, float eps, const float* pos,
+                    int64_t ld_pos, int pos_div, const float* freqs, int n_freqs, void* stream);
+
+/* Variable-length multi-head attention, non-causal, head_dim 128, bf16 in/out, f32 softmax.
+ * problems: int32[n_problems][5] = {q_start, q_len, k_start, k_len, v_start} (rows).
+ * For every problem p and head h: O[q_start+i, h*128:(h+1)*128] =
+ *   softmax(scale * Q_i K_j^T, j < k_len) V_j . */
+int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                void* o, int64_t ldo, const int32_t* problems, int n_problems, int max_q_len, int n_heads,
+                int head_dim, float scale, void* stream);
+
+/* Shifted-window attention over n_images patch grids [grid_h, grid_w] stored row-major (token
+ * r = img*gh*gw + y*gw + x); windows of window x window tokens on the grid rolled by -shift,
+ * Swin region mask when shift > 0.  Output written back to the un-rolled token positions. */
+int rf_swin_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                     void* o, int64_t ldo, int n_images, int grid_h, int grid_w, int window, int shift,
+                     int n_heads, int head_dim, float scale, void* stream);
+
+/* texture: f32 [n_rows, channels, patch_elems]; channels >= channels-log_channels are log10(x+1)
+ * encoded IN PLACE for every row; rows with dst_row[r] >= 0 are written as bf16 to out[dst_row[r]]. */
+int rf_texture_pack(float* texture, int64_t n_rows, int channels, int patch_elems, int log_channels,
+                    const int32_t* dst_row, void* out, int64_t ldo, void* stream);
+
+/* NeRF encoding (include_input) of vn f32 [n_rows, 9] into bf16 out[dst_row[r], 0:ldo] (zero padded). */
+int rf_vn_encode(const float* vn, int64_t n_rows, const int32_t* dst_row, int n_freqs, void* out,
+                 int64_t ldo, void* stream);
+
+/* Pinhole rays for n_views cameras (c2w f32 [n_views,4,4], fov degrees [n_views]) at res x res,
+ * normalised, patchified into bf16 tokens out[view*R + t, c*patch*patch + p1*patch + p2];
+ * ray_pos[view, 9] = camera origin repeated 3x. */
+int rf_ray_tokens(const float* c2w, const float* fov_deg, int n_views, int res, int patch, void* out,
+                  float* ray_pos, void* stream);
+
+/* rays_d f32 [n_views, res, res, 3] (already generated) -> the same bf16 token layout as rf_ray_tokens. */
+int rf_patchify_rays(const float* rays_d, int n_views, int res, int patch, void* out, void* stream);
+
+/* Triangle positions for RoPE.  tris f32 [*, 9]; valid_idx int32 [sum n_b] (rows into tris, grouped by
+ * scene, offsets scene_off[B+1]).  For each set s (s = b when c2w == NULL, else s = b*n_views + v with the
+ * camera transform p -> R^T (p - t)), writes n_reg centre rows then the n_b triangle rows to
+ * pos_out[set_off[s] ...]. */
+int rf_scene_pos(const float* tris, const int32_t* valid_idx, const int32_t* scene_off, const float* c2w,
+                 int n_scenes, int n_views, int n_reg, float* pos_out, const int32_t* set_off, void* stream);
+
+/* out[out_rows[r]] = base[r % base_rows] + sum_t rmsnorm(in_t[r]) * w_t   (f32; in_t / w_t may be NULL). */
+int rf_embed(float* out, int64_t ldo, const int32_t* out_rows, int rows, int dim, const float* base,
+             int base_rows, const float* in0, int64_t ld0, const float* w0, float eps0, const float* in1,
+             int64_t ld1, const float* w1, float eps1, void* stream);
+
+/* out = decode(elu(logits f32 [n, c, h, w], alpha)), decode = 10^x - 1 if log_decode; out is laid out
+ * [n, h, w, c] when channels_last, else [n, c, h, w]. */
+int rf_hdr_output(const float* logits, float* out, int n, int c, int h, int w, float elu_alpha, int log_decode,
+                  int channels_last, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RF_H */

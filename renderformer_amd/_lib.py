@@ -1,0 +1,84 @@
+"""ctypes binding of librfhip.so (the C ABI declared in include/rf.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` into
+``renderformer_amd/lib/librfhip.so``.  There is deliberately no fallback: if
+the library is missing or no HIP device is present, ``lib()`` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RF_LIB", os.path.join(_HERE, "lib", "librfhip.so"))
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_int64
+_F = ctypes.c_float
+
+# name -> argtypes (every function returns int status)
+SIGNATURES = {
+    "rf_gemm_bf16": [_P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _P],
+    "rf_rmsnorm": [_P, _L, _P, _F, _P, _L, _I, _I, _P],
+    "rf_qk_norm_rope": [_P, _L, _P, _L, _P, _I, _I, _I, _P, _F, _P, _L, _I, _P, _I, _P],
+    "rf_attn_fwd": [_P, _L, _P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _F, _P],
+    "rf_swin_attn_fwd": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _I, _I, _F, _P],
+    "rf_texture_pack": [_P, _L, _I, _I, _I, _P, _P, _L, _P],
+    "rf_vn_encode": [_P, _L, _P, _I, _P, _L, _P],
+    "rf_ray_tokens": [_P, _P, _I, _I, _I, _P, _P, _P],
+    "rf_patchify_rays": [_P, _I, _I, _I, _P, _P],
+    "rf_scene_pos": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P],
+    "rf_embed": [_P, _L, _P, _I, _I, _P, _I, _P, _L, _P, _F, _P, _L, _P, _F, _P],
+    "rf_hdr_output": [_P, _P, _I, _I, _I, _I, _F, _I, _I, _P],
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class HipLibraryError(RuntimeError):
+    pass
+
+
+def load(require_device: bool = True):
+    """Load librfhip.so (torch must be imported first so both share one HIP runtime)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise HipLibraryError(
+                    f"librfhip.so not found at {LIB_PATH}; build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, args in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.argtypes = args
+                fn.restype = ctypes.c_int
+            lib.rf_last_error.restype = ctypes.c_char_p
+            lib.rf_last_error.argtypes = []
+            lib.rf_abi_version.restype = ctypes.c_int
+            _lib = lib
+    if require_device and not torch.cuda.is_available():
+        raise HipLibraryError("renderformer_amd needs a HIP device (MI355X); none is visible")
+    return _lib
+
+
+def call(name: str, *args) -> None:
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.rf_last_error().decode(errors="replace")
+        if rc == 1:
+            raise ValueError(msg)
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream

@@ -1,0 +1,167 @@
+// Row-wise kernels: RMSNorm (f32 residual -> bf16 GEMM operand), full-width q/k
+// RMSNorm fused with the triangle RoPE, and token-embedding assembly.
+//
+// All are HBM-bound streaming kernels: one wave64 per row, fp32 reductions with
+// xor-shuffles, 8-16 B per lane accesses where the layout allows.
+#include <math.h>
+
+#include "common.h"
+
+namespace {
+
+constexpr int ROWS_PER_BLOCK = 4;  // 4 waves, one row each
+
+// ----------------------------------------------------------------------------- RMSNorm
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ x, int64_t ldx,
+                                                      const float* __restrict__ w, float eps,
+                                                      bf16_t* __restrict__ out, int64_t ldo, int rows, int dim) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float* xr = x + (int64_t)row * ldx;
+    float ss = 0.f;
+    for (int c = lane * 4; c < dim; c += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(xr + c);
+        ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    ss = wave_sum(ss);
+    const float inv = 1.0f / sqrtf(ss / (float)dim + eps);
+    bf16_t* orow = out + (int64_t)row * ldo;
+    for (int c = lane * 4; c < dim; c += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(xr + c);
+        const float4 g = *reinterpret_cast<const float4*>(w + c);
+        uint2 pk;
+        pk.x = pack_bf16x2(v.x * inv * g.x, v.y * inv * g.y);
+        pk.y = pack_bf16x2(v.z * inv * g.z, v.w * inv * g.w);
+        *reinterpret_cast<uint2*>(orow + c) = pk;
+    }
+}
+
+// ----------------------------------------------------------------------------- q/k norm + RoPE
+// Lane i owns, for every head, the rotation pair (i, i + 64) of that head, so the
+// half-split rotation happens in registers and the row can be rewritten in place.
+constexpr int MAX_HEADS = 16;
+
+__global__ __launch_bounds__(256) void qk_norm_rope_kernel(const bf16_t* src, int64_t ld_src, bf16_t* dst,
+                                                           int64_t ld_dst, const int32_t* __restrict__ src_rows,
+                                                           int rows, int n_heads, const float* __restrict__ norm_w,
+                                                           float eps, const float* __restrict__ pos, int64_t ld_pos,
+                                                           int pos_div, const float* __restrict__ freqs, int n_freqs) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int srow = src_rows ? src_rows[row] : row;
+    const bf16_t* s = src + (int64_t)srow * ld_src;
+    float lo[MAX_HEADS], hi[MAX_HEADS];
+    float ss = 0.f;
+#pragma unroll
+    for (int h = 0; h < MAX_HEADS; ++h) {
+        if (h < n_heads) {
+            lo[h] = bf16_to_f32(s[h * 128 + lane]);
+            hi[h] = bf16_to_f32(s[h * 128 + 64 + lane]);
+            ss += lo[h] * lo[h] + hi[h] * hi[h];
+        }
+    }
+    float inv = 1.f;
+    if (norm_w) {
+        ss = wave_sum(ss);
+        inv = 1.0f / sqrtf(ss / (float)(n_heads * 128) + eps);
+    }
+    float cs = 1.f, sn = 0.f;
+    if (pos && lane < 9 * n_freqs) {
+        const float* pr = pos + (int64_t)(row / pos_div) * ld_pos;
+        const float theta = pr[lane / n_freqs] * freqs[lane % n_freqs];
+        sincosf(theta, &sn, &cs);
+    }
+    bf16_t* d = dst + (int64_t)row * ld_dst;
+#pragma unroll
+    for (int h = 0; h < MAX_HEADS; ++h) {
+        if (h < n_heads) {
+            float a = lo[h] * inv, b = hi[h] * inv;
+            if (norm_w) {
+                a *= norm_w[h * 128 + lane];
+                b *= norm_w[h * 128 + 64 + lane];
+            }
+            // rotate in fp32 straight after the norm; one rounding to the bf16 attention operand
+            const float ra = a * cs - b * sn;
+            const float rb = b * cs + a * sn;
+            d[h * 128 + lane] = f32_to_bf16(ra);
+            d[h * 128 + 64 + lane] = f32_to_bf16(rb);
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------- embedding assembly
+__global__ __launch_bounds__(256) void embed_kernel(float* __restrict__ out, int64_t ldo,
+                                                    const int32_t* __restrict__ out_rows, int rows, int dim,
+                                                    const float* __restrict__ base, int base_rows,
+                                                    const float* __restrict__ in0, int64_t ld0,
+                                                    const float* __restrict__ w0, float eps0,
+                                                    const float* __restrict__ in1, int64_t ld1,
+                                                    const float* __restrict__ w1, float eps1) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    float s0 = 0.f, s1 = 0.f;
+    const float* r0 = in0 ? in0 + (int64_t)row * ld0 : nullptr;
+    const float* r1 = in1 ? in1 + (int64_t)row * ld1 : nullptr;
+    if (r0) {
+        float ss = 0.f;
+        for (int c = lane; c < dim; c += 64) ss += r0[c] * r0[c];
+        s0 = 1.0f / sqrtf(wave_sum(ss) / (float)dim + eps0);
+    }
+    if (r1) {
+        float ss = 0.f;
+        for (int c = lane; c < dim; c += 64) ss += r1[c] * r1[c];
+        s1 = 1.0f / sqrtf(wave_sum(ss) / (float)dim + eps1);
+    }
+    const float* b = base ? base + (int64_t)(row % base_rows) * dim : nullptr;
+    float* o = out + (int64_t)(out_rows ? out_rows[row] : row) * ldo;
+    for (int c = lane; c < dim; c += 64) {
+        // same association as the reference: (token + tex_emb) + vn_emb (renderformer.py:158)
+        float v = b ? b[c] : 0.f;
+        if (r0) v = v + r0[c] * s0 * w0[c];
+        if (r1) v = v + r1[c] * s1 * w1[c];
+        o[c] = v;
+    }
+}
+
+}  // namespace
+
+extern "C" int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, float eps, void* out, int64_t ldo,
+                          int rows, int dim, void* stream) {
+    RF_REQUIRE(x && weight && out, "rf_rmsnorm: null pointer");
+    RF_REQUIRE(dim % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0, "rf_rmsnorm: dim/ld must be multiples of 4");
+    if (rows <= 0) return RF_OK;
+    hipLaunchKernelGGL(rmsnorm_kernel, dim3((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), dim3(256), 0,
+                       (hipStream_t)stream, x, ldx, weight, eps, (bf16_t*)out, ldo, rows, dim);
+    return rf::check_launch("rf_rmsnorm");
+}
+
+extern "C" int rf_qk_norm_rope(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, const int32_t* src_rows,
+                               int rows, int dim, int n_heads, const float* norm_w, float eps, const float* pos,
+                               int64_t ld_pos, int pos_div, const float* freqs, int n_freqs, void* stream) {
+    RF_REQUIRE(src && dst, "rf_qk_norm_rope: null pointer");
+    RF_REQUIRE(dim == n_heads * 128 && n_heads <= MAX_HEADS, "rf_qk_norm_rope: need head_dim 128, <=%d heads",
+               MAX_HEADS);
+    RF_REQUIRE(!pos || (freqs && n_freqs > 0 && 9 * n_freqs <= 64 && pos_div > 0),
+               "rf_qk_norm_rope: rope needs freqs with 9*n_freqs <= 64");
+    if (rows <= 0) return RF_OK;
+    hipLaunchKernelGGL(qk_norm_rope_kernel, dim3((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16_t*)src, ld_src, (bf16_t*)dst, ld_dst, src_rows, rows, n_heads,
+                       norm_w, eps, pos, ld_pos, pos_div, freqs, n_freqs);
+    return rf::check_launch("rf_qk_norm_rope");
+}
+
+extern "C" int rf_embed(float* out, int64_t ldo, const int32_t* out_rows, int rows, int dim, const float* base,
+                        int base_rows, const float* in0, int64_t ld0, const float* w0, float eps0, const float* in1,
+                        int64_t ld1, const float* w1, float eps1, void* stream) {
+    RF_REQUIRE(out, "rf_embed: null output");
+    RF_REQUIRE((!in0 || w0) && (!in1 || w1), "rf_embed: input without norm weight");
+    RF_REQUIRE(!base || base_rows > 0, "rf_embed: base_rows must be > 0");
+    if (rows <= 0) return RF_OK;
+    hipLaunchKernelGGL(embed_kernel, dim3((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), dim3(256), 0,
+                       (hipStream_t)stream, out, ldo, out_rows, rows, dim, base, base_rows, in0, ld0, w0, eps0, in1,
+                       ld1, w1, eps1);
+    return rf::check_launch("rf_embed");
+}

@@ -1,0 +1,444 @@
+"""RenderFormer on MI355X: the two-stage transformer driven through librfhip.
+
+Public surface mirrors the reference ``RenderFormer`` (renderformer/models/
+renderformer.py:13-206): ``RenderFormer(config)``, ``from_pretrained``,
+``load_state_dict``/``state_dict``, ``to``/``eval``/``device`` and
+``forward(tri_vpos_list, texture_patch_list, valid_mask, vns, rays_o, rays_d,
+tri_vpos_view_tf, tf32_view_tf=False)``.
+
+Execution model: every scene is *unpadded* into a packed token
+matrix — stage 1 holds ``16 + n_b`` rows per scene (register tokens then the
+valid triangles), stage 2 ``R = (res/8)^2`` ray-token rows per (scene, view).
+All GEMMs run over the packed rows of the whole batch at once; attention
+kernels receive per-problem row ranges.  The residual streams are fp32,
+GEMM operands bf16, attention softmax fp32, the DPT head fp32.
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+
+from . import ops
+from ._lib import load as _load_lib
+from .config import RenderFormerConfig, named_config
+from .dpt import dpt_forward, dpt_weights
+from .weights import check_state_dict, load_snapshot, synthetic_state_dict
+
+EPS = 1e-6  # layers/attention.py:16
+SWIN_WINDOW, SWIN_SHIFT = 8, 4  # attention.py:604-605
+
+
+def _bf16(t, device):
+    return t.to(device=device, dtype=torch.bfloat16).contiguous()
+
+
+def _f32(t, device):
+    return t.to(device=device, dtype=torch.float32).contiguous()
+
+
+def _interleave_swiglu(w1: torch.Tensor, w3: torch.Tensor) -> torch.Tensor:
+    """[F, D] x2 -> [2F, D] in 16-row groups (w1 block g, w3 block g) for the SwiGLU GEMM epilogue."""
+    f, d = w1.shape
+    return torch.stack([w1.view(f // 16, 16, d), w3.view(f // 16, 16, d)], dim=1).reshape(2 * f, d)
+
+
+class _Layer:
+    pass
+
+
+class _DeviceWeights:
+    """Weights packed for the kernels: bf16 GEMM operands, fp32 norms/biases/tokens."""
+
+    def __init__(self, cfg: RenderFormerConfig, sd: Dict[str, torch.Tensor], device):
+        d = cfg.latent_dim
+        self.tri_token = _f32(sd["tri_token"].reshape(-1), device)
+        self.reg_tokens = _f32(sd["reg_tokens"].reshape(cfg.num_register_tokens, d), device)
+        vn_w = sd["vn_encoding_proj.weight"]
+        self.vn_k = ((vn_w.shape[1] + 63) // 64) * 64
+        self.vn_w = _bf16(torch.nn.functional.pad(vn_w, (0, self.vn_k - vn_w.shape[1])), device)
+        self.vn_b = _f32(sd["vn_encoding_proj.bias"], device)
+        self.vn_norm = _f32(sd["vn_encoder_norm.weight"], device)
+        self.tex_w = _bf16(sd["texture_encoder.weight"], device)
+        self.tex_b = _f32(sd["texture_encoder.bias"], device)
+        self.tex_norm = _f32(sd["texture_encoder_norm.weight"], device)
+        self.enc_freqs = _f32(sd["transformer.rope_emb.freqs"], device)
+        self.enc = []
+        for i in range(cfg.num_layers):
+            p = f"transformer.layers.{i}."
+            L = _Layer()
+            L.w_in = _bf16(sd[p + "multihead_attn.in_proj.weight"], device)
+            L.w_out = _bf16(sd[p + "multihead_attn.out_proj.weight"], device)
+            L.q_norm = _f32(sd[p + "multihead_attn.q_norm.weight"], device)
+            L.k_norm = _f32(sd[p + "multihead_attn.k_norm.weight"], device)
+            L.query_norm = _f32(sd[p + "query_norm.weight"], device)
+            L.w13 = _bf16(_interleave_swiglu(sd[p + "ffn.w1.weight"], sd[p + "ffn.w3.weight"]), device)
+            L.w2 = _bf16(sd[p + "ffn.w2.weight"], device)
+            L.ffn_norm = _f32(sd[p + "ffn_norm.weight"], device)
+            self.enc.append(L)
+        vt = "view_transformer."
+        self.patch_token = _f32(sd[vt + "ray_map_patch_token"].reshape(-1), device)
+        self.ray_w = _bf16(sd[vt + "ray_map_encoder.weight"], device)
+        self.ray_b = _f32(sd[vt + "ray_map_encoder.bias"], device)
+        self.ray_norm = _f32(sd[vt + "ray_map_encoder_norm.weight"], device)
+        self.dec_freqs = _f32(sd[vt + "transformer.rope_emb.freqs"], device)
+        self.dec = []
+        for i in range(cfg.view_transformer_n_layers):
+            p = f"{vt}transformer.layers.{i}."
+            a = p + "multihead_attn."
+            L = _Layer()
+            L.wq = _bf16(sd[a + "q_proj.weight"], device)
+            L.wkv = _bf16(torch.cat([sd[a + "k_proj.weight"], sd[a + "v_proj.weight"]], 0), device)
+            L.wo = _bf16(sd[a + "out_proj.weight"], device)
+            L.q_norm = _f32(sd[a + "q_norm.weight"], device)
+            L.k_norm = _f32(sd[a + "k_norm.weight"], device)
+            L.query_norm = _f32(sd[p + "query_norm.weight"], device)
+            L.kv_norm = _f32(sd[p + "kv_norm.weight"], device)
+            if cfg.view_transformer_include_self_attn:
+                s = p + "self_attn."
+                L.ws_in = _bf16(sd[s + "in_proj.weight"], device)
+                L.ws_out = _bf16(sd[s + "out_proj.weight"], device)
+                L.sq_norm = _f32(sd[s + "q_norm.weight"], device)
+                L.sk_norm = _f32(sd[s + "k_norm.weight"], device)
+                L.self_norm = _f32(sd[p + "self_attn_norm.weight"], device)
+            L.w13 = _bf16(_interleave_swiglu(sd[p + "ffn.w1.weight"], sd[p + "ffn.w3.weight"]), device)
+            L.w2 = _bf16(sd[p + "ffn.w2.weight"], device)
+            L.ffn_norm = _f32(sd[p + "ffn_norm.weight"], device)
+            self.dec.append(L)
+        self.dpt = dpt_weights(sd, vt + "out_dpt", device)
+
+
+@dataclass
+class _Plan:
+    """Packed-row bookkeeping for one batch (built once per mask pattern / view count / resolution)."""
+    B: int
+    V: int
+    res: int
+    counts: List[int]
+    T_tri: int
+    T1: int
+    T_kv: int
+    R: int
+    hp: int
+    wp: int
+    max_s: int
+    valid_flat: torch.Tensor   # int32 [T_tri] rows into [B*N]
+    dst_row: torch.Tensor      # int32 [B*N] -> packed triangle index or -1
+    tri_rows: torch.Tensor     # int32 [T_tri] -> stage-1 row
+    reg_rows: torch.Tensor     # int32 [16 B]
+    scene_off: torch.Tensor    # int32 [B+1] into valid_flat
+    cu1: torch.Tensor          # int32 [B+1] stage-1 row offsets
+    kv_off: torch.Tensor       # int32 [P+1] per-view K row offsets
+    kv_src_rows: torch.Tensor  # int32 [T_kv] -> stage-1 row
+    prob1: torch.Tensor        # int32 [B, 5]
+    prob2: torch.Tensor        # int32 [P, 5]
+    prob_self: torch.Tensor    # int32 [P, 5]
+    view_valid: Optional[torch.Tensor] = None  # for forward(): valid rows into [P*N]
+    view_off: Optional[torch.Tensor] = None
+
+
+def _build_plan(mask: torch.Tensor, V: int, res: int, patch: int, n_reg: int, device) -> _Plan:
+    B, N = mask.shape
+    counts = [int(c) for c in mask.sum(dim=1).tolist()]  # host sync (like flash_attn unpad_input)
+    flat = mask.reshape(-1)
+    valid_flat = torch.nonzero(flat).squeeze(1).to(torch.int32)
+    T_tri = int(valid_flat.numel())
+    dst_row = torch.full((B * N,), -1, dtype=torch.int32, device=device)
+    dst_row[valid_flat.long()] = torch.arange(T_tri, dtype=torch.int32, device=device)
+    S = [n_reg + c for c in counts]
+    cu1 = [0]
+    for s in S:
+        cu1.append(cu1[-1] + s)
+    tri_rows, reg_rows, prob1 = [], [], []
+    for b in range(B):
+        tri_rows.append(torch.arange(cu1[b] + n_reg, cu1[b + 1], dtype=torch.int32))
+        reg_rows.append(torch.arange(cu1[b], cu1[b] + n_reg, dtype=torch.int32))
+        prob1.append([cu1[b], S[b], cu1[b], S[b], cu1[b]])
+    scene_off = [0]
+    for c in counts:
+        scene_off.append(scene_off[-1] + c)
+    hp = wp = res // patch
+    R = hp * wp
+    P = B * V
+    kv_off, kv_src, prob2, prob_self = [0], [], [], []
+    for p in range(P):
+        b = p // V
+        kv_src.append(torch.arange(cu1[b], cu1[b + 1], dtype=torch.int32))
+        prob2.append([p * R, R, kv_off[-1], S[b], cu1[b]])
+        prob_self.append([p * R, R, p * R, R, p * R])
+        kv_off.append(kv_off[-1] + S[b])
+
+    def dev(x):
+        return (torch.cat(x) if isinstance(x, list) and x and torch.is_tensor(x[0]) else torch.tensor(x, dtype=torch.int32)).to(device)
+
+    return _Plan(B=B, V=V, res=res, counts=counts, T_tri=T_tri, T1=cu1[-1], T_kv=kv_off[-1], R=R, hp=hp, wp=wp,
+                 max_s=max(S), valid_flat=valid_flat, dst_row=dst_row, tri_rows=dev(tri_rows), reg_rows=dev(reg_rows),
+                 scene_off=dev(scene_off), cu1=dev(cu1), kv_off=dev(kv_off), kv_src_rows=dev(kv_src),
+                 prob1=dev(prob1).view(-1, 5), prob2=dev(prob2).view(-1, 5), prob_self=dev(prob_self).view(-1, 5))
+
+
+class RenderFormer:
+    """Drop-in for renderformer.models.renderformer.RenderFormer (inference only)."""
+
+    def __init__(self, config: RenderFormerConfig, state_dict: Optional[Dict[str, torch.Tensor]] = None,
+                 seed: int = 0):
+        self.config = config
+        cfg = config
+        if cfg.latent_dim // cfg.num_heads != 128 or cfg.vt_head_dim != 128:
+            raise ValueError("head_dim must be 128 (triangle RoPE constraint, rope.py:91-92)")
+        if cfg.vdir_num_freqs != 0 or cfg.vdir_pe_type != "nerf":
+            raise ValueError("only vdir_num_freqs=0 ray encoding is supported")
+        self._sd = state_dict if state_dict is not None else synthetic_state_dict(cfg, seed)
+        check_state_dict(cfg, self._sd, strict=state_dict is None)
+        self._device = torch.device("cpu")
+        self._w: Optional[_DeviceWeights] = None
+        self._plans: Dict = {}
+        self.skip_token_num = cfg.num_register_tokens
+
+    # ------------------------------------------------------------------ module-like API
+    @classmethod
+    def from_pretrained(cls, model_id: str, synthetic_seed: Optional[int] = None, **_):
+        """Local snapshot dir (config.json + model.safetensors) or, with synthetic_seed, a named config
+        with deterministic random weights.  Remote hub downloads are not supported (no network)."""
+        if os.path.isdir(model_id):
+            return cls(named_config(model_id), load_snapshot(model_id))
+        if synthetic_seed is None:
+            raise FileNotFoundError(f"{model_id!r} is not a local snapshot directory; pass synthetic_seed= for "
+                                    "random-init weights of the named architecture")
+        return cls(named_config(model_id), seed=synthetic_seed)
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        check_state_dict(self.config, sd, strict=strict)
+        self._sd = {k: v.detach().float().cpu() for k, v in sd.items()}
+        if self._w is not None:
+            self._w = _DeviceWeights(self.config, self._sd, self._device)
+        return self
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        return dict(self._sd)
+
+    def eval(self):
+        return self
+
+    def to(self, device):
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise ValueError("renderformer_amd runs on HIP devices only (no CPU path)")
+        _load_lib()
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self._device = device
+        self._w = _DeviceWeights(self.config, self._sd, device)
+        return self
+
+    cuda = lambda self, i=None: self.to("cuda" if i is None else f"cuda:{i}")  # noqa: E731
+
+    @property
+    def device(self):
+        return self._device
+
+    def parameters(self):
+        return iter(self._sd.values())
+
+    def _require(self):
+        if self._w is None:
+            raise RuntimeError("call .to('cuda') before running the model")
+        _load_lib()
+
+    def _plan(self, mask, V, res):
+        key = (tuple(mask.shape), mask.sum(1).cpu().numpy().tobytes(), mask.cpu().numpy().tobytes(), V, res)
+        plan = self._plans.get(key)
+        if plan is None:
+            if len(self._plans) > 16:
+                self._plans.clear()
+            plan = _build_plan(mask, V, res, self.config.patch_size, self.config.num_register_tokens, self._device)
+            self._plans[key] = plan
+        return plan
+
+    # ------------------------------------------------------------------ stages
+    def _embed_triangles(self, plan: _Plan, texture: torch.Tensor, vns: torch.Tensor, log_encode: bool):
+        cfg, W, dev = self.config, self._w, self._device
+        D = cfg.latent_dim
+        kt = cfg.texture_channels * cfg.texture_encode_patch_size ** 2
+        tex_in = torch.empty(plan.T_tri, kt, dtype=torch.bfloat16, device=dev)
+        ops.texture_pack(texture, 3 if log_encode else 0, plan.dst_row, tex_in)
+        vn_in = torch.empty(plan.T_tri, W.vn_k, dtype=torch.bfloat16, device=dev)
+        ops.vn_encode(vns, plan.dst_row, cfg.vn_pe_num_freqs, vn_in)
+        tex_lin = torch.empty(plan.T_tri, D, dtype=torch.float32, device=dev)
+        vn_lin = torch.empty(plan.T_tri, D, dtype=torch.float32, device=dev)
+        if plan.T_tri:
+            ops.gemm(tex_in, W.tex_w, tex_lin, W.tex_b, ops.EPI_F32)
+            ops.gemm(vn_in, W.vn_w, vn_lin, W.vn_b, ops.EPI_F32)
+        x = torch.empty(plan.T1, D, dtype=torch.float32, device=dev)
+        ops.embed(x, plan.tri_rows, plan.T_tri, W.tri_token, 1, tex_lin, W.tex_norm, ops.FLT_EPS, vn_lin, W.vn_norm,
+                  ops.FLT_EPS)
+        ops.embed(x, plan.reg_rows, plan.B * cfg.num_register_tokens, W.reg_tokens, cfg.num_register_tokens)
+        return x
+
+    def _stage1(self, plan: _Plan, x: torch.Tensor, pos1: torch.Tensor):
+        """TransformerEncoder (attention.py:579-590): pre-norm MHA with q/k norm + triangle RoPE, SwiGLU."""
+        cfg, W, dev = self.config, self._w, self._device
+        D, H, F = cfg.latent_dim, cfg.num_heads, cfg.dim_feedforward
+        T = plan.T1
+        h = torch.empty(T, D, dtype=torch.bfloat16, device=dev)
+        qkv = torch.empty(T, 3 * D, dtype=torch.bfloat16, device=dev)
+        att = torch.empty(T, D, dtype=torch.bfloat16, device=dev)
+        g = torch.empty(T, F, dtype=torch.bfloat16, device=dev)
+        q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+        for L in W.enc:
+            ops.rmsnorm(x, L.query_norm, EPS, h)
+            ops.gemm(h, L.w_in, qkv)
+            ops.qk_norm_rope(q, q, H, L.q_norm if cfg.view_indep_qk_norm else None, EPS, pos1, W.enc_freqs)
+            ops.qk_norm_rope(k, k, H, L.k_norm if cfg.view_indep_qk_norm else None, EPS, pos1, W.enc_freqs)
+            ops.attention(q, k, v, att, plan.prob1, plan.max_s, H)
+            ops.gemm(att, L.w_out, x, None, ops.EPI_ADD_F32)
+            ops.rmsnorm(x, L.ffn_norm, EPS, h)
+            ops.gemm(h, L.w13, g, None, ops.EPI_SWIGLU)
+            ops.gemm(g, L.w2, x, None, ops.EPI_ADD_F32)
+        return x
+
+    def _stage2(self, plan: _Plan, x: torch.Tensor, ctx: torch.Tensor, pos2: torch.Tensor, ray_pos: torch.Tensor):
+        """TransformerDecoder (attention.py:673-688): cross-attn rays->triangles, Swin/full self-attn, SwiGLU."""
+        cfg, W, dev = self.config, self._w, self._device
+        D, H, F = cfg.view_transformer_latent_dim, cfg.view_transformer_n_heads, cfg.view_transformer_ffn_hidden_dim
+        T2, R, P = x.shape[0], plan.R, plan.B * plan.V
+        qk = cfg.qk_norm
+        h = torch.empty(T2, D, dtype=torch.bfloat16, device=dev)
+        q2 = torch.empty(T2, D, dtype=torch.bfloat16, device=dev)
+        att = torch.empty(T2, D, dtype=torch.bfloat16, device=dev)
+        g = torch.empty(T2, F, dtype=torch.bfloat16, device=dev)
+        hc = torch.empty(plan.T1, ctx.shape[1], dtype=torch.bfloat16, device=dev)
+        kv = torch.empty(plan.T1, 2 * D, dtype=torch.bfloat16, device=dev)
+        kview = torch.empty(plan.T_kv, D, dtype=torch.bfloat16, device=dev)
+        qkv = torch.empty(T2, 3 * D, dtype=torch.bfloat16, device=dev) if cfg.view_transformer_include_self_attn else None
+        swin = cfg.view_transformer_use_swin_attn
+        taps = []
+        outl = set(cfg.out_layers)
+        for i, L in enumerate(W.dec):
+            # (i) cross-attention: K/V projections once per scene, K rotated per view
+            ops.rmsnorm(x, L.query_norm, EPS, h)
+            ops.gemm(h, L.wq, q2)
+            ops.rmsnorm(ctx, L.kv_norm, EPS, hc)
+            ops.gemm(hc, L.wkv, kv)
+            ops.qk_norm_rope(q2, q2, H, L.q_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R)
+            ops.qk_norm_rope(kv[:, :D], kview, H, L.k_norm if qk else None, EPS, pos2, W.dec_freqs,
+                             src_rows=plan.kv_src_rows)
+            ops.attention(q2, kview, kv[:, D:], att, plan.prob2, R, H)
+            ops.gemm(att, L.wo, x, None, ops.EPI_ADD_F32)
+            # (ii) self-attention between ray tokens
+            if qkv is not None:
+                ops.rmsnorm(x, L.self_norm, EPS, h)
+                ops.gemm(h, L.ws_in, qkv)
+                qs, ks, vs = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+                if swin:
+                    ops.qk_norm_rope(qs, qs, H, L.sq_norm if qk else None, EPS)
+                    ops.qk_norm_rope(ks, ks, H, L.sk_norm if qk else None, EPS)
+                    ops.swin_attention(qs, ks, vs, att, P, plan.hp, plan.wp, 0 if i % 2 == 0 else SWIN_SHIFT, H,
+                                       SWIN_WINDOW)
+                else:
+                    ops.qk_norm_rope(qs, qs, H, L.sq_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R)
+                    ops.qk_norm_rope(ks, ks, H, L.sk_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R)
+                    ops.attention(qs, ks, vs, att, plan.prob_self, R, H)
+                ops.gemm(att, L.ws_out, x, None, ops.EPI_ADD_F32)
+            # (iii) FFN
+            ops.rmsnorm(x, L.ffn_norm, EPS, h)
+            ops.gemm(h, L.w13, g, None, ops.EPI_SWIGLU)
+            ops.gemm(g, L.w2, x, None, ops.EPI_ADD_F32)
+            if i in outl:
+                taps.append(x.clone())
+        return taps
+
+    def _ray_embed(self, plan: _Plan, ray_in: torch.Tensor):
+        cfg, W, dev = self.config, self._w, self._device
+        D = cfg.view_transformer_latent_dim
+        T2 = ray_in.shape[0]
+        ray_lin = torch.empty(T2, D, dtype=torch.float32, device=dev)
+        ops.gemm(ray_in, W.ray_w, ray_lin, W.ray_b, ops.EPI_F32)
+        x2 = torch.empty(T2, D, dtype=torch.float32, device=dev)
+        ops.embed(x2, None, T2, W.patch_token, 1, ray_lin, W.ray_norm, ops.FLT_EPS)
+        return x2
+
+    def _decode(self, plan: _Plan, taps, log_decode: bool, channels_last: bool):
+        P = plan.B * plan.V
+        pt = self.config.patch_size
+        logits = dpt_forward(self._w.dpt, taps, P, plan.hp, plan.wp, pt)
+        c = logits.shape[1]
+        if channels_last:
+            out = torch.empty(P, plan.res, plan.res, c, dtype=torch.float32, device=self._device)
+        else:
+            out = torch.empty(P, c, plan.res, plan.res, dtype=torch.float32, device=self._device)
+        ops.hdr_output(logits, out, 1e-3, log_decode, channels_last)
+        return out
+
+    # ------------------------------------------------------------------ entry points
+    @torch.no_grad()
+    def render_views(self, triangles, texture, mask, vn, c2w, fov, resolution: int, log_encode: bool = True,
+                     timings: Optional[dict] = None) -> torch.Tensor:
+        """Pipeline fast path: rays, camera transform and positions are generated on the device.
+        Returns [B, V, res, res, C] linear HDR (log-decoded unless use_ldr)."""
+        self._require()
+        cfg, dev = self.config, self._device
+        B, V = c2w.shape[:2]
+        for t, n in ((triangles, "triangles"), (texture, "texture"), (mask, "mask"), (vn, "vn"), (c2w, "c2w"),
+                     (fov, "fov")):
+            if t.device != dev:
+                raise ValueError(f"{n} must be on {dev} (got {t.device})")
+        if resolution % (cfg.patch_size * (SWIN_WINDOW if cfg.view_transformer_use_swin_attn else 1)) != 0:
+            raise ValueError(f"resolution {resolution} incompatible with patch/window size")
+        plan = self._plan(mask, V, resolution)
+        tris = triangles.reshape(B, -1, 9).float().contiguous()
+        x1 = self._embed_triangles(plan, texture, vn.reshape(B, -1, 9).float().contiguous(), log_encode)
+        pos1 = torch.empty(plan.T1, 9, dtype=torch.float32, device=dev)
+        ops.scene_pos(tris, plan.valid_flat, plan.scene_off, None, B, 1, cfg.num_register_tokens, pos1, plan.cu1)
+        x1 = self._stage1(plan, x1, pos1)
+        P = B * V
+        c2w_v = c2w.reshape(P, 4, 4).float().contiguous()
+        eye = torch.eye(4, dtype=torch.float32, device=dev).expand(P, 4, 4).contiguous()
+        rays_c2w, pos_c2w = (eye, c2w_v) if cfg.turn_to_cam_coord else (c2w_v, eye)
+        ray_in = torch.empty(P * plan.R, 3 * cfg.patch_size ** 2, dtype=torch.bfloat16, device=dev)
+        ray_pos = torch.empty(P, 9, dtype=torch.float32, device=dev)
+        ops.ray_tokens(rays_c2w, fov.reshape(P).float().contiguous(), resolution, cfg.patch_size, ray_in, ray_pos)
+        x2 = self._ray_embed(plan, ray_in)
+        pos2 = torch.empty(plan.T_kv, 9, dtype=torch.float32, device=dev)
+        ops.scene_pos(tris, plan.valid_flat, plan.scene_off, pos_c2w, B, V, cfg.num_register_tokens, pos2,
+                      plan.kv_off)
+        taps = self._stage2(plan, x2, x1, pos2, ray_pos)
+        out = self._decode(plan, taps, log_decode=not cfg.use_ldr, channels_last=True)
+        return out.view(B, V, resolution, resolution, -1)
+
+    @torch.no_grad()
+    def forward(self, tri_vpos_list, texture_patch_list, valid_mask, vns, rays_o, rays_d, tri_vpos_view_tf,
+                tf32_view_tf=False):
+        """Reference signature (renderformer.py:171-206).  Returns ELU'd log-space images [B, V, C, H, W]."""
+        self._require()
+        cfg, dev = self.config, self._device
+        B, V = rays_o.shape[:2]
+        res = rays_d.shape[2]
+        plan = self._plan(valid_mask, V, res)
+        tris = tri_vpos_list.reshape(B, -1, 9).float().contiguous()
+        x1 = self._embed_triangles(plan, texture_patch_list.float().contiguous(),
+                                   vns.reshape(B, -1, 9).float().contiguous(), log_encode=False)
+        pos1 = torch.empty(plan.T1, 9, dtype=torch.float32, device=dev)
+        ops.scene_pos(tris, plan.valid_flat, plan.scene_off, None, B, 1, cfg.num_register_tokens, pos1, plan.cu1)
+        x1 = self._stage1(plan, x1, pos1)
+        P = B * V
+        ray_in = torch.empty(P * plan.R, 3 * cfg.patch_size ** 2, dtype=torch.bfloat16, device=dev)
+        ops.patchify_rays(rays_d.reshape(P, res, res, 3).float().contiguous(), cfg.patch_size, ray_in)
+        ray_pos = rays_o.reshape(P, 1, 3).float().expand(P, 3, 3).reshape(P, 9).contiguous()
+        x2 = self._ray_embed(plan, ray_in)
+        # per-view positions: every (b, v) is its own set over the [P*N, 9] camera-frame triangles
+        N = valid_mask.shape[1]
+        vmask = valid_mask.repeat_interleave(V, dim=0)
+        view_valid = torch.nonzero(vmask.reshape(-1)).squeeze(1).to(torch.int32)
+        view_off = torch.tensor([0] + [c for c in plan.counts for _ in range(V)], device=dev).cumsum(0).to(torch.int32)
+        pos2 = torch.empty(plan.T_kv, 9, dtype=torch.float32, device=dev)
+        ops.scene_pos(tri_vpos_view_tf.reshape(P * N, 9).float().contiguous(), view_valid, view_off, None, P, 1,
+                      cfg.num_register_tokens, pos2, plan.kv_off)
+        taps = self._stage2(plan, x2, x1, pos2, ray_pos)
+        out = self._decode(plan, taps, log_decode=False, channels_last=False)
+        return out.view(B, V, *out.shape[1:])
+
+    __call__ = forward

@@ -1,0 +1,162 @@
+"""Tensor-level wrappers over the librfhip C ABI.
+
+PyTorch is only plumbing here (device memory, streams): every op validates
+shapes/dtypes like the reference's asserts (raising ValueError) and launches a
+HIP kernel on the current stream.  Nothing in this module computes on the CPU
+or falls back to eager PyTorch math.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from ._lib import call, ptr, stream
+
+EPI_BF16, EPI_F32, EPI_ADD_F32, EPI_SWIGLU = 0, 1, 2, 3
+FLT_EPS = float(torch.finfo(torch.float32).eps)  # nn.RMSNorm(eps=None) on fp32 inputs
+
+
+def _check(cond, msg):
+    if not cond:
+        raise ValueError(msg)
+
+
+def _dev(t, dtype, name):
+    _check(t.is_cuda, f"{name} must be a device tensor")
+    _check(t.dtype == dtype, f"{name} must be {dtype}, got {t.dtype}")
+    _check(t.stride(-1) == 1, f"{name} must be contiguous in its last dim")
+
+
+def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias: Optional[torch.Tensor] = None,
+         epilogue: int = EPI_BF16) -> torch.Tensor:
+    """out (epilogue)= a @ w.T ; a [M,K] bf16, w [N,K] bf16."""
+    _dev(a, torch.bfloat16, "a")
+    _dev(w, torch.bfloat16, "w")
+    m, k = a.shape
+    n, k2 = w.shape
+    _check(k == k2, f"gemm: K mismatch {k} vs {k2}")
+    want = torch.bfloat16 if epilogue in (EPI_BF16, EPI_SWIGLU) else torch.float32
+    _dev(out, want, "out")
+    ncols = n // 2 if epilogue == EPI_SWIGLU else n
+    _check(out.shape[0] == m and out.shape[1] == ncols, f"gemm: out shape {tuple(out.shape)} != ({m}, {ncols})")
+    if bias is not None:
+        _dev(bias, torch.float32, "bias")
+    call("rf_gemm_bf16", ptr(a), a.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), ptr(bias), m, n, k,
+         epilogue, stream())
+    return out
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor) -> torch.Tensor:
+    _dev(x, torch.float32, "x")
+    _dev(out, torch.bfloat16, "out")
+    _check(x.shape == out.shape and w.numel() == x.shape[1], "rmsnorm: shape mismatch")
+    call("rf_rmsnorm", ptr(x), x.stride(0), ptr(w), eps, ptr(out), out.stride(0), x.shape[0], x.shape[1], stream())
+    return out
+
+
+def qk_norm_rope(src: torch.Tensor, dst: torch.Tensor, n_heads: int, norm_w: Optional[torch.Tensor], eps: float,
+                 pos: Optional[torch.Tensor] = None, freqs: Optional[torch.Tensor] = None, pos_div: int = 1,
+                 src_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dst[r] = rope(rmsnorm(src[src_rows[r]])) over the full width (attention.py:127-141)."""
+    _dev(src, torch.bfloat16, "src")
+    _dev(dst, torch.bfloat16, "dst")
+    rows, dim = dst.shape
+    _check(src.shape[1] == dim, "qk_norm_rope: width mismatch")
+    if src_rows is None:
+        _check(src.shape[0] == rows, "qk_norm_rope: row mismatch")
+    else:
+        _dev(src_rows, torch.int32, "src_rows")
+    if pos is not None:
+        _dev(pos, torch.float32, "pos")
+        _check(pos.shape[1] == 9 and freqs is not None, "qk_norm_rope: pos must be [*, 9] with freqs")
+    call("rf_qk_norm_rope", ptr(src), src.stride(0), ptr(dst), dst.stride(0), ptr(src_rows), rows, dim, n_heads,
+         ptr(norm_w), eps, ptr(pos), pos.stride(0) if pos is not None else 0, pos_div, ptr(freqs),
+         freqs.numel() if freqs is not None else 0, stream())
+    return dst
+
+
+def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int,
+              scale: Optional[float] = None) -> torch.Tensor:
+    """Varlen attention; problems int32 [P, 5] = (q_start, q_len, k_start, k_len, v_start)."""
+    for t, nme in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
+        _dev(t, torch.bfloat16, nme)
+    _dev(problems, torch.int32, "problems")
+    _check(problems.dim() == 2 and problems.shape[1] == 5, "attention: problems must be [P, 5]")
+    hd = q.shape[1] // n_heads
+    scale = 1.0 / math.sqrt(hd) if scale is None else scale
+    call("rf_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out), out.stride(0),
+         ptr(problems), problems.shape[0], max_q_len, n_heads, hd, scale, stream())
+    return out
+
+
+def swin_attention(q, k, v, out, n_images: int, grid_h: int, grid_w: int, shift: int, n_heads: int,
+                   window: int = 8) -> torch.Tensor:
+    for t, nme in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
+        _dev(t, torch.bfloat16, nme)
+    hd = q.shape[1] // n_heads
+    call("rf_swin_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out), out.stride(0),
+         n_images, grid_h, grid_w, window, shift, n_heads, hd, 1.0 / math.sqrt(hd), stream())
+    return out
+
+
+def texture_pack(texture: torch.Tensor, log_channels: int, dst_row: torch.Tensor, out: torch.Tensor):
+    _dev(texture, torch.float32, "texture")
+    _check(texture.is_contiguous(), "texture must be contiguous")
+    b, n, c = texture.shape[:3]
+    pe = texture[0, 0, 0].numel() if texture.dim() > 3 else 1
+    call("rf_texture_pack", ptr(texture), b * n, c, pe, log_channels, ptr(dst_row), ptr(out), out.stride(0), stream())
+    return out
+
+
+def vn_encode(vn: torch.Tensor, dst_row: torch.Tensor, n_freqs: int, out: torch.Tensor):
+    _dev(vn, torch.float32, "vn")
+    _check(vn.is_contiguous() and vn.shape[-1] == 9, "vn must be contiguous [..., 9]")
+    call("rf_vn_encode", ptr(vn), vn.numel() // 9, ptr(dst_row), n_freqs, ptr(out), out.stride(0), stream())
+    return out
+
+
+def ray_tokens(c2w: torch.Tensor, fov_deg: torch.Tensor, res: int, patch: int, out: torch.Tensor,
+               ray_pos: torch.Tensor):
+    _dev(c2w, torch.float32, "c2w")
+    _check(c2w.is_contiguous() and fov_deg.is_contiguous(), "c2w/fov must be contiguous")
+    call("rf_ray_tokens", ptr(c2w), ptr(fov_deg), c2w.numel() // 16, res, patch, ptr(out), ptr(ray_pos), stream())
+    return out
+
+
+def patchify_rays(rays_d: torch.Tensor, patch: int, out: torch.Tensor):
+    _dev(rays_d, torch.float32, "rays_d")
+    _check(rays_d.is_contiguous() and rays_d.shape[-1] == 3 and rays_d.shape[-2] == rays_d.shape[-3],
+           "rays_d must be contiguous [*, res, res, 3]")
+    res = rays_d.shape[-2]
+    call("rf_patchify_rays", ptr(rays_d), rays_d.numel() // (res * res * 3), res, patch, ptr(out), stream())
+    return out
+
+
+def scene_pos(tris: torch.Tensor, valid_idx, scene_off, c2w: Optional[torch.Tensor], n_scenes: int, n_views: int,
+              n_reg: int, pos_out: torch.Tensor, set_off: torch.Tensor):
+    _dev(tris, torch.float32, "tris")
+    _check(tris.is_contiguous(), "tris must be contiguous")
+    call("rf_scene_pos", ptr(tris), ptr(valid_idx), ptr(scene_off), ptr(c2w), n_scenes, n_views, n_reg, ptr(pos_out),
+         ptr(set_off), stream())
+    return pos_out
+
+
+def embed(out: torch.Tensor, out_rows: Optional[torch.Tensor], rows: int, base: Optional[torch.Tensor],
+          base_rows: int, in0=None, w0=None, eps0: float = FLT_EPS, in1=None, w1=None, eps1: float = FLT_EPS):
+    _dev(out, torch.float32, "out")
+    dim = out.shape[1]
+    call("rf_embed", ptr(out), out.stride(0), ptr(out_rows), rows, dim, ptr(base), base_rows, ptr(in0),
+         in0.stride(0) if in0 is not None else 0, ptr(w0), eps0, ptr(in1), in1.stride(0) if in1 is not None else 0,
+         ptr(w1), eps1, stream())
+    return out
+
+
+def hdr_output(logits: torch.Tensor, out: torch.Tensor, elu_alpha: float, log_decode: bool,
+               channels_last: bool = True):
+    _dev(logits, torch.float32, "logits")
+    _check(logits.is_contiguous() and out.is_contiguous(), "hdr_output: contiguous tensors required")
+    n, c, h, w = logits.shape
+    call("rf_hdr_output", ptr(logits), ptr(out), n, c, h, w, elu_alpha, int(log_decode), int(channels_last), stream())
+    return out

@@ -1,0 +1,262 @@
+"""Per-kernel numerics of librfhip against fp32/fp64 PyTorch references of the same op.
+
+Inputs are rounded to bf16 first, so the reference sees exactly the kernel's
+operands; remaining differences are accumulation order and output rounding.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import rf_ref
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from renderformer_amd import _lib
+    _lib.load()
+
+
+def _ops():
+    from renderformer_amd import ops
+    return ops
+
+
+def relerr(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("m,n,k", [(1, 128, 64), (77, 256, 128), (333, 384, 192), (5649, 1024, 1024),
+                                   (1000, 128, 13312), (4096, 3072, 1024)])
+def test_gemm_f32_bf16(m, n, k):
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(m * 7 + n)
+    a = torch.randn(m, k, generator=g).bfloat16().to(dev)
+    w = (torch.randn(n, k, generator=g) / math.sqrt(k)).bfloat16().to(dev)
+    bias = torch.randn(n, generator=g).to(dev)
+    ref = a.double() @ w.double().t() + bias.double()
+    out = torch.empty(m, n, device=dev)
+    ops.gemm(a, w, out, bias, ops.EPI_F32)
+    assert relerr(out, ref) < 1e-5
+    outb = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+    ops.gemm(a, w, outb, bias, ops.EPI_BF16)
+    assert relerr(outb.float(), ref) < 4e-3
+    acc = torch.randn(m, n, generator=g).to(dev)
+    ref2 = acc.double() + ref
+    ops.gemm(a, w, acc, bias, ops.EPI_ADD_F32)
+    assert relerr(acc, ref2) < 1e-5
+
+
+def test_gemm_asymmetric_identity():
+    """A = I with an asymmetric W catches a transposed C write (guide §3)."""
+    ops = _ops()
+    n = 128
+    a = torch.eye(n, 128, device=dev).bfloat16()
+    w = (torch.arange(n * 128, device=dev).float().view(n, 128) % 251).bfloat16()
+    out = torch.empty(n, n, device=dev)
+    ops.gemm(a, w, out, None, ops.EPI_F32)
+    assert torch.equal(out, w.float().t())
+
+
+@pytest.mark.parametrize("m,f,k", [(77, 512, 256), (1234, 3072, 768)])
+def test_gemm_swiglu(m, f, k):
+    ops = _ops()
+    from renderformer_amd.model import _interleave_swiglu
+    g = torch.Generator(device="cpu").manual_seed(f)
+    a = torch.randn(m, k, generator=g).bfloat16()
+    w1 = (torch.randn(f, k, generator=g) / math.sqrt(k)).bfloat16()
+    w3 = (torch.randn(f, k, generator=g) / math.sqrt(k)).bfloat16()
+    ref = F.silu(a.double() @ w1.double().t()) * (a.double() @ w3.double().t())
+    out = torch.empty(m, f, device=dev, dtype=torch.bfloat16)
+    ops.gemm(a.to(dev), _interleave_swiglu(w1, w3).to(dev), out, None, ops.EPI_SWIGLU)
+    assert relerr(out.float().cpu(), ref) < 5e-3
+
+
+def test_rmsnorm():
+    ops = _ops()
+    x = torch.randn(333, 768, device=dev) * 3
+    w = torch.rand(768, device=dev) + 0.5
+    out = torch.empty(333, 768, device=dev, dtype=torch.bfloat16)
+    ops.rmsnorm(x, w, 1e-6, out)
+    ref = F.rms_norm(x.double(), (768,), w.double(), 1e-6)
+    assert relerr(out.float(), ref) < 4e-3
+
+
+def test_qk_norm_rope_matches_oracle():
+    ops = _ops()
+    T, H = 300, 8
+    D = H * 128
+    src = torch.randn(T, 3 * D).bfloat16()
+    w = torch.rand(D) + 0.5
+    pos = torch.rand(T, 9) * 2 - 1
+    freqs = 2 ** torch.linspace(0, math.log2(5), 6)
+    q = src[:, :D].float()
+    qn = F.rms_norm(q, (D,), w, 1e-6)
+    cos, sin = rf_ref.rope_cos_sin(pos[None], freqs, 128)
+    ref = rf_ref.rope_apply(qn.view(1, T, H, 128).transpose(1, 2), cos, sin).transpose(1, 2).reshape(T, D)
+    s = src.to(dev)
+    ops.qk_norm_rope(s[:, :D], s[:, :D], H, w.to(dev), 1e-6, pos.to(dev), freqs.to(dev))
+    assert relerr(s[:, :D].float().cpu(), ref) < 4e-3
+    assert torch.equal(s[:, D:].cpu(), src[:, D:])  # other columns untouched
+    # gather + per-row pos divisor (ray tokens: one position per view)
+    rows = torch.tensor([5, 0, 299, 5], dtype=torch.int32)
+    dst = torch.empty(4, D, device=dev, dtype=torch.bfloat16)
+    vpos = torch.rand(2, 9)
+    ops.qk_norm_rope(src[:, D:2 * D].to(dev), dst, H, None, 1e-6, vpos.to(dev), freqs.to(dev), pos_div=2,
+                     src_rows=rows.to(dev))
+    kk = src[:, D:2 * D].float()[rows.long()]
+    cos, sin = rf_ref.rope_cos_sin(vpos.repeat_interleave(2, 0)[None], freqs, 128)
+    ref2 = rf_ref.rope_apply(kk.view(1, 4, H, 128).transpose(1, 2), cos, sin).transpose(1, 2).reshape(4, D)
+    assert relerr(dst.float().cpu(), ref2) < 4e-3
+
+
+def _ref_attn(q, k, v, H):
+    lq, lk = q.shape[0], k.shape[0]
+    qh = q.double().view(lq, H, 128).transpose(0, 1)
+    kh = k.double().view(lk, H, 128).transpose(0, 1)
+    vh = v.double().view(lk, H, 128).transpose(0, 1)
+    s = qh @ kh.transpose(1, 2) / math.sqrt(128)
+    return (torch.softmax(s, -1) @ vh).transpose(0, 1).reshape(lq, H * 128)
+
+
+@pytest.mark.parametrize("lens", [[1], [63], [64, 65], [77, 200, 1], [5649]])
+def test_attention_varlen_self(lens):
+    ops = _ops()
+    H = 2
+    D = H * 128
+    T = sum(lens)
+    g = torch.Generator(device="cpu").manual_seed(sum(lens))
+    qkv = (torch.randn(T, 3 * D, generator=g) * 2).bfloat16()
+    probs, off = [], 0
+    for n in lens:
+        probs.append([off, n, off, n, off])
+        off += n
+    out = torch.zeros(T, D, device=dev, dtype=torch.bfloat16)
+    d = qkv.to(dev)
+    ops.attention(d[:, :D], d[:, D:2 * D], d[:, 2 * D:], out, torch.tensor(probs, dtype=torch.int32, device=dev),
+                  max(lens), H)
+    out = out.float().cpu()
+    off = 0
+    for n in lens:
+        sl = slice(off, off + n)
+        ref = _ref_attn(qkv[sl, :D].float(), qkv[sl, D:2 * D].float(), qkv[sl, 2 * D:].float(), H)
+        assert relerr(out[sl], ref) < 6e-3, n
+        off += n
+
+
+def test_attention_cross_shared_v():
+    """Stage-2 form: per-view K rows, V rows shared by the views of a scene."""
+    ops = _ops()
+    H, D, R = 2, 256, 64
+    S = [70, 33]
+    Vn = 2
+    g = torch.Generator(device="cpu").manual_seed(3)
+    q = torch.randn(len(S) * Vn * R, D, generator=g).bfloat16()
+    kview = torch.randn(sum(S) * Vn, D, generator=g).bfloat16()
+    vsc = torch.randn(sum(S), D, generator=g).bfloat16()
+    probs, koff, voff, p = [], 0, 0, 0
+    for b, s in enumerate(S):
+        for _ in range(Vn):
+            probs.append([p * R, R, koff, s, voff])
+            koff += s
+            p += 1
+        voff += s
+    out = torch.empty_like(q).to(dev)
+    ops.attention(q.to(dev), kview.to(dev), vsc.to(dev), out, torch.tensor(probs, dtype=torch.int32, device=dev), R, H)
+    out = out.float().cpu()
+    for pr in probs:
+        qs, ql, ks, kl, vs = pr
+        ref = _ref_attn(q[qs:qs + ql].float(), kview[ks:ks + kl].float(), vsc[vs:vs + kl].float(), H)
+        assert relerr(out[qs:qs + ql], ref) < 6e-3
+
+
+@pytest.mark.parametrize("grid,shift", [(8, 0), (8, 4), (16, 4), (16, 0)])
+def test_swin_attention_matches_oracle_layout(grid, shift):
+    ops = _ops()
+    H, D, n_img = 2, 256, 2
+    T = n_img * grid * grid
+    g = torch.Generator(device="cpu").manual_seed(grid + shift)
+    q, k, v = [torch.randn(T, D, generator=g).bfloat16() for _ in range(3)]
+    out = torch.empty(T, D, device=dev, dtype=torch.bfloat16)
+    ops.swin_attention(q.to(dev), k.to(dev), v.to(dev), out, n_img, grid, grid, shift, H)
+    # reference: roll, partition, masked SDPA, reverse (attention.py:316-370 with identity projections)
+    def part(x):
+        x = x.float().view(n_img, grid, grid, D)
+        if shift:
+            x = torch.roll(x, (-shift, -shift), (1, 2))
+        return x.view(n_img, grid // 8, 8, grid // 8, 8, D).permute(0, 1, 3, 2, 4, 5).reshape(-1, 64, H, 128).transpose(1, 2)
+    qw, kw, vw = part(q), part(k), part(v)
+    mask = rf_ref.swin_mask(grid, grid, 8, shift).repeat(n_img, 1, 1)[:, None] if shift else None
+    o = F.scaled_dot_product_attention(qw.double(), kw.double(), vw.double(), attn_mask=mask)
+    o = o.transpose(1, 2).reshape(n_img, grid // 8, grid // 8, 8, 8, D).permute(0, 1, 3, 2, 4, 5).reshape(n_img, grid, grid, D)
+    if shift:
+        o = torch.roll(o, (shift, shift), (1, 2))
+    assert relerr(out.float().cpu(), o.reshape(T, D)) < 6e-3
+
+
+def test_prologue_kernels_match_oracle():
+    ops = _ops()
+    from renderformer_amd.scenes import batch_scenes, synthetic_scene
+    scenes = [synthetic_scene(40, 2, seed=3), synthetic_scene(25, 2, seed=4)]
+    bt = batch_scenes(scenes, padding_length=48)
+    B, N = 2, 48
+    mask = bt["mask"]
+    valid = torch.nonzero(mask.reshape(-1)).squeeze(1).int()
+    dst = torch.full((B * N,), -1, dtype=torch.int32)
+    dst[valid.long()] = torch.arange(valid.numel(), dtype=torch.int32)
+    # texture: in-place log encode of every row + packed bf16 of valid rows
+    tex = bt["texture"].clone().to(dev)
+    out = torch.empty(valid.numel(), 13 * 1024, device=dev, dtype=torch.bfloat16)
+    ops.texture_pack(tex, 3, dst.to(dev), out)
+    ref = bt["texture"].clone()
+    ref[:, :, -3:] = torch.log10(ref[:, :, -3:] + 1)
+    assert torch.allclose(tex.cpu(), ref, rtol=1e-6, atol=1e-6)
+    assert torch.equal(out.cpu(), ref.reshape(B * N, -1)[valid.long()].bfloat16())
+    # vn NeRF encoding
+    vo = torch.empty(valid.numel(), 128, device=dev, dtype=torch.bfloat16)
+    ops.vn_encode(bt["vn"].reshape(B, N, 9).contiguous().to(dev), dst.to(dev), 6, vo)
+    refv = rf_ref.nerf_encode(bt["vn"].reshape(B * N, 9)[valid.long()], 6)
+    assert torch.allclose(vo[:, :117].float().cpu(), refv.bfloat16().float(), atol=1e-2)
+    assert (vo[:, 117:] == 0).all()
+    # rays (+ patchify) vs RayGenerator restatement
+    res, P = 64, 4
+    c2w = bt["c2w"].reshape(P, 4, 4).contiguous()
+    fov = bt["fov"].reshape(P).contiguous()
+    ro, rd = rf_ref.ray_gen(c2w, fov[:, None] / 180.0 * torch.pi, res)
+    tok = torch.empty(P * 64, 192, device=dev, dtype=torch.bfloat16)
+    rpos = torch.empty(P, 9, device=dev)
+    ops.ray_tokens(c2w.to(dev), fov.to(dev), res, 8, tok, rpos)
+    reft = rd.view(P, 8, 8, 8, 8, 3).permute(0, 1, 3, 5, 2, 4).reshape(P * 64, 192)
+    assert (tok.float().cpu() - reft.bfloat16().float()).abs().max() < 1e-2
+    assert torch.allclose(rpos.cpu(), ro.repeat(1, 3))
+    tok2 = torch.empty_like(tok)
+    ops.patchify_rays(rd.contiguous().to(dev), 8, tok2)
+    assert torch.equal(tok2.cpu(), reft.bfloat16())
+    # RoPE positions: camera transform + register-token centre
+    counts = mask.sum(1).tolist()
+    scene_off = torch.tensor([0, counts[0], counts[0] + counts[1]], dtype=torch.int32)
+    S = [16 + c for c in counts]
+    set_off = torch.tensor([0, S[0], 2 * S[0], 2 * S[0] + S[1], 2 * S[0] + 2 * S[1]], dtype=torch.int32)
+    pos = torch.empty(int(set_off[-1]), 9, device=dev)
+    ops.scene_pos(bt["triangles"].reshape(B * N, 9).contiguous().to(dev), valid.to(dev), scene_off.to(dev),
+                  c2w.to(dev), B, 2, 16, pos, set_off.to(dev))
+    tcam = rf_ref.cam_transform(c2w, torch.repeat_interleave(bt["triangles"], 2, 0)).reshape(P, N, 9)
+    refp, _ = rf_ref.center_pos(tcam, torch.repeat_interleave(mask, 2, 0), 16)
+    for p in range(P):
+        n = counts[p // 2]
+        got = pos[int(set_off[p]):int(set_off[p + 1])].cpu()
+        assert torch.allclose(got, refp[p, :16 + n], atol=2e-6), p
+
+
+def test_hdr_output():
+    ops = _ops()
+    logits = torch.randn(2, 3, 16, 16, device=dev)
+    out = torch.empty(2, 16, 16, 3, device=dev)
+    ops.hdr_output(logits, out, 1e-3, True)
+    ref = torch.pow(10.0, F.elu(logits, 1e-3).permute(0, 2, 3, 1)) - 1
+    assert torch.allclose(out, ref, rtol=1e-6, atol=1e-6)
