@@ -18,6 +18,38 @@ EPI_BF16, EPI_F32, EPI_ADD_F32, EPI_SWIGLU = 0, 1, 2, 3
 FLT_EPS = float(torch.finfo(torch.float32).eps)  # nn.RMSNorm(eps=None) on fp32 inputs
 
 
+class KernelTimer:
+    """Brackets every launch of one tagged op with HIP events on the launch stream (bench.py roofline)."""
+
+    def __init__(self, tag: str):
+        self.tag = tag
+        self.pairs = []
+
+    def start(self, tag):
+        if tag != self.tag:
+            return None
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        self.pairs.append((e0, e1))
+        return e1
+
+    def durations_ms(self):
+        torch.cuda.synchronize()
+        return [a.elapsed_time(b) for a, b in self.pairs]
+
+
+TIMER: Optional[KernelTimer] = None
+
+
+def _t0(tag):
+    return TIMER.start(tag) if TIMER is not None and tag is not None else None
+
+
+def _t1(ev):
+    if ev is not None:
+        ev.record()
+
+
 def _check(cond, msg):
     if not cond:
         raise ValueError(msg)
@@ -30,7 +62,7 @@ def _dev(t, dtype, name):
 
 
 def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias: Optional[torch.Tensor] = None,
-         epilogue: int = EPI_BF16) -> torch.Tensor:
+         epilogue: int = EPI_BF16, tag: Optional[str] = None) -> torch.Tensor:
     """out (epilogue)= a @ w.T ; a [M,K] bf16, w [N,K] bf16."""
     _dev(a, torch.bfloat16, "a")
     _dev(w, torch.bfloat16, "w")
@@ -43,8 +75,10 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias: Optional[tor
     _check(out.shape[0] == m and out.shape[1] == ncols, f"gemm: out shape {tuple(out.shape)} != ({m}, {ncols})")
     if bias is not None:
         _dev(bias, torch.float32, "bias")
+    ev = _t0(tag)
     call("rf_gemm_bf16", ptr(a), a.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), ptr(bias), m, n, k,
          epilogue, stream())
+    _t1(ev)
     return out
 
 
@@ -78,7 +112,7 @@ def qk_norm_rope(src: torch.Tensor, dst: torch.Tensor, n_heads: int, norm_w: Opt
 
 
 def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int,
-              scale: Optional[float] = None) -> torch.Tensor:
+              scale: Optional[float] = None, tag: Optional[str] = None) -> torch.Tensor:
     """Varlen attention; problems int32 [P, 5] = (q_start, q_len, k_start, k_len, v_start)."""
     for t, nme in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
         _dev(t, torch.bfloat16, nme)
@@ -86,8 +120,10 @@ def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int
     _check(problems.dim() == 2 and problems.shape[1] == 5, "attention: problems must be [P, 5]")
     hd = q.shape[1] // n_heads
     scale = 1.0 / math.sqrt(hd) if scale is None else scale
+    ev = _t0(tag)
     call("rf_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out), out.stride(0),
          ptr(problems), problems.shape[0], max_q_len, n_heads, hd, scale, stream())
+    _t1(ev)
     return out
 
 
