@@ -38,8 +38,11 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
 }
 
 // ----------------------------------------------------------------------------- q/k norm + RoPE
-// Lane i owns, for every head, the rotation pair (i, i + 64) of that head, so the
-// half-split rotation happens in registers and the row can be rewritten in place.
+// Work unit = (head h, 8-element chunk j of the first half): it owns chunks j and j+8
+// of that head, i.e. the rotation pairs (8j+e, 8j+e+64), so the half-split rotation is
+// done in registers and the row can be rewritten in place.  Loads/stores are 16 B per
+// lane.  The 64 angles of a row are computed once (lane i -> angle i, accurate
+// sincosf) and broadcast with cross-lane shuffles.
 constexpr int MAX_HEADS = 16;
 
 __global__ __launch_bounds__(256) void qk_norm_rope_kernel(const bf16_t* src, int64_t ld_src, bf16_t* dst,
@@ -47,46 +50,79 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(const bf16_t* src, in
                                                            int rows, int n_heads, const float* __restrict__ norm_w,
                                                            float eps, const float* __restrict__ pos, int64_t ld_pos,
                                                            int pos_div, const float* __restrict__ freqs, int n_freqs) {
+    constexpr int UPL = MAX_HEADS * 8 / 64;  // max units per lane
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
     if (row >= rows) return;
     const int srow = src_rows ? src_rows[row] : row;
     const bf16_t* s = src + (int64_t)srow * ld_src;
-    float lo[MAX_HEADS], hi[MAX_HEADS];
+    const int units = n_heads * 8;
+    u32x4 lo[UPL], hi[UPL];
     float ss = 0.f;
 #pragma unroll
-    for (int h = 0; h < MAX_HEADS; ++h) {
-        if (h < n_heads) {
-            lo[h] = bf16_to_f32(s[h * 128 + lane]);
-            hi[h] = bf16_to_f32(s[h * 128 + 64 + lane]);
-            ss += lo[h] * lo[h] + hi[h] * hi[h];
+    for (int u = 0; u < UPL; ++u) {
+        const int unit = lane + 64 * u;
+        if (unit < units) {
+            const int h = unit >> 3, j = unit & 7;
+            lo[u] = *reinterpret_cast<const u32x4*>(s + h * 128 + 8 * j);
+            hi[u] = *reinterpret_cast<const u32x4*>(s + h * 128 + 64 + 8 * j);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float a0 = __uint_as_float(lo[u][e] << 16), a1 = __uint_as_float(lo[u][e] & 0xffff0000u);
+                const float b0 = __uint_as_float(hi[u][e] << 16), b1 = __uint_as_float(hi[u][e] & 0xffff0000u);
+                ss += a0 * a0 + a1 * a1 + b0 * b0 + b1 * b1;
+            }
         }
     }
     float inv = 1.f;
-    if (norm_w) {
-        ss = wave_sum(ss);
-        inv = 1.0f / sqrtf(ss / (float)(n_heads * 128) + eps);
-    }
-    float cs = 1.f, sn = 0.f;
+    if (norm_w) inv = 1.0f / sqrtf(wave_sum(ss) / (float)(n_heads * 128) + eps);
+    float my_c = 1.f, my_s = 0.f;
     if (pos && lane < 9 * n_freqs) {
         const float* pr = pos + (int64_t)(row / pos_div) * ld_pos;
-        const float theta = pr[lane / n_freqs] * freqs[lane % n_freqs];
-        sincosf(theta, &sn, &cs);
+        sincosf(pr[lane / n_freqs] * freqs[lane % n_freqs], &my_s, &my_c);
+    }
+    // every unit of this lane has chunk index j = lane & 7: fetch its 8 (cos, sin) pairs once,
+    // with all 64 lanes active (cross-lane reads from inactive lanes are undefined)
+    float cs[8], sn[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        cs[k] = pos ? __shfl(my_c, 8 * (lane & 7) + k, 64) : 1.f;
+        sn[k] = pos ? __shfl(my_s, 8 * (lane & 7) + k, 64) : 0.f;
     }
     bf16_t* d = dst + (int64_t)row * ld_dst;
 #pragma unroll
-    for (int h = 0; h < MAX_HEADS; ++h) {
-        if (h < n_heads) {
-            float a = lo[h] * inv, b = hi[h] * inv;
-            if (norm_w) {
-                a *= norm_w[h * 128 + lane];
-                b *= norm_w[h * 128 + 64 + lane];
+    for (int u = 0; u < UPL; ++u) {
+        const int unit = lane + 64 * u;
+        if (unit < units) {
+            const int h = unit >> 3, j = unit & 7;
+            float a[8], b[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                a[2 * e] = __uint_as_float(lo[u][e] << 16);
+                a[2 * e + 1] = __uint_as_float(lo[u][e] & 0xffff0000u);
+                b[2 * e] = __uint_as_float(hi[u][e] << 16);
+                b[2 * e + 1] = __uint_as_float(hi[u][e] & 0xffff0000u);
             }
-            // rotate in fp32 straight after the norm; one rounding to the bf16 attention operand
-            const float ra = a * cs - b * sn;
-            const float rb = b * cs + a * sn;
-            d[h * 128 + lane] = f32_to_bf16(ra);
-            d[h * 128 + 64 + lane] = f32_to_bf16(rb);
+            u32x4 olo, ohi;
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+                float ra[2], rb[2];
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const int i = 8 * j + e + t;
+                    float x0 = a[e + t] * inv, x1 = b[e + t] * inv;
+                    if (norm_w) {
+                        x0 *= norm_w[h * 128 + i];
+                        x1 *= norm_w[h * 128 + 64 + i];
+                    }
+                    ra[t] = x0 * cs[e + t] - x1 * sn[e + t];  // rotate_half_hf: (-x2, x1)
+                    rb[t] = x1 * cs[e + t] + x0 * sn[e + t];
+                }
+                olo[e / 2] = pack_bf16x2(ra[0], ra[1]);
+                ohi[e / 2] = pack_bf16x2(rb[0], rb[1]);
+            }
+            *reinterpret_cast<u32x4*>(d + h * 128 + 8 * j) = olo;
+            *reinterpret_cast<u32x4*>(d + h * 128 + 64 + 8 * j) = ohi;
         }
     }
 }
@@ -144,6 +180,8 @@ extern "C" int rf_qk_norm_rope(const void* src, int64_t ld_src, void* dst, int64
     RF_REQUIRE(src && dst, "rf_qk_norm_rope: null pointer");
     RF_REQUIRE(dim == n_heads * 128 && n_heads <= MAX_HEADS, "rf_qk_norm_rope: need head_dim 128, <=%d heads",
                MAX_HEADS);
+    RF_REQUIRE(ld_src % 8 == 0 && ld_dst % 8 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0,
+               "rf_qk_norm_rope: rows must be 16-B aligned");
     RF_REQUIRE(!pos || (freqs && n_freqs > 0 && 9 * n_freqs <= 64 && pos_div > 0),
                "rf_qk_norm_rope: rope needs freqs with 9*n_freqs <= 64");
     if (rows <= 0) return RF_OK;

@@ -25,7 +25,7 @@ import torch
 from . import ops
 from ._lib import load as _load_lib
 from .config import RenderFormerConfig, named_config
-from .dpt import dpt_forward, dpt_weights
+from .dpt import DPTHead
 from .weights import check_state_dict, load_snapshot, synthetic_state_dict
 
 EPS = 1e-6  # layers/attention.py:16
@@ -108,7 +108,7 @@ class _DeviceWeights:
             L.w2 = _bf16(sd[p + "ffn.w2.weight"], device)
             L.ffn_norm = _f32(sd[p + "ffn_norm.weight"], device)
             self.dec.append(L)
-        self.dpt = dpt_weights(sd, vt + "out_dpt", device)
+        self.dpt = DPTHead(sd, vt + "out_dpt", device)
 
 
 @dataclass
@@ -362,16 +362,9 @@ class RenderFormer:
         return x2
 
     def _decode(self, plan: _Plan, taps, log_decode: bool, channels_last: bool):
-        P = plan.B * plan.V
-        pt = self.config.patch_size
-        logits = dpt_forward(self._w.dpt, taps, P, plan.hp, plan.wp, pt)
-        c = logits.shape[1]
-        if channels_last:
-            out = torch.empty(P, plan.res, plan.res, c, dtype=torch.float32, device=self._device)
-        else:
-            out = torch.empty(P, c, plan.res, plan.res, dtype=torch.float32, device=self._device)
-        ops.hdr_output(logits, out, 1e-3, log_decode, channels_last)
-        return out
+        """DPT head + ELU(1e-3) (+ 10^x - 1) — the last two fused into the final conv."""
+        return self._w.dpt(taps, plan.B * plan.V, plan.hp, plan.wp, self.config.patch_size, 1e-3, log_decode,
+                           channels_last)
 
     # ------------------------------------------------------------------ entry points
     @torch.no_grad()
