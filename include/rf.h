@@ -29,6 +29,7 @@
  *   rf_conv2d_bf16x3   DPT nn.Conv2d (dpt.py:44-52, 69-72, 124-125, 184-192, 208-213, 232-240; aten conv2d) with
  *                      the ResidualConvUnit SiLU/skip (dpt.py:86-92) and fusion sum (:141-143) fused; FINAL mode
  *                      also fuses output_conv2 SiLU + 1x1 (dpt.py:234-240), ELU and the log decode
+ *   rf_split_planes    (operand preparation for the above; no reference counterpart)
  *   rf_deconv2d_bf16x3 DPT nn.ConvTranspose2d kernel == stride (dpt.py:195-206; aten conv_transpose2d)
  *   rf_upsample_bilinear F.interpolate(bilinear, align_corners=True) (dpt.py:154-155, 269-270)
  */
@@ -123,28 +124,37 @@ int rf_embed(float* out, int64_t ldo, const int32_t* out_rows, int rows, int dim
 int rf_hdr_output(const float* logits, float* out, int n, int c, int h, int w, float elu_alpha, int log_decode,
                   int channels_last, void* stream);
 
-/* DPT convolutions: NHWC fp32 activations, weights pre-split into bf16 hi/lo planes
- * [cout_pad][kh][kw][cin_pad] (zero padded), products evaluated as hi*hi + hi*lo + lo*hi with fp32
- * accumulation.  out[n, y, x, co] = conv(silu?(in)) + bias + res1 + res2, then silu? (flags).
- * RF_CONV_FINAL: cout <= 32; out[pixel, f] = elu(sum_c silu(conv_c) * w_fin[f, c] + b_fin[f], alpha),
+/* DPT convolutions on the GEMM engine.  Activations are NHWC; a convolution reads its input as two
+ * bf16 planes (hi = bf16(x), lo = bf16(x - hi); channel stride cin_pad, padded channels zero) and its
+ * weights as bf16 hi/lo [cout_pad][kh][kw][cin_pad]; products are hi*hi + hi*lo + lo*hi with fp32
+ * accumulation.  Epilogue: v = conv + bias + res1 + res2 (f32 NHWC, channel stride cout), then silu if
+ * RF_CONV_SILU_OUT; v is stored to `out` (f32, may be NULL) and/or split into the output planes
+ * p_hi/p_lo (channel stride p_ld), of silu(v) when RF_CONV_PLANE_SILU.
+ * RF_CONV_FINAL (cout <= 64): out[pixel, f] = elu(sum_c silu(v_c) * w_fin[f, c] + b_fin[f], alpha),
  * then 10^x - 1 with RF_CONV_LOG_DECODE; [n, n_fin, h, w] layout with RF_CONV_NCHW_OUT. */
-#define RF_CONV_SILU_IN 1
+#define RF_CONV_PLANE_SILU 1
 #define RF_CONV_SILU_OUT 2
 #define RF_CONV_FINAL 4
 #define RF_CONV_LOG_DECODE 8
 #define RF_CONV_NCHW_OUT 16
-int rf_conv2d_bf16x3(const float* in, int n_img, int hi, int wi, int cin, const void* w_hi, const void* w_lo,
-                     int cin_pad, int cout, int cout_pad, int kh, int kw, int stride, int pad, const float* bias,
-                     const float* res1, const float* res2, float* out, int flags, const float* w_fin,
-                     const float* b_fin, int n_fin, float elu_alpha, void* stream);
+int rf_conv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, int wi, int cin_pad, const void* w_hi,
+                     const void* w_lo, int cout, int cout_pad, int kh, int kw, int stride, int pad, const float* bias,
+                     const float* res1, const float* res2, float* out, void* p_hi, void* p_lo, int p_ld, int flags,
+                     const float* w_fin, const float* b_fin, int n_fin, float elu_alpha, void* stream);
 
 /* ConvTranspose2d with kernel == stride == k: out[n, k y + dy, k x + dx, co] = sum_ci in[n, y, x, ci] *
- * W[ci, co, dy, dx] + bias[co]; weights given as bf16 hi/lo [(dy, dx, co)][cin_pad]. */
-int rf_deconv2d_bf16x3(const float* in, int n_img, int hi, int wi, int cin, const void* w_hi, const void* w_lo,
-                       int cin_pad, int cout, int k, const float* bias, float* out, void* stream);
+ * W[ci, co, dy, dx] + bias[co]; input planes as above, weights bf16 hi/lo [(dy, dx, co)][cin_pad]. */
+int rf_deconv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, int wi, int cin_pad, const void* w_hi,
+                       const void* w_lo, int cout, int k, const float* bias, float* out, void* p_hi, void* p_lo,
+                       int p_ld, void* stream);
 
-/* Bilinear resize, align_corners=True, NHWC fp32 (c % 4 == 0). */
-int rf_upsample_bilinear(const float* in, int n_img, int hi, int wi, int c, float* out, int ho, int wo, void* stream);
+/* f32 rows x[r, 0:c] (row stride ldx) -> bf16 hi/lo planes (row stride p_ld), of silu(x) if silu_act. */
+int rf_split_planes(const float* x, int64_t rows, int c, int64_t ldx, void* p_hi, void* p_lo, int p_ld, int silu_act,
+                    void* stream);
+
+/* Bilinear resize, align_corners=True, NHWC fp32 (c % 4 == 0) into `out` and/or hi/lo planes. */
+int rf_upsample_bilinear(const float* in, int n_img, int hi, int wi, int c, float* out, int ho, int wo, void* p_hi,
+                         void* p_lo, int p_ld, void* stream);
 
 #ifdef __cplusplus
 }

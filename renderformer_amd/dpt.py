@@ -1,26 +1,36 @@
-"""DPT patch decode (renderformer/layers/dpt.py:174-273) on librfhip's bf16x3 NHWC convolutions.
+"""DPT patch decode (renderformer/layers/dpt.py:174-273) on librfhip's GEMM engine.
 
-Layout: every activation is NHWC fp32; the four decoder taps are already NHWC
-(token-major patch rows), so no permutes are needed.  Weights are re-laid out
-once to [cout_pad][kh][kw][cin_pad] and split into bf16 hi/lo planes.
+Layout: every activation is NHWC.  A tensor that feeds a convolution is kept as
+two bf16 planes (hi, lo) — optionally of silu(x), the ResidualConvUnit
+pre-activation — produced directly by the epilogue of the conv (or resize) that
+wrote it; tensors that are also needed as residuals are additionally kept in
+fp32.  Convolutions evaluate hi*hi + hi*lo + lo*hi with fp32 accumulation
+("bf16x3"), i.e. fp32-level accuracy at 3/16 of the fp32-MFMA cost (a plain
+bf16 DPT costs 2.0e-3 relative L2, SURVEY Appendix C, over the 1e-3 budget).
 
-Graph (dpt.py:242-273), with two exact rewrites:
+Graph with two exact rewrites:
 * FeatureFusionBlock's 1x1 ``out_conv`` is linear and the bilinear resize
   preserves constants, so ``out_conv(resize(x)) == resize(out_conv(x))``: the
   1x1 runs at the lower resolution (4x fewer pixels) before the resize.
 * The final ``F.interpolate`` to (hp*patch, wp*patch) is the identity (path_1 is
-  already 8*hp with patch 8, align_corners=True) and is skipped; output_conv2's
+  already 8*hp for patch 8, align_corners=True) and is skipped; output_conv2's
   SiLU + 1x1 + the ELU + 10^x - 1 decode are fused into the last 3x3 conv.
 """
 from __future__ import annotations
 
-from typing import Dict, List
+from dataclasses import dataclass
+from typing import Dict, List, Optional
 
 import torch
 
 from ._lib import call, ptr, stream
 
-SILU_IN, SILU_OUT, FINAL, LOG_DECODE, NCHW_OUT = 1, 2, 4, 8, 16
+PLANE_SILU, SILU_OUT, FINAL, LOG_DECODE, NCHW_OUT = 1, 2, 4, 8, 16
+BK, BN = 32, 128
+
+
+def _pad(c: int, m: int) -> int:
+    return -(-c // m) * m
 
 
 def _split(w: torch.Tensor):
@@ -29,80 +39,112 @@ def _split(w: torch.Tensor):
     return hi.contiguous(), lo.contiguous()
 
 
+@dataclass
+class Planes:
+    hi: torch.Tensor  # bf16 [n, h, w, ld]
+    lo: torch.Tensor
+    c: int            # real channels (ld - c padded channels are zero)
+
+    @property
+    def shape(self):
+        return self.hi.shape
+
+    @staticmethod
+    def empty(n, h, w, c, ld, device):
+        alloc = torch.zeros if ld > c else torch.empty
+        return Planes(alloc(n, h, w, ld, dtype=torch.bfloat16, device=device),
+                      alloc(n, h, w, ld, dtype=torch.bfloat16, device=device), c)
+
+
+def split_planes(x: torch.Tensor, ld: int, silu: bool = False) -> Planes:
+    """fp32 NHWC -> bf16 hi/lo planes with channel stride ld."""
+    n, h, w, c = x.shape
+    pl = Planes.empty(n, h, w, c, ld, x.device)
+    call("rf_split_planes", ptr(x), n * h * w, c, x.stride(2), ptr(pl.hi), ptr(pl.lo), ld, int(silu), stream())
+    return pl
+
+
+def upsample(x: torch.Tensor, ho: int, wo: int, out_f32: bool = True, planes_ld: Optional[int] = None):
+    n, h, w, c = x.shape
+    out = torch.empty(n, ho, wo, c, device=x.device) if out_f32 else None
+    pl = Planes.empty(n, ho, wo, c, planes_ld, x.device) if planes_ld else None
+    call("rf_upsample_bilinear", ptr(x), n, h, w, c, ptr(out), ho, wo, ptr(pl.hi if pl else None),
+         ptr(pl.lo if pl else None), planes_ld or 0, stream())
+    return out, pl
+
+
 class _Conv:
+    """One nn.Conv2d / nn.ConvTranspose2d(kernel == stride) with weights split for the bf16x3 engine."""
+
     def __init__(self, w: torch.Tensor, b, device, deconv: bool = False):
         w = w.detach().float().cpu()
-        if deconv:  # ConvTranspose2d weight [cin, cout, k, k] -> [(dy, dx, co), ci]
+        if deconv:  # ConvTranspose2d weight [cin, cout, k, k] -> rows (dy, dx, co), cols ci
             cin, cout, k, _ = w.shape
-            self.k = k
-            mat = w.permute(2, 3, 1, 0).reshape(k * k * cout, cin)
-            self.kh = self.kw = 1
+            self.k, self.kh, self.kw = k, 1, 1
+            self.cin_pad = _pad(cin, BK)
+            mat = torch.zeros(k * k * cout, self.cin_pad)
+            mat[:, :cin] = w.permute(2, 3, 1, 0).reshape(k * k * cout, cin)
             self.cout_pad = k * k * cout
         else:
             cout, cin, kh, kw = w.shape
-            self.k = 0
-            self.kh, self.kw = kh, kw
-            bn = 32 if cout <= 32 else 128
-            self.cout_pad = -(-cout // bn) * bn
-            mat = w.permute(0, 2, 3, 1)  # [cout, kh, kw, cin]
+            self.k, self.kh, self.kw = 0, kh, kw
+            self.cin_pad = _pad(cin, BK)
+            self.cout_pad = _pad(cout, BN)
+            mat = torch.zeros(self.cout_pad, kh, kw, self.cin_pad)
+            mat[:cout, :, :, :cin] = w.permute(0, 2, 3, 1)
+            mat = mat.reshape(self.cout_pad, -1)
         self.cin, self.cout = cin, cout
-        self.cin_pad = -(-cin // 64) * 64
-        if deconv:
-            full = torch.zeros(self.cout_pad, self.cin_pad)
-            full[:, :cin] = mat
-        else:
-            full = torch.zeros(self.cout_pad, self.kh, self.kw, self.cin_pad)
-            full[:cout, :, :, :cin] = mat
-        hi, lo = _split(full.reshape(self.cout_pad, -1))
+        hi, lo = _split(mat)
         self.w_hi, self.w_lo = hi.to(device), lo.to(device)
         self.b = None if b is None else b.detach().float().to(device).contiguous()
 
-    def __call__(self, x: torch.Tensor, stride=1, pad=None, flags=0, res1=None, res2=None, out=None,
-                 final=None):
-        n, h, w, c = x.shape
-        if c != self.cin or x.dtype != torch.float32 or not x.is_contiguous():
-            raise ValueError(f"conv input must be contiguous fp32 NHWC with {self.cin} channels, got {tuple(x.shape)}")
+    def __call__(self, x: Planes, stride=1, pad=None, res1=None, res2=None, out_f32=False,
+                 planes_ld: Optional[int] = None, planes_silu=False, final=None, final_flags=0):
+        n, h, w, ld = x.shape
+        if ld != self.cin_pad or x.c != self.cin:
+            raise ValueError(f"conv input planes must have {self.cin} channels padded to {self.cin_pad}, got "
+                             f"{x.c}/{ld}")
+        dev = x.hi.device
         if self.k:
-            if out is None:
-                out = torch.empty(n, h * self.k, w * self.k, self.cout, device=x.device)
-            call("rf_deconv2d_bf16x3", ptr(x), n, h, w, c, ptr(self.w_hi), ptr(self.w_lo), self.cin_pad, self.cout,
-                 self.k, ptr(self.b), ptr(out), stream())
-            return out
-        pad = self.kh // 2 if pad is None else pad
-        ho = (h + 2 * pad - self.kh) // stride + 1
-        wo = (w + 2 * pad - self.kw) // stride + 1
-        w_fin = b_fin = None
-        n_fin, alpha = 0, 0.0
+            ho, wo = h * self.k, w * self.k
+        else:
+            pad = self.kh // 2 if pad is None else pad
+            ho = (h + 2 * pad - self.kh) // stride + 1
+            wo = (w + 2 * pad - self.kw) // stride + 1
         if final is not None:
             w_fin, b_fin, alpha = final
-            n_fin = w_fin.shape[0]
-        if out is None:
-            out = torch.empty(n, ho, wo, n_fin if final is not None else self.cout, device=x.device)
+            nf = w_fin.shape[0]
+            shape = (n, nf, ho, wo) if final_flags & NCHW_OUT else (n, ho, wo, nf)
+            out = torch.empty(shape, device=dev)
+            call("rf_conv2d_bf16x3", ptr(x.hi), ptr(x.lo), n, h, w, ld, ptr(self.w_hi), ptr(self.w_lo), self.cout,
+                 self.cout_pad, self.kh, self.kw, stride, pad, ptr(self.b), 0, 0, ptr(out), 0, 0, 0,
+                 FINAL | final_flags, ptr(w_fin), ptr(b_fin), nf, alpha, stream())
+            return out
+        out = torch.empty(n, ho, wo, self.cout, device=dev) if out_f32 else None
+        pl = Planes.empty(n, ho, wo, self.cout, planes_ld, dev) if planes_ld else None
         for r in (res1, res2):
-            if r is not None and (r.shape != out.shape or not r.is_contiguous()):
+            if r is not None and (tuple(r.shape) != (n, ho, wo, self.cout) or not r.is_contiguous()):
                 raise ValueError("residual must match the conv output")
-        call("rf_conv2d_bf16x3", ptr(x), n, h, w, c, ptr(self.w_hi), ptr(self.w_lo), self.cin_pad, self.cout,
-             self.cout_pad, self.kh, self.kw, stride, pad, ptr(self.b), ptr(res1), ptr(res2), ptr(out), flags,
-             ptr(w_fin), ptr(b_fin), n_fin, alpha, stream())
-        return out
-
-
-def upsample(x: torch.Tensor, ho: int, wo: int) -> torch.Tensor:
-    n, h, w, c = x.shape
-    if (h, w) == (ho, wo):
-        return x  # align_corners=True resize to the same size is the identity
-    out = torch.empty(n, ho, wo, c, device=x.device)
-    call("rf_upsample_bilinear", ptr(x), n, h, w, c, ptr(out), ho, wo, stream())
-    return out
+        flags = PLANE_SILU if planes_silu else 0
+        if self.k:
+            call("rf_deconv2d_bf16x3", ptr(x.hi), ptr(x.lo), n, h, w, ld, ptr(self.w_hi), ptr(self.w_lo), self.cout,
+                 self.k, ptr(self.b), ptr(out), ptr(pl.hi if pl else None), ptr(pl.lo if pl else None),
+                 planes_ld or 0, stream())
+        else:
+            call("rf_conv2d_bf16x3", ptr(x.hi), ptr(x.lo), n, h, w, ld, ptr(self.w_hi), ptr(self.w_lo), self.cout,
+                 self.cout_pad, self.kh, self.kw, stride, pad, ptr(self.b), ptr(res1), ptr(res2), ptr(out),
+                 ptr(pl.hi if pl else None), ptr(pl.lo if pl else None), planes_ld or 0, flags, 0, 0, 0, 0.0,
+                 stream())
+        return out, pl
 
 
 class DPTHead:
     def __init__(self, sd: Dict[str, torch.Tensor], prefix: str, device):
         g = lambda n: sd.get(f"{prefix}.{n}")  # noqa: E731
         self.projects = [_Conv(g(f"projects.{i}.weight"), g(f"projects.{i}.bias"), device) for i in range(4)]
-        self.resize0 = _Conv(g("resize_layers.0.weight"), g("resize_layers.0.bias"), device, deconv=True)
-        self.resize1 = _Conv(g("resize_layers.1.weight"), g("resize_layers.1.bias"), device, deconv=True)
-        self.resize3 = _Conv(g("resize_layers.3.weight"), g("resize_layers.3.bias"), device)
+        self.resize = {0: _Conv(g("resize_layers.0.weight"), g("resize_layers.0.bias"), device, deconv=True),
+                       1: _Conv(g("resize_layers.1.weight"), g("resize_layers.1.bias"), device, deconv=True),
+                       3: _Conv(g("resize_layers.3.weight"), g("resize_layers.3.bias"), device)}
         self.rn = [_Conv(g(f"scratch.layer{i + 1}_rn.weight"), None, device) for i in range(4)]
         self.refine = {}
         for r in (1, 2, 3, 4):
@@ -117,43 +159,56 @@ class DPTHead:
         wf = g("scratch.output_conv2.2.weight")
         self.w_fin = wf.detach().float().reshape(wf.shape[0], -1).to(device).contiguous()
         self.b_fin = g("scratch.output_conv2.2.bias").detach().float().to(device).contiguous()
-        if self.out2.cout > 32:
-            raise ValueError("output_conv2 must have <= 32 channels for the fused head")
+        if self.out2.cout > 64:
+            raise ValueError("output_conv2 must have <= 64 channels for the fused head")
+        self.feat_ld = self.refine[1][0][2][0].cin_pad
 
-    def _rcu_pair(self, convs, x, extra=None):
-        """ResidualConvUnit (dpt.py:76-92): conv2(silu(conv1(silu(x)))) + x (+ extra: fusion-block sum)."""
-        t = convs[0](x, flags=SILU_IN)
-        return convs[1](t, flags=SILU_IN, res1=x, res2=extra)
+    def _rcu(self, convs, x32, xs: Planes, extra=None, want_f32=False, next_silu=True, next_ld=None):
+        """ResidualConvUnit (dpt.py:76-92): conv2(silu(conv1(silu(x)))) + x (+ extra = fusion-block x0)."""
+        _, t = convs[0](xs, planes_ld=convs[1].cin_pad, planes_silu=True)
+        return convs[1](t, res1=x32, res2=extra, out_f32=want_f32, planes_ld=next_ld, planes_silu=next_silu)
 
-    def _fuse(self, r, x0, x1, size):
+    def _fuse(self, r, x0, x1, x1s, size, last=False):
         """FeatureFusionBlock (dpt.py:133-159) with the 1x1 out_conv moved before the resize."""
         units, out_conv = self.refine[r]
-        out = x0 if x1 is None else self._rcu_pair(units[1], x1, extra=x0)
-        out = self._rcu_pair(units[2], out)
-        out = out_conv(out)
-        return upsample(out, *size)
+        if x1 is None:
+            out, outs = x0, split_planes(x0, self.feat_ld, silu=True)
+        else:
+            out, outs = self._rcu(units[1], x1, x1s, extra=x0, want_f32=True, next_ld=self.feat_ld)
+        _, y = self._rcu(units[2], out, outs, next_silu=False, next_ld=out_conv.cin_pad)
+        y32, _ = out_conv(y, out_f32=True)
+        if last:
+            return upsample(y32, *size, out_f32=False, planes_ld=self.out1.cin_pad)[1]
+        return upsample(y32, *size)[0]
 
     @torch.no_grad()
     def __call__(self, taps: List[torch.Tensor], n_img: int, hp: int, wp: int, patch: int, elu_alpha: float,
                  log_decode: bool, channels_last: bool) -> torch.Tensor:
         layers = []
         for i, t in enumerate(taps):
-            x = self.projects[i](t.view(n_img, hp, wp, t.shape[-1]))
-            if i == 0:
-                x = self.resize0(x)
-            elif i == 1:
-                x = self.resize1(x)
-            elif i == 3:
-                x = self.resize3(x, stride=2, pad=1)
+            x = split_planes(t.view(n_img, hp, wp, t.shape[-1]), self.projects[i].cin_pad)
+            nxt = self.resize[i] if i in self.resize else self.rn[i]
+            _, x = self.projects[i](x, planes_ld=nxt.cin_pad)
+            if i in self.resize:
+                _, x = self.resize[i](x, stride=2 if i == 3 else 1, pad=1 if i == 3 else None,
+                                      planes_ld=self.rn[i].cin_pad)
             layers.append(x)
-        rn = [self.rn[i](layers[i]) for i in range(4)]
+        rn, rns = [], []
+        for i in range(4):
+            o, s = self.rn[i](layers[i], out_f32=True, planes_ld=self.feat_ld, planes_silu=True)
+            rn.append(o)
+            rns.append(s)
         size = lambda t: (t.shape[1], t.shape[2])  # noqa: E731
-        p4 = self._fuse(4, rn[3], None, size(rn[2]))
-        p3 = self._fuse(3, p4, rn[2], size(rn[1]))
-        p2 = self._fuse(2, p3, rn[1], size(rn[0]))
-        p1 = self._fuse(1, p2, rn[0], (2 * rn[0].shape[1], 2 * rn[0].shape[2]))
-        out = self.out1(p1)
-        if (out.shape[1], out.shape[2]) != (hp * patch, wp * patch):
-            out = upsample(out, hp * patch, wp * patch)
-        flags = FINAL | (LOG_DECODE if log_decode else 0) | (0 if channels_last else NCHW_OUT)
-        return self.out2(out, flags=flags, final=(self.w_fin, self.b_fin, elu_alpha))
+        # refinenet4: only RCU2 on layer4_rn (its input planes hold silu(rn4))
+        units4, oc4 = self.refine[4]
+        _, y = self._rcu(units4[2], rn[3], rns[3], next_silu=False, next_ld=oc4.cin_pad)
+        y32, _ = oc4(y, out_f32=True)
+        p4 = upsample(y32, *size(rn[2]))[0]
+        p3 = self._fuse(3, p4, rn[2], rns[2], size(rn[1]))
+        p2 = self._fuse(2, p3, rn[1], rns[1], size(rn[0]))
+        p1 = self._fuse(1, p2, rn[0], rns[0], (2 * rn[0].shape[1], 2 * rn[0].shape[2]), last=True)
+        if (p1.shape[1], p1.shape[2]) != (hp * patch, wp * patch):
+            raise ValueError("DPT output size mismatch (patch size must be 8)")
+        _, o1 = self.out1(p1, planes_ld=self.out2.cin_pad)
+        flags = (LOG_DECODE if log_decode else 0) | (0 if channels_last else NCHW_OUT)
+        return self.out2(o1, final=(self.w_fin, self.b_fin, elu_alpha), final_flags=flags)

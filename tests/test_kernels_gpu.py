@@ -266,7 +266,7 @@ def test_hdr_output():
 @pytest.mark.parametrize("cin,cout,k,stride,hw", [(64, 128, 3, 1, 17), (256, 256, 3, 1, 32), (16, 32, 3, 1, 20),
                                                    (1024, 128, 1, 1, 16), (128, 128, 3, 2, 16), (48, 200, 3, 1, 9)])
 def test_conv_bf16x3_matches_fp64(cin, cout, k, stride, hw):
-    from renderformer_amd.dpt import SILU_IN, _Conv
+    from renderformer_amd.dpt import _Conv, split_planes
     g = torch.Generator(device="cpu").manual_seed(cin + cout)
     w = torch.randn(cout, cin, k, k, generator=g) / math.sqrt(cin * k * k)
     b = torch.randn(cout, generator=g)
@@ -275,25 +275,29 @@ def test_conv_bf16x3_matches_fp64(cin, cout, k, stride, hw):
     xn = x.permute(0, 2, 3, 1).contiguous().to(dev)
     pad = k // 2
     ref = F.conv2d(x.double(), w.double(), b.double(), stride=stride, padding=pad).permute(0, 2, 3, 1)
-    out = conv(xn, stride=stride, pad=pad)
+    out, _ = conv(split_planes(xn, conv.cin_pad), stride=stride, pad=pad, out_f32=True)
     assert relerr(out.cpu(), ref) < 2e-5
     if stride == 1 and k == 3 and cin == cout:
         r1 = torch.randn(ref.shape, generator=g)
         r2 = torch.randn(ref.shape, generator=g)
-        out = conv(xn, flags=SILU_IN, res1=r1.to(dev), res2=r2.to(dev))
+        out, pl = conv(split_planes(xn, conv.cin_pad, silu=True), res1=r1.to(dev), res2=r2.to(dev), out_f32=True,
+                       planes_ld=cout + 32, planes_silu=True)
         ref2 = F.conv2d(F.silu(x.double()), w.double(), b.double(), padding=pad).permute(0, 2, 3, 1) + r1 + r2
         assert relerr(out.cpu(), ref2) < 2e-5
+        both = pl.hi.float() + pl.lo.float()
+        assert relerr(both[..., :cout].cpu(), F.silu(ref2)) < 2e-5
+        assert (pl.hi[..., cout:] == 0).all() and (pl.lo[..., cout:] == 0).all()
 
 
 @pytest.mark.parametrize("cin,cout,k", [(128, 128, 4), (256, 256, 2), (16, 16, 4), (32, 32, 2)])
 def test_deconv_bf16x3(cin, cout, k):
-    from renderformer_amd.dpt import _Conv
+    from renderformer_amd.dpt import _Conv, split_planes
     g = torch.Generator(device="cpu").manual_seed(k * cin)
     w = torch.randn(cin, cout, k, k, generator=g) / math.sqrt(cin)
     b = torch.randn(cout, generator=g)
     x = torch.randn(2, cin, 8, 8, generator=g)
     conv = _Conv(w, b, dev, deconv=True)
-    out = conv(x.permute(0, 2, 3, 1).contiguous().to(dev))
+    out, _ = conv(split_planes(x.permute(0, 2, 3, 1).contiguous().to(dev), conv.cin_pad), out_f32=True)
     ref = F.conv_transpose2d(x.double(), w.double(), b.double(), stride=k).permute(0, 2, 3, 1)
     assert relerr(out.cpu(), ref) < 2e-5
 
@@ -302,13 +306,14 @@ def test_deconv_bf16x3(cin, cout, k):
 def test_upsample_bilinear_align_corners(hi, ho):
     from renderformer_amd.dpt import upsample
     x = torch.randn(2, 12, hi, hi)
-    out = upsample(x.permute(0, 2, 3, 1).contiguous().to(dev), ho, ho)
+    out, pl = upsample(x.permute(0, 2, 3, 1).contiguous().to(dev), ho, ho, planes_ld=32)
     ref = F.interpolate(x, size=(ho, ho), mode="bilinear", align_corners=True).permute(0, 2, 3, 1)
-    assert torch.allclose(out.cpu(), ref, atol=2e-6, rtol=1e-5)
+    assert torch.allclose(out.cpu(), ref, atol=1e-5, rtol=1e-5)
+    assert torch.allclose((pl.hi.float() + pl.lo.float())[..., :12].cpu(), ref, atol=1e-5, rtol=1e-5)
 
 
 def test_conv_final_head():
-    from renderformer_amd.dpt import FINAL, LOG_DECODE, NCHW_OUT, _Conv
+    from renderformer_amd.dpt import LOG_DECODE, NCHW_OUT, _Conv, split_planes
     g = torch.Generator(device="cpu").manual_seed(9)
     w = torch.randn(32, 64, 3, 3, generator=g) / 24
     b = torch.randn(32, generator=g) * 0.1
@@ -318,9 +323,9 @@ def test_conv_final_head():
     conv = _Conv(w, b, dev)
     y = F.conv2d(F.silu(F.conv2d(x.double(), w.double(), b.double(), padding=1)), wf.double(), bf.double())
     y = F.elu(y, 1e-3)
-    xn = x.permute(0, 2, 3, 1).contiguous().to(dev)
+    xs = split_planes(x.permute(0, 2, 3, 1).contiguous().to(dev), conv.cin_pad)
     fin = (wf.reshape(3, 32).to(dev), bf.to(dev), 1e-3)
-    out = conv(xn, flags=FINAL | LOG_DECODE, final=fin)
+    out = conv(xs, final=fin, final_flags=LOG_DECODE)
     assert relerr(out.cpu(), (10 ** y - 1).permute(0, 2, 3, 1)) < 2e-5
-    out2 = conv(xn, flags=FINAL | NCHW_OUT, final=fin, out=torch.empty(2, 3, 24, 24, device=dev))
+    out2 = conv(xs, final=fin, final_flags=NCHW_OUT)
     assert relerr(out2.cpu(), y) < 2e-5
