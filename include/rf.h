@@ -15,7 +15,8 @@
  *   rf_qk_norm_rope    q/k RMSNorm over full width (attention.py:127-133) fused with the
  *                      triangle RoPE (rope.py:106-149 apply_rotary_emb_*cossin, :78-103, :315-333)
  *   rf_attn_fwd        flash_attn_varlen_qkvpacked_func / flash_attn_varlen_kvpacked_func
- *                      (attention.py:164-198) and the masked SDPA branch (attention.py:143-161)
+ *                      (attention.py:164-198) and the masked SDPA branch (attention.py:143-161);
+ *                      rf_attn_combine / rf_attn_workspace_bytes belong to its split-KV mode
  *   rf_swin_attn_fwd   SwinSelfAttention roll + window_partition + masked SDPA + window_reverse
  *                      (attention.py:205-271, 316-370), with the roll done as index math
  *   rf_texture_pack    rendering_pipeline.py:67-68 (in-place log10 encode) + renderformer.py:145-147
@@ -77,10 +78,16 @@ int rf_qk_norm_rope(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, 
 /* Variable-length multi-head attention, non-causal, head_dim 128, bf16 in/out, f32 softmax.
  * problems: int32[n_problems][5] = {q_start, q_len, k_start, k_len, v_start} (rows).
  * For every problem p and head h: O[q_start+i, h*128:(h+1)*128] =
- *   softmax(scale * Q_i K_j^T, j < k_len) V_j . */
+ *   softmax(scale * Q_i K_j^T, j < k_len) V_j .
+ * n_split > 1 splits every key range over n_split workgroups (for launches that would leave CUs
+ * idle): partials go to `workspace` (rf_attn_workspace_bytes(ws_rows, n_heads, n_split) bytes, ws_rows
+ * >= every output row + 1) and rf_attn_combine(rows = NULL, n_rows = ws_rows) writes O. */
 int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                 void* o, int64_t ldo, const int32_t* problems, int n_problems, int max_q_len, int n_heads,
-                int head_dim, float scale, void* stream);
+                int head_dim, float scale, int n_split, void* workspace, int64_t ws_rows, void* stream);
+int64_t rf_attn_workspace_bytes(int64_t rows, int n_heads, int n_split);
+int rf_attn_combine(const void* workspace, int64_t ws_rows, int n_split, int n_heads, const int32_t* rows,
+                    int n_rows, void* o, int64_t ldo, void* stream);
 
 /* Shifted-window attention over n_images patch grids [grid_h, grid_w] stored row-major (token
  * r = img*gh*gw + y*gw + x); windows of window x window tokens on the grid rolled by -shift,

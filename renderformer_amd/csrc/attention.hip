@@ -13,25 +13,33 @@
 //     index math on load/store and the shift mask (attention.py:237-271) is
 //     computed from region labels in registers.
 //
-// Wave layout (each wave owns 32 query rows, the whole workgroup streams the
-// same K/V tiles of 64 keys through LDS):
+// Wave layout (each wave owns 32 query rows, the workgroup streams the same
+// K/V tiles of 64 keys through LDS):
 //   S^T[key][q] = K Q^T with v_mfma_f32_32x32x16_bf16, K from LDS as the A
 //   operand, Q held in registers as the B operand.  The accumulator has the
 //   query on the lane and 16 keys in registers, so the row max/sum need one
 //   cross-half exchange only, and the probabilities feed the next MFMA
 //   (O^T = V^T P^T) as its B operand without any lane movement; V^T comes
 //   straight from the row-major V tile with ds_read_b64_tr_b16.
+// VALU diet (the loop is VALU-bound otherwise): the softmax scale is folded into
+// one FMA feeding v_exp_f32 directly, the key mask only runs on the tail tile,
+// row maxima use max3, and the O rescale is skipped when no row max of the wave
+// moved (exact: alpha == 1).
+// Long key ranges are split over several workgroups (flash-decoding style) when a
+// launch would otherwise leave CUs idle; rf_attn_combine merges the partials.
 // LDS images use the 256-B-row XOR swizzle off(row, ch) = 256 row +
 // 16 (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))), conflict-free for both the
-// K ds_read_b128 and the V transposed reads (checked with the bank model in
-// tools/banks.py).  K/V tiles are register-staged with the issue-early /
-// write-late split: the next tile's global loads fly under this tile's MFMAs.
+// K ds_read_b128 and the V transposed reads (tools/banks.py).  K/V tiles are
+// register-staged with the issue-early / write-late split, double-buffered.
+// Workgroups are mapped so that every XCD processes a contiguous range of
+// (problem, head, split, q-block): the q-blocks sharing one K/V stream sit on one
+// XCD and read it from that XCD's L2.
 #include "common.h"
 
 namespace {
 
 constexpr int HD = 128;
-constexpr int KT = 64;                 // keys per tile
+constexpr int KT = 64;                   // keys per tile
 constexpr int TILE_BYTES = KT * HD * 2;  // 16 KiB
 constexpr float NEG = -1.0e30f;
 
@@ -45,11 +53,21 @@ struct AttnArgs {
     float c;                  // softmax scale * log2(e)
     // swin
     int gh, gw, shift, window;
+    // varlen grid decomposition
+    int n_qblk, n_heads, n_split, n_total;
+    // split partials: O [split][rows][D] f32, M/L [split][rows][H] f32
+    float* part_o;
+    float* part_ml;
+    int64_t part_rows;
 };
 
 RF_DEV int swz_off(int row, int ch) { return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4); }
 
 RF_DEV int region(int c, int g, int window, int shift) { return c < g - window ? 0 : (c < g - shift ? 1 : 2); }
+
+RF_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+RF_DEV float max3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
 
 template <bool SWIN, int NW>
 __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(AttnArgs p) {
@@ -62,29 +80,45 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(AttnArgs p) {
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int half = lane >> 5;
-    const int h = blockIdx.y;
-    const int hoff = h * HD;
 
-    int q_start = 0, q_len = 0, k_start = 0, k_len = 0, v_start = 0, q0 = 0;
+    int h, q_start = 0, q_len = 0, k_start = 0, k_len = 0, v_start = 0, q0 = 0;
+    int split = 0, t_begin = 0, t_end = 0;
     int img_row0 = 0, wy = 0, wx = 0;
     if constexpr (SWIN) {
         const int nwx = p.gw / p.window;
+        h = blockIdx.y;
         wy = blockIdx.x / nwx;
         wx = blockIdx.x % nwx;
         img_row0 = blockIdx.z * p.gh * p.gw;
         q_len = k_len = KT;
+        t_end = 1;
     } else {
-        const int32_t* d = p.problems + blockIdx.z * 5;
+        // XCD-aware bijective remap: hardware ids round-robin over 8 XCDs; hand each XCD a
+        // contiguous range of logical ids ordered (problem, head, split, q-block).
+        const int nwg = p.n_total, hwid = blockIdx.x;
+        const int xcd = hwid & 7, qq = nwg >> 3, rr = nwg & 7;
+        int id = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (hwid >> 3);
+        const int qb = id % p.n_qblk;
+        id /= p.n_qblk;
+        split = id % p.n_split;
+        id /= p.n_split;
+        h = id % p.n_heads;
+        const int prob = id / p.n_heads;
+        const int32_t* d = p.problems + prob * 5;
         q_start = d[0];
         q_len = d[1];
         k_start = d[2];
         k_len = d[3];
         v_start = d[4];
-        q0 = blockIdx.x * (NW * 32);
+        q0 = qb * (NW * 32);
         if (q0 >= q_len) return;
+        const int nt_all = (k_len + KT - 1) / KT;
+        const int per = (nt_all + p.n_split - 1) / p.n_split;
+        t_begin = split * per;
+        t_end = min(nt_all, t_begin + per);
     }
+    const int hoff = h * HD;
 
-    // window-local token -> global row (swin) ; query/key index -> row (varlen)
     auto swin_row = [&](int i) {
         const int hs = wy * p.window + i / p.window;
         const int ws = wx * p.window + i % p.window;
@@ -100,7 +134,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(AttnArgs p) {
     };
 
     // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[q][16 s + 8 half + 0..7]
-    const int qi = wave * 32 + (lane & 31);  // query index within block
+    const int qi = wave * 32 + (lane & 31);
     int qrow;
     if constexpr (SWIN) {
         qrow = swin_row(qi);
@@ -154,19 +188,21 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(AttnArgs p) {
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
-    float m_run = NEG, l_run = 0.f;
+    float m_run = NEG, l_run = 0.f;  // m_run in raw score units (before * c)
+    const float c = p.c;
 
-    const int nt = (k_len + KT - 1) / KT;
-    load_tile(0);
-    write_tile(0);
+    if (t_begin < t_end) {
+        load_tile(t_begin);
+        write_tile(0);
+    }
     __syncthreads();
 
     // tr-read lane geometry (ds_read_b64_tr_b16): group g = lane>>4, lane 4qq+pp of the group
     const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
 
-    for (int kt = 0; kt < nt; ++kt) {
-        const int cur = SWIN ? 0 : (kt & 1);
-        if (!SWIN && kt + 1 < nt) load_tile(kt + 1);
+    for (int kt = t_begin; kt < t_end; ++kt) {
+        const int cur = SWIN ? 0 : ((kt - t_begin) & 1);
+        if (!SWIN && kt + 1 < t_end) load_tile(kt + 1);
         const char* kb = smem + cur * 2 * TILE_BYTES;
         const char* vb = kb + TILE_BYTES;
 
@@ -183,40 +219,58 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(AttnArgs p) {
             }
         }
 
-        // ---- scale, mask, online softmax (query on the lane; keys split across lane halves)
-        float mt = NEG;
+        // ---- mask (tail tile / swin regions only), row max
+        bool masked;
+        if constexpr (SWIN) {
+            masked = p.shift > 0;
+        } else {
+            masked = (kt + 1) * KT > k_len;
+        }
+        if (masked) {
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+            for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int key = b * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                float val = s[b][r] * p.c;
-                if constexpr (SWIN) {
-                    if (p.shift > 0 && swin_label(key) != qlabel) val = NEG;
-                } else {
-                    if (kt * KT + key >= k_len) val = NEG;
+                for (int r = 0; r < 16; ++r) {
+                    const int key = b * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                    bool drop;
+                    if constexpr (SWIN) {
+                        drop = swin_label(key) != qlabel;
+                    } else {
+                        drop = kt * KT + key >= k_len;
+                    }
+                    s[b][r] = drop ? NEG : s[b][r];
                 }
-                s[b][r] = val;
-                mt = fmaxf(mt, val);
-            }
-        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-        const float m_new = fmaxf(m_run, mt);
-        const float alpha = exp2f(m_run - m_new);
+        }
+        float mt = max3(s[0][0], s[0][1], s[0][2]);
+#pragma unroll
+        for (int r = 3; r < 15; r += 2) mt = max3(mt, s[0][r], s[0][r + 1]);
+        mt = max3(mt, s[0][15], s[1][0]);
+#pragma unroll
+        for (int r = 1; r < 15; r += 2) mt = max3(mt, s[1][r], s[1][r + 1]);
+        mt = __builtin_fmaxf(mt, s[1][15]);
+        mt = __builtin_fmaxf(mt, __shfl_xor(mt, 32, 64));
+        const float m_new = __builtin_fmaxf(m_run, mt);
+        // rescale O/l only if some row max of this wave moved (exact skip: alpha == 1 otherwise)
+        if (__any(m_new > m_run)) {
+            const float alpha = fast_exp2((m_run - m_new) * c);
+            l_run *= alpha;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+        }
         m_run = m_new;
+        const float mc = m_new * c;
         float ls = 0.f;
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float pv = exp2f(s[b][r] - m_new);
+                const float pv = fast_exp2(__builtin_fmaf(s[b][r], c, -mc));
                 s[b][r] = pv;
                 ls += pv;
             }
-        l_run = l_run * alpha + ls;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+        l_run += ls;
 
         // ---- O^T += V^T P^T : P (accumulator layout) is the B operand as-is
         bf16x8 pf[2][2];
@@ -245,13 +299,12 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(AttnArgs p) {
                 }
         }
 
-        if (!SWIN && kt + 1 < nt) write_tile(cur ^ 1);
+        if (!SWIN && kt + 1 < t_end) write_tile(cur ^ 1);
         __syncthreads();
     }
 
-    // ---- normalise and store: lane owns query (lane & 31), d = dt*32 + 8 gq + 4 half + 0..3
+    // ---- epilogue: lane owns query (lane & 31), d = dt*32 + 8 gq + 4 half + 0..3
     const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-    const float inv = l_tot > 0.f ? 1.0f / l_tot : 0.f;
     int orow;
     if constexpr (SWIN) {
         orow = swin_row(qi);
@@ -260,6 +313,23 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(AttnArgs p) {
         if (qq2 >= q_len) return;
         orow = q_start + qq2;
     }
+    if (!SWIN && p.n_split > 1) {
+        // unnormalised partials for rf_attn_combine (rows indexed like the output)
+        float* po = p.part_o + ((int64_t)split * p.part_rows + orow) * (p.n_heads * HD) + hoff;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq)
+                *reinterpret_cast<float4*>(po + dt * 32 + 8 * gq + 4 * half) =
+                    make_float4(o[dt][4 * gq], o[dt][4 * gq + 1], o[dt][4 * gq + 2], o[dt][4 * gq + 3]);
+        if (half == 0) {
+            float* pm = p.part_ml + (((int64_t)split * p.part_rows + orow) * p.n_heads + h) * 2;
+            pm[0] = m_run * c;
+            pm[1] = l_tot;
+        }
+        return;
+    }
+    const float inv = l_tot > 0.f ? 1.0f / l_tot : 0.f;
     bf16_t* dst = p.o + (int64_t)orow * p.ldo + hoff;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
@@ -272,24 +342,89 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(AttnArgs p) {
         }
 }
 
+// merge split partials: out = sum_s 2^(m_s - M) O_s / sum_s 2^(m_s - M) l_s   (one wave per (row, head))
+__global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restrict__ part_o,
+                                                           const float* __restrict__ part_ml, int64_t part_rows,
+                                                           int n_split, int n_heads, const int32_t* __restrict__ rows,
+                                                           int n_rows, bf16_t* __restrict__ o, int64_t ldo) {
+    const int lane = threadIdx.x & 63;
+    const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (item >= (int64_t)n_rows * n_heads) return;
+    const int h = (int)(item % n_heads);
+    const int row = rows ? rows[item / n_heads] : (int)(item / n_heads);
+    float mx = NEG;
+    for (int s = 0; s < n_split; ++s) mx = fmaxf(mx, part_ml[(((int64_t)s * part_rows + row) * n_heads + h) * 2]);
+    float l = 0.f, a0 = 0.f, a1 = 0.f;
+    for (int s = 0; s < n_split; ++s) {
+        const float* ml = part_ml + (((int64_t)s * part_rows + row) * n_heads + h) * 2;
+        const float w = exp2f(ml[0] - mx);
+        l += w * ml[1];
+        const float* po = part_o + ((int64_t)s * part_rows + row) * (n_heads * HD) + h * HD;
+        a0 += w * po[lane];
+        a1 += w * po[lane + 64];
+    }
+    const float inv = l > 0.f ? 1.0f / l : 0.f;
+    bf16_t* dst = o + (int64_t)row * ldo + h * HD;
+    dst[lane] = f32_to_bf16(a0 * inv);
+    dst[lane + 64] = f32_to_bf16(a1 * inv);
+}
+
 constexpr float LOG2E = 1.4426950408889634f;
 
 }  // namespace
 
 extern "C" int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                            void* o, int64_t ldo, const int32_t* problems, int n_problems, int max_q_len, int n_heads,
-                           int head_dim, float scale, void* stream) {
+                           int head_dim, float scale, int n_split, void* workspace, int64_t ws_rows, void* stream) {
     RF_REQUIRE(q && k && v && o && problems, "rf_attn_fwd: null pointer");
     RF_REQUIRE(head_dim == HD, "rf_attn_fwd: head_dim must be 128 (got %d)", head_dim);
     RF_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0, "rf_attn_fwd: strides must be 16-B aligned");
-    RF_REQUIRE(n_problems < 65536 && n_heads < 65536, "rf_attn_fwd: grid too large");
+    RF_REQUIRE(n_split >= 1 && n_split <= 16, "rf_attn_fwd: n_split must be 1..16");
+    RF_REQUIRE(n_split == 1 || (workspace && ws_rows > 0), "rf_attn_fwd: split needs a workspace");
     if (n_problems <= 0 || max_q_len <= 0) return RF_OK;
-    AttnArgs a{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, ldq, ldk, ldv, ldo, problems,
-               scale * LOG2E, 0, 0, 0, 8};
     constexpr int NW = 4;
-    dim3 grid((max_q_len + NW * 32 - 1) / (NW * 32), n_heads, n_problems);
-    hipLaunchKernelGGL((attn_fwd_kernel<false, NW>), grid, dim3(NW * 64), 0, (hipStream_t)stream, a);
+    const int n_qblk = (max_q_len + NW * 32 - 1) / (NW * 32);
+    const int64_t total = (int64_t)n_qblk * n_heads * n_split * n_problems;
+    RF_REQUIRE(total < (1ll << 31), "rf_attn_fwd: grid too large");
+    AttnArgs a{};
+    a.q = (const bf16_t*)q;
+    a.k = (const bf16_t*)k;
+    a.v = (const bf16_t*)v;
+    a.o = (bf16_t*)o;
+    a.ldq = ldq;
+    a.ldk = ldk;
+    a.ldv = ldv;
+    a.ldo = ldo;
+    a.problems = problems;
+    a.c = scale * LOG2E;
+    a.window = 8;
+    a.n_qblk = n_qblk;
+    a.n_heads = n_heads;
+    a.n_split = n_split;
+    a.n_total = (int)total;
+    a.part_rows = ws_rows;
+    if (n_split > 1) {
+        a.part_o = (float*)workspace;
+        a.part_ml = a.part_o + (int64_t)n_split * ws_rows * n_heads * HD;
+    }
+    hipLaunchKernelGGL((attn_fwd_kernel<false, NW>), dim3((unsigned)total), dim3(NW * 64), 0, (hipStream_t)stream, a);
     return rf::check_launch("rf_attn_fwd");
+}
+
+extern "C" int64_t rf_attn_workspace_bytes(int64_t rows, int n_heads, int n_split) {
+    return n_split <= 1 ? 0 : (int64_t)n_split * rows * n_heads * (HD + 2) * (int64_t)sizeof(float);
+}
+
+extern "C" int rf_attn_combine(const void* workspace, int64_t ws_rows, int n_split, int n_heads, const int32_t* rows,
+                               int n_rows, void* o, int64_t ldo, void* stream) {
+    RF_REQUIRE(workspace && o, "rf_attn_combine: null pointer");
+    if (n_rows <= 0) return RF_OK;
+    const float* po = (const float*)workspace;
+    const float* pml = po + (int64_t)n_split * ws_rows * n_heads * HD;
+    const int64_t items = (int64_t)n_rows * n_heads;
+    hipLaunchKernelGGL(attn_combine_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, (hipStream_t)stream, po,
+                       pml, ws_rows, n_split, n_heads, rows, n_rows, (bf16_t*)o, ldo);
+    return rf::check_launch("rf_attn_combine");
 }
 
 extern "C" int rf_swin_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
@@ -303,8 +438,21 @@ extern "C" int rf_swin_attn_fwd(const void* q, int64_t ldq, const void* k, int64
     RF_REQUIRE(shift >= 0 && shift < window, "rf_swin_attn_fwd: bad shift");
     RF_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0, "rf_swin_attn_fwd: strides must be 16-B aligned");
     if (n_images <= 0) return RF_OK;
-    AttnArgs a{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, ldq, ldk, ldv, ldo, nullptr,
-               scale * LOG2E, grid_h, grid_w, shift, window};
+    AttnArgs a{};
+    a.q = (const bf16_t*)q;
+    a.k = (const bf16_t*)k;
+    a.v = (const bf16_t*)v;
+    a.o = (bf16_t*)o;
+    a.ldq = ldq;
+    a.ldk = ldk;
+    a.ldv = ldv;
+    a.ldo = ldo;
+    a.c = scale * LOG2E;
+    a.gh = grid_h;
+    a.gw = grid_w;
+    a.shift = shift;
+    a.window = window;
+    a.n_split = 1;
     dim3 grid((grid_h / window) * (grid_w / window), n_heads, n_images);
     hipLaunchKernelGGL((attn_fwd_kernel<true, 2>), grid, dim3(128), 0, (hipStream_t)stream, a);
     return rf::check_launch("rf_swin_attn_fwd");

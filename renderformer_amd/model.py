@@ -293,7 +293,7 @@ class RenderFormer:
             ops.gemm(h, L.w_in, qkv)
             ops.qk_norm_rope(q, q, H, L.q_norm if cfg.view_indep_qk_norm else None, EPS, pos1, W.enc_freqs)
             ops.qk_norm_rope(k, k, H, L.k_norm if cfg.view_indep_qk_norm else None, EPS, pos1, W.enc_freqs)
-            ops.attention(q, k, v, att, plan.prob1, plan.max_s, H, tag="attn_stage1")
+            ops.attention(q, k, v, att, plan.prob1, plan.max_s, H, tag="attn_stage1", max_k_len=plan.max_s)
             ops.gemm(att, L.w_out, x, None, ops.EPI_ADD_F32)
             ops.rmsnorm(x, L.ffn_norm, EPS, h)
             ops.gemm(h, L.w13, g, None, ops.EPI_SWIGLU, tag="gemm_w13_stage1")
@@ -326,7 +326,7 @@ class RenderFormer:
             ops.qk_norm_rope(q2, q2, H, L.q_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R)
             ops.qk_norm_rope(kv[:, :D], kview, H, L.k_norm if qk else None, EPS, pos2, W.dec_freqs,
                              src_rows=plan.kv_src_rows)
-            ops.attention(q2, kview, kv[:, D:], att, plan.prob2, R, H, tag="attn_cross")
+            ops.attention(q2, kview, kv[:, D:], att, plan.prob2, R, H, tag="attn_cross", max_k_len=plan.max_s)
             ops.gemm(att, L.wo, x, None, ops.EPI_ADD_F32)
             # (ii) self-attention between ray tokens
             if qkv is not None:
@@ -341,7 +341,7 @@ class RenderFormer:
                 else:
                     ops.qk_norm_rope(qs, qs, H, L.sq_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R)
                     ops.qk_norm_rope(ks, ks, H, L.sk_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R)
-                    ops.attention(qs, ks, vs, att, plan.prob_self, R, H)
+                    ops.attention(qs, ks, vs, att, plan.prob_self, R, H, max_k_len=R)
                 ops.gemm(att, L.ws_out, x, None, ops.EPI_ADD_F32)
             # (iii) FFN
             ops.rmsnorm(x, L.ffn_norm, EPS, h)

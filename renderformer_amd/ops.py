@@ -8,14 +8,16 @@ or falls back to eager PyTorch math.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
 
-from ._lib import call, ptr, stream
+from ._lib import call, load, ptr, stream
 
 EPI_BF16, EPI_F32, EPI_ADD_F32, EPI_SWIGLU = 0, 1, 2, 3
 FLT_EPS = float(torch.finfo(torch.float32).eps)  # nn.RMSNorm(eps=None) on fp32 inputs
+CUS = 256  # MI355X compute units
 
 
 class KernelTimer:
@@ -111,8 +113,21 @@ def qk_norm_rope(src: torch.Tensor, dst: torch.Tensor, n_heads: int, norm_w: Opt
     return dst
 
 
+def _auto_split(n_wg: int, kv_tiles: int) -> int:
+    """Split key ranges when the launch would not give every CU two workgroups (SURVEY §8 work balance)."""
+    env = os.environ.get("RF_ATTN_SPLIT")
+    if env:
+        return max(1, int(env))
+    target = 2 * CUS
+    s = 1
+    while n_wg * s < target and s < 8 and kv_tiles // (2 * s) >= 4:
+        s *= 2
+    return s
+
+
 def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int,
-              scale: Optional[float] = None, tag: Optional[str] = None) -> torch.Tensor:
+              scale: Optional[float] = None, tag: Optional[str] = None, max_k_len: Optional[int] = None,
+              n_split: Optional[int] = None) -> torch.Tensor:
     """Varlen attention; problems int32 [P, 5] = (q_start, q_len, k_start, k_len, v_start)."""
     for t, nme in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
         _dev(t, torch.bfloat16, nme)
@@ -120,9 +135,18 @@ def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int
     _check(problems.dim() == 2 and problems.shape[1] == 5, "attention: problems must be [P, 5]")
     hd = q.shape[1] // n_heads
     scale = 1.0 / math.sqrt(hd) if scale is None else scale
+    n_wg = -(-max_q_len // 128) * n_heads * problems.shape[0]
+    if n_split is None:
+        n_split = _auto_split(n_wg, -(-(max_k_len or 0) // 64))
+    ws, rows = None, out.shape[0]
+    if n_split > 1:
+        nbytes = load().rf_attn_workspace_bytes(rows, n_heads, n_split)
+        ws = torch.empty(nbytes // 4, dtype=torch.float32, device=out.device)
     ev = _t0(tag)
     call("rf_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out), out.stride(0),
-         ptr(problems), problems.shape[0], max_q_len, n_heads, hd, scale, stream())
+         ptr(problems), problems.shape[0], max_q_len, n_heads, hd, scale, n_split, ptr(ws), rows, stream())
+    if n_split > 1:
+        call("rf_attn_combine", ptr(ws), rows, n_split, n_heads, None, rows, ptr(out), out.stride(0), stream())
     _t1(ev)
     return out
 

@@ -1,0 +1,91 @@
+"""Kernel micro-benchmarks at the bench workload's shapes (large-proxy, cbox N=5633, 512^2).
+
+python tools/kbench.py [attn|gemm|conv|all]   — prints achieved TFLOP/s per kernel (HIP events, 20 reps)."""
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from renderformer_amd import ops  # noqa: E402
+from renderformer_amd._lib import load  # noqa: E402
+
+load()
+dev = "cuda"
+S, R, D, H, F = 5649, 4096, 1024, 8, 4096
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def attn():
+    qkv = (torch.randn(S, 3 * D, device=dev) * 2).bfloat16()
+    out = torch.empty(S, D, device=dev, dtype=torch.bfloat16)
+    prob = torch.tensor([[0, S, 0, S, 0]], dtype=torch.int32, device=dev)
+    fl = 4 * S * S * D
+    for sp in (1, 2, 3, 4):
+        ms = timeit(lambda: ops.attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], out, prob, S, H, n_split=sp))
+        print(f"attn stage1 S={S} split={sp}: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF")
+    q = torch.randn(R, D, device=dev).bfloat16()
+    kv = torch.randn(S, 2 * D, device=dev).bfloat16()
+    prob2 = torch.tensor([[0, R, 0, S, 0]], dtype=torch.int32, device=dev)
+    o2 = torch.empty(R, D, device=dev, dtype=torch.bfloat16)
+    fl = 4 * R * S * D
+    for sp in (1, 2, 4):
+        ms = timeit(lambda: ops.attention(q, kv[:, :D], kv[:, D:], o2, prob2, R, H, n_split=sp))
+        print(f"attn cross R={R} S={S} split={sp}: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF")
+    qkv2 = torch.randn(R, 3 * D, device=dev).bfloat16()
+    for sh in (0, 4):
+        ms = timeit(lambda: ops.swin_attention(qkv2[:, :D], qkv2[:, D:2 * D], qkv2[:, 2 * D:], o2, 1, 64, 64, sh, H))
+        print(f"swin shift={sh}: {ms*1e3:8.1f} us  {4*R*64*D/ms/1e9:7.1f} TF")
+
+
+def gemm():
+    shapes = [("s1 qkv", S, 3 * D, D, ops.EPI_BF16), ("s1 out", S, D, D, ops.EPI_ADD_F32),
+              ("s1 w13", S, 2 * F, D, ops.EPI_SWIGLU), ("s1 w2", S, D, F, ops.EPI_ADD_F32),
+              ("s2 q", R, D, D, ops.EPI_BF16), ("s2 kv", S, 2 * D, D, ops.EPI_BF16),
+              ("s2 w13", R, 2 * F, D, ops.EPI_SWIGLU), ("s2 w2", R, D, F, ops.EPI_ADD_F32),
+              ("tex", 5633, D, 13312, ops.EPI_F32), ("sq8k", 8192, 8192, 8192, ops.EPI_BF16)]
+    for name, m, n, k, epi in shapes:
+        a = torch.randn(m, k, device=dev).bfloat16()
+        w = (torch.randn(n, k, device=dev) / math.sqrt(k)).bfloat16()
+        if epi == ops.EPI_SWIGLU:
+            c = torch.empty(m, n // 2, device=dev, dtype=torch.bfloat16)
+        elif epi == ops.EPI_BF16:
+            c = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+        else:
+            c = torch.zeros(m, n, device=dev)
+        ms = timeit(lambda: ops.gemm(a, w, c, None, epi), reps=10 if k > 8000 else 20)
+        print(f"gemm {name:8s} {m}x{n}x{k}: {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF")
+    a = torch.randn(8192, 8192, device=dev).bfloat16()
+    b = torch.randn(8192, 8192, device=dev).bfloat16()
+    ms = timeit(lambda: a @ b, reps=10)
+    print(f"torch/hipBLASLt 8192^3 reference: {2*8192**3/ms/1e9:7.1f} TF")
+
+
+def conv():
+    from renderformer_amd.dpt import _Conv, split_planes
+    for cin, cout, hw in [(256, 256, 256), (256, 128, 512), (256, 256, 128), (128, 256, 256)]:
+        conv = _Conv(torch.randn(cout, cin, 3, 3) / 48, torch.randn(cout), dev)
+        x = split_planes(torch.randn(1, hw, hw, cin, device=dev), conv.cin_pad)
+        ms = timeit(lambda: conv(x, out_f32=True), reps=10)
+        fl = 2 * hw * hw * cin * cout * 9
+        print(f"conv3x3 {cin}->{cout} @{hw}: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF(fp32-equiv)  {3*fl/ms/1e9:7.1f} TF(bf16 MFMA)")
+
+
+if __name__ == "__main__":
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    for name, fn in (("attn", attn), ("gemm", gemm), ("conv", conv)):
+        if what in (name, "all"):
+            fn()
