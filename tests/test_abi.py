@@ -9,7 +9,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_functions():
     text = open(os.path.join(REPO, "include", "rf.h")).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(rf_\w+)\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(rf_\w+)\(", text, flags=re.M)))
 
 
 def test_header_lists_entry_points():
@@ -27,7 +27,8 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, fn), fn
     assert lib.rf_abi_version() == 1
     # every int-returning entry point has a ctypes signature in the binding
-    assert set(_lib.SIGNATURES) == set(header_functions()) - {"rf_last_error", "rf_abi_version"}
+    assert set(_lib.SIGNATURES) == set(header_functions()) - {"rf_last_error", "rf_abi_version",
+                                                               "rf_attn_workspace_bytes"}
 
 
 def test_invalid_arguments_raise_value_error_without_device():
@@ -42,5 +43,5 @@ def test_invalid_arguments_raise_value_error_without_device():
                           10, 100, 64, 0, None)  # N % 128 != 0
     assert rc == 1 and b"multiple of 128" in lib.rf_last_error()
     rc = lib.rf_attn_fwd(ctypes.c_void_p(16), 256, ctypes.c_void_p(16), 256, ctypes.c_void_p(16), 256,
-                         ctypes.c_void_p(16), 256, ctypes.c_void_p(16), 1, 10, 2, 64, 1.0, None)
+                         ctypes.c_void_p(16), 256, ctypes.c_void_p(16), 1, 10, 2, 64, 1.0, 1, None, 0, None)
     assert rc == 1 and b"head_dim" in lib.rf_last_error()
