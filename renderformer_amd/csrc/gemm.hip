@@ -22,15 +22,27 @@
 //   residual loads and SwiGLU pairs are 8-16 B vectors per lane.
 // * blockIdx is remapped so each XCD walks a contiguous band of tiles (T1).
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 32, THREADS = 256, STAGES = 3;
-constexpr int TILE = BM * BK * 2;  // 8 KiB per operand plane per stage
+constexpr int BK = 32;
 
 enum Epi { E_BF16 = RF_EPI_BF16, E_F32 = RF_EPI_F32, E_ADD = RF_EPI_ADD_F32, E_SWIGLU = RF_EPI_SWIGLU, E_CONV = 16 };
+
+// Tile configuration: BM x BN block tile, WGM x WGN waves (each (BM/WGM) x (BN/WGN)), S-deep LDS ring.
+template <int BM_, int BN_, int WGM_, int WGN_, int STAGES_>
+struct Tile {
+    static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_, STAGES = STAGES_;
+    static constexpr int NWAVE = WGM * WGN, THREADS = NWAVE * 64;
+    static constexpr int MW = BM / WGM, NWD = BN / WGN, TI = MW / 16, TJ = NWD / 16;
+    static constexpr int PA = BM / 16 / NWAVE, PB = BN / 16 / NWAVE;  // 1-KiB LDS-DMA pieces per wave per plane
+    static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+    static_assert(PA >= 1 && PB >= 1 && PA * NWAVE * 16 == BM && PB * NWAVE * 16 == BN, "tile/wave mismatch");
+    static_assert(TI >= 1 && TJ >= 2 && TJ % 2 == 0, "wave tile too small");
+};
 
 struct EngineArgs {
     const bf16_t* a;
@@ -41,7 +53,7 @@ struct EngineArgs {
     int64_t ldw;
     int m, n, k;
     // gathered A (convolution): NHWC plane [img][hi][wi][cin_pad]
-    int gather, hi, wi, cin_pad, ho, wo, kw, stride, pad;
+    int hi, wi, cin_pad, ho, wo, kw, stride, pad;
     const bf16_t* zero;
     // epilogue
     void* c;
@@ -62,11 +74,26 @@ RF_DEV int lds_off(int row, int ch) { return row * 64 + ((ch ^ ((row >> 1) & 3))
 
 RF_DEV float silu(float x) { return x / (1.0f + expf(-x)); }
 
-template <int EPI, int NTERM, bool GATHER>
-__global__ __launch_bounds__(THREADS, 2) void engine_kernel(EngineArgs p) {
-    constexpr int PLANES = NTERM == 3 ? 4 : 2;  // A, W (+ A_lo, W_lo)
-    constexpr int STAGE_BYTES = PLANES * TILE;
-    __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE_BYTES];
+template <int N>
+RF_DEV void wait_vm() {
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else static_assert(N < 0, "unsupported vmcnt");
+}
+
+template <class C, int EPI, int NTERM, bool GATHER>
+__global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
+    constexpr int BM = C::BM, BN = C::BN, S = C::STAGES, TI = C::TI, TJ = C::TJ, PA = C::PA, PB = C::PB;
+    constexpr int PLANE_A = C::A_BYTES, PLANE_B = C::B_BYTES;
+    constexpr int STAGE_BYTES = (NTERM == 3 ? 2 : 1) * (PLANE_A + PLANE_B);
+    constexpr int GPS = (NTERM == 3 ? 2 : 1) * (PA + PB);  // LDS-DMA instructions per thread per stage
+    __shared__ __attribute__((aligned(16))) char smem[S * STAGE_BYTES];
 
     const int tiles_n = p.n / BN;
     const int tiles_m = (p.m + BM - 1) / BM;
@@ -79,48 +106,53 @@ __global__ __launch_bounds__(THREADS, 2) void engine_kernel(EngineArgs p) {
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / C::WGN, wn = wave % C::WGN;
 
-    // ---- per-lane staging geometry: piece pc (0..1) of this wave covers rows (wave*2+pc)*16 .. +16
-    int row_of[2], lc_of[2];
+    // ---- staging geometry: piece pc of this wave covers 16 rows x 64 B; lane -> (row, 16-B chunk)
+    int arow[PA], alc[PA], brow[PB], blc[PB];
 #pragma unroll
-    for (int pc = 0; pc < 2; ++pc) {
-        const int row = (wave * 2 + pc) * 16 + (lane >> 2);
-        row_of[pc] = row;
-        lc_of[pc] = (lane & 3) ^ ((row >> 1) & 3);
+    for (int pc = 0; pc < PA; ++pc) {
+        arow[pc] = (wave * PA + pc) * 16 + (lane >> 2);
+        alc[pc] = (lane & 3) ^ ((arow[pc] >> 1) & 3);
     }
-    int g_img[2] = {0, 0}, g_iy[2] = {0, 0}, g_ix[2] = {0, 0};
-    const bf16_t* a_row_ptr[2];
-    const bf16_t* a_row_ptr_lo[2];
 #pragma unroll
-    for (int pc = 0; pc < 2; ++pc) {
-        int m = m0 + row_of[pc];
+    for (int pc = 0; pc < PB; ++pc) {
+        brow[pc] = (wave * PB + pc) * 16 + (lane >> 2);
+        blc[pc] = (lane & 3) ^ ((brow[pc] >> 1) & 3);
+    }
+    int g_img[PA], g_iy[PA], g_ix[PA];
+    const bf16_t* a_row[PA];
+    const bf16_t* a_row_lo[PA];
+#pragma unroll
+    for (int pc = 0; pc < PA; ++pc) {
+        int m = m0 + arow[pc];
         const bool ok = m < p.m;
         m = ok ? m : p.m - 1;
+        g_img[pc] = g_iy[pc] = g_ix[pc] = 0;
         if constexpr (GATHER) {
             const int ox = m % p.wo, t = m / p.wo;
             g_img[pc] = ok ? t / p.ho : -1;
             g_iy[pc] = (t % p.ho) * p.stride - p.pad;
             g_ix[pc] = ox * p.stride - p.pad;
         }
-        a_row_ptr[pc] = p.a + (int64_t)m * p.lda;
-        a_row_ptr_lo[pc] = NTERM == 3 ? p.a_lo + (int64_t)m * p.lda : nullptr;
+        a_row[pc] = p.a + (int64_t)m * p.lda;
+        a_row_lo[pc] = NTERM == 3 ? p.a_lo + (int64_t)m * p.lda : nullptr;
     }
 
     auto issue = [&](int kt, int buf) {
         char* st = smem + buf * STAGE_BYTES;
         const int k0 = kt * BK;
-        int tap = 0, cb = k0, ky = 0, kx = 0;
+        int cb = k0, ky = 0, kx = 0;
         if constexpr (GATHER) {
-            tap = k0 / p.cin_pad;
+            const int tap = k0 / p.cin_pad;
             cb = k0 - tap * p.cin_pad;
             ky = tap / p.kw;
             kx = tap - ky * p.kw;
         }
 #pragma unroll
-        for (int pc = 0; pc < 2; ++pc) {
-            const int piece = wave * 2 + pc;
-            const int kofs = lc_of[pc] * 8;
+        for (int pc = 0; pc < PA; ++pc) {
+            const int piece = wave * PA + pc;
+            const int kofs = alc[pc] * 8;
             const bf16_t* sa;
             const bf16_t* sa_lo = nullptr;
             if constexpr (GATHER) {
@@ -130,90 +162,99 @@ __global__ __launch_bounds__(THREADS, 2) void engine_kernel(EngineArgs p) {
                 sa = ok ? p.a + off : p.zero;
                 if constexpr (NTERM == 3) sa_lo = ok ? p.a_lo + off : p.zero;
             } else {
-                sa = a_row_ptr[pc] + k0 + kofs;
-                if constexpr (NTERM == 3) sa_lo = a_row_ptr_lo[pc] + k0 + kofs;
+                sa = a_row[pc] + k0 + kofs;
+                if constexpr (NTERM == 3) sa_lo = a_row_lo[pc] + k0 + kofs;
             }
-            const bf16_t* sw = p.w + (int64_t)(n0 + row_of[pc]) * p.ldw + k0 + kofs;
             __builtin_amdgcn_global_load_lds(GLB_PTR(void, sa), LDS_PTR(void, st + piece * 1024), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(GLB_PTR(void, sw), LDS_PTR(void, st + TILE + piece * 1024), 16, 0, 0);
-            if constexpr (NTERM == 3) {
-                const bf16_t* sw_lo = p.w_lo + (int64_t)(n0 + row_of[pc]) * p.ldw + k0 + kofs;
-                __builtin_amdgcn_global_load_lds(GLB_PTR(void, sa_lo), LDS_PTR(void, st + 2 * TILE + piece * 1024),
-                                                 16, 0, 0);
-                __builtin_amdgcn_global_load_lds(GLB_PTR(void, sw_lo), LDS_PTR(void, st + 3 * TILE + piece * 1024),
-                                                 16, 0, 0);
-            }
+            if constexpr (NTERM == 3)
+                __builtin_amdgcn_global_load_lds(GLB_PTR(void, sa_lo),
+                                                 LDS_PTR(void, st + PLANE_A + PLANE_B + piece * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int pc = 0; pc < PB; ++pc) {
+            const int piece = wave * PB + pc;
+            const int64_t woff = (int64_t)(n0 + brow[pc]) * p.ldw + k0 + blc[pc] * 8;
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, p.w + woff), LDS_PTR(void, st + PLANE_A + piece * 1024), 16,
+                                             0, 0);
+            if constexpr (NTERM == 3)
+                __builtin_amdgcn_global_load_lds(GLB_PTR(void, p.w_lo + woff),
+                                                 LDS_PTR(void, st + 2 * PLANE_A + PLANE_B + piece * 1024), 16, 0, 0);
         }
     };
 
-    f32x4 acc[4][4];
+    f32x4 acc[TI][TJ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int nk = p.k / BK;
-    issue(0, 0);
-    if (nk > 1) issue(1, 1);
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+        if (s < nk) issue(s, s);
     const int frag_row = lane & 15, frag_ch = lane >> 4;
     for (int kt = 0; kt < nk; ++kt) {
-        // tile kt landed for this wave: leave only tile kt+1's loads in flight
-        if (kt + 1 < nk) {
-            if constexpr (NTERM == 3)
-                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        // tile kt landed for this wave: the (up to S-2) younger tiles may stay in flight
+        const int ahead = nk - 1 - kt;
+        if (ahead >= S - 2) wait_vm<GPS * (S - 2)>();
+        else if constexpr (S > 3) {
+            if (ahead == 1) wait_vm<GPS>();
+            else wait_vm<0>();
         } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wait_vm<0>();
         }
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        if (kt + 2 < nk) issue(kt + 2, (kt + 2) % STAGES);
-        const char* st = smem + (kt % STAGES) * STAGE_BYTES;
-        bf16x8 fa[4], fw[4];
+        if (kt + S - 1 < nk) issue(kt + S - 1, (kt + S - 1) % S);
+        const char* st = smem + (kt % S) * STAGE_BYTES;
+        bf16x8 fa[TI], fw[TJ];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(st + lds_off(wm * 64 + i * 16 + frag_row, frag_ch));
+        for (int i = 0; i < TI; ++i)
+            fa[i] = *reinterpret_cast<const bf16x8*>(st + lds_off(wm * C::MW + i * 16 + frag_row, frag_ch));
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            fw[j] = *reinterpret_cast<const bf16x8*>(st + TILE + lds_off(wn * 64 + j * 16 + frag_row, frag_ch));
+        for (int j = 0; j < TJ; ++j)
+            fw[j] = *reinterpret_cast<const bf16x8*>(st + PLANE_A + lds_off(wn * C::NWD + j * 16 + frag_row, frag_ch));
         if constexpr (NTERM == 3) {
-            bf16x8 fal[4], fwl[4];
+            bf16x8 fal[TI], fwl[TJ];
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                fal[i] = *reinterpret_cast<const bf16x8*>(st + 2 * TILE + lds_off(wm * 64 + i * 16 + frag_row, frag_ch));
+            for (int i = 0; i < TI; ++i)
+                fal[i] = *reinterpret_cast<const bf16x8*>(st + PLANE_A + PLANE_B +
+                                                          lds_off(wm * C::MW + i * 16 + frag_row, frag_ch));
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                fwl[j] = *reinterpret_cast<const bf16x8*>(st + 3 * TILE + lds_off(wn * 64 + j * 16 + frag_row, frag_ch));
+            for (int j = 0; j < TJ; ++j)
+                fwl[j] = *reinterpret_cast<const bf16x8*>(st + 2 * PLANE_A + PLANE_B +
+                                                          lds_off(wn * C::NWD + j * 16 + frag_row, frag_ch));
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < TI; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < TJ; ++j) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fwl[j], fa[i], acc[i][j], 0, 0, 0);
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fal[i], acc[i][j], 0, 0, 0);
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);
                 }
         } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < TI; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < TJ; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);
         }
     }
 
     // ------------------------------------------------------------------ epilogue
-    // acc[i][j][e] = C[row][col + e], row = m0 + wm*64 + i*16 + (lane & 15),
-    //                                  col = n0 + wn*64 + j*16 + 4*(lane >> 4)
+    // acc[i][j][e] = C[row][col + e], row = m0 + wm*MW + i*16 + (lane & 15),
+    //                                  col = n0 + wn*NWD + j*16 + 4*(lane >> 4)
     const int rl = lane & 15, cq = 4 * (lane >> 4);
+    const int rbase = m0 + wm * C::MW, cbase = n0 + wn * C::NWD;
     if constexpr (EPI == E_SWIGLU) {
         bf16_t* c = reinterpret_cast<bf16_t*>(p.c);
 #pragma unroll
-        for (int pair = 0; pair < 2; ++pair) {
-            const int gcol = n0 + wn * 64 + pair * 32;  // 32-row interleave group: [w1 x16 | w3 x16]
+        for (int pair = 0; pair < TJ / 2; ++pair) {
+            const int gcol = cbase + pair * 32;  // 32-row interleave group: [w1 x16 | w3 x16]
             const int ocol = (gcol >> 5) * 16 + cq;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int row = m0 + wm * 64 + i * 16 + rl;
+            for (int i = 0; i < TI; ++i) {
+                const int row = rbase + i * 16 + rl;
                 if (row < p.m) {
                     float o[4];
 #pragma unroll
@@ -233,17 +274,16 @@ __global__ __launch_bounds__(THREADS, 2) void engine_kernel(EngineArgs p) {
         return;
     } else if constexpr (EPI == E_CONV) {
         if (p.flags & RF_CONV_FINAL) {
-            // SiLU -> 1x1 (cout <= 32 channels -> n_fin) -> ELU -> [10^x - 1]; pixel row = lane & 15,
-            // its channels spread over j tiles, e and the four lane>>4 groups.
+            // SiLU -> 1x1 (cout <= NWD channels, all in the wn == 0 waves) -> ELU -> [10^x - 1]
             for (int f = 0; f < p.n_fin; ++f) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
+                for (int i = 0; i < TI; ++i) {
                     float s = 0.f;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+                    for (int j = 0; j < TJ; ++j)
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
-                            const int col = n0 + wn * 64 + j * 16 + cq + e;
+                            const int col = cbase + j * 16 + cq + e;
                             if (col < p.cout) {
                                 const float v = silu(acc[i][j][e] + (p.bias ? p.bias[col] : 0.f));
                                 s += v * p.w_fin[f * p.cout + col];
@@ -251,7 +291,7 @@ __global__ __launch_bounds__(THREADS, 2) void engine_kernel(EngineArgs p) {
                         }
                     s += __shfl_xor(s, 16, 64);
                     s += __shfl_xor(s, 32, 64);
-                    const int m = m0 + wm * 64 + i * 16 + rl;
+                    const int m = rbase + i * 16 + rl;
                     if (lane < 16 && wn == 0 && m < p.m) {
                         float y = s + p.b_fin[f];
                         y = y > 0.f ? y : p.elu_alpha * expm1f(y);
@@ -268,10 +308,9 @@ __global__ __launch_bounds__(THREADS, 2) void engine_kernel(EngineArgs p) {
         const int kk = p.deconv;
         const int nreal = kk ? p.cout * kk * kk : p.cout;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int m = m0 + wm * 64 + i * 16 + rl;
+        for (int i = 0; i < TI; ++i) {
+            const int m = rbase + i * 16 + rl;
             if (m >= p.m) continue;
-            // output pixel base for the (deconv) scatter
             int img = 0, y = 0, x = 0;
             if (kk) {
                 x = m % p.wo;
@@ -279,11 +318,12 @@ __global__ __launch_bounds__(THREADS, 2) void engine_kernel(EngineArgs p) {
                 y = t % p.ho;
                 img = t / p.ho;
             }
-            float4 r1[4], r2[4];
-            int64_t obase[4];
+            float4 r1[TJ], r2[TJ];
+            int64_t pixv[TJ];
+            int cov[TJ];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int col = n0 + wn * 64 + j * 16 + cq;
+            for (int j = 0; j < TJ; ++j) {
+                const int col = cbase + j * 16 + cq;
                 int64_t pix = m;
                 int co = col;
                 if (kk) {
@@ -291,18 +331,21 @@ __global__ __launch_bounds__(THREADS, 2) void engine_kernel(EngineArgs p) {
                     co = col - tap * p.cout;
                     pix = ((int64_t)img * p.ho * kk + y * kk + dy) * (p.wo * kk) + x * kk + dx;
                 }
-                obase[j] = pix * 65536 + co;  // packed (pixel, channel)
+                pixv[j] = pix;
+                cov[j] = co;
+                r1[j] = float4{0.f, 0.f, 0.f, 0.f};
+                r2[j] = float4{0.f, 0.f, 0.f, 0.f};
                 if (col < nreal) {
-                    r1[j] = p.res1 ? *reinterpret_cast<const float4*>(p.res1 + pix * p.cout + co) : float4{0, 0, 0, 0};
-                    r2[j] = p.res2 ? *reinterpret_cast<const float4*>(p.res2 + pix * p.cout + co) : float4{0, 0, 0, 0};
+                    if (p.res1) r1[j] = *reinterpret_cast<const float4*>(p.res1 + pix * p.cout + co);
+                    if (p.res2) r2[j] = *reinterpret_cast<const float4*>(p.res2 + pix * p.cout + co);
                 }
             }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int col = n0 + wn * 64 + j * 16 + cq;
+            for (int j = 0; j < TJ; ++j) {
+                const int col = cbase + j * 16 + cq;
                 if (col >= nreal) continue;
-                const int64_t pix = obase[j] >> 16;
-                const int co = (int)(obase[j] & 65535);
+                const int64_t pix = pixv[j];
+                const int co = cov[j];
                 float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
                 const float rr1[4] = {r1[j].x, r1[j].y, r1[j].z, r1[j].w};
                 const float rr2[4] = {r2[j].x, r2[j].y, r2[j].z, r2[j].w};
@@ -336,19 +379,19 @@ __global__ __launch_bounds__(THREADS, 2) void engine_kernel(EngineArgs p) {
         return;
     } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int row = m0 + wm * 64 + i * 16 + rl;
+        for (int i = 0; i < TI; ++i) {
+            const int row = rbase + i * 16 + rl;
             if (row >= p.m) continue;
-            float4 old[4];
+            float4 old[TJ];
             if constexpr (EPI == E_ADD) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < TJ; ++j)
                     old[j] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.c) + (int64_t)row * p.ldc +
-                                                              n0 + wn * 64 + j * 16 + cq);
+                                                              cbase + j * 16 + cq);
             }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int col = n0 + wn * 64 + j * 16 + cq;
+            for (int j = 0; j < TJ; ++j) {
+                const int col = cbase + j * 16 + cq;
                 float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
                 if (p.bias) {
                     const float4 b = *reinterpret_cast<const float4*>(p.bias + col);
@@ -372,11 +415,28 @@ __global__ __launch_bounds__(THREADS, 2) void engine_kernel(EngineArgs p) {
     }
 }
 
-template <int EPI, int NTERM, bool GATHER = false>
+// Tile configurations.  T128: 128x128, 4 waves of 64x64, 3-stage ring (48 KiB / 96 KiB LDS).
+// T256: 256x256, 8 waves of 128x64, 4-stage ring (128 KiB).  T256x128: 8 waves of 64x64, bf16x3 3-stage (144 KiB).
+using T128 = Tile<128, 128, 2, 2, 3>;
+using T256 = Tile<256, 256, 2, 4, 4>;
+using T256x128 = Tile<256, 128, 4, 2, 3>;
+
+template <class C, int EPI, int NTERM, bool GATHER = false>
 int launch(const EngineArgs& a, void* stream, const char* what) {
-    const int nwg = (a.n / BN) * ((a.m + BM - 1) / BM);
-    hipLaunchKernelGGL((engine_kernel<EPI, NTERM, GATHER>), dim3(nwg), dim3(THREADS), 0, (hipStream_t)stream, a);
+    const int nwg = (a.n / C::BN) * ((a.m + C::BM - 1) / C::BM);
+    hipLaunchKernelGGL((engine_kernel<C, EPI, NTERM, GATHER>), dim3(nwg), dim3(C::THREADS), 0, (hipStream_t)stream, a);
     return rf::check_launch(what);
+}
+
+// Tile choice: the 256x256 tile halves the L2 traffic per FLOP but needs enough tiles to fill
+// 256 CUs (one 512-thread block per CU); smaller problems keep the 128x128 tile (2-3 blocks per CU).
+int pick_cfg(int m, int n) {
+    if (const char* env = getenv("RF_GEMM_TILE")) return atoi(env);
+    if (n % 256 == 0) {
+        const int t256 = (n / 256) * ((m + 255) / 256);
+        if (t256 >= 2 * 256) return 256;
+    }
+    return 128;
 }
 
 __device__ __attribute__((aligned(16))) bf16_t g_zero_row[64];  // stays zero: source of padded conv taps
@@ -388,7 +448,7 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
     RF_REQUIRE(a && w && c, "rf_gemm_bf16: null pointer");
     RF_REQUIRE(m > 0 && n > 0 && k > 0, "rf_gemm_bf16: empty problem m=%d n=%d k=%d", m, n, k);
     RF_REQUIRE(k % BK == 0, "rf_gemm_bf16: K=%d must be a multiple of %d", k, BK);
-    RF_REQUIRE(n % BN == 0, "rf_gemm_bf16: N=%d must be a multiple of %d", n, BN);
+    RF_REQUIRE(n % 128 == 0, "rf_gemm_bf16: N=%d must be a multiple of 128", n);
     RF_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && lda >= k && ldw >= k, "rf_gemm_bf16: lda/ldw must be >=K and 16-B aligned");
     RF_REQUIRE(((uintptr_t)a & 15) == 0 && ((uintptr_t)w & 15) == 0, "rf_gemm_bf16: operands must be 16-B aligned");
     RF_REQUIRE(epilogue >= RF_EPI_BF16 && epilogue <= RF_EPI_SWIGLU, "rf_gemm_bf16: bad epilogue %d", epilogue);
@@ -405,15 +465,21 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
     p.c = c;
     p.ldc = ldc;
     p.bias = bias;
+    const bool big = pick_cfg(m, n) == 256 && n % 256 == 0;
     switch (epilogue) {
-        case RF_EPI_BF16: return launch<E_BF16, 1>(p, stream, "rf_gemm_bf16");
-        case RF_EPI_F32: return launch<E_F32, 1>(p, stream, "rf_gemm_bf16");
-        case RF_EPI_ADD_F32: return launch<E_ADD, 1>(p, stream, "rf_gemm_bf16");
-        default: return launch<E_SWIGLU, 1>(p, stream, "rf_gemm_bf16");
+        case RF_EPI_BF16:
+            return big ? launch<T256, E_BF16, 1>(p, stream, "rf_gemm_bf16") : launch<T128, E_BF16, 1>(p, stream, "rf_gemm_bf16");
+        case RF_EPI_F32:
+            return big ? launch<T256, E_F32, 1>(p, stream, "rf_gemm_bf16") : launch<T128, E_F32, 1>(p, stream, "rf_gemm_bf16");
+        case RF_EPI_ADD_F32:
+            return big ? launch<T256, E_ADD, 1>(p, stream, "rf_gemm_bf16") : launch<T128, E_ADD, 1>(p, stream, "rf_gemm_bf16");
+        default:
+            return big ? launch<T256, E_SWIGLU, 1>(p, stream, "rf_gemm_bf16")
+                       : launch<T128, E_SWIGLU, 1>(p, stream, "rf_gemm_bf16");
     }
 }
 
-static int conv_common(EngineArgs& p, const void* w_hi, const void* w_lo, int cout, int cout_pad, float* out,
+static int conv_common(EngineArgs& p, bool gather, const void* w_hi, const void* w_lo, int cout, int cout_pad, float* out,
                        const float* bias, const float* res1, const float* res2, void* p_hi, void* p_lo, int p_ld,
                        int flags, const float* w_fin, const float* b_fin, int n_fin, float elu_alpha, void* stream,
                        const char* what) {
@@ -447,7 +513,10 @@ static int conv_common(EngineArgs& p, const void* w_hi, const void* w_lo, int co
     p.n_fin = n_fin;
     p.elu_alpha = elu_alpha;
     if (p.m <= 0) return RF_OK;
-    return p.gather ? launch<E_CONV, 3, true>(p, stream, what) : launch<E_CONV, 3, false>(p, stream, what);
+    const bool big = p.n % 128 == 0 && getenv("RF_CONV_TILE") == nullptr;
+    if (gather)
+        return big ? launch<T256x128, E_CONV, 3, true>(p, stream, what) : launch<T128, E_CONV, 3, true>(p, stream, what);
+    return big ? launch<T256x128, E_CONV, 3, false>(p, stream, what) : launch<T128, E_CONV, 3, false>(p, stream, what);
 }
 
 extern "C" int rf_conv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, int wi, int cin_pad,
@@ -457,12 +526,11 @@ extern "C" int rf_conv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img,
                                 int n_fin, float elu_alpha, void* stream) {
     RF_REQUIRE(in_hi && in_lo, "rf_conv2d_bf16x3: null input");
     RF_REQUIRE(cin_pad % BK == 0, "rf_conv2d_bf16x3: cin_pad %d must be a multiple of %d", cin_pad, BK);
-    RF_REQUIRE(cout_pad % BN == 0 && cout_pad >= cout, "rf_conv2d_bf16x3: cout_pad %d must be a multiple of %d",
-               cout_pad, BN);
+    RF_REQUIRE(cout_pad % 128 == 0 && cout_pad >= cout, "rf_conv2d_bf16x3: cout_pad %d must be a multiple of 128",
+               cout_pad);
     EngineArgs p{};
     p.a = (const bf16_t*)in_hi;
     p.a_lo = (const bf16_t*)in_lo;
-    p.gather = 1;
     p.hi = hi;
     p.wi = wi;
     p.cin_pad = cin_pad;
@@ -474,8 +542,8 @@ extern "C" int rf_conv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img,
     p.m = n_img * p.ho * p.wo;
     p.k = kh * kw * cin_pad;
     p.ldw = p.k;
-    return conv_common(p, w_hi, w_lo, cout, cout_pad, out, bias, res1, res2, p_hi, p_lo, p_ld, flags, w_fin, b_fin,
-                       n_fin, elu_alpha, stream, "rf_conv2d_bf16x3");
+    return conv_common(p, true, w_hi, w_lo, cout, cout_pad, out, bias, res1, res2, p_hi, p_lo, p_ld, flags, w_fin,
+                       b_fin, n_fin, elu_alpha, stream, "rf_conv2d_bf16x3");
 }
 
 extern "C" int rf_deconv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, int wi, int cin_pad,
@@ -483,7 +551,7 @@ extern "C" int rf_deconv2d_bf16x3(const void* in_hi, const void* in_lo, int n_im
                                   void* p_hi, void* p_lo, int p_ld, void* stream) {
     RF_REQUIRE(in_hi && in_lo, "rf_deconv2d_bf16x3: null input");
     RF_REQUIRE(cin_pad % BK == 0, "rf_deconv2d_bf16x3: cin_pad must be a multiple of %d", BK);
-    RF_REQUIRE((k * k * cout) % BN == 0 && cout < 65536, "rf_deconv2d_bf16x3: k*k*cout must be a multiple of %d", BN);
+    RF_REQUIRE((k * k * cout) % 128 == 0 && cout < 65536, "rf_deconv2d_bf16x3: k*k*cout must be a multiple of 128");
     EngineArgs p{};
     p.a = (const bf16_t*)in_hi;
     p.a_lo = (const bf16_t*)in_lo;
@@ -494,6 +562,6 @@ extern "C" int rf_deconv2d_bf16x3(const void* in_hi, const void* in_lo, int n_im
     p.k = cin_pad;
     p.ldw = cin_pad;
     p.deconv = k;
-    return conv_common(p, w_hi, w_lo, cout, k * k * cout, out, bias, nullptr, nullptr, p_hi, p_lo, p_ld, 0, nullptr,
+    return conv_common(p, false, w_hi, w_lo, cout, k * k * cout, out, bias, nullptr, nullptr, p_hi, p_lo, p_ld, 0, nullptr,
                        nullptr, 0, 0.f, stream, "rf_deconv2d_bf16x3");
 }

@@ -66,8 +66,11 @@ def gemm():
             c = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
         else:
             c = torch.zeros(m, n, device=dev)
-        ms = timeit(lambda: ops.gemm(a, w, c, None, epi), reps=10 if k > 8000 else 20)
-        print(f"gemm {name:8s} {m}x{n}x{k}: {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF")
+        for tile in ("128", "256"):
+            os.environ["RF_GEMM_TILE"] = tile
+            ms = timeit(lambda: ops.gemm(a, w, c, None, epi), reps=10 if k > 8000 else 20)
+            print(f"gemm {name:8s} {m}x{n}x{k} tile{tile}: {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF")
+        os.environ.pop("RF_GEMM_TILE")
     a = torch.randn(8192, 8192, device=dev).bfloat16()
     b = torch.randn(8192, 8192, device=dev).bfloat16()
     ms = timeit(lambda: a @ b, reps=10)
@@ -79,9 +82,14 @@ def conv():
     for cin, cout, hw in [(256, 256, 256), (256, 128, 512), (256, 256, 128), (128, 256, 256)]:
         conv = _Conv(torch.randn(cout, cin, 3, 3) / 48, torch.randn(cout), dev)
         x = split_planes(torch.randn(1, hw, hw, cin, device=dev), conv.cin_pad)
-        ms = timeit(lambda: conv(x, out_f32=True), reps=10)
         fl = 2 * hw * hw * cin * cout * 9
-        print(f"conv3x3 {cin}->{cout} @{hw}: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF(fp32-equiv)  {3*fl/ms/1e9:7.1f} TF(bf16 MFMA)")
+        for small in (True, False):
+            if small:
+                os.environ["RF_CONV_TILE"] = "128"
+            ms = timeit(lambda: conv(x, out_f32=True), reps=10)
+            os.environ.pop("RF_CONV_TILE", None)
+            print(f"conv3x3 {cin}->{cout} @{hw} {'128x128' if small else '256x128'}: {ms*1e3:8.1f} us  "
+                  f"{fl/ms/1e9:7.1f} TF(fp32-equiv)  {3*fl/ms/1e9:7.1f} TF(bf16 MFMA)")
 
 
 if __name__ == "__main__":
