@@ -69,10 +69,12 @@ int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, float eps, void
                int rows, int dim, void* stream);
 
 /* dst[r] = rope(rmsnorm(src[src_rows ? src_rows[r] : r]))  (bf16 -> bf16, may alias when src_rows == NULL)
- * norm_w may be NULL (no norm); pos may be NULL (no rope).  RoPE: head_dim 128, per head the half-split
- * rotation with angle[i] = pos[r / pos_div][i / n_freqs] * freqs[i % n_freqs] for i < 9*n_freqs, else 0. */
+ * over n_seg consecutive segments of width dim (q and k of one qkv row), each with its own full-width
+ * RMSNorm weights norm_w[seg*dim ...] (norm_w may be NULL: no norm); pos may be NULL (no rope).
+ * RoPE: head_dim 128, per head the half-split rotation with
+ * angle[i] = pos[r / pos_div][i / n_freqs] * freqs[i % n_freqs] for i < 9*n_freqs, else 0. */
 int rf_qk_norm_rope(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, const int32_t* src_rows,
-                    int rows, int dim, int n_heads, const float* norm_w, float eps, const float* pos,
+                    int rows, int dim, int n_heads, int n_seg, const float* norm_w, float eps, const float* pos,
                     int64_t ld_pos, int pos_div, const float* freqs, int n_freqs, void* stream);
 
 /* Variable-length multi-head attention, non-causal, head_dim 128, bf16 in/out, f32 softmax.

@@ -513,7 +513,10 @@ static int conv_common(EngineArgs& p, bool gather, const void* w_hi, const void*
     p.n_fin = n_fin;
     p.elu_alpha = elu_alpha;
     if (p.m <= 0) return RF_OK;
-    const bool big = p.n % 128 == 0 && getenv("RF_CONV_TILE") == nullptr;
+    // 256x128 (8 waves) halves the L2 traffic per FLOP of the 128x128 tile but runs one block per CU:
+    // use it only when it still yields >= one tile per CU.
+    const char* env = getenv("RF_CONV_TILE");
+    const bool big = env ? atoi(env) == 256 : ((p.m + 255) / 256) * (p.n / 128) >= 256;
     if (gather)
         return big ? launch<T256x128, E_CONV, 3, true>(p, stream, what) : launch<T128, E_CONV, 3, true>(p, stream, what);
     return big ? launch<T256x128, E_CONV, 3, false>(p, stream, what) : launch<T128, E_CONV, 3, false>(p, stream, what);

@@ -38,91 +38,115 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
 }
 
 // ----------------------------------------------------------------------------- q/k norm + RoPE
-// Work unit = (head h, 8-element chunk j of the first half): it owns chunks j and j+8
-// of that head, i.e. the rotation pairs (8j+e, 8j+e+64), so the half-split rotation is
-// done in registers and the row can be rewritten in place.  Loads/stores are 16 B per
-// lane.  The 64 angles of a row are computed once (lane i -> angle i, accurate
-// sincosf) and broadcast with cross-lane shuffles.
-constexpr int MAX_HEADS = 16;
+// Work unit = (segment, head h, 8-element chunk j of the first half): it owns chunks j and
+// j+8 of that head, i.e. the rotation pairs (8j+e, 8j+e+64), so the half-split rotation is
+// done in registers and the row can be rewritten in place.  A wave owns a fixed unit set
+// and walks rows grid-stride, so the norm weights are loaded into registers once.  The 64
+// angles of a row are computed once (lane i -> angle i, accurate sincosf) and broadcast
+// with cross-lane shuffles (all lanes active).  Segments (q and k of one qkv row) share
+// the angles; each has its own full-width RMSNorm.
+constexpr int MAX_UNITS = 256;  // segments * heads * 8
+constexpr int UPL = MAX_UNITS / 64;
 
 __global__ __launch_bounds__(256) void qk_norm_rope_kernel(const bf16_t* src, int64_t ld_src, bf16_t* dst,
                                                            int64_t ld_dst, const int32_t* __restrict__ src_rows,
-                                                           int rows, int n_heads, const float* __restrict__ norm_w,
-                                                           float eps, const float* __restrict__ pos, int64_t ld_pos,
-                                                           int pos_div, const float* __restrict__ freqs, int n_freqs) {
-    constexpr int UPL = MAX_HEADS * 8 / 64;  // max units per lane
+                                                           int rows, int n_heads, int n_seg,
+                                                           const float* __restrict__ norm_w, float eps,
+                                                           const float* __restrict__ pos, int64_t ld_pos, int pos_div,
+                                                           const float* __restrict__ freqs, int n_freqs) {
     const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
-    if (row >= rows) return;
-    const int srow = src_rows ? src_rows[row] : row;
-    const bf16_t* s = src + (int64_t)srow * ld_src;
-    const int units = n_heads * 8;
-    u32x4 lo[UPL], hi[UPL];
-    float ss = 0.f;
+    const int units = n_seg * n_heads * 8;
+    const int dim = n_heads * 128;
+    // unit -> (segment, head, chunk); column of the first chunk element
+    int col[UPL];
+    float wlo[UPL][8], whi[UPL][8];
 #pragma unroll
     for (int u = 0; u < UPL; ++u) {
         const int unit = lane + 64 * u;
-        if (unit < units) {
-            const int h = unit >> 3, j = unit & 7;
-            lo[u] = *reinterpret_cast<const u32x4*>(s + h * 128 + 8 * j);
-            hi[u] = *reinterpret_cast<const u32x4*>(s + h * 128 + 64 + 8 * j);
+        const int seg = unit / (n_heads * 8), hj = unit % (n_heads * 8);
+        col[u] = seg * dim + (hj >> 3) * 128 + 8 * (hj & 7);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float a0 = __uint_as_float(lo[u][e] << 16), a1 = __uint_as_float(lo[u][e] & 0xffff0000u);
-                const float b0 = __uint_as_float(hi[u][e] << 16), b1 = __uint_as_float(hi[u][e] & 0xffff0000u);
-                ss += a0 * a0 + a1 * a1 + b0 * b0 + b1 * b1;
-            }
+        for (int e = 0; e < 8; ++e) {
+            wlo[u][e] = (norm_w && unit < units) ? norm_w[col[u] + e] : 1.f;
+            whi[u][e] = (norm_w && unit < units) ? norm_w[col[u] + 64 + e] : 1.f;
         }
     }
-    float inv = 1.f;
-    if (norm_w) inv = 1.0f / sqrtf(wave_sum(ss) / (float)(n_heads * 128) + eps);
-    float my_c = 1.f, my_s = 0.f;
-    if (pos && lane < 9 * n_freqs) {
-        const float* pr = pos + (int64_t)(row / pos_div) * ld_pos;
-        sincosf(pr[lane / n_freqs] * freqs[lane % n_freqs], &my_s, &my_c);
-    }
-    // every unit of this lane has chunk index j = lane & 7: fetch its 8 (cos, sin) pairs once,
-    // with all 64 lanes active (cross-lane reads from inactive lanes are undefined)
-    float cs[8], sn[8];
+    const int stride = gridDim.x * ROWS_PER_BLOCK;
+    for (int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6); row < rows; row += stride) {
+        const int srow = src_rows ? src_rows[row] : row;
+        const bf16_t* s = src + (int64_t)srow * ld_src;
+        u32x4 lo[UPL], hi[UPL];
+        float ss[UPL];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        cs[k] = pos ? __shfl(my_c, 8 * (lane & 7) + k, 64) : 1.f;
-        sn[k] = pos ? __shfl(my_s, 8 * (lane & 7) + k, 64) : 0.f;
-    }
-    bf16_t* d = dst + (int64_t)row * ld_dst;
+        for (int u = 0; u < UPL; ++u) {
+            ss[u] = 0.f;
+            if (lane + 64 * u < units) {
+                lo[u] = *reinterpret_cast<const u32x4*>(s + col[u]);
+                hi[u] = *reinterpret_cast<const u32x4*>(s + col[u] + 64);
 #pragma unroll
-    for (int u = 0; u < UPL; ++u) {
-        const int unit = lane + 64 * u;
-        if (unit < units) {
-            const int h = unit >> 3, j = unit & 7;
-            float a[8], b[8];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                a[2 * e] = __uint_as_float(lo[u][e] << 16);
-                a[2 * e + 1] = __uint_as_float(lo[u][e] & 0xffff0000u);
-                b[2 * e] = __uint_as_float(hi[u][e] << 16);
-                b[2 * e + 1] = __uint_as_float(hi[u][e] & 0xffff0000u);
-            }
-            u32x4 olo, ohi;
-#pragma unroll
-            for (int e = 0; e < 8; e += 2) {
-                float ra[2], rb[2];
-#pragma unroll
-                for (int t = 0; t < 2; ++t) {
-                    const int i = 8 * j + e + t;
-                    float x0 = a[e + t] * inv, x1 = b[e + t] * inv;
-                    if (norm_w) {
-                        x0 *= norm_w[h * 128 + i];
-                        x1 *= norm_w[h * 128 + 64 + i];
-                    }
-                    ra[t] = x0 * cs[e + t] - x1 * sn[e + t];  // rotate_half_hf: (-x2, x1)
-                    rb[t] = x1 * cs[e + t] + x0 * sn[e + t];
+                for (int e = 0; e < 4; ++e) {
+                    const float a0 = __uint_as_float(lo[u][e] << 16), a1 = __uint_as_float(lo[u][e] & 0xffff0000u);
+                    const float b0 = __uint_as_float(hi[u][e] << 16), b1 = __uint_as_float(hi[u][e] & 0xffff0000u);
+                    ss[u] += a0 * a0 + a1 * a1 + b0 * b0 + b1 * b1;
                 }
-                olo[e / 2] = pack_bf16x2(ra[0], ra[1]);
-                ohi[e / 2] = pack_bf16x2(rb[0], rb[1]);
             }
-            *reinterpret_cast<u32x4*>(d + h * 128 + 8 * j) = olo;
-            *reinterpret_cast<u32x4*>(d + h * 128 + 64 + 8 * j) = ohi;
+        }
+        // per-segment sum of squares: a segment spans n_heads*8 units = whole 64-lane groups when
+        // n_heads*8 is a multiple of 64, otherwise a lane sub-range; reduce per segment explicitly.
+        float inv[UPL];
+#pragma unroll
+        for (int u = 0; u < UPL; ++u) inv[u] = 1.f;
+        if (norm_w) {
+            const int upsg = n_heads * 8;
+            for (int sg = 0; sg < n_seg; ++sg) {
+                float part = 0.f;
+#pragma unroll
+                for (int u = 0; u < UPL; ++u) {
+                    const int unit = lane + 64 * u;
+                    part += (unit < units && unit / upsg == sg) ? ss[u] : 0.f;
+                }
+                const float tot = wave_sum(part);
+                const float iv = 1.0f / sqrtf(tot / (float)dim + eps);
+#pragma unroll
+                for (int u = 0; u < UPL; ++u)
+                    if ((lane + 64 * u) / upsg == sg) inv[u] = iv;
+            }
+        }
+        float my_c = 1.f, my_s = 0.f;
+        if (pos && lane < 9 * n_freqs) {
+            const float* pr = pos + (int64_t)(row / pos_div) * ld_pos;
+            sincosf(pr[lane / n_freqs] * freqs[lane % n_freqs], &my_s, &my_c);
+        }
+        // every unit of this lane has chunk index j = lane & 7 (64 is a multiple of 8)
+        float cs[8], sn[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            cs[k] = pos ? __shfl(my_c, 8 * (lane & 7) + k, 64) : 1.f;
+            sn[k] = pos ? __shfl(my_s, 8 * (lane & 7) + k, 64) : 0.f;
+        }
+        bf16_t* d = dst + (int64_t)row * ld_dst;
+#pragma unroll
+        for (int u = 0; u < UPL; ++u) {
+            if (lane + 64 * u < units) {
+                u32x4 olo, ohi;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float ra[2], rb[2];
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const int i = 2 * e + t;
+                        const float a = (t ? __uint_as_float(lo[u][e] & 0xffff0000u) : __uint_as_float(lo[u][e] << 16));
+                        const float b = (t ? __uint_as_float(hi[u][e] & 0xffff0000u) : __uint_as_float(hi[u][e] << 16));
+                        const float x0 = a * inv[u] * wlo[u][i], x1 = b * inv[u] * whi[u][i];
+                        ra[t] = x0 * cs[i] - x1 * sn[i];  // rotate_half_hf: (-x2, x1)
+                        rb[t] = x1 * cs[i] + x0 * sn[i];
+                    }
+                    olo[e] = pack_bf16x2(ra[0], ra[1]);
+                    ohi[e] = pack_bf16x2(rb[0], rb[1]);
+                }
+                *reinterpret_cast<u32x4*>(d + col[u]) = olo;
+                *reinterpret_cast<u32x4*>(d + col[u] + 64) = ohi;
+            }
         }
     }
 }
@@ -175,19 +199,21 @@ extern "C" int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, floa
 }
 
 extern "C" int rf_qk_norm_rope(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, const int32_t* src_rows,
-                               int rows, int dim, int n_heads, const float* norm_w, float eps, const float* pos,
-                               int64_t ld_pos, int pos_div, const float* freqs, int n_freqs, void* stream) {
+                               int rows, int dim, int n_heads, int n_seg, const float* norm_w, float eps,
+                               const float* pos, int64_t ld_pos, int pos_div, const float* freqs, int n_freqs,
+                               void* stream) {
     RF_REQUIRE(src && dst, "rf_qk_norm_rope: null pointer");
-    RF_REQUIRE(dim == n_heads * 128 && n_heads <= MAX_HEADS, "rf_qk_norm_rope: need head_dim 128, <=%d heads",
-               MAX_HEADS);
+    RF_REQUIRE(dim == n_heads * 128 && n_seg >= 1 && n_seg * n_heads * 8 <= MAX_UNITS,
+               "rf_qk_norm_rope: need head_dim 128 and n_seg*n_heads <= %d", MAX_UNITS / 8);
     RF_REQUIRE(ld_src % 8 == 0 && ld_dst % 8 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0,
                "rf_qk_norm_rope: rows must be 16-B aligned");
     RF_REQUIRE(!pos || (freqs && n_freqs > 0 && 9 * n_freqs <= 64 && pos_div > 0),
                "rf_qk_norm_rope: rope needs freqs with 9*n_freqs <= 64");
     if (rows <= 0) return RF_OK;
-    hipLaunchKernelGGL(qk_norm_rope_kernel, dim3((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), dim3(256), 0,
-                       (hipStream_t)stream, (const bf16_t*)src, ld_src, (bf16_t*)dst, ld_dst, src_rows, rows, n_heads,
-                       norm_w, eps, pos, ld_pos, pos_div, freqs, n_freqs);
+    const int blocks = (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
+    hipLaunchKernelGGL(qk_norm_rope_kernel, dim3(blocks < 2048 ? blocks : 2048), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)src, ld_src, (bf16_t*)dst, ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps,
+                       pos, ld_pos, pos_div, freqs, n_freqs);
     return rf::check_launch("rf_qk_norm_rope");
 }
 

@@ -72,8 +72,8 @@ class _DeviceWeights:
             L = _Layer()
             L.w_in = _bf16(sd[p + "multihead_attn.in_proj.weight"], device)
             L.w_out = _bf16(sd[p + "multihead_attn.out_proj.weight"], device)
-            L.q_norm = _f32(sd[p + "multihead_attn.q_norm.weight"], device)
-            L.k_norm = _f32(sd[p + "multihead_attn.k_norm.weight"], device)
+            L.qk_norm = _f32(torch.cat([sd[p + "multihead_attn.q_norm.weight"], sd[p + "multihead_attn.k_norm.weight"]]),
+                             device)
             L.query_norm = _f32(sd[p + "query_norm.weight"], device)
             L.w13 = _bf16(_interleave_swiglu(sd[p + "ffn.w1.weight"], sd[p + "ffn.w3.weight"]), device)
             L.w2 = _bf16(sd[p + "ffn.w2.weight"], device)
@@ -101,8 +101,7 @@ class _DeviceWeights:
                 s = p + "self_attn."
                 L.ws_in = _bf16(sd[s + "in_proj.weight"], device)
                 L.ws_out = _bf16(sd[s + "out_proj.weight"], device)
-                L.sq_norm = _f32(sd[s + "q_norm.weight"], device)
-                L.sk_norm = _f32(sd[s + "k_norm.weight"], device)
+                L.sqk_norm = _f32(torch.cat([sd[s + "q_norm.weight"], sd[s + "k_norm.weight"]]), device)
                 L.self_norm = _f32(sd[p + "self_attn_norm.weight"], device)
             L.w13 = _bf16(_interleave_swiglu(sd[p + "ffn.w1.weight"], sd[p + "ffn.w3.weight"]), device)
             L.w2 = _bf16(sd[p + "ffn.w2.weight"], device)
@@ -288,11 +287,12 @@ class RenderFormer:
         att = torch.empty(T, D, dtype=torch.bfloat16, device=dev)
         g = torch.empty(T, F, dtype=torch.bfloat16, device=dev)
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+        qk_pair = qkv[:, :2 * D]
         for L in W.enc:
             ops.rmsnorm(x, L.query_norm, EPS, h)
             ops.gemm(h, L.w_in, qkv)
-            ops.qk_norm_rope(q, q, H, L.q_norm if cfg.view_indep_qk_norm else None, EPS, pos1, W.enc_freqs)
-            ops.qk_norm_rope(k, k, H, L.k_norm if cfg.view_indep_qk_norm else None, EPS, pos1, W.enc_freqs)
+            ops.qk_norm_rope(qk_pair, qk_pair, H, L.qk_norm if cfg.view_indep_qk_norm else None, EPS, pos1, W.enc_freqs,
+                             n_seg=2)
             ops.attention(q, k, v, att, plan.prob1, plan.max_s, H, tag="attn_stage1", max_k_len=plan.max_s)
             ops.gemm(att, L.w_out, x, None, ops.EPI_ADD_F32)
             ops.rmsnorm(x, L.ffn_norm, EPS, h)
@@ -333,14 +333,14 @@ class RenderFormer:
                 ops.rmsnorm(x, L.self_norm, EPS, h)
                 ops.gemm(h, L.ws_in, qkv)
                 qs, ks, vs = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+                qks = qkv[:, :2 * D]
                 if swin:
-                    ops.qk_norm_rope(qs, qs, H, L.sq_norm if qk else None, EPS)
-                    ops.qk_norm_rope(ks, ks, H, L.sk_norm if qk else None, EPS)
+                    ops.qk_norm_rope(qks, qks, H, L.sqk_norm if qk else None, EPS, n_seg=2)
                     ops.swin_attention(qs, ks, vs, att, P, plan.hp, plan.wp, 0 if i % 2 == 0 else SWIN_SHIFT, H,
                                        SWIN_WINDOW)
                 else:
-                    ops.qk_norm_rope(qs, qs, H, L.sq_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R)
-                    ops.qk_norm_rope(ks, ks, H, L.sk_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R)
+                    ops.qk_norm_rope(qks, qks, H, L.sqk_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R,
+                                     n_seg=2)
                     ops.attention(qs, ks, vs, att, plan.prob_self, R, H, max_k_len=R)
                 ops.gemm(att, L.ws_out, x, None, ops.EPI_ADD_F32)
             # (iii) FFN

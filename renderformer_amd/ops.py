@@ -94,21 +94,25 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor) -> 
 
 def qk_norm_rope(src: torch.Tensor, dst: torch.Tensor, n_heads: int, norm_w: Optional[torch.Tensor], eps: float,
                  pos: Optional[torch.Tensor] = None, freqs: Optional[torch.Tensor] = None, pos_div: int = 1,
-                 src_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dst[r] = rope(rmsnorm(src[src_rows[r]])) over the full width (attention.py:127-141)."""
+                 src_rows: Optional[torch.Tensor] = None, n_seg: int = 1) -> torch.Tensor:
+    """dst[r] = rope(rmsnorm(src[src_rows[r]])) over the full width (attention.py:127-141), for n_seg
+    consecutive width-(n_heads*128) segments (q and k of a qkv row) with weights norm_w [n_seg*dim]."""
     _dev(src, torch.bfloat16, "src")
     _dev(dst, torch.bfloat16, "dst")
-    rows, dim = dst.shape
-    _check(src.shape[1] == dim, "qk_norm_rope: width mismatch")
+    rows, width = dst.shape
+    dim = n_heads * 128
+    _check(width == n_seg * dim and src.shape[1] == width, "qk_norm_rope: width mismatch")
     if src_rows is None:
         _check(src.shape[0] == rows, "qk_norm_rope: row mismatch")
     else:
         _dev(src_rows, torch.int32, "src_rows")
+    if norm_w is not None:
+        _check(norm_w.numel() == n_seg * dim, "qk_norm_rope: norm weight size")
     if pos is not None:
         _dev(pos, torch.float32, "pos")
         _check(pos.shape[1] == 9 and freqs is not None, "qk_norm_rope: pos must be [*, 9] with freqs")
     call("rf_qk_norm_rope", ptr(src), src.stride(0), ptr(dst), dst.stride(0), ptr(src_rows), rows, dim, n_heads,
-         ptr(norm_w), eps, ptr(pos), pos.stride(0) if pos is not None else 0, pos_div, ptr(freqs),
+         n_seg, ptr(norm_w), eps, ptr(pos), pos.stride(0) if pos is not None else 0, pos_div, ptr(freqs),
          freqs.numel() if freqs is not None else 0, stream())
     return dst
 

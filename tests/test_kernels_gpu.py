@@ -115,6 +115,25 @@ def test_qk_norm_rope_matches_oracle():
     assert relerr(dst.float().cpu(), ref2) < 4e-3
 
 
+def test_qk_norm_rope_two_segments():
+    """q and k of one qkv row in a single launch, each with its own full-width norm."""
+    ops = _ops()
+    T, H = 77, 2
+    D = H * 128
+    src = torch.randn(T, 3 * D).bfloat16()
+    w = torch.rand(2 * D) + 0.5
+    pos = torch.rand(T, 9) * 2 - 1
+    freqs = 2 ** torch.linspace(0, math.log2(5), 6)
+    cos, sin = rf_ref.rope_cos_sin(pos[None], freqs, 128)
+    s = src.to(dev)
+    ops.qk_norm_rope(s[:, :2 * D], s[:, :2 * D], H, w.to(dev), 1e-6, pos.to(dev), freqs.to(dev), n_seg=2)
+    for sg in range(2):
+        x = F.rms_norm(src[:, sg * D:(sg + 1) * D].float(), (D,), w[sg * D:(sg + 1) * D], 1e-6)
+        ref = rf_ref.rope_apply(x.view(1, T, H, 128).transpose(1, 2), cos, sin).transpose(1, 2).reshape(T, D)
+        assert relerr(s[:, sg * D:(sg + 1) * D].float().cpu(), ref) < 4e-3
+    assert torch.equal(s[:, 2 * D:].cpu(), src[:, 2 * D:])
+
+
 def _ref_attn(q, k, v, H):
     lq, lk = q.shape[0], k.shape[0]
     qh = q.double().view(lq, H, 128).transpose(0, 1)

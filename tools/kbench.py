@@ -84,8 +84,7 @@ def conv():
         x = split_planes(torch.randn(1, hw, hw, cin, device=dev), conv.cin_pad)
         fl = 2 * hw * hw * cin * cout * 9
         for small in (True, False):
-            if small:
-                os.environ["RF_CONV_TILE"] = "128"
+            os.environ["RF_CONV_TILE"] = "128" if small else "256"
             ms = timeit(lambda: conv(x, out_f32=True), reps=10)
             os.environ.pop("RF_CONV_TILE", None)
             print(f"conv3x3 {cin}->{cout} @{hw} {'128x128' if small else '256x128'}: {ms*1e3:8.1f} us  "
