@@ -89,6 +89,7 @@ def main():
     from renderformer_amd import RenderFormer, RenderFormerRenderingPipeline, ops
     from renderformer_amd.config import named_config
     from renderformer_amd.flops import frame_flops
+    from renderformer_amd.parallel import max_over_ranks
     from renderformer_amd.scenes import batch_scenes, synthetic_scene
     from renderformer_amd.weights import synthetic_state_dict
 
@@ -123,10 +124,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     timer, ops.TIMER = ops.TIMER, None
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, device=dev)
     if not torch.isfinite(out).all():
         raise RuntimeError("non-finite output")
 

@@ -46,8 +46,8 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
 // with cross-lane shuffles (all lanes active).  Segments (q and k of one qkv row) share
 // the angles; each has its own full-width RMSNorm.
 constexpr int MAX_UNITS = 256;  // segments * heads * 8
-constexpr int UPL = MAX_UNITS / 64;
 
+template <int UPL>
 __global__ __launch_bounds__(256) void qk_norm_rope_kernel(const bf16_t* src, int64_t ld_src, bf16_t* dst,
                                                            int64_t ld_dst, const int32_t* __restrict__ src_rows,
                                                            int rows, int n_heads, int n_seg,
@@ -65,10 +65,20 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(const bf16_t* src, in
         const int unit = lane + 64 * u;
         const int seg = unit / (n_heads * 8), hj = unit % (n_heads * 8);
         col[u] = seg * dim + (hj >> 3) * 128 + 8 * (hj & 7);
+        if (norm_w && unit < units) {
+            const float4* wl = reinterpret_cast<const float4*>(norm_w + col[u]);
+            const float4* wh = reinterpret_cast<const float4*>(norm_w + col[u] + 64);
+            const float4 l0 = wl[0], l1 = wl[1], h0 = wh[0], h1 = wh[1];
+            const float lv[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+            const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            wlo[u][e] = (norm_w && unit < units) ? norm_w[col[u] + e] : 1.f;
-            whi[u][e] = (norm_w && unit < units) ? norm_w[col[u] + 64 + e] : 1.f;
+            for (int e = 0; e < 8; ++e) {
+                wlo[u][e] = lv[e];
+                whi[u][e] = hv[e];
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) wlo[u][e] = whi[u][e] = 1.f;
         }
     }
     const int stride = gridDim.x * ROWS_PER_BLOCK;
@@ -114,8 +124,9 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(const bf16_t* src, in
         }
         float my_c = 1.f, my_s = 0.f;
         if (pos && lane < 9 * n_freqs) {
+            // hardware sin/cos: ~1e-6 absolute, far below the bf16 rounding of the rotated output
             const float* pr = pos + (int64_t)(row / pos_div) * ld_pos;
-            sincosf(pr[lane / n_freqs] * freqs[lane % n_freqs], &my_s, &my_c);
+            __sincosf(pr[lane / n_freqs] * freqs[lane % n_freqs], &my_s, &my_c);
         }
         // every unit of this lane has chunk index j = lane & 7 (64 is a multiple of 8)
         float cs[8], sn[8];
@@ -210,10 +221,18 @@ extern "C" int rf_qk_norm_rope(const void* src, int64_t ld_src, void* dst, int64
     RF_REQUIRE(!pos || (freqs && n_freqs > 0 && 9 * n_freqs <= 64 && pos_div > 0),
                "rf_qk_norm_rope: rope needs freqs with 9*n_freqs <= 64");
     if (rows <= 0) return RF_OK;
+    RF_REQUIRE(!norm_w || ((uintptr_t)norm_w & 15) == 0, "rf_qk_norm_rope: norm weights must be 16-B aligned");
     const int blocks = (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
-    hipLaunchKernelGGL(qk_norm_rope_kernel, dim3(blocks < 2048 ? blocks : 2048), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)src, ld_src, (bf16_t*)dst, ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps,
-                       pos, ld_pos, pos_div, freqs, n_freqs);
+    const dim3 grid(blocks < 2048 ? blocks : 2048);
+    const int units = n_seg * n_heads * 8;
+    hipStream_t st = (hipStream_t)stream;
+#define RF_QKN(U)                                                                                                 \
+    hipLaunchKernelGGL(qk_norm_rope_kernel<U>, grid, dim3(256), 0, st, (const bf16_t*)src, ld_src, (bf16_t*)dst,  \
+                       ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, pos, ld_pos, pos_div, freqs, n_freqs)
+    if (units <= 64) RF_QKN(1);
+    else if (units <= 128) RF_QKN(2);
+    else RF_QKN(4);
+#undef RF_QKN
     return rf::check_launch("rf_qk_norm_rope");
 }
 
