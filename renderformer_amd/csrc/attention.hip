@@ -23,8 +23,10 @@
 //   straight from the row-major V tile with ds_read_b64_tr_b16.
 // VALU diet (the loop is VALU-bound otherwise): the softmax scale is folded into
 // one FMA feeding v_exp_f32 directly, the key mask only runs on the tail tile,
-// row maxima use max3, and the O rescale is skipped when no row max of the wave
-// moved (exact: alpha == 1).
+// row maxima use max3, and the O rescale is deferred until a row max grows by
+// more than 2^8 (guide T13).  The next tile's global loads are issued after the
+// QK^T MFMAs (issuing them earlier makes hipcc's loop-carried vmcnt waits stall
+// the QK^T on them) and land under the softmax and PV.
 // Long key ranges are split over several workgroups (flash-decoding style) when a
 // launch would otherwise leave CUs idle; rf_attn_combine merges the partials.
 // LDS images use the 256-B-row XOR swizzle off(row, ch) = 256 row +
@@ -42,6 +44,7 @@ constexpr int HD = 128;
 constexpr int KT = 64;                   // keys per tile
 constexpr int TILE_BYTES = KT * HD * 2;  // 16 KiB
 constexpr float NEG = -1.0e30f;
+constexpr float RESCALE_LOG2 = 8.0f;
 
 struct AttnArgs {
     const bf16_t* q;
@@ -202,7 +205,6 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(AttnArgs p) {
 
     for (int kt = t_begin; kt < t_end; ++kt) {
         const int cur = SWIN ? 0 : ((kt - t_begin) & 1);
-        if (!SWIN && kt + 1 < t_end) load_tile(kt + 1);
         const char* kb = smem + cur * 2 * TILE_BYTES;
         const char* vb = kb + TILE_BYTES;
 
@@ -218,6 +220,9 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(AttnArgs p) {
                 s[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[st], s[b], 0, 0, 0);
             }
         }
+
+        // next tile's K/V loads fly under the softmax and the PV MFMAs (written to LDS after them)
+        if (!SWIN && kt + 1 < t_end) load_tile(kt + 1);
 
         // ---- mask (tail tile / swin regions only), row max
         bool masked;
@@ -249,18 +254,20 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(AttnArgs p) {
         for (int r = 1; r < 15; r += 2) mt = max3(mt, s[1][r], s[1][r + 1]);
         mt = __builtin_fmaxf(mt, s[1][15]);
         mt = __builtin_fmaxf(mt, __shfl_xor(mt, 32, 64));
-        const float m_new = __builtin_fmaxf(m_run, mt);
-        // rescale O/l only if some row max of this wave moved (exact skip: alpha == 1 otherwise)
-        if (__any(m_new > m_run)) {
+        // deferred rescale (guide T13): keep the running max unless some row of the wave grew by
+        // more than RESCALE_LOG2 (in log2 units); probabilities are then bounded by 2^RESCALE_LOG2,
+        // harmless for the fp32 sums and for bf16 P (relative precision is scale-free).
+        if (__any((mt - m_run) * c > RESCALE_LOG2)) {
+            const float m_new = __builtin_fmaxf(m_run, mt);
             const float alpha = fast_exp2((m_run - m_new) * c);
             l_run *= alpha;
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+            m_run = m_new;
         }
-        m_run = m_new;
-        const float mc = m_new * c;
+        const float mc = m_run * c;
         float ls = 0.f;
 #pragma unroll
         for (int b = 0; b < 2; ++b)
