@@ -154,25 +154,46 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(AttnArgs p) {
     int qlabel = 0;
     if constexpr (SWIN) qlabel = p.shift > 0 ? swin_label(qi) : 0;
 
-    // ---- K/V staging (register-staged; rows clamped, tail masked later)
+    // ---- K/V staging (register-staged; rows clamped, tail masked later).  Thread tid stages 16-B chunk
+    // (tid & 15) of rows (tid >> 4) + 16 i, i < CPT; its K/V row pointers advance by one tile per step
+    // and only a tile that crosses k_len takes the clamped slow path.
     u32x4 kreg[CPT], vreg[CPT];
+    const int srow = tid >> 4, sch = tid & 15;
+    const bf16_t* kbase;
+    const bf16_t* vbase;
+    if constexpr (SWIN) {
+        kbase = p.k + hoff + sch * 8;
+        vbase = p.v + hoff + sch * 8;
+    } else {
+        kbase = p.k + (int64_t)(k_start + t_begin * KT + srow) * p.ldk + hoff + sch * 8;
+        vbase = p.v + (int64_t)(v_start + t_begin * KT + srow) * p.ldv + hoff + sch * 8;
+    }
+    const int64_t k16 = (int64_t)(T / 16) * p.ldk, v16 = (int64_t)(T / 16) * p.ldv;
     auto load_tile = [&](int kt) {
+        if constexpr (SWIN) {
 #pragma unroll
-        for (int i = 0; i < CPT; ++i) {
-            const int c = i * T + tid;
-            const int row = c >> 4, ch = c & 15;
-            int kr, vr;
-            if constexpr (SWIN) {
-                kr = vr = swin_row(row);
-            } else {
-                int j = kt * KT + row;
-                j = j < k_len ? j : k_len - 1;
-                kr = k_start + j;
-                vr = v_start + j;
+            for (int i = 0; i < CPT; ++i) {
+                const int r = swin_row(srow + i * (T / 16));
+                kreg[i] = *reinterpret_cast<const u32x4*>(kbase + (int64_t)r * p.ldk);
+                vreg[i] = *reinterpret_cast<const u32x4*>(vbase + (int64_t)r * p.ldv);
             }
-            kreg[i] = *reinterpret_cast<const u32x4*>(p.k + (int64_t)kr * p.ldk + hoff + ch * 8);
-            vreg[i] = *reinterpret_cast<const u32x4*>(p.v + (int64_t)vr * p.ldv + hoff + ch * 8);
+        } else if ((kt + 1) * KT <= k_len) {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                kreg[i] = *reinterpret_cast<const u32x4*>(kbase + i * k16);
+                vreg[i] = *reinterpret_cast<const u32x4*>(vbase + i * v16);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int over = kt * KT + srow + i * (T / 16) - (k_len - 1);
+                const int64_t back = over > 0 ? over : 0;
+                kreg[i] = *reinterpret_cast<const u32x4*>(kbase + i * k16 - back * p.ldk);
+                vreg[i] = *reinterpret_cast<const u32x4*>(vbase + i * v16 - back * p.ldv);
+            }
         }
+        kbase += KT * p.ldk;
+        vbase += KT * p.ldv;
     };
     auto write_tile = [&](int buf) {
         char* kb = smem + buf * 2 * TILE_BYTES;
