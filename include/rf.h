@@ -48,7 +48,7 @@ extern "C" {
 #define RF_ERR_LAUNCH 2
 #define RF_ERR_UNSUPPORTED 3
 
-#define RF_ABI_VERSION 1
+#define RF_ABI_VERSION 2
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -60,9 +60,14 @@ extern "C" {
 const char* rf_last_error(void);
 int rf_abi_version(void);
 
-/* C[M,N] (epilogue) A[M,K] * W[N,K]^T ; A, W bf16; K % 64 == 0, N % 128 == 0, 16-B aligned rows. */
+/* C[M,N] (epilogue) A[M,K] * W[N,K]^T ; A, W bf16; K % 32 == 0, N % 128 == 0, 16-B aligned rows.
+ * workspace (optional, NULL = data-parallel tiles only): rf_gemm_workspace_bytes() bytes, zero-filled once
+ * when allocated, used by one stream at a time; it enables the stream-K split for GEMMs whose tile count
+ * would leave CUs idle. */
 int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
-                 const float* bias, int m, int n, int k, int epilogue, void* stream);
+                 const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
+                 void* stream);
+int64_t rf_gemm_workspace_bytes(void);
 
 /* out(bf16)[r, :] = x[r, :] * rsqrt(mean(x^2) + eps) * weight ; x f32. */
 int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, float eps, void* out, int64_t ldo,

@@ -22,7 +22,7 @@ _F = ctypes.c_float
 
 # name -> argtypes (every function returns int status)
 SIGNATURES = {
-    "rf_gemm_bf16": [_P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _P],
+    "rf_gemm_bf16": [_P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _L, _P],
     "rf_rmsnorm": [_P, _L, _P, _F, _P, _L, _I, _I, _P],
     "rf_qk_norm_rope": [_P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _F, _P, _L, _I, _P, _I, _P],
     "rf_attn_fwd": [_P, _L, _P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _F, _I, _P, _L, _P],
@@ -67,6 +67,8 @@ def load(require_device: bool = True):
             lib.rf_last_error.argtypes = []
             lib.rf_abi_version.restype = ctypes.c_int
             lib.rf_attn_workspace_bytes.restype = ctypes.c_int64
+            lib.rf_gemm_workspace_bytes.restype = ctypes.c_int64
+            lib.rf_gemm_workspace_bytes.argtypes = []
             lib.rf_attn_workspace_bytes.argtypes = [_L, _I, _I]
             _lib = lib
     if require_device and not torch.cuda.is_available():

@@ -73,7 +73,7 @@ RF_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 RF_DEV float max3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
 
 template <bool SWIN, int NW>
-__global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(AttnArgs p) {
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_fwd_kernel(AttnArgs p) {
     constexpr int T = NW * 64;
     constexpr int CPT = (KT * HD / 8) / T;  // 16-B chunks per thread per tile (per operand)
     constexpr int NBUF = SWIN ? 1 : 2;
@@ -370,6 +370,250 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(AttnArgs p) {
         }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Varlen kernel (rf_attn_fwd): 8 waves x 32 query rows per workgroup, K/V tiles streamed
+// global->LDS by DMA (global_load_lds, no VGPR staging) through a 3-stage ring, and the loop
+// software-pipelined inside each wave: S(t+1) = K(t+1) Q^T is issued in the same basic block as
+// the softmax of S(t), so the exp/convert VALU work of one tile runs under the QK^T MFMAs of the
+// next one (the loop was VALU-bound when the two phases were serial).  One barrier per tile.
+// The per-tile row max is taken per lane half only (no cross-lane exchange on the common path):
+// the running max m is shared by both halves and only moves, with one exchange, in the rare
+// deferred-rescale branch.
+constexpr int NW3 = 8;
+constexpr int QBLK3 = NW3 * 32;
+constexpr int NST3 = 3;
+
+template <int N>
+RF_DEV void attn_wait_vm() {
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+}
+
+__global__ __launch_bounds__(NW3 * 64, 1) void attn_v3_kernel(AttnArgs p) {
+    __shared__ __attribute__((aligned(16))) char smem[NST3 * 2 * TILE_BYTES];  // 96 KiB
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int half = lane >> 5;
+
+    // XCD-aware bijective remap (see attn_fwd_kernel)
+    const int nwg = p.n_total, hwid = blockIdx.x;
+    const int xcd = hwid & 7, qd = nwg >> 3, rm = nwg & 7;
+    int id = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + (hwid >> 3);
+    const int qb = id % p.n_qblk;
+    id /= p.n_qblk;
+    const int split = id % p.n_split;
+    id /= p.n_split;
+    const int h = id % p.n_heads;
+    const int prob = id / p.n_heads;
+    const int32_t* d = p.problems + prob * 5;
+    const int q_start = d[0], q_len = d[1], k_start = d[2], k_len = d[3], v_start = d[4];
+    const int q0 = qb * QBLK3;
+    if (q0 >= q_len) return;
+    const int nt_all = (k_len + KT - 1) / KT;
+    const int per = (nt_all + p.n_split - 1) / p.n_split;
+    const int t_begin = split * per;
+    const int t_end = min(nt_all, t_begin + per);
+    const int nt = t_end - t_begin;
+    const int hoff = h * HD;
+
+    // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[q][16 s + 8 half + 0..7]
+    const int qi = wave * 32 + (lane & 31);
+    bf16x8 qf[8];
+    {
+        const int qq = q0 + qi;
+        const int qrow = q_start + (qq < q_len ? qq : q_len - 1);
+        const bf16_t* src = p.q + (int64_t)qrow * p.ldq + hoff + 8 * half;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(src + 16 * s);
+    }
+
+    // ---- DMA geometry: a 1-KiB piece is 4 tile rows; wave w fills K and V pieces 2w and 2w+1.
+    // Lane l writes LDS bytes piece*1024 + 16 l, i.e. row 4 piece + (l >> 4), physical chunk l & 15,
+    // so it fetches the logical chunk that the swizzle maps there.
+    const int r_a = 8 * wave + (lane >> 4), r_b = r_a + 4;
+    const int lc_a = (lane & 15) ^ (((r_a & 3) << 2) | ((r_a >> 2) & 3));
+    const int lc_b = (lane & 15) ^ (((r_b & 3) << 2) | ((r_b >> 2) & 3));
+    const bf16_t* ka = p.k + (int64_t)(k_start + t_begin * KT + r_a) * p.ldk + hoff + lc_a * 8;
+    const bf16_t* kb = p.k + (int64_t)(k_start + t_begin * KT + r_b) * p.ldk + hoff + lc_b * 8;
+    const bf16_t* va = p.v + (int64_t)(v_start + t_begin * KT + r_a) * p.ldv + hoff + lc_a * 8;
+    const bf16_t* vb = p.v + (int64_t)(v_start + t_begin * KT + r_b) * p.ldv + hoff + lc_b * 8;
+    const int64_t kstep = KT * p.ldk, vstep = KT * p.ldv;
+    auto issue = [&](int kt, int stage) {  // called for kt = t_begin, t_begin + 1, ... in order
+        char* kd = smem + stage * 2 * TILE_BYTES + wave * 2048;
+        char* vd = kd + TILE_BYTES;
+        if ((kt + 1) * KT <= k_len) {
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, ka), LDS_PTR(void, kd), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, kb), LDS_PTR(void, kd + 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, va), LDS_PTR(void, vd), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, vb), LDS_PTR(void, vd + 1024), 16, 0, 0);
+        } else {  // tail tile: rows past k_len re-read row k_len - 1 (masked out of the softmax)
+            const int oa = kt * KT + r_a - (k_len - 1), ob = kt * KT + r_b - (k_len - 1);
+            const int64_t ba = oa > 0 ? oa : 0, bb = ob > 0 ? ob : 0;
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, ka - ba * p.ldk), LDS_PTR(void, kd), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, kb - bb * p.ldk), LDS_PTR(void, kd + 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, va - ba * p.ldv), LDS_PTR(void, vd), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, vb - bb * p.ldv), LDS_PTR(void, vd + 1024), 16, 0, 0);
+        }
+        ka += kstep;
+        kb += kstep;
+        va += vstep;
+        vb += vstep;
+    };
+
+    f32x16 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+    float m_run = NEG, l_run = 0.f;  // m_run in raw score units, identical in both lane halves
+    const float c = p.c;
+    const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;  // ds_read_b64_tr_b16 lane geometry
+
+    auto qk = [&](const char* kt_lds, f32x16* s) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[b][r] = 0.f;
+#pragma unroll
+            for (int st = 0; st < 8; ++st) {
+                const bf16x8 a =
+                    *reinterpret_cast<const bf16x8*>(kt_lds + swz_off(b * 32 + (lane & 31), 2 * st + half));
+                s[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[st], s[b], 0, 0, 0);
+            }
+        }
+    };
+
+    if (nt > 0) {
+        issue(t_begin, 0);
+        if (nt > 1) {
+            issue(t_begin + 1, 1);
+            attn_wait_vm<4>();
+        } else {
+            attn_wait_vm<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    f32x16 s[2];
+    if (nt > 0) qk(smem, s);
+    int cur = 0, nxt = 1, fre = 2;
+
+    for (int i = 0; i < nt; ++i) {
+        const int kt = t_begin + i;
+        // tile kt+1 (the only DMA in flight) landed for every wave, and every wave is done with
+        // tile kt-1, whose stage now takes tile kt+2
+        __builtin_amdgcn_sched_barrier(0);
+        attn_wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (i + 2 < nt) issue(kt + 2, fre);
+
+        if ((kt + 1) * KT > k_len) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = b * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                    s[b][r] = kt * KT + key >= k_len ? NEG : s[b][r];
+                }
+        }
+        float mt = max3(s[0][0], s[0][1], s[0][2]);
+#pragma unroll
+        for (int r = 3; r < 15; r += 2) mt = max3(mt, s[0][r], s[0][r + 1]);
+        mt = max3(mt, s[0][15], s[1][0]);
+#pragma unroll
+        for (int r = 1; r < 15; r += 2) mt = max3(mt, s[1][r], s[1][r + 1]);
+        mt = __builtin_fmaxf(mt, s[1][15]);
+        if (__any((mt - m_run) * c > RESCALE_LOG2)) {
+            const float mrow = __builtin_fmaxf(mt, __shfl_xor(mt, 32, 64));
+            const float m_new = __builtin_fmaxf(m_run, mrow);
+            const float alpha = fast_exp2((m_run - m_new) * c);
+            l_run *= alpha;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+            m_run = m_new;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+
+        // ---- one basic block: P(t) = exp2(S c - m c) -> bf16, S(t+1) = K(t+1) Q^T, O^T += V(t)^T P^T
+        const char* kl = smem + nxt * 2 * TILE_BYTES;
+        const char* vl = smem + cur * 2 * TILE_BYTES + TILE_BYTES;
+        const float nm = -m_run * c;
+        float ls0 = 0.f, ls1 = 0.f;
+        bf16x8 pf[2][2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+                const float e0 = fast_exp2(__builtin_fmaf(s[b][r], c, nm));
+                const float e1 = fast_exp2(__builtin_fmaf(s[b][r + 1], c, nm));
+                ls0 += e0;
+                ls1 += e1;
+                pf[b][r >> 3][r & 7] = (__bf16)e0;
+                pf[b][r >> 3][(r & 7) + 1] = (__bf16)e1;
+            }
+        l_run += ls0 + ls1;
+        qk(kl, s);  // last iteration: harmless MFMAs on a stale stage, result unused
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            const int col = dt * 32 + 16 * (g & 1) + 4 * pp;
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int sp = 0; sp < 2; ++sp) {
+                    const int row = b * 32 + 16 * sp + 4 * (g >> 1) + qq;
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        LDS_PTR(s16x4, vl + swz_off(row, col >> 3) + (col & 7) * 2));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        LDS_PTR(s16x4, vl + swz_off(row + 8, col >> 3) + (col & 7) * 2));
+                    const auto a16 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a16), pf[b][sp],
+                                                                    o[dt], 0, 0, 0);
+                }
+        }
+        const int t0 = cur;
+        cur = nxt;
+        nxt = fre;
+        fre = t0;
+    }
+
+    // ---- epilogue: lane owns query (lane & 31), d = dt*32 + 8 gq + 4 half + 0..3
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const int qrow_o = q0 + qi;
+    if (qrow_o >= q_len) return;
+    const int orow = q_start + qrow_o;
+    if (p.n_split > 1) {
+        float* po = p.part_o + ((int64_t)split * p.part_rows + orow) * (p.n_heads * HD) + hoff;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq)
+                *reinterpret_cast<float4*>(po + dt * 32 + 8 * gq + 4 * half) =
+                    make_float4(o[dt][4 * gq], o[dt][4 * gq + 1], o[dt][4 * gq + 2], o[dt][4 * gq + 3]);
+        if (half == 0) {
+            float* pm = p.part_ml + (((int64_t)split * p.part_rows + orow) * p.n_heads + h) * 2;
+            pm[0] = nt > 0 ? m_run * c : NEG;
+            pm[1] = l_tot;
+        }
+        return;
+    }
+    const float inv = l_tot > 0.f ? 1.0f / l_tot : 0.f;
+    bf16_t* dst = p.o + (int64_t)orow * p.ldo + hoff;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+            uint2 pk;
+            pk.x = pack_bf16x2(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
+            pk.y = pack_bf16x2(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
+            *reinterpret_cast<uint2*>(dst + dt * 32 + 8 * gq + 4 * half) = pk;
+        }
+}
+
 // merge split partials: out = sum_s 2^(m_s - M) O_s / sum_s 2^(m_s - M) l_s   (one wave per (row, head))
 __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restrict__ part_o,
                                                            const float* __restrict__ part_ml, int64_t part_rows,
@@ -410,8 +654,9 @@ extern "C" int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ld
     RF_REQUIRE(n_split >= 1 && n_split <= 16, "rf_attn_fwd: n_split must be 1..16");
     RF_REQUIRE(n_split == 1 || (workspace && ws_rows > 0), "rf_attn_fwd: split needs a workspace");
     if (n_problems <= 0 || max_q_len <= 0) return RF_OK;
-    constexpr int NW = 4;
-    const int n_qblk = (max_q_len + NW * 32 - 1) / (NW * 32);
+    static const int kv = getenv("RF_ATTN_KERNEL") ? atoi(getenv("RF_ATTN_KERNEL")) : 2;
+    const int qrows = kv == 2 ? 128 : 256;
+    const int n_qblk = (max_q_len + qrows - 1) / qrows;
     const int64_t total = (int64_t)n_qblk * n_heads * n_split * n_problems;
     RF_REQUIRE(total < (1ll << 31), "rf_attn_fwd: grid too large");
     AttnArgs a{};
@@ -435,7 +680,12 @@ extern "C" int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ld
         a.part_o = (float*)workspace;
         a.part_ml = a.part_o + (int64_t)n_split * ws_rows * n_heads * HD;
     }
-    hipLaunchKernelGGL((attn_fwd_kernel<false, NW>), dim3((unsigned)total), dim3(NW * 64), 0, (hipStream_t)stream, a);
+    if (kv == 3)
+        hipLaunchKernelGGL(attn_v3_kernel, dim3((unsigned)total), dim3(NW3 * 64), 0, (hipStream_t)stream, a);
+    else if (kv == 28)
+        hipLaunchKernelGGL((attn_fwd_kernel<false, 8>), dim3((unsigned)total), dim3(512), 0, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL((attn_fwd_kernel<false, 4>), dim3((unsigned)total), dim3(256), 0, (hipStream_t)stream, a);
     return rf::check_launch("rf_attn_fwd");
 }
 

@@ -68,6 +68,10 @@ struct EngineArgs {
     const float* w_fin;
     const float* b_fin;
     float elu_alpha;
+    // stream-K: per-CTA partial tiles [grid][BM*BN] f32, then one int flag per CTA
+    float* sk_part;
+    int* sk_flag;
+    int sk_epoch;
 };
 
 RF_DEV int lds_off(int row, int ch) { return row * 64 + ((ch ^ ((row >> 1) & 3)) << 4); }
@@ -87,22 +91,19 @@ RF_DEV void wait_vm() {
     else static_assert(N < 0, "unsupported vmcnt");
 }
 
-template <class C, int EPI, int NTERM, bool GATHER>
-__global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
-    constexpr int BM = C::BM, BN = C::BN, S = C::STAGES, TI = C::TI, TJ = C::TJ, PA = C::PA, PB = C::PB;
-    constexpr int PLANE_A = C::A_BYTES, PLANE_B = C::B_BYTES;
-    constexpr int STAGE_BYTES = (NTERM == 3 ? 2 : 1) * (PLANE_A + PLANE_B);
-    constexpr int GPS = (NTERM == 3 ? 2 : 1) * (PA + PB);  // LDS-DMA instructions per thread per stage
-    __shared__ __attribute__((aligned(16))) char smem[S * STAGE_BYTES];
+template <class C, int NTERM>
+constexpr int stage_bytes() {
+    return (NTERM == 3 ? 2 : 1) * (C::A_BYTES + C::B_BYTES);
+}
 
-    const int tiles_n = p.n / BN;
-    const int tiles_m = (p.m + BM - 1) / BM;
-    const int nwg = tiles_n * tiles_m;
-    const int hw = blockIdx.x;
-    const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
-    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
-    const int tm = wg % tiles_m, tn = wg / tiles_m;
-    const int m0 = tm * BM, n0 = tn * BN;
+// acc = A[m0:m0+BM, kbeg*BK:kend*BK] * W[n0:n0+BN, same]^T for this wave's sub-tile
+template <class C, int NTERM, bool GATHER>
+RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int kbeg, int kend,
+                            f32x4 (&acc)[C::TI][C::TJ]) {
+    constexpr int S = C::STAGES, TI = C::TI, TJ = C::TJ, PA = C::PA, PB = C::PB;
+    constexpr int PLANE_A = C::A_BYTES, PLANE_B = C::B_BYTES;
+    constexpr int STAGE_BYTES = stage_bytes<C, NTERM>();
+    constexpr int GPS = (NTERM == 3 ? 2 : 1) * (PA + PB);  // LDS-DMA instructions per thread per stage
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -182,16 +183,15 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
         }
     };
 
-    f32x4 acc[TI][TJ];
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = p.k / BK;
+    const int nk = kend - kbeg;
 #pragma unroll
     for (int s = 0; s < S - 1; ++s)
-        if (s < nk) issue(s, s);
+        if (s < nk) issue(kbeg + s, s);
     const int frag_row = lane & 15, frag_ch = lane >> 4;
     for (int kt = 0; kt < nk; ++kt) {
         // tile kt landed for this wave: the (up to S-2) younger tiles may stay in flight
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
         }
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        if (kt + S - 1 < nk) issue(kt + S - 1, (kt + S - 1) % S);
+        if (kt + S - 1 < nk) issue(kbeg + kt + S - 1, (kt + S - 1) % S);
         const char* st = smem + (kt % S) * STAGE_BYTES;
         bf16x8 fa[TI], fw[TJ];
 #pragma unroll
@@ -241,6 +241,14 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
         }
     }
 
+}
+
+template <class C, int EPI>
+RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&acc)[C::TI][C::TJ]) {
+    constexpr int TI = C::TI, TJ = C::TJ;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave / C::WGN, wn = wave % C::WGN;
     // ------------------------------------------------------------------ epilogue
     // acc[i][j][e] = C[row][col + e], row = m0 + wm*MW + i*16 + (lane & 15),
     //                                  col = n0 + wn*NWD + j*16 + 4*(lane >> 4)
@@ -415,6 +423,84 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
     }
 }
 
+// Data-parallel (one output tile per block) or stream-K (SK): the grid's blocks split the
+// tiles x K-steps iteration space evenly; a block that starts inside a tile stores its partial
+// sum and raises its flag, the block that holds the tile's first K-step (it reaches that tile
+// last) folds the partials in and runs the epilogue.  The grid never exceeds the co-resident
+// capacity, so every awaited block is running; the spin is bounded regardless.
+template <class C, int EPI, int NTERM, bool GATHER, bool SK>
+__global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
+    constexpr int BM = C::BM, BN = C::BN, TI = C::TI, TJ = C::TJ;
+    __shared__ __attribute__((aligned(16))) char smem[C::STAGES * stage_bytes<C, NTERM>()];
+
+    const int tiles_m = (p.m + BM - 1) / BM;
+    const int nwg = gridDim.x;
+    const int hw = blockIdx.x;
+    const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
+    f32x4 acc[TI][TJ];
+    if constexpr (!SK) {
+        const int m0 = (wg % tiles_m) * BM, n0 = (wg / tiles_m) * BN;
+        engine_mainloop<C, NTERM, GATHER>(p, smem, m0, n0, 0, p.k / BK, acc);
+        engine_epilogue<C, EPI>(p, m0, n0, acc);
+    } else {
+        const int iters = p.k / BK;
+        const int64_t total = (int64_t)tiles_m * (p.n / BN) * iters;
+        int64_t it = total * wg / nwg;
+        const int64_t it_end = total * (wg + 1) / nwg;
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        while (it < it_end) {
+            const int tile = (int)(it / iters), kf = (int)(it % iters);
+            const int kl = (int)min((int64_t)iters, kf + (it_end - it));
+            const int m0 = (tile % tiles_m) * BM, n0 = (tile / tiles_m) * BN;
+            wait_vm<0>();
+            __syncthreads();  // the previous segment's LDS readers are done with the ring
+            engine_mainloop<C, NTERM, GATHER>(p, smem, m0, n0, kf, kl, acc);
+            if (kf != 0) {
+                // partial tile, in accumulator order: fully coalesced 1 KiB per wave-instruction
+                float4* dst = reinterpret_cast<float4*>(p.sk_part + (int64_t)wg * (BM * BN)) + wave * TI * TJ * 64 + lane;
+#pragma unroll
+                for (int i = 0; i < TI; ++i)
+#pragma unroll
+                    for (int j = 0; j < TJ; ++j)
+                        dst[(i * TJ + j) * 64] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                __syncthreads();
+                if (threadIdx.x == 0) __hip_atomic_store(p.sk_flag + wg, p.sk_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                if (kl < iters) {
+                    const int64_t tile_end = (int64_t)(tile + 1) * iters;
+                    for (int c = wg + 1; c < nwg && total * c / nwg < tile_end; ++c) {
+                        if (total * (c + 1) / nwg == total * c / nwg) continue;  // empty range: no partial
+                        if (threadIdx.x == 0) {
+                            int spins = 0;
+                            while (__hip_atomic_load(p.sk_flag + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.sk_epoch &&
+                                   ++spins < (1 << 24))
+                                __builtin_amdgcn_s_sleep(1);
+                        }
+                        __syncthreads();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        const float4* src =
+                            reinterpret_cast<const float4*>(p.sk_part + (int64_t)c * (BM * BN)) + wave * TI * TJ * 64 + lane;
+#pragma unroll
+                        for (int i = 0; i < TI; ++i)
+#pragma unroll
+                            for (int j = 0; j < TJ; ++j) {
+                                const float4 v = src[(i * TJ + j) * 64];
+                                acc[i][j][0] += v.x;
+                                acc[i][j][1] += v.y;
+                                acc[i][j][2] += v.z;
+                                acc[i][j][3] += v.w;
+                            }
+                    }
+                }
+                engine_epilogue<C, EPI>(p, m0, n0, acc);
+            }
+            it += kl - kf;
+        }
+    }
+}
+
 // Tile configurations.  T128: 128x128, 4 waves of 64x64, 3-stage ring (48 KiB / 96 KiB LDS).
 // T256: 256x256, 8 waves of 128x64, 4-stage ring (128 KiB).  T256x128: 8 waves of 64x64, bf16x3 3-stage (144 KiB).
 using T128 = Tile<128, 128, 2, 2, 3>;
@@ -424,8 +510,36 @@ using T256x128 = Tile<256, 128, 4, 2, 3>;
 template <class C, int EPI, int NTERM, bool GATHER = false>
 int launch(const EngineArgs& a, void* stream, const char* what) {
     const int nwg = (a.n / C::BN) * ((a.m + C::BM - 1) / C::BM);
-    hipLaunchKernelGGL((engine_kernel<C, EPI, NTERM, GATHER>), dim3(nwg), dim3(C::THREADS), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL((engine_kernel<C, EPI, NTERM, GATHER, false>), dim3(nwg), dim3(C::THREADS), 0, (hipStream_t)stream,
+                       a);
     return rf::check_launch(what);
+}
+
+template <class C, int EPI>
+int launch_sk(const EngineArgs& a, int grid, void* stream, const char* what) {
+    hipLaunchKernelGGL((engine_kernel<C, EPI, 1, false, true>), dim3(grid), dim3(C::THREADS), 0, (hipStream_t)stream, a);
+    return rf::check_launch(what);
+}
+
+constexpr int SK_MAX_GRID = 768;  // 3 blocks of T128 per CU
+constexpr int64_t SK_WS_BYTES = (int64_t)SK_MAX_GRID * 128 * 128 * 4 + SK_MAX_GRID * 4;
+
+// Stream-K grid for the 128x128 tile, or 0 for the data-parallel launch: used when whole-tile
+// rounds of 2 blocks per CU would leave >10% of the slots idle and each block keeps >= 8 K-steps.
+int sk_grid(int m, int n, int k) {
+    const char* env = getenv("RF_GEMM_SK");
+    int grid = 2 * 256;
+    if (!env) return 0;  // opt-in until validated on the GPU
+    if (env) {
+        grid = atoi(env);
+        if (grid <= 0) return 0;
+        grid = grid > SK_MAX_GRID ? SK_MAX_GRID : grid;
+    }
+    const int64_t tiles = (int64_t)((m + 127) / 128) * (n / 128);
+    const int64_t rounds = (tiles + 511) / 512;
+    const double eff = (double)tiles / (rounds * 512);
+    if (!env && (eff >= 0.9 || tiles * (k / BK) < 8LL * grid)) return 0;
+    return grid;
 }
 
 // Tile choice: the 256x256 tile halves the L2 traffic per FLOP but needs enough tiles to fill
@@ -443,8 +557,11 @@ __device__ __attribute__((aligned(16))) bf16_t g_zero_row[64];  // stays zero: s
 
 }  // namespace
 
+extern "C" int64_t rf_gemm_workspace_bytes(void) { return SK_WS_BYTES; }
+
 extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
-                            const float* bias, int m, int n, int k, int epilogue, void* stream) {
+                            const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
+                            void* stream) {
     RF_REQUIRE(a && w && c, "rf_gemm_bf16: null pointer");
     RF_REQUIRE(m > 0 && n > 0 && k > 0, "rf_gemm_bf16: empty problem m=%d n=%d k=%d", m, n, k);
     RF_REQUIRE(k % BK == 0, "rf_gemm_bf16: K=%d must be a multiple of %d", k, BK);
@@ -466,6 +583,19 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
     p.ldc = ldc;
     p.bias = bias;
     const bool big = pick_cfg(m, n) == 256 && n % 256 == 0;
+    const int grid = (!big && workspace && ws_bytes >= SK_WS_BYTES) ? sk_grid(m, n, k) : 0;
+    if (grid) {
+        static int epoch = 0;  // flags from earlier launches never equal the current epoch (workspace zeroed once)
+        p.sk_part = (float*)workspace;
+        p.sk_flag = (int*)(p.sk_part + (int64_t)SK_MAX_GRID * 128 * 128);
+        p.sk_epoch = ++epoch;
+        switch (epilogue) {
+            case RF_EPI_BF16: return launch_sk<T128, E_BF16>(p, grid, stream, "rf_gemm_bf16");
+            case RF_EPI_F32: return launch_sk<T128, E_F32>(p, grid, stream, "rf_gemm_bf16");
+            case RF_EPI_ADD_F32: return launch_sk<T128, E_ADD>(p, grid, stream, "rf_gemm_bf16");
+            default: return launch_sk<T128, E_SWIGLU>(p, grid, stream, "rf_gemm_bf16");
+        }
+    }
     switch (epilogue) {
         case RF_EPI_BF16:
             return big ? launch<T256, E_BF16, 1>(p, stream, "rf_gemm_bf16") : launch<T128, E_BF16, 1>(p, stream, "rf_gemm_bf16");

@@ -63,6 +63,19 @@ def _dev(t, dtype, name):
     _check(t.stride(-1) == 1, f"{name} must be contiguous in its last dim")
 
 
+_GEMM_WS = {}
+
+
+def _gemm_workspace(device) -> torch.Tensor:
+    """Stream-K partial tiles + flags: one zero-filled buffer per device, reused by every GEMM (one stream)."""
+    key = (device.type, device.index)
+    ws = _GEMM_WS.get(key)
+    if ws is None:
+        ws = torch.zeros(int(load().rf_gemm_workspace_bytes()), dtype=torch.uint8, device=device)
+        _GEMM_WS[key] = ws
+    return ws
+
+
 def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias: Optional[torch.Tensor] = None,
          epilogue: int = EPI_BF16, tag: Optional[str] = None) -> torch.Tensor:
     """out (epilogue)= a @ w.T ; a [M,K] bf16, w [N,K] bf16."""
@@ -77,9 +90,10 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias: Optional[tor
     _check(out.shape[0] == m and out.shape[1] == ncols, f"gemm: out shape {tuple(out.shape)} != ({m}, {ncols})")
     if bias is not None:
         _dev(bias, torch.float32, "bias")
+    ws = _gemm_workspace(a.device)
     ev = _t0(tag)
     call("rf_gemm_bf16", ptr(a), a.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), ptr(bias), m, n, k,
-         epilogue, stream())
+         epilogue, ptr(ws), ws.numel(), stream())
     _t1(ev)
     return out
 
@@ -117,16 +131,23 @@ def qk_norm_rope(src: torch.Tensor, dst: torch.Tensor, n_heads: int, norm_w: Opt
     return dst
 
 
+ATTN_QBLK = 128 if os.environ.get("RF_ATTN_KERNEL", "2") == "2" else 256  # query rows per rf_attn_fwd workgroup
+
+
 def _auto_split(n_wg: int, kv_tiles: int) -> int:
-    """Split key ranges when the launch would not give every CU two workgroups (SURVEY §8 work balance)."""
+    """Split each key range over s workgroups (flash-decoding) to fill the 256 CUs (one workgroup each):
+    minimise rounds(n_wg * s) * (tiles per split + fixed cost of ~3 tiles for prologue/epilogue/combine)."""
     env = os.environ.get("RF_ATTN_SPLIT")
     if env:
         return max(1, int(env))
-    target = 2 * CUS
-    s = 1
-    while n_wg * s < target and s < 8 and kv_tiles // (2 * s) >= 4:
-        s *= 2
-    return s
+    best, best_cost = 1, None
+    for s in range(1, 9):
+        if s > 1 and kv_tiles < 4 * s:
+            break
+        cost = -(-n_wg * s // CUS) * (-(-kv_tiles // s) + 3)
+        if best_cost is None or cost < best_cost:
+            best, best_cost = s, cost
+    return best
 
 
 def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int,
@@ -139,7 +160,7 @@ def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int
     _check(problems.dim() == 2 and problems.shape[1] == 5, "attention: problems must be [P, 5]")
     hd = q.shape[1] // n_heads
     scale = 1.0 / math.sqrt(hd) if scale is None else scale
-    n_wg = -(-max_q_len // 128) * n_heads * problems.shape[0]
+    n_wg = -(-max_q_len // ATTN_QBLK) * n_heads * problems.shape[0]
     if n_split is None:
         n_split = _auto_split(n_wg, -(-(max_k_len or 0) // 64))
     ws, rows = None, out.shape[0]

@@ -25,10 +25,10 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load(require_device=False)
     for fn in header_functions():
         assert hasattr(lib, fn), fn
-    assert lib.rf_abi_version() == 1
+    assert lib.rf_abi_version() == 2
     # every int-returning entry point has a ctypes signature in the binding
     assert set(_lib.SIGNATURES) == set(header_functions()) - {"rf_last_error", "rf_abi_version",
-                                                               "rf_attn_workspace_bytes"}
+                                                               "rf_attn_workspace_bytes", "rf_gemm_workspace_bytes"}
 
 
 def test_invalid_arguments_raise_value_error_without_device():
@@ -40,7 +40,7 @@ def test_invalid_arguments_raise_value_error_without_device():
         pytest.skip("librfhip.so not built")
     lib = _lib.load(require_device=False)
     rc = lib.rf_gemm_bf16(ctypes.c_void_p(16), 64, ctypes.c_void_p(16), 64, ctypes.c_void_p(16), 128, None,
-                          10, 100, 64, 0, None)  # N % 128 != 0
+                          10, 100, 64, 0, None, 0, None)  # N % 128 != 0
     assert rc == 1 and b"multiple of 128" in lib.rf_last_error()
     rc = lib.rf_attn_fwd(ctypes.c_void_p(16), 256, ctypes.c_void_p(16), 256, ctypes.c_void_p(16), 256,
                          ctypes.c_void_p(16), 256, ctypes.c_void_p(16), 1, 10, 2, 64, 1.0, 1, None, 0, None)

@@ -52,6 +52,35 @@ def test_gemm_f32_bf16(m, n, k):
     assert relerr(acc, ref2) < 1e-5
 
 
+@pytest.mark.parametrize("grid", ["512", "768", "37"])
+@pytest.mark.parametrize("m,n,k", [(1000, 1024, 1024), (300, 256, 4096), (129, 128, 96), (5649, 1024, 64)])
+def test_gemm_stream_k(monkeypatch, grid, m, n, k):
+    """Stream-K split (forced grid sizes, incl. an odd one where a tile spans 3+ blocks) vs fp64, every epilogue."""
+    ops = _ops()
+    monkeypatch.setenv("RF_GEMM_SK", grid)
+    g = torch.Generator(device="cpu").manual_seed(m + n + k)
+    a = torch.randn(m, k, generator=g).bfloat16().to(dev)
+    w = (torch.randn(n, k, generator=g) / math.sqrt(k)).bfloat16().to(dev)
+    bias = torch.randn(n, generator=g).to(dev)
+    ref = a.double() @ w.double().t() + bias.double()
+    for _ in range(2):  # second pass reuses the workspace flags with a new epoch
+        out = torch.empty(m, n, device=dev)
+        ops.gemm(a, w, out, bias, ops.EPI_F32)
+        assert relerr(out, ref) < 1e-5
+    acc = torch.randn(m, n, generator=g).to(dev)
+    ref2 = acc.double() + ref
+    ops.gemm(a, w, acc, bias, ops.EPI_ADD_F32)
+    assert relerr(acc, ref2) < 1e-5
+    outb = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+    ops.gemm(a, w, outb, bias, ops.EPI_BF16)
+    assert relerr(outb.float(), ref) < 4e-3
+    from renderformer_amd.model import _interleave_swiglu
+    outs = torch.empty(m, n // 2, device=dev, dtype=torch.bfloat16)
+    ops.gemm(a, _interleave_swiglu(w[: n // 2].cpu(), w[n // 2:].cpu()).to(dev), outs, None, ops.EPI_SWIGLU)
+    refs = F.silu(a.double() @ w[: n // 2].double().t()) * (a.double() @ w[n // 2:].double().t())
+    assert relerr(outs.float(), refs) < 5e-3
+
+
 def test_gemm_asymmetric_identity():
     """A = I with an asymmetric W catches a transposed C write (guide §3)."""
     ops = _ops()

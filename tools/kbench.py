@@ -29,12 +29,34 @@ def timeit(fn, reps=20):
     return e0.elapsed_time(e1) / reps
 
 
+def attn_check():
+    """numerics of the selected attention kernel vs torch fp32 (two problems, ragged tails)"""
+    g = torch.Generator(device=dev).manual_seed(0)
+    lens = [1000, 333]
+    T = sum(lens)
+    qkv = torch.randn(T, 3 * D, device=dev, generator=g).bfloat16()
+    out = torch.empty(T, D, device=dev, dtype=torch.bfloat16)
+    prob = torch.tensor([[0, 1000, 0, 1000, 0], [1000, 333, 1000, 333, 1000]], dtype=torch.int32, device=dev)
+    worst = 0.0
+    for sp in (1, 3):
+        ops.attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], out, prob, 1000, H, n_split=sp)
+        st = 0
+        for n in lens:
+            q, k, v = (qkv[st:st + n, i * D:(i + 1) * D].float().view(n, H, 128).transpose(0, 1) for i in range(3))
+            ref = torch.softmax(q @ k.transpose(1, 2) / math.sqrt(128), -1) @ v
+            got = out[st:st + n].float().view(n, H, 128).transpose(0, 1)
+            worst = max(worst, float((got - ref).norm() / ref.norm()))
+            st += n
+    print(f"attn check rel-L2 worst {worst:.2e} ({'OK' if worst < 1e-2 else 'FAIL'})")
+
+
 def attn():
+    attn_check()
     qkv = (torch.randn(S, 3 * D, device=dev) * 2).bfloat16()
     out = torch.empty(S, D, device=dev, dtype=torch.bfloat16)
     prob = torch.tensor([[0, S, 0, S, 0]], dtype=torch.int32, device=dev)
     fl = 4 * S * S * D
-    for sp in (1, 2, 3, 4):
+    for sp in (1, 2, 3, 4, 6):
         ms = timeit(lambda: ops.attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], out, prob, S, H, n_split=sp))
         print(f"attn stage1 S={S} split={sp}: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF")
     q = torch.randn(R, D, device=dev).bfloat16()
@@ -42,7 +64,7 @@ def attn():
     prob2 = torch.tensor([[0, R, 0, S, 0]], dtype=torch.int32, device=dev)
     o2 = torch.empty(R, D, device=dev, dtype=torch.bfloat16)
     fl = 4 * R * S * D
-    for sp in (1, 2, 4):
+    for sp in (1, 2, 3, 4):
         ms = timeit(lambda: ops.attention(q, kv[:, :D], kv[:, D:], o2, prob2, R, H, n_split=sp))
         print(f"attn cross R={R} S={S} split={sp}: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF")
     qkv2 = torch.randn(R, 3 * D, device=dev).bfloat16()
@@ -66,11 +88,17 @@ def gemm():
             c = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
         else:
             c = torch.zeros(m, n, device=dev)
-        for tile in ("128", "256"):
-            os.environ["RF_GEMM_TILE"] = tile
+        for label, tile, sk in (("dp128", "128", "0"), ("sk512", "128", "512"), ("sk768", "128", "768"),
+                                ("dp256", "256", "0"), ("auto", None, None)):
+            for key, val in (("RF_GEMM_TILE", tile), ("RF_GEMM_SK", sk)):
+                if val is None:
+                    os.environ.pop(key, None)
+                else:
+                    os.environ[key] = val
+            if label == "dp256" and n % 256:
+                continue
             ms = timeit(lambda: ops.gemm(a, w, c, None, epi), reps=10 if k > 8000 else 20)
-            print(f"gemm {name:8s} {m}x{n}x{k} tile{tile}: {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF")
-        os.environ.pop("RF_GEMM_TILE")
+            print(f"gemm {name:8s} {m}x{n}x{k} {label}: {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF")
     a = torch.randn(8192, 8192, device=dev).bfloat16()
     b = torch.randn(8192, 8192, device=dev).bfloat16()
     ms = timeit(lambda: a @ b, reps=10)
