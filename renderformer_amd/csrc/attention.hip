@@ -654,7 +654,7 @@ extern "C" int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ld
     RF_REQUIRE(n_split >= 1 && n_split <= 16, "rf_attn_fwd: n_split must be 1..16");
     RF_REQUIRE(n_split == 1 || (workspace && ws_rows > 0), "rf_attn_fwd: split needs a workspace");
     if (n_problems <= 0 || max_q_len <= 0) return RF_OK;
-    static const int kv = getenv("RF_ATTN_KERNEL") ? atoi(getenv("RF_ATTN_KERNEL")) : 2;
+    static const int kv = getenv("RF_ATTN_KERNEL") ? atoi(getenv("RF_ATTN_KERNEL")) : 3;
     const int qrows = kv == 2 ? 128 : 256;
     const int n_qblk = (max_q_len + qrows - 1) / qrows;
     const int64_t total = (int64_t)n_qblk * n_heads * n_split * n_problems;

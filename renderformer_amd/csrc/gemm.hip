@@ -457,14 +457,19 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
             __syncthreads();  // the previous segment's LDS readers are done with the ring
             engine_mainloop<C, NTERM, GATHER>(p, smem, m0, n0, kf, kl, acc);
             if (kf != 0) {
-                // partial tile, in accumulator order: fully coalesced 1 KiB per wave-instruction
-                float4* dst = reinterpret_cast<float4*>(p.sk_part + (int64_t)wg * (BM * BN)) + wave * TI * TJ * 64 + lane;
+                // partial tile in accumulator order (1 KiB per wave-instruction), stored write-through
+                // (sc1) so no release fence is needed; every storing wave drains, then one lane flags
+                // (guide Guideline 16, R1)
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    p.sk_part + (int64_t)wg * (BM * BN), 0, BM * BN * 4, 0x00020000);
 #pragma unroll
                 for (int i = 0; i < TI; ++i)
 #pragma unroll
-                    for (int j = 0; j < TJ; ++j)
-                        dst[(i * TJ + j) * 64] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    for (int j = 0; j < TJ; ++j) {
+                        const int off = (((wave * TI + i) * TJ + j) * 64 + lane) * 16;
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16);
+                    }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 if (threadIdx.x == 0) __hip_atomic_store(p.sk_flag + wg, p.sk_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
@@ -477,9 +482,10 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
                             while (__hip_atomic_load(p.sk_flag + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.sk_epoch &&
                                    ++spins < (1 << 24))
                                 __builtin_amdgcn_s_sleep(1);
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // ONE acquire after the match
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         }
                         __syncthreads();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                         const float4* src =
                             reinterpret_cast<const float4*>(p.sk_part + (int64_t)c * (BM * BN)) + wave * TI * TJ * 64 + lane;
 #pragma unroll

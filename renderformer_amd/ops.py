@@ -131,7 +131,7 @@ def qk_norm_rope(src: torch.Tensor, dst: torch.Tensor, n_heads: int, norm_w: Opt
     return dst
 
 
-ATTN_QBLK = 128 if os.environ.get("RF_ATTN_KERNEL", "2") == "2" else 256  # query rows per rf_attn_fwd workgroup
+ATTN_QBLK = 128 if os.environ.get("RF_ATTN_KERNEL", "3") == "2" else 256  # query rows per rf_attn_fwd workgroup
 
 
 def _auto_split(n_wg: int, kv_tiles: int) -> int:
