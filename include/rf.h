@@ -60,6 +60,9 @@ extern "C" {
 const char* rf_last_error(void);
 int rf_abi_version(void);
 
+/* workspace / ws_bytes of the GEMM and convolution entry points: optional (NULL = one block per
+ * output tile), rf_gemm_workspace_bytes() bytes, zero-filled once when allocated, used by one stream at a
+ * time; with it, launches whose output tiles cannot fill the CUs split the K loop stream-K style. */
 /* C[M,N] (epilogue) A[M,K] * W[N,K]^T ; A, W bf16; K % 32 == 0, N % 128 == 0, 16-B aligned rows.
  * workspace (optional, NULL = data-parallel tiles only): rf_gemm_workspace_bytes() bytes, zero-filled once
  * when allocated, used by one stream at a time; it enables the stream-K split for GEMMs whose tile count
@@ -154,13 +157,14 @@ int rf_hdr_output(const float* logits, float* out, int n, int c, int h, int w, f
 int rf_conv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, int wi, int cin_pad, const void* w_hi,
                      const void* w_lo, int cout, int cout_pad, int kh, int kw, int stride, int pad, const float* bias,
                      const float* res1, const float* res2, float* out, void* p_hi, void* p_lo, int p_ld, int flags,
-                     const float* w_fin, const float* b_fin, int n_fin, float elu_alpha, void* stream);
+                     const float* w_fin, const float* b_fin, int n_fin, float elu_alpha, void* workspace,
+                     int64_t ws_bytes, void* stream);
 
 /* ConvTranspose2d with kernel == stride == k: out[n, k y + dy, k x + dx, co] = sum_ci in[n, y, x, ci] *
  * W[ci, co, dy, dx] + bias[co]; input planes as above, weights bf16 hi/lo [(dy, dx, co)][cin_pad]. */
 int rf_deconv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, int wi, int cin_pad, const void* w_hi,
                        const void* w_lo, int cout, int k, const float* bias, float* out, void* p_hi, void* p_lo,
-                       int p_ld, void* stream);
+                       int p_ld, void* workspace, int64_t ws_bytes, void* stream);
 
 /* f32 rows x[r, 0:c] (row stride ldx) -> bf16 hi/lo planes (row stride p_ld), of silu(x) if silu_act. */
 int rf_split_planes(const float* x, int64_t rows, int c, int64_t ldx, void* p_hi, void* p_lo, int p_ld, int silu_act,

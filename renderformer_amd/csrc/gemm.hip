@@ -21,6 +21,7 @@
 //   accumulator holds 4 consecutive output COLUMNS of one row: epilogue stores,
 //   residual loads and SwiGLU pairs are 8-16 B vectors per lane.
 // * blockIdx is remapped so each XCD walks a contiguous band of tiles (T1).
+#include <algorithm>
 #include <math.h>
 #include <stdlib.h>
 
@@ -521,14 +522,24 @@ int launch(const EngineArgs& a, void* stream, const char* what) {
     return rf::check_launch(what);
 }
 
-template <class C, int EPI>
+constexpr int SK_MAX_GRID = 768;  // 3 blocks of T128 per CU
+constexpr int64_t SK_WS_BYTES = (int64_t)SK_MAX_GRID * 128 * 128 * 4 + SK_MAX_GRID * 4;
+
+template <class C, int EPI, int NTERM = 1, bool GATHER = false>
 int launch_sk(const EngineArgs& a, int grid, void* stream, const char* what) {
-    hipLaunchKernelGGL((engine_kernel<C, EPI, 1, false, true>), dim3(grid), dim3(C::THREADS), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL((engine_kernel<C, EPI, NTERM, GATHER, true>), dim3(grid), dim3(C::THREADS), 0,
+                       (hipStream_t)stream, a);
     return rf::check_launch(what);
 }
 
-constexpr int SK_MAX_GRID = 768;  // 3 blocks of T128 per CU
-constexpr int64_t SK_WS_BYTES = (int64_t)SK_MAX_GRID * 128 * 128 * 4 + SK_MAX_GRID * 4;
+int g_sk_epoch = 0;  // flags from earlier launches never equal the current epoch (workspace zeroed once)
+
+void sk_setup(EngineArgs& p, void* workspace) {
+    p.sk_part = (float*)workspace;
+    p.sk_flag = (int*)(p.sk_part + (int64_t)SK_MAX_GRID * 128 * 128);
+    p.sk_epoch = ++g_sk_epoch;
+}
+
 
 // Stream-K grid for the 128x128 tile, or 0 for the data-parallel launch: used when whole-tile
 // rounds of 2 blocks per CU would leave >10% of the slots idle and each block keeps >= 8 K-steps.
@@ -591,10 +602,7 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
     const bool big = pick_cfg(m, n) == 256 && n % 256 == 0;
     const int grid = (!big && workspace && ws_bytes >= SK_WS_BYTES) ? sk_grid(m, n, k) : 0;
     if (grid) {
-        static int epoch = 0;  // flags from earlier launches never equal the current epoch (workspace zeroed once)
-        p.sk_part = (float*)workspace;
-        p.sk_flag = (int*)(p.sk_part + (int64_t)SK_MAX_GRID * 128 * 128);
-        p.sk_epoch = ++epoch;
+        sk_setup(p, workspace);
         switch (epilogue) {
             case RF_EPI_BF16: return launch_sk<T128, E_BF16>(p, grid, stream, "rf_gemm_bf16");
             case RF_EPI_F32: return launch_sk<T128, E_F32>(p, grid, stream, "rf_gemm_bf16");
@@ -617,8 +625,8 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
 
 static int conv_common(EngineArgs& p, bool gather, const void* w_hi, const void* w_lo, int cout, int cout_pad, float* out,
                        const float* bias, const float* res1, const float* res2, void* p_hi, void* p_lo, int p_ld,
-                       int flags, const float* w_fin, const float* b_fin, int n_fin, float elu_alpha, void* stream,
-                       const char* what) {
+                       int flags, const float* w_fin, const float* b_fin, int n_fin, float elu_alpha, void* workspace,
+                       int64_t ws_bytes, void* stream, const char* what) {
     RF_REQUIRE(w_hi && w_lo, "%s: null weights", what);
     RF_REQUIRE(cout % 4 == 0, "%s: cout must be a multiple of 4", what);
     RF_REQUIRE(out || p_hi, "%s: no output", what);
@@ -653,6 +661,19 @@ static int conv_common(EngineArgs& p, bool gather, const void* w_hi, const void*
     // use it only when it still yields >= one tile per CU.
     const char* env = getenv("RF_CONV_TILE");
     const bool big = env ? atoi(env) == 256 : ((p.m + 255) / 256) * (p.n / 128) >= 256;
+    // Too few 128x128 tiles for 256 CUs (one bf16x3 block per CU): stream-K over the K loop, each block
+    // keeping >= 8 K-steps.
+    const char* sk_env = getenv("RF_CONV_SK");
+    if (!big && workspace && ws_bytes >= SK_WS_BYTES && !(sk_env && atoi(sk_env) == 0)) {
+        const int64_t tiles = (int64_t)((p.m + 127) / 128) * (p.n / 128);
+        const int64_t work = tiles * (p.k / BK);
+        const int64_t grid = std::min<int64_t>(256, work / 8);
+        if (tiles < 192 && grid > tiles) {
+            sk_setup(p, workspace);
+            return gather ? launch_sk<T128, E_CONV, 3, true>(p, (int)grid, stream, what)
+                          : launch_sk<T128, E_CONV, 3, false>(p, (int)grid, stream, what);
+        }
+    }
     if (gather)
         return big ? launch<T256x128, E_CONV, 3, true>(p, stream, what) : launch<T128, E_CONV, 3, true>(p, stream, what);
     return big ? launch<T256x128, E_CONV, 3, false>(p, stream, what) : launch<T128, E_CONV, 3, false>(p, stream, what);
@@ -662,7 +683,7 @@ extern "C" int rf_conv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img,
                                 const void* w_hi, const void* w_lo, int cout, int cout_pad, int kh, int kw, int stride,
                                 int pad, const float* bias, const float* res1, const float* res2, float* out,
                                 void* p_hi, void* p_lo, int p_ld, int flags, const float* w_fin, const float* b_fin,
-                                int n_fin, float elu_alpha, void* stream) {
+                                int n_fin, float elu_alpha, void* workspace, int64_t ws_bytes, void* stream) {
     RF_REQUIRE(in_hi && in_lo, "rf_conv2d_bf16x3: null input");
     RF_REQUIRE(cin_pad % BK == 0, "rf_conv2d_bf16x3: cin_pad %d must be a multiple of %d", cin_pad, BK);
     RF_REQUIRE(cout_pad % 128 == 0 && cout_pad >= cout, "rf_conv2d_bf16x3: cout_pad %d must be a multiple of 128",
@@ -682,12 +703,12 @@ extern "C" int rf_conv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img,
     p.k = kh * kw * cin_pad;
     p.ldw = p.k;
     return conv_common(p, true, w_hi, w_lo, cout, cout_pad, out, bias, res1, res2, p_hi, p_lo, p_ld, flags, w_fin,
-                       b_fin, n_fin, elu_alpha, stream, "rf_conv2d_bf16x3");
+                       b_fin, n_fin, elu_alpha, workspace, ws_bytes, stream, "rf_conv2d_bf16x3");
 }
 
 extern "C" int rf_deconv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, int wi, int cin_pad,
                                   const void* w_hi, const void* w_lo, int cout, int k, const float* bias, float* out,
-                                  void* p_hi, void* p_lo, int p_ld, void* stream) {
+                                  void* p_hi, void* p_lo, int p_ld, void* workspace, int64_t ws_bytes, void* stream) {
     RF_REQUIRE(in_hi && in_lo, "rf_deconv2d_bf16x3: null input");
     RF_REQUIRE(cin_pad % BK == 0, "rf_deconv2d_bf16x3: cin_pad must be a multiple of %d", BK);
     RF_REQUIRE((k * k * cout) % 128 == 0 && cout < 65536, "rf_deconv2d_bf16x3: k*k*cout must be a multiple of 128");
@@ -702,5 +723,5 @@ extern "C" int rf_deconv2d_bf16x3(const void* in_hi, const void* in_lo, int n_im
     p.ldw = cin_pad;
     p.deconv = k;
     return conv_common(p, false, w_hi, w_lo, cout, k * k * cout, out, bias, nullptr, nullptr, p_hi, p_lo, p_ld, 0, nullptr,
-                       nullptr, 0, 0.f, stream, "rf_deconv2d_bf16x3");
+                       nullptr, 0, 0.f, workspace, ws_bytes, stream, "rf_deconv2d_bf16x3");
 }

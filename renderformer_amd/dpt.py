@@ -105,6 +105,8 @@ class _Conv:
             raise ValueError(f"conv input planes must have {self.cin} channels padded to {self.cin_pad}, got "
                              f"{x.c}/{ld}")
         dev = x.hi.device
+        from .ops import _gemm_workspace
+        ws = _gemm_workspace(dev)
         if self.k:
             ho, wo = h * self.k, w * self.k
         else:
@@ -118,7 +120,7 @@ class _Conv:
             out = torch.empty(shape, device=dev)
             call("rf_conv2d_bf16x3", ptr(x.hi), ptr(x.lo), n, h, w, ld, ptr(self.w_hi), ptr(self.w_lo), self.cout,
                  self.cout_pad, self.kh, self.kw, stride, pad, ptr(self.b), 0, 0, ptr(out), 0, 0, 0,
-                 FINAL | final_flags, ptr(w_fin), ptr(b_fin), nf, alpha, stream())
+                 FINAL | final_flags, ptr(w_fin), ptr(b_fin), nf, alpha, ptr(ws), ws.numel(), stream())
             return out
         out = torch.empty(n, ho, wo, self.cout, device=dev) if out_f32 else None
         pl = Planes.empty(n, ho, wo, self.cout, planes_ld, dev) if planes_ld else None
@@ -129,12 +131,12 @@ class _Conv:
         if self.k:
             call("rf_deconv2d_bf16x3", ptr(x.hi), ptr(x.lo), n, h, w, ld, ptr(self.w_hi), ptr(self.w_lo), self.cout,
                  self.k, ptr(self.b), ptr(out), ptr(pl.hi if pl else None), ptr(pl.lo if pl else None),
-                 planes_ld or 0, stream())
+                 planes_ld or 0, ptr(ws), ws.numel(), stream())
         else:
             call("rf_conv2d_bf16x3", ptr(x.hi), ptr(x.lo), n, h, w, ld, ptr(self.w_hi), ptr(self.w_lo), self.cout,
                  self.cout_pad, self.kh, self.kw, stride, pad, ptr(self.b), ptr(res1), ptr(res2), ptr(out),
                  ptr(pl.hi if pl else None), ptr(pl.lo if pl else None), planes_ld or 0, flags, 0, 0, 0, 0.0,
-                 stream())
+                 ptr(ws), ws.numel(), stream())
         return out, pl
 
 

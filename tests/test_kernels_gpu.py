@@ -377,3 +377,32 @@ def test_conv_final_head():
     assert relerr(out.cpu(), (10 ** y - 1).permute(0, 2, 3, 1)) < 2e-5
     out2 = conv(xs, final=fin, final_flags=NCHW_OUT)
     assert relerr(out2.cpu(), y) < 2e-5
+
+
+@pytest.mark.parametrize("final", [False, True])
+def test_conv_stream_k_matches_data_parallel(monkeypatch, final):
+    """Few output tiles (the DPT's 32x32 / 64x64 levels): the stream-K split (8 blocks per tile here) must
+    agree with the one-block-per-tile launch and with fp64, including residuals, planes and the fused head."""
+    from renderformer_amd.dpt import LOG_DECODE, _Conv, split_planes
+    g = torch.Generator(device="cpu").manual_seed(77)
+    cin = cout = 256 if not final else 64
+    w = torch.randn(cout if not final else 32, cin, 3, 3, generator=g) / math.sqrt(cin * 9)
+    b = torch.randn(w.shape[0], generator=g)
+    x = torch.randn(2, cin, 32, 32, generator=g)
+    conv = _Conv(w, b, dev)
+    xs = split_planes(x.permute(0, 2, 3, 1).contiguous().to(dev), conv.cin_pad, silu=True)
+    outs = []
+    fin = (torch.randn(3, 32, generator=g).to(dev) / 6, torch.zeros(3, device=dev), 1e-3)
+    for sk in ("1", "0"):
+        monkeypatch.setenv("RF_CONV_SK", sk)
+        if final:
+            outs.append((conv(xs, final=fin, final_flags=LOG_DECODE), None))
+        else:
+            r1 = torch.ones(2, 32, 32, cout, device=dev)
+            outs.append(conv(xs, res1=r1, out_f32=True, planes_ld=cout, planes_silu=True))
+    (a, pa), (bb, pb) = outs
+    assert relerr(a, bb) < 1e-6
+    if not final:
+        ref = F.conv2d(F.silu(x.double()), w.double(), b.double(), padding=1).permute(0, 2, 3, 1) + 1.0
+        assert relerr(a.cpu(), ref) < 2e-5
+        assert relerr(pa.hi.float() + pa.lo.float(), pb.hi.float() + pb.lo.float()) < 1e-6
