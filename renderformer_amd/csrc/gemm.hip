@@ -190,58 +190,79 @@ RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
         for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int nk = kend - kbeg;
-#pragma unroll
-    for (int s = 0; s < S - 1; ++s)
-        if (s < nk) issue(kbeg + s, s);
     const int frag_row = lane & 15, frag_ch = lane >> 4;
-    for (int kt = 0; kt < nk; ++kt) {
-        // tile kt landed for this wave: the (up to S-2) younger tiles may stay in flight
-        const int ahead = nk - 1 - kt;
-        if (ahead >= S - 2) wait_vm<GPS * (S - 2)>();
-        else if constexpr (S > 3) {
-            if (ahead == 1) wait_vm<GPS>();
-            else wait_vm<0>();
-        } else {
-            wait_vm<0>();
+    constexpr int TL = NTERM == 3 ? 1 : 0;  // lo-plane fragments present
+    struct Frags {
+        bf16x8 a[TI], w[TJ], al[TL ? TI : 1], wl[TL ? TJ : 1];
+    };
+    auto load_frags = [&](int kt, Frags& f) {
+        const char* st = smem + (kt % S) * STAGE_BYTES;
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+            f.a[i] = *reinterpret_cast<const bf16x8*>(st + lds_off(wm * C::MW + i * 16 + frag_row, frag_ch));
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+            f.w[j] = *reinterpret_cast<const bf16x8*>(st + PLANE_A + lds_off(wn * C::NWD + j * 16 + frag_row, frag_ch));
+        if constexpr (TL) {
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+                f.al[i] = *reinterpret_cast<const bf16x8*>(st + PLANE_A + PLANE_B +
+                                                           lds_off(wm * C::MW + i * 16 + frag_row, frag_ch));
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+                f.wl[j] = *reinterpret_cast<const bf16x8*>(st + 2 * PLANE_A + PLANE_B +
+                                                           lds_off(wn * C::NWD + j * 16 + frag_row, frag_ch));
+        }
+    };
+    auto mma = [&](const Frags& f) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) {
+                if constexpr (TL) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.wl[j], f.a[i], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[j], f.al[i], acc[i][j], 0, 0, 0);
+                }
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[j], f.a[i], acc[i][j], 0, 0, 0);
+            }
+    };
+    // wait until this wave's DMA of tile t landed, given that tiles up to `last` were issued
+    auto wait_tile = [&](int younger) {
+        if (younger >= 2) wait_vm<GPS * 2>();
+        else if (younger == 1) wait_vm<GPS>();
+        else wait_vm<0>();
+    };
+
+    // Ring of S stages.  Fragments are register double-buffered: step kt runs the MFMAs of tile kt
+    // (fragments read during step kt-1) while the ds_reads of tile kt+1 and the DMA of tile kt+S
+    // are in flight.  One barrier per step; before it, every wave's reads of tile kt have completed,
+    // so tile kt's stage is free for tile kt+S right after it.
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+        if (s < nk) issue(kbeg + s, s);
+    wait_tile(std::min(S, nk) - 1);  // (with 3+ younger tiles this waits for tile 1 as well)
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    Frags f0, f1;
+    load_frags(0, f0);
+    auto step = [&](int kt, Frags& cur, Frags& nxt) {
+        // lgkmcnt(0) as the builtin (not inline asm): hipcc's waitcnt pass sees it, knows `cur` is
+        // complete and does not put a wait for the `nxt` reads in front of the MFMAs below
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (kt + 1 < nk) {
+            const int y = std::min(S - 2, nk - 2 - kt);
+            wait_tile(y < 0 ? 0 : y);
         }
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        if (kt + S - 1 < nk) issue(kbeg + kt + S - 1, (kt + S - 1) % S);
-        const char* st = smem + (kt % S) * STAGE_BYTES;
-        bf16x8 fa[TI], fw[TJ];
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-            fa[i] = *reinterpret_cast<const bf16x8*>(st + lds_off(wm * C::MW + i * 16 + frag_row, frag_ch));
-#pragma unroll
-        for (int j = 0; j < TJ; ++j)
-            fw[j] = *reinterpret_cast<const bf16x8*>(st + PLANE_A + lds_off(wn * C::NWD + j * 16 + frag_row, frag_ch));
-        if constexpr (NTERM == 3) {
-            bf16x8 fal[TI], fwl[TJ];
-#pragma unroll
-            for (int i = 0; i < TI; ++i)
-                fal[i] = *reinterpret_cast<const bf16x8*>(st + PLANE_A + PLANE_B +
-                                                          lds_off(wm * C::MW + i * 16 + frag_row, frag_ch));
-#pragma unroll
-            for (int j = 0; j < TJ; ++j)
-                fwl[j] = *reinterpret_cast<const bf16x8*>(st + 2 * PLANE_A + PLANE_B +
-                                                          lds_off(wn * C::NWD + j * 16 + frag_row, frag_ch));
-#pragma unroll
-            for (int i = 0; i < TI; ++i)
-#pragma unroll
-                for (int j = 0; j < TJ; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fwl[j], fa[i], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fal[i], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);
-                }
-        } else {
-#pragma unroll
-            for (int i = 0; i < TI; ++i)
-#pragma unroll
-                for (int j = 0; j < TJ; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);
-        }
+        if (kt + S < nk) issue(kbeg + kt + S, kt % S);
+        if (kt + 1 < nk) load_frags(kt + 1, nxt);
+        mma(cur);
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+        step(kt, f0, f1);
+        if (kt + 1 < nk) step(kt + 1, f1, f0);
     }
-
 }
 
 template <class C, int EPI>

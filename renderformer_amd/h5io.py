@@ -195,6 +195,8 @@ class File:
     def _object_messages(self, addr: int) -> List[Tuple[int, bytes]]:
         p = self.base + addr
         b = self._buf
+        if addr == UNDEF or p + 16 > len(b):
+            raise H5FormatError(f"object header address {addr:#x} outside the file")
         msgs: List[Tuple[int, bytes]] = []
         if b[p:p + 4] == b"OHDR":
             flags = b[p + 5]
@@ -284,6 +286,8 @@ class File:
                 e = q + i * ent
                 noff = self._uint(e, self.sz_off)
                 oaddr = self._uint(e + self.sz_off, self.sz_off)
+                if self._uint(e + 2 * self.sz_off, 4) == 2:
+                    continue  # soft link (cache type 2): not followed
                 name = names[noff:names.index(b"\0", noff)].decode()
                 out[name] = oaddr
         return out

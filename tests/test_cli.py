@@ -1,0 +1,102 @@
+"""infer.py / batch_infer.py (reference CLIs) and the image writers."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from golden_util import load_case, rel_l2  # noqa: E402
+from renderformer_amd import h5io  # noqa: E402
+from renderformer_amd.images import hdr_to_ldr, read_exr, read_png, write_exr, write_png  # noqa: E402
+
+
+def test_exr_png_roundtrip(tmp_path):
+    rng = np.random.default_rng(1)
+    hdr = (rng.standard_normal((17, 23, 3)) * 100).astype(np.float32)
+    write_exr(str(tmp_path / "a.exr"), hdr)
+    np.testing.assert_array_equal(read_exr(str(tmp_path / "a.exr")), hdr)
+    ldr = hdr_to_ldr(hdr)
+    assert ldr.dtype == np.uint8 and ldr.max() <= 255
+    write_png(str(tmp_path / "a.png"), ldr)
+    np.testing.assert_array_equal(read_png(str(tmp_path / "a.png")), ldr)
+    with open(tmp_path / "a.exr", "rb") as f:
+        assert f.read(4) == bytes([0x76, 0x2F, 0x31, 0x01])  # OpenEXR magic
+    with open(tmp_path / "a.png", "rb") as f:
+        assert f.read(8) == b"\x89PNG\r\n\x1a\n"
+
+
+def test_natural_sort_padding_and_collate(tmp_path):
+    import batch_infer
+    names = ["s10.h5", "s2.h5", "s1.h5", "S3.h5"]
+    assert sorted(names, key=batch_infer.natural_key) == ["s1.h5", "s2.h5", "S3.h5", "s10.h5"]
+    rng = np.random.default_rng(0)
+    for i, n in enumerate((5, 9)):
+        h5io.write_scene(str(tmp_path / f"s{i}.h5"), rng.random((n, 3, 3)), rng.random((n, 3, 3)),
+                         rng.random((n, 13, 32, 32)), rng.random((2, 4, 4)), [37.5, 40.0])
+    a = batch_infer.load_scene(str(tmp_path / "s0.h5"), padding_length=12)
+    assert a["triangles"].shape == (12, 3, 3) and int(a["mask"].sum()) == 5 and not a["mask"][5:].any()
+    assert float(a["texture"][5:].abs().sum()) == 0.0
+    b = batch_infer.load_scene(str(tmp_path / "s1.h5"), padding_length=12)
+    assert batch_infer.collate([a, b])["texture"].shape == (2, 12, 13, 32, 32)
+    with pytest.raises(ValueError):
+        batch_infer.collate([batch_infer.load_scene(str(tmp_path / "s0.h5")),
+                             batch_infer.load_scene(str(tmp_path / "s1.h5"))])
+    with pytest.raises(ValueError):
+        batch_infer.load_scene(str(tmp_path / "s1.h5"), padding_length=4)
+
+
+def test_cli_rejects_unavailable_tone_mapper(tmp_path):
+    import infer
+    with pytest.raises(SystemExit):
+        infer.main(["--h5_file", str(tmp_path / "x.h5"), "--tone_mapper", "agx", "--model_id", "x"])
+
+
+def _snapshot_and_scene(tmp_path):
+    """tiny_swin golden: local snapshot dir (config.json + model.safetensors) + its scene 0 (valid triangles
+    only; the reference output is padding-invariant) as an HDF5 file."""
+    from safetensors.torch import save_file
+    cfg, sd, inp, res, z = load_case("tiny_swin")
+    snap = tmp_path / "snap"
+    snap.mkdir()
+    (snap / "config.json").write_text(json.dumps(cfg.to_dict()))
+    save_file({k: v.contiguous() for k, v in sd.items()}, str(snap / "model.safetensors"))
+    m = inp["mask"][0].numpy().astype(bool)
+    h5 = tmp_path / "scenes" / "tiny.h5"
+    h5.parent.mkdir()
+    h5io.write_scene(str(h5), inp["triangles"][0].numpy()[m], inp["vn"][0].numpy()[m],
+                     inp["texture"][0].numpy()[m].astype(np.float16), inp["c2w"][0].numpy(),
+                     inp["fov"][0].numpy().reshape(-1))
+    return snap, h5, res, z
+
+
+@pytest.mark.gpu
+def test_infer_cli_matches_reference(tmp_path):
+    import infer
+    snap, h5, res, z = _snapshot_and_scene(tmp_path)
+    out = tmp_path / "out"
+    assert infer.main(["--h5_file", str(h5), "--model_id", str(snap), "--resolution", str(res),
+                       "--output_dir", str(out)]) == 0
+    nv = z["hdr"].shape[1]
+    for i in range(nv):
+        hdr = read_exr(str(out / f"tiny_view_{i}.exr"))
+        assert rel_l2(hdr, z["hdr"][0, i]) < 1e-3
+        np.testing.assert_array_equal(read_png(str(out / f"tiny_view_{i}.png")), hdr_to_ldr(hdr))
+
+
+@pytest.mark.gpu
+def test_batch_infer_cli(tmp_path):
+    import batch_infer
+    snap, h5, res, z = _snapshot_and_scene(tmp_path)
+    os.link(h5, h5.parent / "tiny2.h5")
+    out = tmp_path / "out"
+    assert batch_infer.main(["--h5_folder", str(h5.parent), "--model_id", str(snap), "--resolution", str(res),
+                             "--output_dir", str(out), "--batch_size", "2"]) == 0
+    a = read_exr(str(out / "tiny_view_0.exr"))
+    b = read_exr(str(out / "tiny2_view_0.exr"))
+    np.testing.assert_array_equal(a, b)
+    assert rel_l2(a, z["hdr"][0, 0]) < 1e-3
