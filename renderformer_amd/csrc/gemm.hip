@@ -22,6 +22,7 @@
 //   residual loads and SwiGLU pairs are 8-16 B vectors per lane.
 // * blockIdx is remapped so each XCD walks a contiguous band of tiles (T1).
 #include <algorithm>
+#include <cmath>
 #include <math.h>
 #include <stdlib.h>
 
@@ -73,7 +74,21 @@ struct EngineArgs {
     float* sk_part;
     int* sk_flag;
     int sk_epoch;
+    int group_m;  // tile raster: groups of group_m m-tiles, n fastest within a group (host-chosen)
 };
+
+// Tile raster.  Each XCD runs a contiguous range of tile ids (see the remap in engine_kernel); with
+// groups of group_m m-tiles walked n-fastest, that range is a ~group_m x (range/group_m) rectangle of
+// the output, so an XCD's L2 serves both the A rows and the W columns it reuses.  The host picks
+// group_m ~ sqrt(range * BN / BM) (square in elements: least L2-miss traffic per XCD).
+RF_DEV void tile_coords(int tile, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
+    const int per_group = group_m * tiles_n;
+    const int g = tile / per_group, r = tile - g * per_group;
+    const int first = g * group_m;
+    const int gm = min(tiles_m - first, group_m);
+    tm = first + r % gm;
+    tn = r / gm;
+}
 
 RF_DEV int lds_off(int row, int ch) { return row * 64 + ((ch ^ ((row >> 1) & 3)) << 4); }
 
@@ -462,7 +477,9 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
     f32x4 acc[TI][TJ];
     if constexpr (!SK) {
-        const int m0 = (wg % tiles_m) * BM, n0 = (wg / tiles_m) * BN;
+        int tm, tn;
+        tile_coords(wg, tiles_m, p.n / BN, p.group_m, tm, tn);
+        const int m0 = tm * BM, n0 = tn * BN;
         engine_mainloop<C, NTERM, GATHER>(p, smem, m0, n0, 0, p.k / BK, acc);
         engine_epilogue<C, EPI>(p, m0, n0, acc);
     } else {
@@ -474,7 +491,9 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
         while (it < it_end) {
             const int tile = (int)(it / iters), kf = (int)(it % iters);
             const int kl = (int)min((int64_t)iters, kf + (it_end - it));
-            const int m0 = (tile % tiles_m) * BM, n0 = (tile / tiles_m) * BN;
+            int tm, tn;
+            tile_coords(tile, tiles_m, p.n / BN, p.group_m, tm, tn);
+            const int m0 = tm * BM, n0 = tn * BN;
             wait_vm<0>();
             __syncthreads();  // the previous segment's LDS readers are done with the ring
             engine_mainloop<C, NTERM, GATHER>(p, smem, m0, n0, kf, kl, acc);
@@ -535,9 +554,20 @@ using T128 = Tile<128, 128, 2, 2, 3>;
 using T256 = Tile<256, 256, 2, 4, 4>;
 using T256x128 = Tile<256, 128, 4, 2, 3>;
 
+int pick_group_m(int tiles_m, int tiles_n, int bm, int bn, int64_t per_xcd) {
+    if (const char* env = getenv("RF_GEMM_GROUP_M")) return std::max(1, std::min(tiles_m, atoi(env)));
+    const double g = std::sqrt((double)per_xcd * bn / bm);
+    int gm = (int)(g + 0.5);
+    gm = std::max(1, std::min(gm, tiles_m));
+    if ((int64_t)gm * tiles_n < per_xcd / 2) gm = std::min<int64_t>(tiles_m, (per_xcd + tiles_n - 1) / tiles_n);
+    return gm;
+}
+
 template <class C, int EPI, int NTERM, bool GATHER = false>
-int launch(const EngineArgs& a, void* stream, const char* what) {
-    const int nwg = (a.n / C::BN) * ((a.m + C::BM - 1) / C::BM);
+int launch(EngineArgs a, void* stream, const char* what) {
+    const int tiles_m = (a.m + C::BM - 1) / C::BM, tiles_n = a.n / C::BN;
+    const int nwg = tiles_n * tiles_m;
+    a.group_m = pick_group_m(tiles_m, tiles_n, C::BM, C::BN, (nwg + 7) / 8);
     hipLaunchKernelGGL((engine_kernel<C, EPI, NTERM, GATHER, false>), dim3(nwg), dim3(C::THREADS), 0, (hipStream_t)stream,
                        a);
     return rf::check_launch(what);
@@ -547,7 +577,9 @@ constexpr int SK_MAX_GRID = 768;  // 3 blocks of T128 per CU
 constexpr int64_t SK_WS_BYTES = (int64_t)SK_MAX_GRID * 128 * 128 * 4 + SK_MAX_GRID * 4;
 
 template <class C, int EPI, int NTERM = 1, bool GATHER = false>
-int launch_sk(const EngineArgs& a, int grid, void* stream, const char* what) {
+int launch_sk(EngineArgs a, int grid, void* stream, const char* what) {
+    const int tiles_m = (a.m + C::BM - 1) / C::BM, tiles_n = a.n / C::BN;
+    a.group_m = pick_group_m(tiles_m, tiles_n, C::BM, C::BN, ((int64_t)tiles_m * tiles_n + 7) / 8);
     hipLaunchKernelGGL((engine_kernel<C, EPI, NTERM, GATHER, true>), dim3(grid), dim3(C::THREADS), 0,
                        (hipStream_t)stream, a);
     return rf::check_launch(what);

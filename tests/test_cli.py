@@ -98,5 +98,5 @@ def test_batch_infer_cli(tmp_path):
                              "--output_dir", str(out), "--batch_size", "2"]) == 0
     a = read_exr(str(out / "tiny_view_0.exr"))
     b = read_exr(str(out / "tiny2_view_0.exr"))
-    np.testing.assert_array_equal(a, b)
+    assert rel_l2(a, b) < 1e-5  # same scene twice in one batch (launch geometry, e.g. the KV split, may differ)
     assert rel_l2(a, z["hdr"][0, 0]) < 1e-3

@@ -88,8 +88,9 @@ def gemm():
             c = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
         else:
             c = torch.zeros(m, n, device=dev)
-        for label, tile, sk in (("dp128", "128", None), ("dp256", "256", None), ("auto", None, None)):
-            for key, val in (("RF_GEMM_TILE", tile), ("RF_GEMM_SK", sk)):
+        for label, tile, sk, gm in (("dp128", "128", None, None), ("dp256", "256", None, None),
+                                    ("auto", None, None, None), ("auto-mfast", None, None, "100000")):
+            for key, val in (("RF_GEMM_TILE", tile), ("RF_GEMM_SK", sk), ("RF_GEMM_GROUP_M", gm)):
                 if val is None:
                     os.environ.pop(key, None)
                 else:
