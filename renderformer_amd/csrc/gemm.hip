@@ -573,8 +573,9 @@ int launch(EngineArgs a, void* stream, const char* what) {
     return rf::check_launch(what);
 }
 
-constexpr int SK_MAX_GRID = 768;  // 3 blocks of T128 per CU
-constexpr int64_t SK_WS_BYTES = (int64_t)SK_MAX_GRID * 128 * 128 * 4 + SK_MAX_GRID * 4;
+constexpr int SK_MAX_GRID = 768;                                  // 3 blocks of T128 per CU
+constexpr int64_t SK_PART_FLOATS = (int64_t)256 * 256 * 256;     // >= grid x BM x BN for every SK config
+constexpr int64_t SK_WS_BYTES = SK_PART_FLOATS * 4 + SK_MAX_GRID * 4;
 
 template <class C, int EPI, int NTERM = 1, bool GATHER = false>
 int launch_sk(EngineArgs a, int grid, void* stream, const char* what) {
@@ -589,7 +590,7 @@ int g_sk_epoch = 0;  // flags from earlier launches never equal the current epoc
 
 void sk_setup(EngineArgs& p, void* workspace) {
     p.sk_part = (float*)workspace;
-    p.sk_flag = (int*)(p.sk_part + (int64_t)SK_MAX_GRID * 128 * 128);
+    p.sk_flag = (int*)(p.sk_part + SK_PART_FLOATS);
     p.sk_epoch = ++g_sk_epoch;
 }
 
@@ -627,6 +628,31 @@ __device__ __attribute__((aligned(16))) bf16_t g_zero_row[64];  // stays zero: s
 
 }  // namespace
 
+template <class C>
+int run_dp_cfg(const EngineArgs& p, int epilogue, void* stream) {
+    switch (epilogue) {
+        case RF_EPI_BF16: return launch<C, E_BF16, 1>(p, stream, "rf_gemm_bf16");
+        case RF_EPI_F32: return launch<C, E_F32, 1>(p, stream, "rf_gemm_bf16");
+        case RF_EPI_ADD_F32: return launch<C, E_ADD, 1>(p, stream, "rf_gemm_bf16");
+        default: return launch<C, E_SWIGLU, 1>(p, stream, "rf_gemm_bf16");
+    }
+}
+
+// cfg codes: 128 = T128, 256 = T256 (needs N % 256 == 0), 1284 / 1285 = 128x128 with a 4 / 5-stage ring,
+// 2561 = 256x128 (8 waves)
+int run_dp(int cfg, const EngineArgs& p, int epilogue, void* stream) {
+    if (cfg == 256 && p.n % 256 == 0) return run_dp_cfg<T256>(p, epilogue, stream);
+    if (cfg == 1284) return run_dp_cfg<Tile<128, 128, 2, 2, 4>>(p, epilogue, stream);
+    if (cfg == 1285) return run_dp_cfg<Tile<128, 128, 2, 2, 5>>(p, epilogue, stream);
+    if (cfg == 2561) return run_dp_cfg<T256x128>(p, epilogue, stream);
+    return run_dp_cfg<T128>(p, epilogue, stream);
+}
+
+bool sk256(int m, int n, int k) {
+    if (const char* env = getenv("RF_GEMM_SK256")) return atoi(env) != 0;
+    return false;  // decided below once measured
+}
+
 extern "C" int64_t rf_gemm_workspace_bytes(void) { return SK_WS_BYTES; }
 
 extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
@@ -652,7 +678,7 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
     p.c = c;
     p.ldc = ldc;
     p.bias = bias;
-    const bool big = pick_cfg(m, n) == 256 && n % 256 == 0;
+    const bool big = pick_cfg(m, n) != 128;
     const int grid = (!big && workspace && ws_bytes >= SK_WS_BYTES) ? sk_grid(m, n, k) : 0;
     if (grid) {
         sk_setup(p, workspace);
@@ -663,17 +689,18 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
             default: return launch_sk<T128, E_SWIGLU>(p, grid, stream, "rf_gemm_bf16");
         }
     }
-    switch (epilogue) {
-        case RF_EPI_BF16:
-            return big ? launch<T256, E_BF16, 1>(p, stream, "rf_gemm_bf16") : launch<T128, E_BF16, 1>(p, stream, "rf_gemm_bf16");
-        case RF_EPI_F32:
-            return big ? launch<T256, E_F32, 1>(p, stream, "rf_gemm_bf16") : launch<T128, E_F32, 1>(p, stream, "rf_gemm_bf16");
-        case RF_EPI_ADD_F32:
-            return big ? launch<T256, E_ADD, 1>(p, stream, "rf_gemm_bf16") : launch<T128, E_ADD, 1>(p, stream, "rf_gemm_bf16");
-        default:
-            return big ? launch<T256, E_SWIGLU, 1>(p, stream, "rf_gemm_bf16")
-                       : launch<T128, E_SWIGLU, 1>(p, stream, "rf_gemm_bf16");
+    // 256x256 tiles at one 512-thread block per CU reach ~1.2 PF/s when every CU has work; when the tile count
+    // would leave a ragged last round, stream-K the K loop over exactly 256 blocks instead.
+    if (workspace && ws_bytes >= SK_WS_BYTES && n % 256 == 0 && sk256(m, n, k)) {
+        sk_setup(p, workspace);
+        switch (epilogue) {
+            case RF_EPI_BF16: return launch_sk<T256, E_BF16>(p, 256, stream, "rf_gemm_bf16");
+            case RF_EPI_F32: return launch_sk<T256, E_F32>(p, 256, stream, "rf_gemm_bf16");
+            case RF_EPI_ADD_F32: return launch_sk<T256, E_ADD>(p, 256, stream, "rf_gemm_bf16");
+            default: return launch_sk<T256, E_SWIGLU>(p, 256, stream, "rf_gemm_bf16");
+        }
     }
+    return run_dp(pick_cfg(m, n), p, epilogue, stream);
 }
 
 static int conv_common(EngineArgs& p, bool gather, const void* w_hi, const void* w_lo, int cout, int cout_pad, float* out,

@@ -52,12 +52,18 @@ def test_gemm_f32_bf16(m, n, k):
     assert relerr(acc, ref2) < 1e-5
 
 
-@pytest.mark.parametrize("grid", ["512", "768", "37"])
+@pytest.mark.parametrize("grid", ["512", "768", "37", "sk256"])
 @pytest.mark.parametrize("m,n,k", [(1000, 1024, 1024), (300, 256, 4096), (129, 128, 96), (5649, 1024, 64)])
 def test_gemm_stream_k(monkeypatch, grid, m, n, k):
-    """Stream-K split (forced grid sizes, incl. an odd one where a tile spans 3+ blocks) vs fp64, every epilogue."""
+    """Stream-K split (forced grid sizes, incl. an odd one where a tile spans 3+ blocks, and the 256x256-tile
+    variant over 256 blocks) vs fp64, every epilogue."""
     ops = _ops()
-    monkeypatch.setenv("RF_GEMM_SK", grid)
+    if grid == "sk256":
+        if n % 256:
+            pytest.skip("256x256 tiles need N % 256 == 0")
+        monkeypatch.setenv("RF_GEMM_SK256", "1")
+    else:
+        monkeypatch.setenv("RF_GEMM_SK", grid)
     g = torch.Generator(device="cpu").manual_seed(m + n + k)
     a = torch.randn(m, k, generator=g).bfloat16().to(dev)
     w = (torch.randn(n, k, generator=g) / math.sqrt(k)).bfloat16().to(dev)
@@ -195,6 +201,37 @@ def test_attention_varlen_self(lens):
         ref = _ref_attn(qkv[sl, :D].float(), qkv[sl, D:2 * D].float(), qkv[sl, 2 * D:].float(), H)
         assert relerr(out[sl], ref) < 6e-3, n
         off += n
+
+
+@pytest.mark.parametrize("n_split", [2, 3, 7])
+def test_attention_split_kv(n_split):
+    """Split-KV partials + merge: ragged problems (incl. one shorter than a key tile, so some splits see no
+    keys), repeated calls on the reused workspace, and a spiked key that forces the deferred-rescale branch
+    inside one split."""
+    ops = _ops()
+    H = 2
+    D = H * 128
+    lens = [700, 37, 300, 1]
+    T = sum(lens)
+    g = torch.Generator(device="cpu").manual_seed(n_split)
+    qkv = torch.randn(T, 3 * D, generator=g).bfloat16()
+    qkv[650, D:2 * D] = 12.0  # one large key row: its score jumps far past the running max
+    probs, off = [], 0
+    for n in lens:
+        probs.append([off, n, off, n, off])
+        off += n
+    d = qkv.to(dev)
+    pt = torch.tensor(probs, dtype=torch.int32, device=dev)
+    for _ in range(3):
+        out = torch.zeros(T, D, device=dev, dtype=torch.bfloat16)
+        ops.attention(d[:, :D], d[:, D:2 * D], d[:, 2 * D:], out, pt, max(lens), H, n_split=n_split)
+        o = out.float().cpu()
+        off = 0
+        for n in lens:
+            sl = slice(off, off + n)
+            ref = _ref_attn(qkv[sl, :D].float(), qkv[sl, D:2 * D].float(), qkv[sl, 2 * D:].float(), H)
+            assert relerr(o[sl], ref) < 6e-3, (n_split, n)
+            off += n
 
 
 def test_attention_cross_shared_v():

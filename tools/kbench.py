@@ -88,14 +88,14 @@ def gemm():
             c = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
         else:
             c = torch.zeros(m, n, device=dev)
-        for label, tile, sk, gm in (("dp128", "128", None, None), ("dp256", "256", None, None),
-                                    ("auto", None, None, None), ("auto-mfast", None, None, "100000")):
-            for key, val in (("RF_GEMM_TILE", tile), ("RF_GEMM_SK", sk), ("RF_GEMM_GROUP_M", gm)):
+        for label, tile, sk, gm in (("dp128", "128", None, "0"), ("dp256", "256", None, "0"),
+                                    ("sk256", None, None, "1"), ("auto", None, None, None)):
+            for key, val in (("RF_GEMM_TILE", tile), ("RF_GEMM_SK", sk), ("RF_GEMM_SK256", gm)):
                 if val is None:
                     os.environ.pop(key, None)
                 else:
                     os.environ[key] = val
-            if label == "dp256" and n % 256:
+            if label in ("dp256", "sk256") and n % 256:
                 continue
             ms = timeit(lambda: ops.gemm(a, w, c, None, epi), reps=10 if k > 8000 else 20)
             print(f"gemm {name:8s} {m}x{n}x{k} {label}: {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF")
