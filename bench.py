@@ -143,6 +143,7 @@ def main():
     if os.path.exists(tpath):
         try:
             traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+            traffic = None if traffic is None else int(traffic)
         except Exception:
             traffic = None
 
@@ -168,11 +169,13 @@ def main():
                 "mfma_frac_bf16_peak": round(fl["total"] / args.views * fps / world / 1e12 / PEAK_BF16_TFLOPS, 4),
             },
             "roofline": {
-                "kernel": "rf_attn_fwd (stage-1 triangle self-attention, attn_fwd_kernel<false,4>)",
+                "kernel": "rf_attn_fwd (+ rf_attn_combine when split-KV) — stage-1 triangle self-attention, attn_v3_kernel",
                 "bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                 "avg_launch_ms": round(kern_ms, 4), "launches_per_step": per_step_launches,
                 "algorithmic_flop_per_launch": kern_flops,
+                # Q, K, V read once + O written once (bf16); traffic above this = K/V re-reads + split partials
+                "algorithmic_bytes_per_launch": 4 * s_len * cfg.latent_dim * 2 * args.scenes,
             },
             "cpu_baseline": None,
         }

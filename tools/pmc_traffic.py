@@ -1,0 +1,44 @@
+"""HBM traffic per launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+python tools/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> [out.json]
+
+Corrections follow MI355X_MICROARCH.md §HBM: both counters are in KiB; on gfx950 FETCH_SIZE
+tallies exactly half of the bytes of wide (16 B/lane) coalesced reads, so it is doubled; WRITE_SIZE
+is exact for 16-B stores.  Rows are grouped by (kernel, grid size) so that e.g. the stage-1 and the
+cross-attention launches of one kernel stay apart.  The stage-1 attention entry (grid of the
+bench workload) is written to profiles/attn_stage1_traffic.json for bench.py's roofline.traffic."""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def load(path, counter):
+    per = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        key = (r["Kernel_Name"], int(r["Grid_Size"]) // max(1, int(r["Workgroup_Size"])))
+        per[key].append(float(r["Counter_Value"]) * 1024.0)
+    return per
+
+
+def main():
+    fetch = load(sys.argv[1], "FETCH_SIZE")
+    write = load(sys.argv[2], "WRITE_SIZE")
+    rows = []
+    for key in sorted(set(fetch) | set(write), key=lambda k: -sum(fetch.get(k, [0]))):
+        f, w = fetch.get(key, []), write.get(key, [])
+        fb = 2.0 * sum(f) / len(f) if f else float("nan")
+        wb = sum(w) / len(w) if w else float("nan")
+        rows.append({"kernel": key[0], "grid": key[1], "launches": len(f), "read_bytes_per_launch": fb,
+                     "write_bytes_per_launch": wb, "hbm_bytes_per_launch": fb + wb})
+    for r in rows[:25]:
+        print(f"{r['hbm_bytes_per_launch']/1e6:10.2f} MB/launch (rd {r['read_bytes_per_launch']/1e6:9.2f} "
+              f"wr {r['write_bytes_per_launch']/1e6:9.2f}) n={r['launches']:4d} grid={r['grid']:6d} {r['kernel'][:90]}")
+    if len(sys.argv) > 3:
+        json.dump(rows, open(sys.argv[3], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
