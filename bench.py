@@ -161,7 +161,7 @@ def main():
                                f"{cfg.view_transformer_use_swin_attn} dpt={cfg.dpt_features}/{cfg.dpt_out_channels}",
                 "global_batch": frames_per_step * world, "seq_len": s_len, "res": args.res,
                 "parallelism": f"dp{world}", "weights": "synthetic seed 0 (no checkpoint offline)",
-                "precision": "bf16 MFMA operands, fp32 accumulate/softmax/residual; DPT fp32",
+                "precision": "bf16 MFMA operands, fp32 accumulate/softmax/residual; DPT fp16 operands, fp32 accumulate",
             },
             "frame": {
                 "gflop_per_frame": round(fl["total"] / args.views / 1e9, 1),

@@ -30,6 +30,7 @@
  *   rf_conv2d_bf16x3   DPT nn.Conv2d (dpt.py:44-52, 69-72, 124-125, 184-192, 208-213, 232-240; aten conv2d) with
  *                      the ResidualConvUnit SiLU/skip (dpt.py:86-92) and fusion sum (:141-143) fused; FINAL mode
  *                      also fuses output_conv2 SiLU + 1x1 (dpt.py:234-240), ELU and the log decode
+ *   rf_conv2d_f16 / rf_deconv2d_f16  the same two DPT convolutions with fp16 operands (one MFMA per product)
  *   rf_split_planes    (operand preparation for the above; no reference counterpart)
  *   rf_deconv2d_bf16x3 DPT nn.ConvTranspose2d kernel == stride (dpt.py:195-206; aten conv_transpose2d)
  *   rf_upsample_bilinear F.interpolate(bilinear, align_corners=True) (dpt.py:154-155, 269-270)
@@ -48,7 +49,7 @@ extern "C" {
 #define RF_ERR_LAUNCH 2
 #define RF_ERR_UNSUPPORTED 3
 
-#define RF_ABI_VERSION 2
+#define RF_ABI_VERSION 3
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -166,11 +167,25 @@ int rf_deconv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, 
                        const void* w_lo, int cout, int k, const float* bias, float* out, void* p_hi, void* p_lo,
                        int p_ld, void* workspace, int64_t ws_bytes, void* stream);
 
-/* f32 rows x[r, 0:c] (row stride ldx) -> bf16 hi/lo planes (row stride p_ld), of silu(x) if silu_act. */
+/* fp16-operand variants: one fp16 input plane (channel stride cin_pad), fp16 weights [cout_pad][kh][kw][cin_pad],
+ * one MFMA per product with fp32 accumulation (11-bit operand mantissa: 9e-5 relative L2 on the large-proxy
+ * DPT against 7e-4 for bf16 operands).  Same epilogue as above; the output plane p_out (may be NULL) is one
+ * fp16 plane.  Values beyond fp16 range (|x| > 65504) become inf in the planes. */
+int rf_conv2d_f16(const void* in, int n_img, int hi, int wi, int cin_pad, const void* w, int cout, int cout_pad, int kh,
+                  int kw, int stride, int pad, const float* bias, const float* res1, const float* res2, float* out,
+                  void* p_out, int p_ld, int flags, const float* w_fin, const float* b_fin, int n_fin, float elu_alpha,
+                  void* workspace, int64_t ws_bytes, void* stream);
+int rf_deconv2d_f16(const void* in, int n_img, int hi, int wi, int cin_pad, const void* w, int cout, int k,
+                    const float* bias, float* out, void* p_out, int p_ld, void* workspace, int64_t ws_bytes,
+                    void* stream);
+
+/* f32 rows x[r, 0:c] (row stride ldx) -> bf16 hi/lo planes (row stride p_ld), of silu(x) if silu_act.
+ * p_lo == NULL: one fp16 plane in p_hi instead (input of rf_conv2d_f16 / rf_deconv2d_f16). */
 int rf_split_planes(const float* x, int64_t rows, int c, int64_t ldx, void* p_hi, void* p_lo, int p_ld, int silu_act,
                     void* stream);
 
-/* Bilinear resize, align_corners=True, NHWC fp32 (c % 4 == 0) into `out` and/or hi/lo planes. */
+/* Bilinear resize, align_corners=True, NHWC fp32 (c % 4 == 0) into `out` and/or hi/lo planes
+ * (p_lo == NULL: one fp16 plane, as rf_split_planes). */
 int rf_upsample_bilinear(const float* in, int n_img, int hi, int wi, int c, float* out, int ho, int wo, void* p_hi,
                          void* p_lo, int p_ld, void* stream);
 

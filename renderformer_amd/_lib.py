@@ -38,6 +38,9 @@ SIGNATURES = {
     "rf_conv2d_bf16x3": [_P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I,
                          _P, _P, _I, _F, _P, _L, _P],
     "rf_deconv2d_bf16x3": [_P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P, _P, _P, _I, _P, _L, _P],
+    "rf_conv2d_f16": [_P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _I, _F,
+                      _P, _L, _P],
+    "rf_deconv2d_f16": [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P, _I, _P, _L, _P],
     "rf_split_planes": [_P, _L, _I, _L, _P, _P, _I, _I, _P],
     "rf_upsample_bilinear": [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _I, _P],
 }

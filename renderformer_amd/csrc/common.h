@@ -31,6 +31,12 @@ RF_DEV uint32_t pack_bf16x2(float lo, float hi) {
     return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
 }
 
+// round-to-nearest-even f32 -> fp16 pair (overflow -> inf, like a torch .half() cast)
+RF_DEV uint32_t pack_f16x2(float lo, float hi) {
+    _Float16 a = (_Float16)lo, b = (_Float16)hi;
+    return (uint32_t)*reinterpret_cast<uint16_t*>(&a) | ((uint32_t)*reinterpret_cast<uint16_t*>(&b) << 16);
+}
+
 RF_DEV float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -3,7 +3,8 @@
 //
 // Activations consumed by a DPT convolution live as two bf16 planes hi = bf16(x),
 // lo = bf16(x - hi) (optionally of silu(x): the ResidualConvUnit pre-activation,
-// dpt.py:86-89, applied once per element instead of once per filter tap).
+// dpt.py:86-89, applied once per element instead of once per filter tap).  With p_lo == NULL the
+// activation is stored as ONE fp16 plane in p_hi instead (the fp16-operand DPT mode).
 #include <math.h>
 
 #include "common.h"
@@ -14,6 +15,14 @@ RF_DEV float silu(float x) { return x / (1.0f + expf(-x)); }
 
 RF_DEV void store_split4(bf16_t* p_hi, bf16_t* p_lo, int64_t off, float4 v, bool act) {
     float x[4] = {v.x, v.y, v.z, v.w};
+    if (!p_lo) {
+        if (act) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] = silu(x[e]);
+        }
+        *reinterpret_cast<uint2*>(p_hi + off) = make_uint2(pack_f16x2(x[0], x[1]), pack_f16x2(x[2], x[3]));
+        return;
+    }
     uint32_t h[2], l[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
@@ -79,7 +88,7 @@ __global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__
 
 extern "C" int rf_split_planes(const float* x, int64_t rows, int c, int64_t ldx, void* p_hi, void* p_lo, int p_ld,
                                int silu_act, void* stream) {
-    RF_REQUIRE(x && p_hi && p_lo, "rf_split_planes: null pointer");
+    RF_REQUIRE(x && p_hi, "rf_split_planes: null pointer");
     RF_REQUIRE(c % 4 == 0 && ldx % 4 == 0 && p_ld % 4 == 0 && p_ld >= c, "rf_split_planes: bad widths");
     const int64_t n = rows * (c / 4);
     if (n <= 0) return RF_OK;
@@ -90,7 +99,7 @@ extern "C" int rf_split_planes(const float* x, int64_t rows, int c, int64_t ldx,
 
 extern "C" int rf_upsample_bilinear(const float* in, int n_img, int hi, int wi, int c, float* out, int ho, int wo,
                                     void* p_hi, void* p_lo, int p_ld, void* stream) {
-    RF_REQUIRE(in && (out || (p_hi && p_lo)), "rf_upsample_bilinear: null pointer");
+    RF_REQUIRE(in && (out || p_hi), "rf_upsample_bilinear: null pointer");
     RF_REQUIRE(c % 4 == 0 && (!p_hi || (p_ld % 4 == 0 && p_ld >= c)), "rf_upsample_bilinear: bad widths");
     const int64_t total = (int64_t)n_img * ho * wo * (c / 4);
     if (total <= 0) return RF_OK;

@@ -7,8 +7,9 @@
 //   rows are either dense (a + m*lda) or gathered (DPT convolutions: im2col of an
 //   NHWC activation plane, one 32-wide K step = one filter tap, out-of-image rows
 //   point at a zero row) — no im2col buffer is ever materialised.
-// * NTERM = 3 evaluates fp32-accurate products from bf16 hi/lo splits of both
-//   operands: a.b ~= ah.bh + ah.bl + al.bh  (DPT head, see dpt.py).
+// * Operand precision NTERM: 1 = bf16; 3 = fp32-accurate products from bf16 hi/lo splits of
+//   both operands, a.b ~= ah.bh + ah.bl + al.bh; 2 = fp16 operands (one MFMA, 11-bit
+//   mantissa: the DPT head's default, see dpt.py).
 // * Tile 128x128x32, 256 threads = 2x2 waves of 64x64 (4x4 v_mfma_f32_16x16x32_bf16).
 //   Both operands go global->LDS with global_load_lds_dwordx4 (no VGPR staging)
 //   through a 3-deep LDS ring: at step kt the wave waits (counted vmcnt) only for
@@ -31,6 +32,8 @@
 namespace {
 
 constexpr int BK = 32;
+constexpr int P_F16 = 2;  // NTERM value of the fp16-operand mode
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 
 enum Epi { E_BF16 = RF_EPI_BF16, E_F32 = RF_EPI_F32, E_ADD = RF_EPI_ADD_F32, E_SWIGLU = RF_EPI_SWIGLU, E_CONV = 16 };
 
@@ -67,6 +70,7 @@ struct EngineArgs {
     bf16_t* p_lo;
     int p_ld;
     int cout, deconv, flags, n_fin;
+    int plane_f16;  // output plane is one fp16 plane (p_hi) instead of bf16 hi/lo
     const float* w_fin;
     const float* b_fin;
     float elu_alpha;
@@ -238,7 +242,11 @@ RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.wl[j], f.a[i], acc[i][j], 0, 0, 0);
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[j], f.al[i], acc[i][j], 0, 0, 0);
                 }
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[j], f.a[i], acc[i][j], 0, 0, 0);
+                if constexpr (NTERM == P_F16)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, f.w[j]),
+                                                                       __builtin_bit_cast(f16x8, f.a[i]), acc[i][j], 0, 0, 0);
+                else
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[j], f.a[i], acc[i][j], 0, 0, 0);
             }
     };
     // wait until this wave's DMA of tile t landed, given that tiles up to `last` were issued
@@ -403,7 +411,15 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                 if (p.c)
                     *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + pix * p.cout + co) =
                         make_float4(v[0], v[1], v[2], v[3]);
-                if (p.p_hi) {
+                if (p.p_hi && p.plane_f16) {
+                    float a[4] = {v[0], v[1], v[2], v[3]};
+                    if (p.flags & RF_CONV_PLANE_SILU) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) a[e] = silu(a[e]);
+                    }
+                    *reinterpret_cast<uint2*>(p.p_hi + pix * p.p_ld + co) = make_uint2(pack_f16x2(a[0], a[1]),
+                                                                                       pack_f16x2(a[2], a[3]));
+                } else if (p.p_hi) {
                     uint32_t h[2], l[2];
 #pragma unroll
                     for (int e = 0; e < 2; ++e) {
@@ -703,14 +719,28 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
     return run_dp(pick_cfg(m, n), p, epilogue, stream);
 }
 
-static int conv_common(EngineArgs& p, bool gather, const void* w_hi, const void* w_lo, int cout, int cout_pad, float* out,
+template <int NT>
+static int conv_dispatch(EngineArgs& p, bool gather, bool big, int64_t sk_grid_n, void* workspace, void* stream,
+                         const char* what) {
+    if (sk_grid_n) {
+        sk_setup(p, workspace);
+        return gather ? launch_sk<T128, E_CONV, NT, true>(p, (int)sk_grid_n, stream, what)
+                      : launch_sk<T128, E_CONV, NT, false>(p, (int)sk_grid_n, stream, what);
+    }
+    if (gather)
+        return big ? launch<T256x128, E_CONV, NT, true>(p, stream, what) : launch<T128, E_CONV, NT, true>(p, stream, what);
+    return big ? launch<T256x128, E_CONV, NT, false>(p, stream, what) : launch<T128, E_CONV, NT, false>(p, stream, what);
+}
+
+// nterm: 3 = bf16x3 hi/lo operands, P_F16 = one fp16 plane per operand (w_lo / in_lo unused)
+static int conv_common(EngineArgs& p, int nterm, bool gather, const void* w_hi, const void* w_lo, int cout, int cout_pad, float* out,
                        const float* bias, const float* res1, const float* res2, void* p_hi, void* p_lo, int p_ld,
                        int flags, const float* w_fin, const float* b_fin, int n_fin, float elu_alpha, void* workspace,
                        int64_t ws_bytes, void* stream, const char* what) {
-    RF_REQUIRE(w_hi && w_lo, "%s: null weights", what);
+    RF_REQUIRE(w_hi && (w_lo || nterm == P_F16), "%s: null weights", what);
     RF_REQUIRE(cout % 4 == 0, "%s: cout must be a multiple of 4", what);
     RF_REQUIRE(out || p_hi, "%s: no output", what);
-    RF_REQUIRE(!p_hi || (p_lo && p_ld % 4 == 0 && p_ld >= cout), "%s: bad plane output", what);
+    RF_REQUIRE(!p_hi || ((p_lo || nterm == P_F16) && p_ld % 4 == 0 && p_ld >= cout), "%s: bad plane output", what);
     RF_REQUIRE(!(flags & RF_CONV_FINAL) || (cout <= 64 && w_fin && b_fin && n_fin > 0 && out),
                "%s: final head needs cout <= 64 and w_fin/b_fin", what);
     static void* z = nullptr;  // device address of the zero row (per process; single device per process)
@@ -730,6 +760,7 @@ static int conv_common(EngineArgs& p, bool gather, const void* w_hi, const void*
     p.p_hi = (bf16_t*)p_hi;
     p.p_lo = (bf16_t*)p_lo;
     p.p_ld = p_ld;
+    p.plane_f16 = nterm == P_F16;
     p.cout = cout;
     p.flags = flags;
     p.w_fin = w_fin;
@@ -744,19 +775,15 @@ static int conv_common(EngineArgs& p, bool gather, const void* w_hi, const void*
     // Too few 128x128 tiles for 256 CUs (one bf16x3 block per CU): stream-K over the K loop, each block
     // keeping >= 8 K-steps.
     const char* sk_env = getenv("RF_CONV_SK");
+    int64_t skg = 0;
     if (!big && workspace && ws_bytes >= SK_WS_BYTES && !(sk_env && atoi(sk_env) == 0)) {
         const int64_t tiles = (int64_t)((p.m + 127) / 128) * (p.n / 128);
         const int64_t work = tiles * (p.k / BK);
         const int64_t grid = std::min<int64_t>(256, work / 8);
-        if (tiles < 192 && grid > tiles) {
-            sk_setup(p, workspace);
-            return gather ? launch_sk<T128, E_CONV, 3, true>(p, (int)grid, stream, what)
-                          : launch_sk<T128, E_CONV, 3, false>(p, (int)grid, stream, what);
-        }
+        if (tiles < 192 && grid > tiles) skg = grid;
     }
-    if (gather)
-        return big ? launch<T256x128, E_CONV, 3, true>(p, stream, what) : launch<T128, E_CONV, 3, true>(p, stream, what);
-    return big ? launch<T256x128, E_CONV, 3, false>(p, stream, what) : launch<T128, E_CONV, 3, false>(p, stream, what);
+    return nterm == P_F16 ? conv_dispatch<P_F16>(p, gather, big, skg, workspace, stream, what)
+                          : conv_dispatch<3>(p, gather, big, skg, workspace, stream, what);
 }
 
 extern "C" int rf_conv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, int wi, int cin_pad,
@@ -782,8 +809,34 @@ extern "C" int rf_conv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img,
     p.m = n_img * p.ho * p.wo;
     p.k = kh * kw * cin_pad;
     p.ldw = p.k;
-    return conv_common(p, true, w_hi, w_lo, cout, cout_pad, out, bias, res1, res2, p_hi, p_lo, p_ld, flags, w_fin,
+    return conv_common(p, 3, true, w_hi, w_lo, cout, cout_pad, out, bias, res1, res2, p_hi, p_lo, p_ld, flags, w_fin,
                        b_fin, n_fin, elu_alpha, workspace, ws_bytes, stream, "rf_conv2d_bf16x3");
+}
+
+extern "C" int rf_conv2d_f16(const void* in, int n_img, int hi, int wi, int cin_pad, const void* w, int cout,
+                             int cout_pad, int kh, int kw, int stride, int pad, const float* bias, const float* res1,
+                             const float* res2, float* out, void* p_out, int p_ld, int flags, const float* w_fin,
+                             const float* b_fin, int n_fin, float elu_alpha, void* workspace, int64_t ws_bytes,
+                             void* stream) {
+    RF_REQUIRE(in, "rf_conv2d_f16: null input");
+    RF_REQUIRE(cin_pad % BK == 0, "rf_conv2d_f16: cin_pad %d must be a multiple of %d", cin_pad, BK);
+    RF_REQUIRE(cout_pad % 128 == 0 && cout_pad >= cout, "rf_conv2d_f16: cout_pad %d must be a multiple of 128",
+               cout_pad);
+    EngineArgs p{};
+    p.a = (const bf16_t*)in;
+    p.hi = hi;
+    p.wi = wi;
+    p.cin_pad = cin_pad;
+    p.ho = (hi + 2 * pad - kh) / stride + 1;
+    p.wo = (wi + 2 * pad - kw) / stride + 1;
+    p.kw = kw;
+    p.stride = stride;
+    p.pad = pad;
+    p.m = n_img * p.ho * p.wo;
+    p.k = kh * kw * cin_pad;
+    p.ldw = p.k;
+    return conv_common(p, P_F16, true, w, nullptr, cout, cout_pad, out, bias, res1, res2, p_out, nullptr, p_ld, flags,
+                       w_fin, b_fin, n_fin, elu_alpha, workspace, ws_bytes, stream, "rf_conv2d_f16");
 }
 
 extern "C" int rf_deconv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, int wi, int cin_pad,
@@ -802,6 +855,25 @@ extern "C" int rf_deconv2d_bf16x3(const void* in_hi, const void* in_lo, int n_im
     p.k = cin_pad;
     p.ldw = cin_pad;
     p.deconv = k;
-    return conv_common(p, false, w_hi, w_lo, cout, k * k * cout, out, bias, nullptr, nullptr, p_hi, p_lo, p_ld, 0, nullptr,
-                       nullptr, 0, 0.f, workspace, ws_bytes, stream, "rf_deconv2d_bf16x3");
+    return conv_common(p, 3, false, w_hi, w_lo, cout, k * k * cout, out, bias, nullptr, nullptr, p_hi, p_lo, p_ld, 0,
+                       nullptr, nullptr, 0, 0.f, workspace, ws_bytes, stream, "rf_deconv2d_bf16x3");
+}
+
+extern "C" int rf_deconv2d_f16(const void* in, int n_img, int hi, int wi, int cin_pad, const void* w, int cout, int k,
+                               const float* bias, float* out, void* p_out, int p_ld, void* workspace, int64_t ws_bytes,
+                               void* stream) {
+    RF_REQUIRE(in, "rf_deconv2d_f16: null input");
+    RF_REQUIRE(cin_pad % BK == 0, "rf_deconv2d_f16: cin_pad must be a multiple of %d", BK);
+    RF_REQUIRE((k * k * cout) % 128 == 0 && cout < 65536, "rf_deconv2d_f16: k*k*cout must be a multiple of 128");
+    EngineArgs p{};
+    p.a = (const bf16_t*)in;
+    p.lda = cin_pad;
+    p.ho = hi;
+    p.wo = wi;
+    p.m = n_img * hi * wi;
+    p.k = cin_pad;
+    p.ldw = cin_pad;
+    p.deconv = k;
+    return conv_common(p, P_F16, false, w, nullptr, cout, k * k * cout, out, bias, nullptr, nullptr, p_out, nullptr,
+                       p_ld, 0, nullptr, nullptr, 0, 0.f, workspace, ws_bytes, stream, "rf_deconv2d_f16");
 }

@@ -1,12 +1,17 @@
 """DPT patch decode (renderformer/layers/dpt.py:174-273) on librfhip's GEMM engine.
 
 Layout: every activation is NHWC.  A tensor that feeds a convolution is kept as
-two bf16 planes (hi, lo) — optionally of silu(x), the ResidualConvUnit
-pre-activation — produced directly by the epilogue of the conv (or resize) that
-wrote it; tensors that are also needed as residuals are additionally kept in
-fp32.  Convolutions evaluate hi*hi + hi*lo + lo*hi with fp32 accumulation
-("bf16x3"), i.e. fp32-level accuracy at 3/16 of the fp32-MFMA cost (a plain
-bf16 DPT costs 2.0e-3 relative L2, SURVEY Appendix C, over the 1e-3 budget).
+operand planes — optionally of silu(x), the ResidualConvUnit pre-activation —
+produced directly by the epilogue of the conv (or resize) that wrote it; tensors
+that are also needed as residuals are additionally kept in fp32.
+
+Operand precision (``precision``):
+* ``"f16"`` (default): one fp16 plane per operand, one MFMA per product, fp32
+  accumulation.  fp16's 11-bit mantissa keeps the DPT at 9e-5 relative L2 on the
+  large-proxy config (bf16 operands: 7e-4 there, 2.0e-3 on v1-base — SURVEY
+  Appendix C — over the 1e-3 budget).  Activations must stay within fp16 range.
+* ``"bf16x3"``: two bf16 planes (hi, lo) per operand and hi*hi + hi*lo + lo*hi,
+  fp32-level accuracy at 3x the MFMA work; no range limit beyond fp32's.
 
 Graph with two exact rewrites:
 * FeatureFusionBlock's 1x1 ``out_conv`` is linear and the bilinear resize
@@ -41,42 +46,51 @@ def _split(w: torch.Tensor):
 
 @dataclass
 class Planes:
-    hi: torch.Tensor  # bf16 [n, h, w, ld]
-    lo: torch.Tensor
-    c: int            # real channels (ld - c padded channels are zero)
+    hi: torch.Tensor            # bf16 hi plane, or the one fp16 plane [n, h, w, ld]
+    lo: Optional[torch.Tensor]  # bf16 lo plane (None for fp16 planes)
+    c: int                      # real channels (ld - c padded channels are zero)
 
     @property
     def shape(self):
         return self.hi.shape
 
+    @property
+    def f16(self) -> bool:
+        return self.lo is None
+
     @staticmethod
-    def empty(n, h, w, c, ld, device):
+    def empty(n, h, w, c, ld, device, f16: bool = False):
         alloc = torch.zeros if ld > c else torch.empty
+        if f16:
+            return Planes(alloc(n, h, w, ld, dtype=torch.float16, device=device), None, c)
         return Planes(alloc(n, h, w, ld, dtype=torch.bfloat16, device=device),
                       alloc(n, h, w, ld, dtype=torch.bfloat16, device=device), c)
 
 
-def split_planes(x: torch.Tensor, ld: int, silu: bool = False) -> Planes:
-    """fp32 NHWC -> bf16 hi/lo planes with channel stride ld."""
+def split_planes(x: torch.Tensor, ld: int, silu: bool = False, f16: bool = False) -> Planes:
+    """fp32 NHWC -> operand planes with channel stride ld (bf16 hi/lo, or one fp16 plane)."""
     n, h, w, c = x.shape
-    pl = Planes.empty(n, h, w, c, ld, x.device)
+    pl = Planes.empty(n, h, w, c, ld, x.device, f16)
     call("rf_split_planes", ptr(x), n * h * w, c, x.stride(2), ptr(pl.hi), ptr(pl.lo), ld, int(silu), stream())
     return pl
 
 
-def upsample(x: torch.Tensor, ho: int, wo: int, out_f32: bool = True, planes_ld: Optional[int] = None):
+def upsample(x: torch.Tensor, ho: int, wo: int, out_f32: bool = True, planes_ld: Optional[int] = None,
+             f16: bool = False):
     n, h, w, c = x.shape
     out = torch.empty(n, ho, wo, c, device=x.device) if out_f32 else None
-    pl = Planes.empty(n, ho, wo, c, planes_ld, x.device) if planes_ld else None
+    pl = Planes.empty(n, ho, wo, c, planes_ld, x.device, f16) if planes_ld else None
     call("rf_upsample_bilinear", ptr(x), n, h, w, c, ptr(out), ho, wo, ptr(pl.hi if pl else None),
          ptr(pl.lo if pl else None), planes_ld or 0, stream())
     return out, pl
 
 
 class _Conv:
-    """One nn.Conv2d / nn.ConvTranspose2d(kernel == stride) with weights split for the bf16x3 engine."""
+    """One nn.Conv2d / nn.ConvTranspose2d(kernel == stride) with weights laid out for the engine
+    (bf16 hi/lo planes, or one fp16 plane with ``f16``)."""
 
-    def __init__(self, w: torch.Tensor, b, device, deconv: bool = False):
+    def __init__(self, w: torch.Tensor, b, device, deconv: bool = False, f16: bool = False):
+        self.f16 = f16
         w = w.detach().float().cpu()
         if deconv:  # ConvTranspose2d weight [cin, cout, k, k] -> rows (dy, dx, co), cols ci
             cin, cout, k, _ = w.shape
@@ -94,8 +108,11 @@ class _Conv:
             mat[:cout, :, :, :cin] = w.permute(0, 2, 3, 1)
             mat = mat.reshape(self.cout_pad, -1)
         self.cin, self.cout = cin, cout
-        hi, lo = _split(mat)
-        self.w_hi, self.w_lo = hi.to(device), lo.to(device)
+        if f16:
+            self.w_hi, self.w_lo = mat.to(torch.float16).contiguous().to(device), None
+        else:
+            hi, lo = _split(mat)
+            self.w_hi, self.w_lo = hi.to(device), lo.to(device)
         self.b = None if b is None else b.detach().float().to(device).contiguous()
 
     def __call__(self, x: Planes, stride=1, pad=None, res1=None, res2=None, out_f32=False,
@@ -104,6 +121,8 @@ class _Conv:
         if ld != self.cin_pad or x.c != self.cin:
             raise ValueError(f"conv input planes must have {self.cin} channels padded to {self.cin_pad}, got "
                              f"{x.c}/{ld}")
+        if x.f16 != self.f16:
+            raise ValueError("conv input planes and weights must use the same operand precision")
         dev = x.hi.device
         from .ops import _gemm_workspace
         ws = _gemm_workspace(dev)
@@ -118,17 +137,29 @@ class _Conv:
             nf = w_fin.shape[0]
             shape = (n, nf, ho, wo) if final_flags & NCHW_OUT else (n, ho, wo, nf)
             out = torch.empty(shape, device=dev)
-            call("rf_conv2d_bf16x3", ptr(x.hi), ptr(x.lo), n, h, w, ld, ptr(self.w_hi), ptr(self.w_lo), self.cout,
-                 self.cout_pad, self.kh, self.kw, stride, pad, ptr(self.b), 0, 0, ptr(out), 0, 0, 0,
-                 FINAL | final_flags, ptr(w_fin), ptr(b_fin), nf, alpha, ptr(ws), ws.numel(), stream())
+            if self.f16:
+                call("rf_conv2d_f16", ptr(x.hi), n, h, w, ld, ptr(self.w_hi), self.cout, self.cout_pad, self.kh,
+                     self.kw, stride, pad, ptr(self.b), 0, 0, ptr(out), 0, 0, FINAL | final_flags, ptr(w_fin),
+                     ptr(b_fin), nf, alpha, ptr(ws), ws.numel(), stream())
+            else:
+                call("rf_conv2d_bf16x3", ptr(x.hi), ptr(x.lo), n, h, w, ld, ptr(self.w_hi), ptr(self.w_lo), self.cout,
+                     self.cout_pad, self.kh, self.kw, stride, pad, ptr(self.b), 0, 0, ptr(out), 0, 0, 0,
+                     FINAL | final_flags, ptr(w_fin), ptr(b_fin), nf, alpha, ptr(ws), ws.numel(), stream())
             return out
         out = torch.empty(n, ho, wo, self.cout, device=dev) if out_f32 else None
-        pl = Planes.empty(n, ho, wo, self.cout, planes_ld, dev) if planes_ld else None
+        pl = Planes.empty(n, ho, wo, self.cout, planes_ld, dev, self.f16) if planes_ld else None
         for r in (res1, res2):
             if r is not None and (tuple(r.shape) != (n, ho, wo, self.cout) or not r.is_contiguous()):
                 raise ValueError("residual must match the conv output")
         flags = PLANE_SILU if planes_silu else 0
-        if self.k:
+        if self.f16 and self.k:
+            call("rf_deconv2d_f16", ptr(x.hi), n, h, w, ld, ptr(self.w_hi), self.cout, self.k, ptr(self.b), ptr(out),
+                 ptr(pl.hi if pl else None), planes_ld or 0, ptr(ws), ws.numel(), stream())
+        elif self.f16:
+            call("rf_conv2d_f16", ptr(x.hi), n, h, w, ld, ptr(self.w_hi), self.cout, self.cout_pad, self.kh, self.kw,
+                 stride, pad, ptr(self.b), ptr(res1), ptr(res2), ptr(out), ptr(pl.hi if pl else None), planes_ld or 0,
+                 flags, 0, 0, 0, 0.0, ptr(ws), ws.numel(), stream())
+        elif self.k:
             call("rf_deconv2d_bf16x3", ptr(x.hi), ptr(x.lo), n, h, w, ld, ptr(self.w_hi), ptr(self.w_lo), self.cout,
                  self.k, ptr(self.b), ptr(out), ptr(pl.hi if pl else None), ptr(pl.lo if pl else None),
                  planes_ld or 0, ptr(ws), ws.numel(), stream())
@@ -140,24 +171,32 @@ class _Conv:
         return out, pl
 
 
+PRECISIONS = ("f16", "bf16x3")
+
+
 class DPTHead:
-    def __init__(self, sd: Dict[str, torch.Tensor], prefix: str, device):
+    def __init__(self, sd: Dict[str, torch.Tensor], prefix: str, device, precision: str = "f16"):
+        if precision not in PRECISIONS:
+            raise ValueError(f"DPT precision must be one of {PRECISIONS}, got {precision!r}")
+        self.precision = precision
+        f16 = self.f16 = precision == "f16"
         g = lambda n: sd.get(f"{prefix}.{n}")  # noqa: E731
-        self.projects = [_Conv(g(f"projects.{i}.weight"), g(f"projects.{i}.bias"), device) for i in range(4)]
-        self.resize = {0: _Conv(g("resize_layers.0.weight"), g("resize_layers.0.bias"), device, deconv=True),
-                       1: _Conv(g("resize_layers.1.weight"), g("resize_layers.1.bias"), device, deconv=True),
-                       3: _Conv(g("resize_layers.3.weight"), g("resize_layers.3.bias"), device)}
-        self.rn = [_Conv(g(f"scratch.layer{i + 1}_rn.weight"), None, device) for i in range(4)]
+        C = lambda w, b, **kw: _Conv(w, b, device, f16=f16, **kw)  # noqa: E731
+        self.projects = [C(g(f"projects.{i}.weight"), g(f"projects.{i}.bias")) for i in range(4)]
+        self.resize = {0: C(g("resize_layers.0.weight"), g("resize_layers.0.bias"), deconv=True),
+                       1: C(g("resize_layers.1.weight"), g("resize_layers.1.bias"), deconv=True),
+                       3: C(g("resize_layers.3.weight"), g("resize_layers.3.bias"))}
+        self.rn = [C(g(f"scratch.layer{i + 1}_rn.weight"), None) for i in range(4)]
         self.refine = {}
         for r in (1, 2, 3, 4):
             p = f"scratch.refinenet{r}"
             units = {}
             for u in ((1, 2) if r != 4 else (2,)):
-                units[u] = [_Conv(g(f"{p}.resConvUnit{u}.conv{c}.weight"), g(f"{p}.resConvUnit{u}.conv{c}.bias"),
-                                  device) for c in (1, 2)]
-            self.refine[r] = (units, _Conv(g(f"{p}.out_conv.weight"), g(f"{p}.out_conv.bias"), device))
-        self.out1 = _Conv(g("scratch.output_conv1.weight"), g("scratch.output_conv1.bias"), device)
-        self.out2 = _Conv(g("scratch.output_conv2.0.weight"), g("scratch.output_conv2.0.bias"), device)
+                units[u] = [C(g(f"{p}.resConvUnit{u}.conv{c}.weight"), g(f"{p}.resConvUnit{u}.conv{c}.bias"))
+                            for c in (1, 2)]
+            self.refine[r] = (units, C(g(f"{p}.out_conv.weight"), g(f"{p}.out_conv.bias")))
+        self.out1 = C(g("scratch.output_conv1.weight"), g("scratch.output_conv1.bias"))
+        self.out2 = C(g("scratch.output_conv2.0.weight"), g("scratch.output_conv2.0.bias"))
         wf = g("scratch.output_conv2.2.weight")
         self.w_fin = wf.detach().float().reshape(wf.shape[0], -1).to(device).contiguous()
         self.b_fin = g("scratch.output_conv2.2.bias").detach().float().to(device).contiguous()
@@ -174,13 +213,13 @@ class DPTHead:
         """FeatureFusionBlock (dpt.py:133-159) with the 1x1 out_conv moved before the resize."""
         units, out_conv = self.refine[r]
         if x1 is None:
-            out, outs = x0, split_planes(x0, self.feat_ld, silu=True)
+            out, outs = x0, split_planes(x0, self.feat_ld, silu=True, f16=self.f16)
         else:
             out, outs = self._rcu(units[1], x1, x1s, extra=x0, want_f32=True, next_ld=self.feat_ld)
         _, y = self._rcu(units[2], out, outs, next_silu=False, next_ld=out_conv.cin_pad)
         y32, _ = out_conv(y, out_f32=True)
         if last:
-            return upsample(y32, *size, out_f32=False, planes_ld=self.out1.cin_pad)[1]
+            return upsample(y32, *size, out_f32=False, planes_ld=self.out1.cin_pad, f16=self.f16)[1]
         return upsample(y32, *size)[0]
 
     @torch.no_grad()
@@ -188,7 +227,7 @@ class DPTHead:
                  log_decode: bool, channels_last: bool) -> torch.Tensor:
         layers = []
         for i, t in enumerate(taps):
-            x = split_planes(t.view(n_img, hp, wp, t.shape[-1]), self.projects[i].cin_pad)
+            x = split_planes(t.view(n_img, hp, wp, t.shape[-1]), self.projects[i].cin_pad, f16=self.f16)
             nxt = self.resize[i] if i in self.resize else self.rn[i]
             _, x = self.projects[i](x, planes_ld=nxt.cin_pad)
             if i in self.resize:

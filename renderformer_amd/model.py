@@ -25,6 +25,7 @@ import torch
 from . import ops
 from ._lib import load as _load_lib
 from .config import RenderFormerConfig, named_config
+from .dpt import PRECISIONS as DPT_PRECISIONS
 from .dpt import DPTHead
 from .weights import check_state_dict, load_snapshot, synthetic_state_dict
 
@@ -53,7 +54,7 @@ class _Layer:
 class _DeviceWeights:
     """Weights packed for the kernels: bf16 GEMM operands, fp32 norms/biases/tokens."""
 
-    def __init__(self, cfg: RenderFormerConfig, sd: Dict[str, torch.Tensor], device):
+    def __init__(self, cfg: RenderFormerConfig, sd: Dict[str, torch.Tensor], device, dpt_precision: str = "f16"):
         d = cfg.latent_dim
         self.tri_token = _f32(sd["tri_token"].reshape(-1), device)
         self.reg_tokens = _f32(sd["reg_tokens"].reshape(cfg.num_register_tokens, d), device)
@@ -107,7 +108,7 @@ class _DeviceWeights:
             L.w2 = _bf16(sd[p + "ffn.w2.weight"], device)
             L.ffn_norm = _f32(sd[p + "ffn_norm.weight"], device)
             self.dec.append(L)
-        self.dpt = DPTHead(sd, vt + "out_dpt", device)
+        self.dpt = DPTHead(sd, vt + "out_dpt", device, precision=dpt_precision)
 
 
 @dataclass
@@ -183,8 +184,12 @@ class RenderFormer:
     """Drop-in for renderformer.models.renderformer.RenderFormer (inference only)."""
 
     def __init__(self, config: RenderFormerConfig, state_dict: Optional[Dict[str, torch.Tensor]] = None,
-                 seed: int = 0):
+                 seed: int = 0, dpt_precision: Optional[str] = None):
         self.config = config
+        # DPT operand precision (dpt.py): "f16" (default) or "bf16x3"; RF_DPT_PRECISION overrides the default
+        self.dpt_precision = dpt_precision or os.environ.get("RF_DPT_PRECISION", "f16")
+        if self.dpt_precision not in DPT_PRECISIONS:
+            raise ValueError(f"dpt_precision must be one of {DPT_PRECISIONS}")
         cfg = config
         if cfg.latent_dim // cfg.num_heads != 128 or cfg.vt_head_dim != 128:
             raise ValueError("head_dim must be 128 (triangle RoPE constraint, rope.py:91-92)")
@@ -199,21 +204,22 @@ class RenderFormer:
 
     # ------------------------------------------------------------------ module-like API
     @classmethod
-    def from_pretrained(cls, model_id: str, synthetic_seed: Optional[int] = None, **_):
+    def from_pretrained(cls, model_id: str, synthetic_seed: Optional[int] = None, dpt_precision: Optional[str] = None,
+                        **_):
         """Local snapshot dir (config.json + model.safetensors) or, with synthetic_seed, a named config
         with deterministic random weights.  Remote hub downloads are not supported (no network)."""
         if os.path.isdir(model_id):
-            return cls(named_config(model_id), load_snapshot(model_id))
+            return cls(named_config(model_id), load_snapshot(model_id), dpt_precision=dpt_precision)
         if synthetic_seed is None:
             raise FileNotFoundError(f"{model_id!r} is not a local snapshot directory; pass synthetic_seed= for "
                                     "random-init weights of the named architecture")
-        return cls(named_config(model_id), seed=synthetic_seed)
+        return cls(named_config(model_id), seed=synthetic_seed, dpt_precision=dpt_precision)
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
         check_state_dict(self.config, sd, strict=strict)
         self._sd = {k: v.detach().float().cpu() for k, v in sd.items()}
         if self._w is not None:
-            self._w = _DeviceWeights(self.config, self._sd, self._device)
+            self._w = _DeviceWeights(self.config, self._sd, self._device, self.dpt_precision)
         return self
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
@@ -230,7 +236,7 @@ class RenderFormer:
         if device.index is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self._device = device
-        self._w = _DeviceWeights(self.config, self._sd, device)
+        self._w = _DeviceWeights(self.config, self._sd, device, self.dpt_precision)
         return self
 
     cuda = lambda self, i=None: self.to("cuda" if i is None else f"cuda:{i}")  # noqa: E731

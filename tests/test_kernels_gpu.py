@@ -347,68 +347,100 @@ def test_hdr_output():
     assert torch.allclose(out, ref, rtol=1e-6, atol=1e-6)
 
 
-# ----------------------------------------------------------------------------- DPT convolutions (bf16x3)
+# ----------------------------------------------------------------------------- DPT convolutions
+# bf16x3 is checked against fp64 at fp32-level accuracy; f16 against fp64 convolutions of the
+# fp16-ROUNDED operands (what one fp16 MFMA with fp32 accumulation computes exactly, up to the sum order).
+PRECS = ["bf16x3", "f16"]
+
+
+def _q(t, prec):
+    """fp64 copy of an operand as the kernel sees it."""
+    return t.double() if prec == "bf16x3" else t.half().double()
+
+
+def _planes_value(pl):
+    return pl.hi.float() if pl.f16 else pl.hi.float() + pl.lo.float()
+
+
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("cin,cout,k,stride,hw", [(64, 128, 3, 1, 17), (256, 256, 3, 1, 32), (16, 32, 3, 1, 20),
                                                    (1024, 128, 1, 1, 16), (128, 128, 3, 2, 16), (48, 200, 3, 1, 9)])
-def test_conv_bf16x3_matches_fp64(cin, cout, k, stride, hw):
+def test_conv_matches_fp64(cin, cout, k, stride, hw, prec):
     from renderformer_amd.dpt import _Conv, split_planes
+    f16 = prec == "f16"
     g = torch.Generator(device="cpu").manual_seed(cin + cout)
     w = torch.randn(cout, cin, k, k, generator=g) / math.sqrt(cin * k * k)
     b = torch.randn(cout, generator=g)
     x = torch.randn(2, cin, hw, hw, generator=g)
-    conv = _Conv(w, b, dev)
+    conv = _Conv(w, b, dev, f16=f16)
     xn = x.permute(0, 2, 3, 1).contiguous().to(dev)
     pad = k // 2
-    ref = F.conv2d(x.double(), w.double(), b.double(), stride=stride, padding=pad).permute(0, 2, 3, 1)
-    out, _ = conv(split_planes(xn, conv.cin_pad), stride=stride, pad=pad, out_f32=True)
+    ref = F.conv2d(_q(x, prec), _q(w, prec), b.double(), stride=stride, padding=pad).permute(0, 2, 3, 1)
+    out, _ = conv(split_planes(xn, conv.cin_pad, f16=f16), stride=stride, pad=pad, out_f32=True)
     assert relerr(out.cpu(), ref) < 2e-5
+    if f16:  # and the fp16 rounding itself stays small against the exact fp64 convolution
+        exact = F.conv2d(x.double(), w.double(), b.double(), stride=stride, padding=pad).permute(0, 2, 3, 1)
+        assert relerr(out.cpu(), exact) < 1e-3
     if stride == 1 and k == 3 and cin == cout:
         r1 = torch.randn(ref.shape, generator=g)
         r2 = torch.randn(ref.shape, generator=g)
-        out, pl = conv(split_planes(xn, conv.cin_pad, silu=True), res1=r1.to(dev), res2=r2.to(dev), out_f32=True,
-                       planes_ld=cout + 32, planes_silu=True)
-        ref2 = F.conv2d(F.silu(x.double()), w.double(), b.double(), padding=pad).permute(0, 2, 3, 1) + r1 + r2
+        out, pl = conv(split_planes(xn, conv.cin_pad, silu=True, f16=f16), res1=r1.to(dev), res2=r2.to(dev),
+                       out_f32=True, planes_ld=cout + 32, planes_silu=True)
+        sx = _q(F.silu(x.double()).float(), prec)
+        ref2 = F.conv2d(sx, _q(w, prec), b.double(), padding=pad).permute(0, 2, 3, 1) + r1 + r2
         assert relerr(out.cpu(), ref2) < 2e-5
-        both = pl.hi.float() + pl.lo.float()
-        assert relerr(both[..., :cout].cpu(), F.silu(ref2)) < 2e-5
-        assert (pl.hi[..., cout:] == 0).all() and (pl.lo[..., cout:] == 0).all()
+        assert relerr(_planes_value(pl)[..., :cout].cpu(), F.silu(ref2)) < (1e-3 if f16 else 2e-5)
+        assert (pl.hi[..., cout:] == 0).all() and (f16 or (pl.lo[..., cout:] == 0).all())
 
 
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("cin,cout,k", [(128, 128, 4), (256, 256, 2), (16, 16, 4), (32, 32, 2)])
-def test_deconv_bf16x3(cin, cout, k):
+def test_deconv(cin, cout, k, prec):
     from renderformer_amd.dpt import _Conv, split_planes
+    f16 = prec == "f16"
     g = torch.Generator(device="cpu").manual_seed(k * cin)
     w = torch.randn(cin, cout, k, k, generator=g) / math.sqrt(cin)
     b = torch.randn(cout, generator=g)
     x = torch.randn(2, cin, 8, 8, generator=g)
-    conv = _Conv(w, b, dev, deconv=True)
-    out, _ = conv(split_planes(x.permute(0, 2, 3, 1).contiguous().to(dev), conv.cin_pad), out_f32=True)
-    ref = F.conv_transpose2d(x.double(), w.double(), b.double(), stride=k).permute(0, 2, 3, 1)
+    conv = _Conv(w, b, dev, deconv=True, f16=f16)
+    xs = split_planes(x.permute(0, 2, 3, 1).contiguous().to(dev), conv.cin_pad, f16=f16)
+    out, _ = conv(xs, out_f32=True)
+    ref = F.conv_transpose2d(_q(x, prec), _q(w, prec), b.double(), stride=k).permute(0, 2, 3, 1)
     assert relerr(out.cpu(), ref) < 2e-5
+    out2, pl = conv(xs, planes_ld=cout)  # plane output only
+    assert out2 is None and relerr(_planes_value(pl).cpu(), ref) < (1e-3 if f16 else 2e-5)
 
 
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("hi,ho", [(8, 16), (16, 32), (32, 64), (7, 13)])
-def test_upsample_bilinear_align_corners(hi, ho):
+def test_upsample_bilinear_align_corners(hi, ho, prec):
     from renderformer_amd.dpt import upsample
+    f16 = prec == "f16"
     x = torch.randn(2, 12, hi, hi)
-    out, pl = upsample(x.permute(0, 2, 3, 1).contiguous().to(dev), ho, ho, planes_ld=32)
+    out, pl = upsample(x.permute(0, 2, 3, 1).contiguous().to(dev), ho, ho, planes_ld=32, f16=f16)
     ref = F.interpolate(x, size=(ho, ho), mode="bilinear", align_corners=True).permute(0, 2, 3, 1)
     assert torch.allclose(out.cpu(), ref, atol=1e-5, rtol=1e-5)
-    assert torch.allclose((pl.hi.float() + pl.lo.float())[..., :12].cpu(), ref, atol=1e-5, rtol=1e-5)
+    if f16:
+        assert torch.equal(pl.hi[..., :12].cpu(), out.cpu().half())  # RNE fp16 of the fp32 value
+        assert (pl.hi[..., 12:] == 0).all()
+    else:
+        assert torch.allclose(_planes_value(pl)[..., :12].cpu(), ref, atol=1e-5, rtol=1e-5)
 
 
-def test_conv_final_head():
+@pytest.mark.parametrize("prec", PRECS)
+def test_conv_final_head(prec):
     from renderformer_amd.dpt import LOG_DECODE, NCHW_OUT, _Conv, split_planes
+    f16 = prec == "f16"
     g = torch.Generator(device="cpu").manual_seed(9)
     w = torch.randn(32, 64, 3, 3, generator=g) / 24
     b = torch.randn(32, generator=g) * 0.1
     wf = torch.randn(3, 32, 1, 1, generator=g) / 6
     bf = torch.randn(3, generator=g) * 0.1
     x = torch.randn(2, 64, 24, 24, generator=g)
-    conv = _Conv(w, b, dev)
-    y = F.conv2d(F.silu(F.conv2d(x.double(), w.double(), b.double(), padding=1)), wf.double(), bf.double())
+    conv = _Conv(w, b, dev, f16=f16)
+    y = F.conv2d(F.silu(F.conv2d(_q(x, prec), _q(w, prec), b.double(), padding=1)), wf.double(), bf.double())
     y = F.elu(y, 1e-3)
-    xs = split_planes(x.permute(0, 2, 3, 1).contiguous().to(dev), conv.cin_pad)
+    xs = split_planes(x.permute(0, 2, 3, 1).contiguous().to(dev), conv.cin_pad, f16=f16)
     fin = (wf.reshape(3, 32).to(dev), bf.to(dev), 1e-3)
     out = conv(xs, final=fin, final_flags=LOG_DECODE)
     assert relerr(out.cpu(), (10 ** y - 1).permute(0, 2, 3, 1)) < 2e-5
@@ -416,8 +448,20 @@ def test_conv_final_head():
     assert relerr(out2.cpu(), y) < 2e-5
 
 
+def test_split_planes_f16_rounding():
+    from renderformer_amd.dpt import split_planes
+    x = torch.randn(3, 5, 7, 20) * 100
+    x[0, 0, 0, :4] = torch.tensor([7e4, -7e4, 1e-8, 65504.0])  # overflow -> inf, underflow -> 0, max exact
+    pl = split_planes(x.to(dev), 24, f16=True)
+    assert pl.hi.dtype == torch.float16 and pl.lo is None
+    assert torch.equal(pl.hi[..., :20].cpu(), x.half())
+    pl = split_planes(x.to(dev), 24, silu=True, f16=True)
+    assert torch.allclose(pl.hi[..., :20].cpu().float(), F.silu(x).half().float(), rtol=1e-3, atol=1e-6)
+
+
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("final", [False, True])
-def test_conv_stream_k_matches_data_parallel(monkeypatch, final):
+def test_conv_stream_k_matches_data_parallel(monkeypatch, final, prec):
     """Few output tiles (the DPT's 32x32 / 64x64 levels): the stream-K split (8 blocks per tile here) must
     agree with the one-block-per-tile launch and with fp64, including residuals, planes and the fused head."""
     from renderformer_amd.dpt import LOG_DECODE, _Conv, split_planes
@@ -426,8 +470,9 @@ def test_conv_stream_k_matches_data_parallel(monkeypatch, final):
     w = torch.randn(cout if not final else 32, cin, 3, 3, generator=g) / math.sqrt(cin * 9)
     b = torch.randn(w.shape[0], generator=g)
     x = torch.randn(2, cin, 32, 32, generator=g)
-    conv = _Conv(w, b, dev)
-    xs = split_planes(x.permute(0, 2, 3, 1).contiguous().to(dev), conv.cin_pad, silu=True)
+    f16 = prec == "f16"
+    conv = _Conv(w, b, dev, f16=f16)
+    xs = split_planes(x.permute(0, 2, 3, 1).contiguous().to(dev), conv.cin_pad, silu=True, f16=f16)
     outs = []
     fin = (torch.randn(3, 32, generator=g).to(dev) / 6, torch.zeros(3, device=dev), 1e-3)
     for sk in ("1", "0"):
@@ -440,6 +485,8 @@ def test_conv_stream_k_matches_data_parallel(monkeypatch, final):
     (a, pa), (bb, pb) = outs
     assert relerr(a, bb) < 1e-6
     if not final:
-        ref = F.conv2d(F.silu(x.double()), w.double(), b.double(), padding=1).permute(0, 2, 3, 1) + 1.0
+        sx = _q(F.silu(x.double()).float(), prec)
+        ref = F.conv2d(sx, _q(w, prec), b.double(), padding=1).permute(0, 2, 3, 1) + 1.0
         assert relerr(a.cpu(), ref) < 2e-5
-        assert relerr(pa.hi.float() + pa.lo.float(), pb.hi.float() + pb.lo.float()) < 1e-6
+        # fp16 planes: a last-bit fp32 difference from the other K split can flip one fp16 rounding
+        assert relerr(_planes_value(pa), _planes_value(pb)) < (1e-4 if f16 else 1e-6)

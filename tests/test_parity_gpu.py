@@ -14,22 +14,22 @@ pytestmark = pytest.mark.gpu
 HDR_TOL = 1e-3
 
 
-def _pipeline(cfg, sd):
+def _pipeline(cfg, sd, dpt_precision=None):
     from renderformer_amd import RenderFormer, RenderFormerRenderingPipeline
-    return RenderFormerRenderingPipeline(RenderFormer(cfg, sd)).to("cuda")
+    return RenderFormerRenderingPipeline(RenderFormer(cfg, sd, dpt_precision=dpt_precision)).to("cuda")
 
 
-@pytest.mark.parametrize("name", CASES)
-def test_pipeline_matches_reference(name):
+@pytest.mark.parametrize("name,dpt", [(c, "f16") for c in CASES] + [("tiny_large", "bf16x3"), ("cbox_base", "bf16x3")])
+def test_pipeline_matches_reference(name, dpt):
     cfg, sd, inp, res, z = load_case(name)
-    pipe = _pipeline(cfg, sd)
+    pipe = _pipeline(cfg, sd, dpt)
     d = {k: v.cuda() for k, v in inp.items()}
     tex = d["texture"]
     out = pipe(d["triangles"], tex, d["mask"], d["vn"], d["c2w"], d["fov"], resolution=res,
                torch_dtype=torch.bfloat16)
     assert tuple(out.shape) == z["hdr"].shape and out.dtype == torch.float32
     err = rel_l2(out.cpu(), z["hdr"])
-    print(f"{name}: rel L2 {err:.3e}")
+    print(f"{name} (DPT {dpt}): rel L2 {err:.3e}")
     assert err < HDR_TOL
     # in-place log encoding side effect (rendering_pipeline.py:67-68)
     assert torch.allclose(tex[:, :, 10, 0, 0].cpu(), torch.from_numpy(z["texture_after_ch10"]), rtol=1e-6, atol=1e-6)

@@ -88,8 +88,12 @@ def gemm():
             c = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
         else:
             c = torch.zeros(m, n, device=dev)
-        for label, tile, sk, gm in (("dp128", "128", None, "0"), ("dp256", "256", None, "0"),
-                                    ("sk256", None, None, "1"), ("auto", None, None, None)):
+        variants = [("dp128", "128", None, "0"), ("dp128s4", "1284", None, "0"), ("dp128s5", "1285", None, "0"),
+                    ("dp256x128", "2561", None, "0"), ("dp256", "256", None, "0"), ("sk128x512", "128", "512", "0"),
+                    ("sk128x768", "128", "768", "0"), ("sk256", None, None, "1"), ("auto", None, None, None)]
+        if os.environ.get("KB_VARIANTS"):
+            variants = [v for v in variants if v[0] in os.environ["KB_VARIANTS"].split(",")]
+        for label, tile, sk, gm in variants:
             for key, val in (("RF_GEMM_TILE", tile), ("RF_GEMM_SK", sk), ("RF_GEMM_SK256", gm)):
                 if val is None:
                     os.environ.pop(key, None)
@@ -110,16 +114,18 @@ def gemm():
 
 def conv():
     from renderformer_amd.dpt import _Conv, split_planes
-    for cin, cout, hw in [(256, 256, 256), (256, 128, 512), (256, 256, 128), (128, 256, 256)]:
-        conv = _Conv(torch.randn(cout, cin, 3, 3) / 48, torch.randn(cout), dev)
-        x = split_planes(torch.randn(1, hw, hw, cin, device=dev), conv.cin_pad)
-        fl = 2 * hw * hw * cin * cout * 9
-        for small in (True, False):
-            os.environ["RF_CONV_TILE"] = "128" if small else "256"
-            ms = timeit(lambda: conv(x, out_f32=True), reps=10)
-            os.environ.pop("RF_CONV_TILE", None)
-            print(f"conv3x3 {cin}->{cout} @{hw} {'128x128' if small else '256x128'}: {ms*1e3:8.1f} us  "
-                  f"{fl/ms/1e9:7.1f} TF(fp32-equiv)  {3*fl/ms/1e9:7.1f} TF(bf16 MFMA)")
+    for f16 in (True, False):
+        for cin, cout, hw in [(256, 256, 256), (256, 128, 512), (256, 256, 128), (128, 256, 256), (128, 32, 512)]:
+            conv = _Conv(torch.randn(cout, cin, 3, 3) / 48, torch.randn(cout), dev, f16=f16)
+            x = split_planes(torch.randn(1, hw, hw, cin, device=dev), conv.cin_pad, f16=f16)
+            fl = 2 * hw * hw * cin * cout * 9
+            mf = 1 if f16 else 3
+            for small in (True, False):
+                os.environ["RF_CONV_TILE"] = "128" if small else "256"
+                ms = timeit(lambda: conv(x, out_f32=True), reps=10)
+                os.environ.pop("RF_CONV_TILE", None)
+                print(f"conv3x3 {'f16 ' if f16 else 'bf16x3'} {cin}->{cout} @{hw} {'128x128' if small else '256x128'}: "
+                      f"{ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF(algorithmic)  {mf*fl/ms/1e9:7.1f} TF(MFMA issued)")
 
 
 if __name__ == "__main__":
