@@ -170,7 +170,8 @@ int rf_deconv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, 
 /* fp16-operand variants: one fp16 input plane (channel stride cin_pad), fp16 weights [cout_pad][kh][kw][cin_pad],
  * one MFMA per product with fp32 accumulation (11-bit operand mantissa: 9e-5 relative L2 on the large-proxy
  * DPT against 7e-4 for bf16 operands).  Same epilogue as above; the output plane p_out (may be NULL) is one
- * fp16 plane.  Values beyond fp16 range (|x| > 65504) become inf in the planes. */
+ * fp16 plane.  Values beyond fp16 range (|x| > 65504) become inf in the planes.  cout_pad: 64 (cout <= 64)
+ * or a multiple of 128. */
 int rf_conv2d_f16(const void* in, int n_img, int hi, int wi, int cin_pad, const void* w, int cout, int cout_pad, int kh,
                   int kw, int stride, int pad, const float* bias, const float* res1, const float* res2, float* out,
                   void* p_out, int p_ld, int flags, const float* w_fin, const float* b_fin, int n_fin, float elu_alpha,

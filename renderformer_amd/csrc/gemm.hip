@@ -104,8 +104,10 @@ RF_DEV void wait_vm() {
     else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else static_assert(N < 0, "unsupported vmcnt");
@@ -328,20 +330,32 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
     } else if constexpr (EPI == E_CONV) {
         if (p.flags & RF_CONV_FINAL) {
             // SiLU -> 1x1 (cout <= NWD channels, all in the wn == 0 waves) -> ELU -> [10^x - 1]
+            f32x4 act[TI][TJ];  // silu(conv + bias), once per element; 0 in padded channels
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int col = cbase + j * 16 + cq + e;
+                    const float b = (p.bias && col < p.cout) ? p.bias[col] : 0.f;
+#pragma unroll
+                    for (int i = 0; i < TI; ++i) act[i][j][e] = col < p.cout ? silu(acc[i][j][e] + b) : 0.f;
+                }
             for (int f = 0; f < p.n_fin; ++f) {
+                float wf[TJ][4];
+#pragma unroll
+                for (int j = 0; j < TJ; ++j)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int col = cbase + j * 16 + cq + e;
+                        wf[j][e] = col < p.cout ? p.w_fin[f * p.cout + col] : 0.f;
+                    }
 #pragma unroll
                 for (int i = 0; i < TI; ++i) {
                     float s = 0.f;
 #pragma unroll
                     for (int j = 0; j < TJ; ++j)
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            const int col = cbase + j * 16 + cq + e;
-                            if (col < p.cout) {
-                                const float v = silu(acc[i][j][e] + (p.bias ? p.bias[col] : 0.f));
-                                s += v * p.w_fin[f * p.cout + col];
-                            }
-                        }
+                        for (int e = 0; e < 4; ++e) s += act[i][j][e] * wf[j][e];
                     s += __shfl_xor(s, 16, 64);
                     s += __shfl_xor(s, 32, 64);
                     const int m = rbase + i * 16 + rl;
@@ -476,6 +490,229 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// 256x256 tile, BK = 64, 8 waves (2 x 4, each 128 x 64): the phased main loop.
+//
+// One K-tile = 4 phases; a phase = {ds_read this phase's fragments, issue LDS-DMA of the next
+// tiles' freed regions, [counted vmcnt], barrier, lgkmcnt(0), 16 MFMAs at raised priority,
+// barrier}.  The wave's 128x64 output is walked in quadrants q0 = (m0, n0), q1 = (m0, n1),
+// q2 = (m1, n1), q3 = (m1, n0) (m = 64 rows, n = 32 columns), so the A/B fragments a phase
+// needs are read once: q0 reads A(m0) + B(n0), q1 B(n1), q2 A(m1), q3 nothing (B(n0) kept).
+// LDS holds two K-tiles, each as four 16-KiB regions: RA0 = A rows {0-63, 128-191} (every wave's
+// m0 rows), RA1 = the m1 rows, RB0 = B rows {64 wc + 0..31}, RB1 = {64 wc + 32..63}.  A region
+// is re-filled with tile t+2 one phase after its last read of tile t (RA0/RB0 in phase 1, RB1
+// in phase 2, RA1 in phase 3), so every DMA has a whole K-tile of MFMA work to land under, and
+// one counted vmcnt per K-tile (end of phase 3: all of tile t+1 landed, tile t+2's 8 in flight)
+// publishes the next tile.  Image: [k-half][row][64 B], 16-B chunk ^ ((row >> 1) & 3) as in the
+// engine above; one 1-KiB LDS-DMA piece = 16 rows x 32 k.
+namespace ph {
+constexpr int BM = 256, BN = 256, BK2 = 64;
+constexpr int REGION = 16384;            // 128 rows x 64 k x 2 B
+constexpr int TILE = 4 * REGION;         // RA0 RA1 RB0 RB1
+constexpr int LDS = 2 * TILE;            // 128 KiB
+enum { RA0 = 0, RA1 = 1, RB0 = 2, RB1 = 3 };
+
+// tile row of region row j (0..127)
+RF_DEV int region_row(int r, int j) {
+    switch (r) {
+        case RA0: return j < 64 ? j : j + 64;
+        case RA1: return j < 64 ? j + 64 : j + 128;
+        case RB0: return (j >> 5) * 64 + (j & 31);
+        default: return (j >> 5) * 64 + 32 + (j & 31);
+    }
+}
+// LDS byte offset of (tile row, k-half, 16-B chunk) inside one operand's half of a K-tile buffer:
+// operand image = [k-half][256 rows][64 B] = 32 KiB
+RF_DEV int img(int row, int kh, int ch) { return kh * 16384 + row * 64 + ((ch ^ ((row >> 1) & 3)) << 4); }
+}  // namespace ph
+
+template <int NTERM, bool GATHER>
+RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, f32x4 (&acc)[8][4]) {
+    using namespace ph;
+    static_assert(NTERM == 1 || NTERM == P_F16, "phased loop: single-term operands");
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int nk = p.k / BK2;
+
+    // ---- DMA geometry: wave w fills region rows 16 w .. 16 w + 15 (both k-halves) of each region
+    const int jrow = 16 * wave + (lane >> 2);
+    int trow[4], grow[4];  // this lane's tile row; first tile row of the wave's 16-row piece (wave-uniform)
+    const bf16_t* src[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        trow[r] = region_row(r, jrow);
+        grow[r] = region_row(r, 16 * wave);
+    }
+    // A rows of regions RA0 / RA1 (gathered for convolutions), W rows of RB0 / RB1
+    int am[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        int m = m0 + trow[r];
+        am[r] = m < p.m ? m : p.m - 1;
+        src[r] = p.a + (int64_t)am[r] * p.lda;
+    }
+    int gi[2], gy[2], gx[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        gi[r] = gy[r] = gx[r] = 0;
+        if constexpr (GATHER) {
+            const int m = m0 + trow[r];
+            const int ox = am[r] % p.wo, t = am[r] / p.wo;
+            gi[r] = m < p.m ? t / p.ho : -1;
+            gy[r] = (t % p.ho) * p.stride - p.pad;
+            gx[r] = ox * p.stride - p.pad;
+        }
+    }
+#pragma unroll
+    for (int r = 2; r < 4; ++r) src[r] = p.w + (int64_t)(n0 + trow[r]) * p.ldw;
+    const int lch = lane & 3;
+
+    // issue region r of K-tile kt into buffer kt & 1 (2 LDS-DMA per lane: the two 32-deep k-halves)
+    auto issue = [&](int kt, int r) {
+        char* base = smem + (kt & 1) * TILE + (r >= 2 ? 2 * REGION : 0);
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+            const int row = trow[r];
+            const int ch = lch ^ ((row >> 1) & 3);  // logical chunk that lands at physical chunk lch
+            const int k0 = kt * BK2 + kh * 32;
+            const bf16_t* g;
+            if constexpr (GATHER) {
+                if (r < 2) {
+                    const int tap = k0 / p.cin_pad, cb = k0 - tap * p.cin_pad;
+                    const int ky = tap / p.kw, kx = tap - ky * p.kw;
+                    const int iy = gy[r] + ky, ix = gx[r] + kx;
+                    const bool ok = gi[r] >= 0 && iy >= 0 && iy < p.hi && ix >= 0 && ix < p.wi;
+                    g = ok ? p.a + (((int64_t)gi[r] * p.hi + iy) * p.wi + ix) * p.cin_pad + cb + ch * 8 : p.zero;
+                } else {
+                    g = src[r] + k0 + ch * 8;
+                }
+            } else {
+                g = src[r] + k0 + ch * 8;
+            }
+            // piece: 16 region rows x 32 k; its 16 tile rows are contiguous (region_row keeps runs of 16)
+            char* dst = base + kh * 16384 + grow[r] * 64;
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, g), LDS_PTR(void, dst), 16, 0, 0);
+        }
+    };
+    auto issue_tile = [&](int kt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) issue(kt, r);
+    };
+
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int frow = lane & 15, fch = lane >> 4;  // fragment lane geometry (16x16x32: 16 rows x 4 chunks)
+    bf16x8 fa[4][2], fb0[2][2], fb1[2][2];        // A(m) 4 frags x 2 k-slices; B(n0), B(n1) 2 frags x 2 k-slices
+    auto read_a = [&](const char* buf, int mi) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+                fa[i][s] = *reinterpret_cast<const bf16x8*>(buf + img(wr * 128 + mi * 64 + i * 16 + frow, s, fch));
+    };
+    auto read_b = [&](const char* buf, int ni, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+                fb[j][s] = *reinterpret_cast<const bf16x8*>(buf + 2 * REGION +
+                                                            img(wc * 64 + ni * 32 + j * 16 + frow, s, fch));
+    };
+    auto mma = [&](int mi, int ni, const bf16x8 (&fb)[2][2]) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    f32x4& c = acc[mi * 4 + i][ni * 2 + j];
+                    if constexpr (NTERM == P_F16)
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[j][s]),
+                                                                   __builtin_bit_cast(f16x8, fa[i][s]), c, 0, 0, 0);
+                    else
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], c, 0, 0, 0);
+                }
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto sync_in = [&]() {
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this phase's fragments are in registers
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto sync_out = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // prologue: tiles 0 and 1 in flight, wait for tile 0
+    issue_tile(0);
+    if (nk > 1) {
+        issue_tile(1);
+        wait_vm<8>();
+    } else {
+        wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+
+    for (int t = 0; t < nk; ++t) {
+        const char* buf = smem + (t & 1) * TILE;
+        const bool pf = t + 2 < nk;
+        // phase 0: q0 = (m0, n0)
+        read_b(buf, 0, fb0);
+        read_a(buf, 0);
+        sync_in();
+        mma(0, 0, fb0);
+        sync_out();
+        // phase 1: q1 = (m0, n1); RA0 / RB0 of tile t were last read in phase 0
+        read_b(buf, 1, fb1);
+        if (pf) {
+            issue(t + 2, RA0);
+            issue(t + 2, RB0);
+        }
+        sync_in();
+        mma(0, 1, fb1);
+        sync_out();
+        // phase 2: q2 = (m1, n1); RB1 free
+        read_a(buf, 1);
+        if (pf) issue(t + 2, RB1);
+        sync_in();
+        mma(1, 1, fb1);
+        sync_out();
+        // phase 3: q3 = (m1, n0), no reads; RA1 free; publish tile t+1
+        if (pf) {
+            issue(t + 2, RA1);
+            wait_vm<8>();
+        } else {
+            wait_vm<0>();
+        }
+        sync_in();
+        mma(1, 0, fb0);
+        sync_out();
+    }
+}
+
+template <int EPI, int NTERM, bool GATHER>
+__global__ __launch_bounds__(512, 1) void phased_kernel(EngineArgs p) {
+    __shared__ __attribute__((aligned(16))) char smem[ph::LDS];
+    const int tiles_m = (p.m + ph::BM - 1) / ph::BM;
+    const int nwg = gridDim.x;
+    const int hw = blockIdx.x;
+    const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
+    int tm, tn;
+    tile_coords(wg, tiles_m, p.n / ph::BN, p.group_m, tm, tn);
+    f32x4 acc[8][4];
+    phased_mainloop<NTERM, GATHER>(p, smem, tm * ph::BM, tn * ph::BN, acc);
+    engine_epilogue<Tile<256, 256, 2, 4, 4>, EPI>(p, tm * ph::BM, tn * ph::BN, acc);
+}
+
 // Data-parallel (one output tile per block) or stream-K (SK): the grid's blocks split the
 // tiles x K-steps iteration space evenly; a block that starts inside a tile stores its partial
 // sum and raises its flag, the block that holds the tile's first K-step (it reaches that tile
@@ -569,6 +806,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
 using T128 = Tile<128, 128, 2, 2, 3>;
 using T256 = Tile<256, 256, 2, 4, 4>;
 using T256x128 = Tile<256, 128, 4, 2, 3>;
+using T256x64 = Tile<256, 64, 4, 1, 4>;  // fp16 convolutions with <= 64 output channels (DPT output_conv2)
 
 int pick_group_m(int tiles_m, int tiles_n, int bm, int bn, int64_t per_xcd) {
     if (const char* env = getenv("RF_GEMM_GROUP_M")) return std::max(1, std::min(tiles_m, atoi(env)));
@@ -644,6 +882,21 @@ __device__ __attribute__((aligned(16))) bf16_t g_zero_row[64];  // stays zero: s
 
 }  // namespace
 
+template <int EPI, int NTERM, bool GATHER>
+int launch_phased(EngineArgs a, void* stream, const char* what) {
+    const int tiles_m = (a.m + 255) / 256, tiles_n = a.n / 256;
+    const int nwg = tiles_n * tiles_m;
+    a.group_m = pick_group_m(tiles_m, tiles_n, 256, 256, (nwg + 7) / 8);
+    hipLaunchKernelGGL((phased_kernel<EPI, NTERM, GATHER>), dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    return rf::check_launch(what);
+}
+
+// the phased 256x256 loop replaces the ring engine's 256x256 tile (RF_GEMM_PHASED=0 restores it)
+bool use_phased(int n, int k) {
+    const char* env = getenv("RF_GEMM_PHASED");
+    return (!env || atoi(env) != 0) && n % 256 == 0 && k % 64 == 0;
+}
+
 template <class C>
 int run_dp_cfg(const EngineArgs& p, int epilogue, void* stream) {
     switch (epilogue) {
@@ -657,6 +910,14 @@ int run_dp_cfg(const EngineArgs& p, int epilogue, void* stream) {
 // cfg codes: 128 = T128, 256 = T256 (needs N % 256 == 0), 1284 / 1285 = 128x128 with a 4 / 5-stage ring,
 // 2561 = 256x128 (8 waves)
 int run_dp(int cfg, const EngineArgs& p, int epilogue, void* stream) {
+    if (cfg == 256 && use_phased(p.n, p.k)) {
+        switch (epilogue) {
+            case RF_EPI_BF16: return launch_phased<E_BF16, 1, false>(p, stream, "rf_gemm_bf16");
+            case RF_EPI_F32: return launch_phased<E_F32, 1, false>(p, stream, "rf_gemm_bf16");
+            case RF_EPI_ADD_F32: return launch_phased<E_ADD, 1, false>(p, stream, "rf_gemm_bf16");
+            default: return launch_phased<E_SWIGLU, 1, false>(p, stream, "rf_gemm_bf16");
+        }
+    }
     if (cfg == 256 && p.n % 256 == 0) return run_dp_cfg<T256>(p, epilogue, stream);
     if (cfg == 1284) return run_dp_cfg<Tile<128, 128, 2, 2, 4>>(p, epilogue, stream);
     if (cfg == 1285) return run_dp_cfg<Tile<128, 128, 2, 2, 5>>(p, epilogue, stream);
@@ -719,9 +980,28 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
     return run_dp(pick_cfg(m, n), p, epilogue, stream);
 }
 
+// fp16 convolutions (one MFMA per product): the 256x256 tile when the filter bank is a multiple of 256
+// wide and there is >= one tile per CU (the im2col gather of A is then read once per pixel tile),
+// 256x64 for <= 64 output channels, else 128x128 (faster than 256x128 on every DPT shape measured)
+template <bool GATHER>
+static int conv_f16_dp(EngineArgs& p, void* stream, const char* what) {
+    const char* env = getenv("RF_CONV_TILE");
+    const int t = env ? atoi(env) : 0;
+    if (p.n == 64) return launch<T256x64, E_CONV, P_F16, GATHER>(p, stream, what);
+    if (t == 128) return launch<T128, E_CONV, P_F16, GATHER>(p, stream, what);
+    if (p.n % 256 == 0 && (t == 256 || (!t && ((p.m + 255) / 256) * (p.n / 256) >= 256)))
+        return use_phased(p.n, p.k) ? launch_phased<E_CONV, P_F16, GATHER>(p, stream, what)
+                                    : launch<T256, E_CONV, P_F16, GATHER>(p, stream, what);
+    if (t == 2561) return launch<T256x128, E_CONV, P_F16, GATHER>(p, stream, what);
+    return launch<T128, E_CONV, P_F16, GATHER>(p, stream, what);
+}
+
 template <int NT>
 static int conv_dispatch(EngineArgs& p, bool gather, bool big, int64_t sk_grid_n, void* workspace, void* stream,
                          const char* what) {
+    if constexpr (NT == P_F16) {
+        if (!sk_grid_n) return gather ? conv_f16_dp<true>(p, stream, what) : conv_f16_dp<false>(p, stream, what);
+    }
     if (sk_grid_n) {
         sk_setup(p, workspace);
         return gather ? launch_sk<T128, E_CONV, NT, true>(p, (int)sk_grid_n, stream, what)
@@ -776,7 +1056,7 @@ static int conv_common(EngineArgs& p, int nterm, bool gather, const void* w_hi, 
     // keeping >= 8 K-steps.
     const char* sk_env = getenv("RF_CONV_SK");
     int64_t skg = 0;
-    if (!big && workspace && ws_bytes >= SK_WS_BYTES && !(sk_env && atoi(sk_env) == 0)) {
+    if (!big && p.n % 128 == 0 && workspace && ws_bytes >= SK_WS_BYTES && !(sk_env && atoi(sk_env) == 0)) {
         const int64_t tiles = (int64_t)((p.m + 127) / 128) * (p.n / 128);
         const int64_t work = tiles * (p.k / BK);
         const int64_t grid = std::min<int64_t>(256, work / 8);
@@ -820,8 +1100,8 @@ extern "C" int rf_conv2d_f16(const void* in, int n_img, int hi, int wi, int cin_
                              void* stream) {
     RF_REQUIRE(in, "rf_conv2d_f16: null input");
     RF_REQUIRE(cin_pad % BK == 0, "rf_conv2d_f16: cin_pad %d must be a multiple of %d", cin_pad, BK);
-    RF_REQUIRE(cout_pad % 128 == 0 && cout_pad >= cout, "rf_conv2d_f16: cout_pad %d must be a multiple of 128",
-               cout_pad);
+    RF_REQUIRE((cout_pad % 128 == 0 || cout_pad == 64) && cout_pad >= cout,
+               "rf_conv2d_f16: cout_pad %d must be 64 or a multiple of 128", cout_pad);
     EngineArgs p{};
     p.a = (const bf16_t*)in;
     p.hi = hi;

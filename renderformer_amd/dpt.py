@@ -103,7 +103,8 @@ class _Conv:
             cout, cin, kh, kw = w.shape
             self.k, self.kh, self.kw = 0, kh, kw
             self.cin_pad = _pad(cin, BK)
-            self.cout_pad = _pad(cout, BN)
+            # fp16 banks of <= 64 filters (output_conv2) run on the engine's 256x64 tile
+            self.cout_pad = 64 if (f16 and cout <= 64) else _pad(cout, BN)
             mat = torch.zeros(self.cout_pad, kh, kw, self.cin_pad)
             mat[:cout, :, :, :cin] = w.permute(0, 2, 3, 1)
             mat = mat.reshape(self.cout_pad, -1)

@@ -87,6 +87,37 @@ def test_gemm_stream_k(monkeypatch, grid, m, n, k):
     assert relerr(outs.float(), refs) < 5e-3
 
 
+@pytest.mark.parametrize("phased", ["1", "0"])
+@pytest.mark.parametrize("m,n,k", [(1, 256, 64), (300, 512, 128), (777, 256, 192), (5649, 3072, 1024),
+                                   (4096, 1024, 4096), (2000, 768, 320)])
+def test_gemm_256_tiles(monkeypatch, phased, m, n, k):
+    """The 256x256 tile: the phased BK=64 loop (default) and the ring engine, forced on every shape (ragged M,
+    one to three K-tiles, long K), every epilogue, against fp64."""
+    ops = _ops()
+    monkeypatch.setenv("RF_GEMM_TILE", "256")
+    monkeypatch.setenv("RF_GEMM_PHASED", phased)
+    g = torch.Generator(device="cpu").manual_seed(m + 3 * n + k)
+    a = torch.randn(m, k, generator=g).bfloat16().to(dev)
+    w = (torch.randn(n, k, generator=g) / math.sqrt(k)).bfloat16().to(dev)
+    bias = torch.randn(n, generator=g).to(dev)
+    ref = a.double() @ w.double().t() + bias.double()
+    out = torch.empty(m, n, device=dev)
+    ops.gemm(a, w, out, bias, ops.EPI_F32)
+    assert relerr(out, ref) < 1e-5
+    acc = torch.randn(m, n, generator=g).to(dev)
+    ref2 = acc.double() + ref
+    ops.gemm(a, w, acc, bias, ops.EPI_ADD_F32)
+    assert relerr(acc, ref2) < 1e-5
+    outb = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+    ops.gemm(a, w, outb, bias, ops.EPI_BF16)
+    assert relerr(outb.float(), ref) < 4e-3
+    from renderformer_amd.model import _interleave_swiglu
+    outs = torch.empty(m, n // 2, device=dev, dtype=torch.bfloat16)
+    ops.gemm(a, _interleave_swiglu(w[: n // 2].cpu(), w[n // 2:].cpu()).to(dev), outs, None, ops.EPI_SWIGLU)
+    refs = F.silu(a.double() @ w[: n // 2].double().t()) * (a.double() @ w[n // 2:].double().t())
+    assert relerr(outs.float(), refs) < 5e-3
+
+
 def test_gemm_asymmetric_identity():
     """A = I with an asymmetric W catches a transposed C write (guide §3)."""
     ops = _ops()

@@ -89,8 +89,9 @@ def gemm():
         else:
             c = torch.zeros(m, n, device=dev)
         variants = [("dp128", "128", None, "0"), ("dp128s4", "1284", None, "0"), ("dp128s5", "1285", None, "0"),
-                    ("dp256x128", "2561", None, "0"), ("dp256", "256", None, "0"), ("sk128x512", "128", "512", "0"),
-                    ("sk128x768", "128", "768", "0"), ("sk256", None, None, "1"), ("auto", None, None, None)]
+                    ("dp256x128", "2561", None, "0"), ("dp256ring", "256", None, "0"), ("dp256ph", "256", None, "0"),
+                    ("sk128x512", "128", "512", "0"), ("sk128x768", "128", "768", "0"), ("sk256", None, None, "1"),
+                    ("auto", None, None, None)]
         if os.environ.get("KB_VARIANTS"):
             variants = [v for v in variants if v[0] in os.environ["KB_VARIANTS"].split(",")]
         for label, tile, sk, gm in variants:
@@ -99,7 +100,8 @@ def gemm():
                     os.environ.pop(key, None)
                 else:
                     os.environ[key] = val
-            if label in ("dp256", "sk256") and n % 256:
+            os.environ["RF_GEMM_PHASED"] = "0" if label in ("dp256ring", "sk256") else "1"
+            if label in ("dp256ring", "dp256ph", "sk256") and n % 256:
                 continue
             ms = timeit(lambda: ops.gemm(a, w, c, None, epi), reps=10 if k > 8000 else 20)
             print(f"gemm {name:8s} {m}x{n}x{k} {label}: {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF")
@@ -120,11 +122,13 @@ def conv():
             x = split_planes(torch.randn(1, hw, hw, cin, device=dev), conv.cin_pad, f16=f16)
             fl = 2 * hw * hw * cin * cout * 9
             mf = 1 if f16 else 3
-            for small in (True, False):
-                os.environ["RF_CONV_TILE"] = "128" if small else "256"
+            tiles = ("128", "256", "2561", "auto") if f16 else ("128", "256")
+            for t in tiles:
+                if t != "auto":
+                    os.environ["RF_CONV_TILE"] = t
                 ms = timeit(lambda: conv(x, out_f32=True), reps=10)
                 os.environ.pop("RF_CONV_TILE", None)
-                print(f"conv3x3 {'f16 ' if f16 else 'bf16x3'} {cin}->{cout} @{hw} {'128x128' if small else '256x128'}: "
+                print(f"conv3x3 {'f16 ' if f16 else 'bf16x3'} {cin}->{cout} @{hw} tile={t}: "
                       f"{ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF(algorithmic)  {mf*fl/ms/1e9:7.1f} TF(MFMA issued)")
 
 
