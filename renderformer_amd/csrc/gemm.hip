@@ -493,9 +493,12 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
 // ---------------------------------------------------------------------------------------------
 // 256x256 tile, BK = 64, 8 waves (2 x 4, each 128 x 64): the phased main loop.
 //
-// One K-tile = 4 phases; a phase = {ds_read this phase's fragments, issue LDS-DMA of the next
-// tiles' freed regions, [counted vmcnt], barrier, lgkmcnt(0), 16 MFMAs at raised priority,
-// barrier}.  The wave's 128x64 output is walked in quadrants q0 = (m0, n0), q1 = (m0, n1),
+// One K-tile = 4 phases; a phase = a load section {ds_read this phase's fragments, issue LDS-DMA
+// of the next tiles' freed regions, [counted vmcnt], lgkmcnt(0)}, barrier, an MFMA section {16
+// MFMAs at raised priority}, barrier.  Waves 4-7 run one barrier behind waves 0-3 (one extra
+// barrier before the loop, matched by one after it for waves 0-3), so on every SIMD one wave's
+// MFMA section overlaps its partner's load section (ping-pong); every LDS hazard below is closed
+// by a wait placed before a barrier that both groups pass before the dependent access.  The wave's 128x64 output is walked in quadrants q0 = (m0, n0), q1 = (m0, n1),
 // q2 = (m1, n1), q3 = (m1, n0) (m = 64 rows, n = 32 columns), so the A/B fragments a phase
 // needs are read once: q0 reads A(m0) + B(n0), q1 B(n1), q2 A(m1), q3 nothing (B(n0) kept).
 // LDS holds two K-tiles, each as four 16-KiB regions: RA0 = A rows {0-63, 128-191} (every wave's
@@ -506,58 +509,71 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
 // publishes the next tile.  Image: [k-half][row][64 B], 16-B chunk ^ ((row >> 1) & 3) as in the
 // engine above; one 1-KiB LDS-DMA piece = 16 rows x 32 k.
 namespace ph {
-constexpr int BM = 256, BN = 256, BK2 = 64;
-constexpr int REGION = 16384;            // 128 rows x 64 k x 2 B
-constexpr int TILE = 4 * REGION;         // RA0 RA1 RB0 RB1
-constexpr int LDS = 2 * TILE;            // 128 KiB
-enum { RA0 = 0, RA1 = 1, RB0 = 2, RB1 = 3 };
-
-// tile row of region row j (0..127)
+constexpr int BN = 256, BK2 = 64;
+constexpr int REGION = 16384;  // 128 rows x 64 k x 2 B
+// BM = 256: regions RA0, RA1, RB0, RB1; BM = 128 (wave tile 64 x 64): RA, RB0, RB1
+template <int BM>
+struct Cfg {
+    static constexpr int NREG = BM == 256 ? 4 : 3;
+    static constexpr int NA = BM == 256 ? 2 : 1;  // A regions come first
+    static constexpr int A_IMG = BM * 128;        // [2 k-halves][BM rows][64 B]
+    static constexpr int TILE = A_IMG + 256 * 128;
+    static constexpr int LDS = 2 * TILE;
+    static constexpr int MI = BM / 32;  // 16-row M fragments per wave
+    static constexpr int GLDS = 2 * NREG;  // LDS-DMA per lane per K-tile
+};
+// tile row of region row j (0..127); runs of 16 consecutive j map to 16 consecutive rows
+template <int BM>
 RF_DEV int region_row(int r, int j) {
-    switch (r) {
-        case RA0: return j < 64 ? j : j + 64;
-        case RA1: return j < 64 ? j + 64 : j + 128;
-        case RB0: return (j >> 5) * 64 + (j & 31);
-        default: return (j >> 5) * 64 + 32 + (j & 31);
+    if constexpr (BM == 256) {
+        switch (r) {
+            case 0: return j < 64 ? j : j + 64;
+            case 1: return j < 64 ? j + 64 : j + 128;
+            case 2: return (j >> 5) * 64 + (j & 31);
+            default: return (j >> 5) * 64 + 32 + (j & 31);
+        }
+    } else {
+        switch (r) {
+            case 0: return j;
+            case 1: return (j >> 5) * 64 + (j & 31);
+            default: return (j >> 5) * 64 + 32 + (j & 31);
+        }
     }
 }
-// LDS byte offset of (tile row, k-half, 16-B chunk) inside one operand's half of a K-tile buffer:
-// operand image = [k-half][256 rows][64 B] = 32 KiB
-RF_DEV int img(int row, int kh, int ch) { return kh * 16384 + row * 64 + ((ch ^ ((row >> 1) & 3)) << 4); }
+// LDS byte offset of (row, k-half, 16-B chunk) in an operand image [2][rows][64 B]
+template <int ROWS>
+RF_DEV int img(int row, int kh, int ch) { return kh * (ROWS * 64) + row * 64 + ((ch ^ ((row >> 1) & 3)) << 4); }
 }  // namespace ph
 
-template <int NTERM, bool GATHER>
-RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, f32x4 (&acc)[8][4]) {
+template <int BM, int NTERM, bool GATHER>
+RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int kbeg, int kend,
+                            f32x4 (&acc)[BM / 32][4]) {
     using namespace ph;
+    using G = Cfg<BM>;
+    constexpr int NREG = G::NREG, NA = G::NA, MI = G::MI;
     static_assert(NTERM == 1 || NTERM == P_F16, "phased loop: single-term operands");
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int wr = wave >> 2, wc = wave & 3;
-    const int nk = p.k / BK2;
+    const int nk = kend - kbeg;  // K-tiles of this call; local tile t is global K-tile kbeg + t
 
     // ---- DMA geometry: wave w fills region rows 16 w .. 16 w + 15 (both k-halves) of each region
     const int jrow = 16 * wave + (lane >> 2);
-    int trow[4], grow[4];  // this lane's tile row; first tile row of the wave's 16-row piece (wave-uniform)
-    const bf16_t* src[4];
+    int trow[NREG], grow[NREG];  // this lane's tile row; first tile row of the wave's 16-row piece (wave-uniform)
+    const bf16_t* src[NREG];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        trow[r] = region_row(r, jrow);
-        grow[r] = region_row(r, 16 * wave);
+    for (int r = 0; r < NREG; ++r) {
+        trow[r] = region_row<BM>(r, jrow);
+        grow[r] = region_row<BM>(r, 16 * wave);
     }
-    // A rows of regions RA0 / RA1 (gathered for convolutions), W rows of RB0 / RB1
-    int am[2];
+    int am[NA], gi[NA], gy[NA], gx[NA];  // A rows (gathered for convolutions)
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        int m = m0 + trow[r];
+    for (int r = 0; r < NA; ++r) {
+        const int m = m0 + trow[r];
         am[r] = m < p.m ? m : p.m - 1;
         src[r] = p.a + (int64_t)am[r] * p.lda;
-    }
-    int gi[2], gy[2], gx[2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
         gi[r] = gy[r] = gx[r] = 0;
         if constexpr (GATHER) {
-            const int m = m0 + trow[r];
             const int ox = am[r] % p.wo, t = am[r] / p.wo;
             gi[r] = m < p.m ? t / p.ho : -1;
             gy[r] = (t % p.ho) * p.stride - p.pad;
@@ -565,62 +581,53 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, f32
         }
     }
 #pragma unroll
-    for (int r = 2; r < 4; ++r) src[r] = p.w + (int64_t)(n0 + trow[r]) * p.ldw;
+    for (int r = NA; r < NREG; ++r) src[r] = p.w + (int64_t)(n0 + trow[r]) * p.ldw;
     const int lch = lane & 3;
 
     // issue region r of K-tile kt into buffer kt & 1 (2 LDS-DMA per lane: the two 32-deep k-halves)
     auto issue = [&](int kt, int r) {
-        char* base = smem + (kt & 1) * TILE + (r >= 2 ? 2 * REGION : 0);
+        const bool is_a = r < NA;
+        char* base = smem + (kt & 1) * G::TILE + (is_a ? 0 : G::A_IMG);
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) {
             const int row = trow[r];
             const int ch = lch ^ ((row >> 1) & 3);  // logical chunk that lands at physical chunk lch
-            const int k0 = kt * BK2 + kh * 32;
-            const bf16_t* g;
+            const int k0 = (kbeg + kt) * BK2 + kh * 32;
+            const bf16_t* g = src[r] + k0 + ch * 8;
             if constexpr (GATHER) {
-                if (r < 2) {
+                if (is_a) {
                     const int tap = k0 / p.cin_pad, cb = k0 - tap * p.cin_pad;
                     const int ky = tap / p.kw, kx = tap - ky * p.kw;
                     const int iy = gy[r] + ky, ix = gx[r] + kx;
                     const bool ok = gi[r] >= 0 && iy >= 0 && iy < p.hi && ix >= 0 && ix < p.wi;
                     g = ok ? p.a + (((int64_t)gi[r] * p.hi + iy) * p.wi + ix) * p.cin_pad + cb + ch * 8 : p.zero;
-                } else {
-                    g = src[r] + k0 + ch * 8;
                 }
-            } else {
-                g = src[r] + k0 + ch * 8;
             }
-            // piece: 16 region rows x 32 k; its 16 tile rows are contiguous (region_row keeps runs of 16)
-            char* dst = base + kh * 16384 + grow[r] * 64;
+            char* dst = base + kh * (is_a ? BM * 64 : 256 * 64) + grow[r] * 64;
             __builtin_amdgcn_global_load_lds(GLB_PTR(void, g), LDS_PTR(void, dst), 16, 0, 0);
         }
     };
-    auto issue_tile = [&](int kt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) issue(kt, r);
-    };
 
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int frow = lane & 15, fch = lane >> 4;  // fragment lane geometry (16x16x32: 16 rows x 4 chunks)
-    bf16x8 fa[4][2], fb0[2][2], fb1[2][2];        // A(m) 4 frags x 2 k-slices; B(n0), B(n1) 2 frags x 2 k-slices
+    bf16x8 fa[4][2], fb0[2][2], fb1[2][2];        // A: 4 frags (64 rows) x 2 k-slices; B(n0), B(n1): 2 x 2
     auto read_a = [&](const char* buf, int mi) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int s = 0; s < 2; ++s)
-                fa[i][s] = *reinterpret_cast<const bf16x8*>(buf + img(wr * 128 + mi * 64 + i * 16 + frow, s, fch));
+                fa[i][s] = *reinterpret_cast<const bf16x8*>(buf + img<BM>(wr * (BM / 2) + mi * 64 + i * 16 + frow, s, fch));
     };
     auto read_b = [&](const char* buf, int ni, bf16x8 (&fb)[2][2]) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int s = 0; s < 2; ++s)
-                fb[j][s] = *reinterpret_cast<const bf16x8*>(buf + 2 * REGION +
-                                                            img(wc * 64 + ni * 32 + j * 16 + frow, s, fch));
+                fb[j][s] = *reinterpret_cast<const bf16x8*>(buf + G::A_IMG + img<256>(wc * 64 + ni * 32 + j * 16 + frow, s, fch));
     };
     auto mma = [&](int mi, int ni, const bf16x8 (&fb)[2][2]) {
         __builtin_amdgcn_s_setprio(1);
@@ -640,8 +647,9 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, f32
         __builtin_amdgcn_s_setprio(0);
     };
     auto sync_in = [&]() {
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this phase's fragments are in registers (and its
+        __builtin_amdgcn_sched_barrier(0);   // LDS reads retired before the barrier: the WAR side of the DMA)
         __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this phase's fragments are in registers
         __builtin_amdgcn_sched_barrier(0);
     };
     auto sync_out = [&]() {
@@ -650,67 +658,169 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, f32
         __builtin_amdgcn_sched_barrier(0);
     };
 
-    // prologue: tiles 0 and 1 in flight, wait for tile 0
-    issue_tile(0);
+    // prologue: tile 0 and (BM = 256) all of tile 1 / (BM = 128) tile 1 minus RB1 in flight; wait for tile 0
+    constexpr int AHEAD = BM == 256 ? 8 : 4;  // LDS-DMA of tile 1 issued here (and of tile t+2 at a tile's wait)
+#pragma unroll
+    for (int r = 0; r < NREG; ++r) issue(0, r);
     if (nk > 1) {
-        issue_tile(1);
-        wait_vm<8>();
+#pragma unroll
+        for (int r = 0; r < (BM == 256 ? NREG : 2); ++r) issue(1, r);
+        wait_vm<AHEAD>();
     } else {
         wait_vm<0>();
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // waves 4-7: the lagging group
+    if (late) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
 
     for (int t = 0; t < nk; ++t) {
-        const char* buf = smem + (t & 1) * TILE;
+        const char* buf = smem + (t & 1) * G::TILE;
         const bool pf = t + 2 < nk;
-        // phase 0: q0 = (m0, n0)
-        read_b(buf, 0, fb0);
-        read_a(buf, 0);
-        sync_in();
-        mma(0, 0, fb0);
-        sync_out();
-        // phase 1: q1 = (m0, n1); RA0 / RB0 of tile t were last read in phase 0
-        read_b(buf, 1, fb1);
-        if (pf) {
-            issue(t + 2, RA0);
-            issue(t + 2, RB0);
-        }
-        sync_in();
-        mma(0, 1, fb1);
-        sync_out();
-        // phase 2: q2 = (m1, n1); RB1 free
-        read_a(buf, 1);
-        if (pf) issue(t + 2, RB1);
-        sync_in();
-        mma(1, 1, fb1);
-        sync_out();
-        // phase 3: q3 = (m1, n0), no reads; RA1 free; publish tile t+1
-        if (pf) {
-            issue(t + 2, RA1);
-            wait_vm<8>();
+        if constexpr (BM == 256) {
+            // phase 0: q0 = (m0, n0)
+            read_b(buf, 0, fb0);
+            read_a(buf, 0);
+            sync_in();
+            mma(0, 0, fb0);
+            sync_out();
+            // phase 1: q1 = (m0, n1); RA0 / RB0 of tile t were last read in phase 0
+            read_b(buf, 1, fb1);
+            if (pf) {
+                issue(t + 2, 0);
+                issue(t + 2, 2);
+            }
+            sync_in();
+            mma(0, 1, fb1);
+            sync_out();
+            // phase 2: q2 = (m1, n1); RB1 free
+            read_a(buf, 1);
+            if (pf) issue(t + 2, 3);
+            sync_in();
+            mma(1, 1, fb1);
+            sync_out();
+            // phase 3: q3 = (m1, n0), no reads; RA1 free; publish tile t+1
+            if (pf) {
+                issue(t + 2, 1);
+                wait_vm<8>();
+            } else {
+                wait_vm<0>();
+            }
+            sync_in();
+            mma(1, 0, fb0);
+            sync_out();
         } else {
-            wait_vm<0>();
+            // phase 0: A (all 64 rows) + B(n0); RB1 of tile t-1 (buffer t+1) is free: tile t+1's RB1
+            read_b(buf, 0, fb0);
+            read_a(buf, 0);
+            if (t + 1 < nk) issue(t + 1, 2);
+            sync_in();
+            mma(0, 0, fb0);
+            sync_out();
+            // phase 1: B(n1); RA / RB0 free: tile t+2's; publish tile t+1
+            read_b(buf, 1, fb1);
+            if (pf) {
+                issue(t + 2, 0);
+                issue(t + 2, 1);
+                wait_vm<4>();
+            } else {
+                wait_vm<0>();
+            }
+            sync_in();
+            mma(0, 1, fb1);
+            sync_out();
         }
-        sync_in();
-        mma(1, 0, fb0);
-        sync_out();
     }
+    if (!late) __builtin_amdgcn_s_barrier();  // re-align the groups' barrier counts
 }
 
-template <int EPI, int NTERM, bool GATHER>
+template <int BM, int EPI, int NTERM, bool GATHER>
 __global__ __launch_bounds__(512, 1) void phased_kernel(EngineArgs p) {
-    __shared__ __attribute__((aligned(16))) char smem[ph::LDS];
-    const int tiles_m = (p.m + ph::BM - 1) / ph::BM;
+    __shared__ __attribute__((aligned(16))) char smem[ph::Cfg<BM>::LDS];
+    const int tiles_m = (p.m + BM - 1) / BM;
     const int nwg = gridDim.x;
     const int hw = blockIdx.x;
     const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
     int tm, tn;
     tile_coords(wg, tiles_m, p.n / ph::BN, p.group_m, tm, tn);
-    f32x4 acc[8][4];
-    phased_mainloop<NTERM, GATHER>(p, smem, tm * ph::BM, tn * ph::BN, acc);
-    engine_epilogue<Tile<256, 256, 2, 4, 4>, EPI>(p, tm * ph::BM, tn * ph::BN, acc);
+    f32x4 acc[BM / 32][4];
+    phased_mainloop<BM, NTERM, GATHER>(p, smem, tm * BM, tn * ph::BN, 0, p.k / ph::BK2, acc);
+    engine_epilogue<Tile<BM, 256, 2, 4, 4>, EPI>(p, tm * BM, tn * ph::BN, acc);
+}
+
+// Stream-K over the phased loop: the grid's blocks (<= one per CU, all co-resident) split the
+// tiles x K-tiles iteration space evenly; partial tiles go to the workspace in accumulator order
+// (sc1 stores), the block holding a tile's first K-tile folds them in and runs the epilogue.
+template <int EPI, int NTERM>
+__global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
+    constexpr int TI = 8, TJ = 4, BM = 256, TS = BM * ph::BN;
+    __shared__ __attribute__((aligned(16))) char smem[ph::Cfg<BM>::LDS];
+    const int tiles_m = (p.m + BM - 1) / BM, tiles_n = p.n / ph::BN;
+    const int nwg = gridDim.x;
+    const int hw = blockIdx.x;
+    const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
+    const int iters = p.k / ph::BK2;
+    const int64_t total = (int64_t)tiles_m * tiles_n * iters;
+    int64_t it = total * wg / nwg;
+    const int64_t it_end = total * (wg + 1) / nwg;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    f32x4 acc[TI][TJ];
+    while (it < it_end) {
+        const int tile = (int)(it / iters), kf = (int)(it % iters);
+        const int kl = (int)min((int64_t)iters, kf + (it_end - it));
+        int tm, tn;
+        tile_coords(tile, tiles_m, tiles_n, p.group_m, tm, tn);
+        const int m0 = tm * BM, n0 = tn * ph::BN;
+        wait_vm<0>();
+        __syncthreads();  // the previous segment's LDS readers are done
+        phased_mainloop<BM, NTERM, false>(p, smem, m0, n0, kf, kl, acc);
+        if (kf != 0) {
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(p.sk_part + (int64_t)wg * TS, 0, TS * 4, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < TJ; ++j) {
+                    const int off = (((wave * TI + i) * TJ + j) * 64 + lane) * 16;
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16);
+                }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) __hip_atomic_store(p.sk_flag + wg, p.sk_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (kl < iters) {
+                const int64_t tile_end = (int64_t)(tile + 1) * iters;
+                for (int c = wg + 1; c < nwg && total * c / nwg < tile_end; ++c) {
+                    if (total * (c + 1) / nwg == total * c / nwg) continue;  // empty range: no partial
+                    if (threadIdx.x == 0) {
+                        int spins = 0;
+                        while (__hip_atomic_load(p.sk_flag + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.sk_epoch &&
+                               ++spins < (1 << 24))
+                            __builtin_amdgcn_s_sleep(1);
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
+                    __syncthreads();
+                    const float4* src = reinterpret_cast<const float4*>(p.sk_part + (int64_t)c * TS) + wave * TI * TJ * 64 + lane;
+#pragma unroll
+                    for (int i = 0; i < TI; ++i)
+#pragma unroll
+                        for (int j = 0; j < TJ; ++j) {
+                            const float4 v = src[(i * TJ + j) * 64];
+                            acc[i][j][0] += v.x;
+                            acc[i][j][1] += v.y;
+                            acc[i][j][2] += v.z;
+                            acc[i][j][3] += v.w;
+                        }
+                }
+            }
+            engine_epilogue<Tile<256, 256, 2, 4, 4>, EPI>(p, m0, n0, acc);
+        }
+        it += kl - kf;
+    }
 }
 
 // Data-parallel (one output tile per block) or stream-K (SK): the grid's blocks split the
@@ -869,12 +979,21 @@ int sk_grid(int m, int n, int k) {
 
 // Tile choice: the 256x256 tile halves the L2 traffic per FLOP but needs enough tiles to fill
 // 256 CUs (one 512-thread block per CU); smaller problems keep the 128x128 tile (2-3 blocks per CU).
-int pick_cfg(int m, int n) {
+int pick_cfg(int m, int n, int k) {
     if (const char* env = getenv("RF_GEMM_TILE")) return atoi(env);
-    if (n % 256 == 0) {
-        const int t256 = (n / 256) * ((m + 255) / 256);
-        if (t256 >= 2 * 256) return 256;
+    const char* ph = getenv("RF_GEMM_PHASED");
+    if (n % 256 == 0 && k % 64 == 0 && (!ph || atoi(ph) != 0)) {
+        // whole-tile rounds x measured time per round (kbench, K = 1024-13312), relative units: 256x256 phased
+        // 1.1 per 256 tiles, 128x256 phased 0.65 per 256 tiles, 128x128 ring 0.52 for <= 256 tiles (one block
+        // per CU) else 0.85 per 512 (two blocks per CU)
+        const int64_t t256 = (int64_t)(n / 256) * ((m + 255) / 256), t1282 = (int64_t)(n / 256) * ((m + 127) / 128);
+        const int64_t t128 = (int64_t)(n / 128) * ((m + 127) / 128);
+        const double c256 = 1.1 * ((t256 + 255) / 256), c1282 = 0.65 * ((t1282 + 255) / 256),
+                     c128 = t128 <= 256 ? 0.52 : 0.85 * ((t128 + 511) / 512);
+        if (c256 <= c1282 && c256 <= c128) return 256;
+        return c1282 <= c128 ? 1282 : 128;
     }
+    if (n % 256 == 0 && (n / 256) * ((m + 255) / 256) >= 2 * 256) return 256;
     return 128;
 }
 
@@ -882,12 +1001,20 @@ __device__ __attribute__((aligned(16))) bf16_t g_zero_row[64];  // stays zero: s
 
 }  // namespace
 
-template <int EPI, int NTERM, bool GATHER>
+template <int EPI, int NTERM, bool GATHER, int BM = 256>
 int launch_phased(EngineArgs a, void* stream, const char* what) {
-    const int tiles_m = (a.m + 255) / 256, tiles_n = a.n / 256;
+    const int tiles_m = (a.m + BM - 1) / BM, tiles_n = a.n / 256;
     const int nwg = tiles_n * tiles_m;
-    a.group_m = pick_group_m(tiles_m, tiles_n, 256, 256, (nwg + 7) / 8);
-    hipLaunchKernelGGL((phased_kernel<EPI, NTERM, GATHER>), dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    a.group_m = pick_group_m(tiles_m, tiles_n, BM, 256, (nwg + 7) / 8);
+    hipLaunchKernelGGL((phased_kernel<BM, EPI, NTERM, GATHER>), dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    return rf::check_launch(what);
+}
+
+template <int EPI>
+int launch_phased_sk(EngineArgs a, int grid, void* stream, const char* what) {
+    const int tiles_m = (a.m + 255) / 256, tiles_n = a.n / 256;
+    a.group_m = pick_group_m(tiles_m, tiles_n, 256, 256, ((int64_t)tiles_m * tiles_n + 7) / 8);
+    hipLaunchKernelGGL((phased_sk_kernel<EPI, 1>), dim3(grid), dim3(512), 0, (hipStream_t)stream, a);
     return rf::check_launch(what);
 }
 
@@ -918,6 +1045,14 @@ int run_dp(int cfg, const EngineArgs& p, int epilogue, void* stream) {
             default: return launch_phased<E_SWIGLU, 1, false>(p, stream, "rf_gemm_bf16");
         }
     }
+    if (cfg == 1282 && use_phased(p.n, p.k)) {
+        switch (epilogue) {
+            case RF_EPI_BF16: return launch_phased<E_BF16, 1, false, 128>(p, stream, "rf_gemm_bf16");
+            case RF_EPI_F32: return launch_phased<E_F32, 1, false, 128>(p, stream, "rf_gemm_bf16");
+            case RF_EPI_ADD_F32: return launch_phased<E_ADD, 1, false, 128>(p, stream, "rf_gemm_bf16");
+            default: return launch_phased<E_SWIGLU, 1, false, 128>(p, stream, "rf_gemm_bf16");
+        }
+    }
     if (cfg == 256 && p.n % 256 == 0) return run_dp_cfg<T256>(p, epilogue, stream);
     if (cfg == 1284) return run_dp_cfg<Tile<128, 128, 2, 2, 4>>(p, epilogue, stream);
     if (cfg == 1285) return run_dp_cfg<Tile<128, 128, 2, 2, 5>>(p, epilogue, stream);
@@ -927,7 +1062,16 @@ int run_dp(int cfg, const EngineArgs& p, int epilogue, void* stream) {
 
 bool sk256(int m, int n, int k) {
     if (const char* env = getenv("RF_GEMM_SK256")) return atoi(env) != 0;
-    return false;  // decided below once measured
+    return false;  // the ring engine's 256x256 stream-K: superseded by the phased one, kept for A/B
+}
+
+// Phased 256x256 stream-K over one block per CU (RF_GEMM_SKPH=1).  Off by default: its partial-tile
+// fix-up costs ~5-10 us per block, and the 128x256 phased tile beat it on every bench shape measured
+// (texture GEMM 5633x1024x13312: 170 us vs 212 us).
+bool skph(int m, int n, int k) {
+    if (!use_phased(n, k)) return false;
+    const char* env = getenv("RF_GEMM_SKPH");
+    return env && atoi(env) != 0;
 }
 
 extern "C" int64_t rf_gemm_workspace_bytes(void) { return SK_WS_BYTES; }
@@ -955,7 +1099,16 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
     p.c = c;
     p.ldc = ldc;
     p.bias = bias;
-    const bool big = pick_cfg(m, n) != 128;
+    if (workspace && ws_bytes >= SK_WS_BYTES && skph(m, n, k)) {
+        sk_setup(p, workspace);
+        switch (epilogue) {
+            case RF_EPI_BF16: return launch_phased_sk<E_BF16>(p, 256, stream, "rf_gemm_bf16");
+            case RF_EPI_F32: return launch_phased_sk<E_F32>(p, 256, stream, "rf_gemm_bf16");
+            case RF_EPI_ADD_F32: return launch_phased_sk<E_ADD>(p, 256, stream, "rf_gemm_bf16");
+            default: return launch_phased_sk<E_SWIGLU>(p, 256, stream, "rf_gemm_bf16");
+        }
+    }
+    const bool big = pick_cfg(m, n, k) != 128;
     const int grid = (!big && workspace && ws_bytes >= SK_WS_BYTES) ? sk_grid(m, n, k) : 0;
     if (grid) {
         sk_setup(p, workspace);
@@ -977,7 +1130,7 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
             default: return launch_sk<T256, E_SWIGLU>(p, 256, stream, "rf_gemm_bf16");
         }
     }
-    return run_dp(pick_cfg(m, n), p, epilogue, stream);
+    return run_dp(pick_cfg(m, n, k), p, epilogue, stream);
 }
 
 // fp16 convolutions (one MFMA per product): the 256x256 tile when the filter bank is a multiple of 256
@@ -990,8 +1143,9 @@ static int conv_f16_dp(EngineArgs& p, void* stream, const char* what) {
     if (p.n == 64) return launch<T256x64, E_CONV, P_F16, GATHER>(p, stream, what);
     if (t == 128) return launch<T128, E_CONV, P_F16, GATHER>(p, stream, what);
     if (p.n % 256 == 0 && (t == 256 || (!t && ((p.m + 255) / 256) * (p.n / 256) >= 256)))
-        return use_phased(p.n, p.k) ? launch_phased<E_CONV, P_F16, GATHER>(p, stream, what)
-                                    : launch<T256, E_CONV, P_F16, GATHER>(p, stream, what);
+        return (getenv("RF_CONV_PHASED") && atoi(getenv("RF_CONV_PHASED")) && use_phased(p.n, p.k))
+                   ? launch_phased<E_CONV, P_F16, GATHER, 256>(p, stream, what)
+                   : launch<T256, E_CONV, P_F16, GATHER>(p, stream, what);
     if (t == 2561) return launch<T256x128, E_CONV, P_F16, GATHER>(p, stream, what);
     return launch<T128, E_CONV, P_F16, GATHER>(p, stream, what);
 }

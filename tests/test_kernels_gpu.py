@@ -52,16 +52,18 @@ def test_gemm_f32_bf16(m, n, k):
     assert relerr(acc, ref2) < 1e-5
 
 
-@pytest.mark.parametrize("grid", ["512", "768", "37", "sk256"])
-@pytest.mark.parametrize("m,n,k", [(1000, 1024, 1024), (300, 256, 4096), (129, 128, 96), (5649, 1024, 64)])
+@pytest.mark.parametrize("grid", ["512", "768", "37", "sk256", "skph"])
+@pytest.mark.parametrize("m,n,k", [(1000, 1024, 1024), (300, 256, 4096), (129, 128, 96), (5649, 1024, 64),
+                                   (5649, 1024, 4096), (4096, 3072, 1024)])
 def test_gemm_stream_k(monkeypatch, grid, m, n, k):
     """Stream-K split (forced grid sizes, incl. an odd one where a tile spans 3+ blocks, and the 256x256-tile
     variant over 256 blocks) vs fp64, every epilogue."""
     ops = _ops()
-    if grid == "sk256":
-        if n % 256:
-            pytest.skip("256x256 tiles need N % 256 == 0")
-        monkeypatch.setenv("RF_GEMM_SK256", "1")
+    if grid in ("sk256", "skph"):
+        if n % 256 or (grid == "skph" and k % 64):
+            pytest.skip("256x256 tiles need N % 256 == 0 (and K % 64 == 0 for the phased loop)")
+        monkeypatch.setenv("RF_GEMM_SK256" if grid == "sk256" else "RF_GEMM_SKPH", "1")
+        monkeypatch.setenv("RF_GEMM_PHASED", "0" if grid == "sk256" else "1")
     else:
         monkeypatch.setenv("RF_GEMM_SK", grid)
     g = torch.Generator(device="cpu").manual_seed(m + n + k)
@@ -87,15 +89,15 @@ def test_gemm_stream_k(monkeypatch, grid, m, n, k):
     assert relerr(outs.float(), refs) < 5e-3
 
 
-@pytest.mark.parametrize("phased", ["1", "0"])
+@pytest.mark.parametrize("tile", ["256ph", "128x256ph", "256ring"])
 @pytest.mark.parametrize("m,n,k", [(1, 256, 64), (300, 512, 128), (777, 256, 192), (5649, 3072, 1024),
                                    (4096, 1024, 4096), (2000, 768, 320)])
-def test_gemm_256_tiles(monkeypatch, phased, m, n, k):
-    """The 256x256 tile: the phased BK=64 loop (default) and the ring engine, forced on every shape (ragged M,
-    one to three K-tiles, long K), every epilogue, against fp64."""
+def test_gemm_256_tiles(monkeypatch, tile, m, n, k):
+    """The 256-wide tiles: the phased BK=64 loop at 256x256 and 128x256 and the ring engine's 256x256, forced on
+    every shape (ragged M, one to three K-tiles, long K), every epilogue, against fp64."""
     ops = _ops()
-    monkeypatch.setenv("RF_GEMM_TILE", "256")
-    monkeypatch.setenv("RF_GEMM_PHASED", phased)
+    monkeypatch.setenv("RF_GEMM_TILE", "1282" if tile == "128x256ph" else "256")
+    monkeypatch.setenv("RF_GEMM_PHASED", "0" if tile == "256ring" else "1")
     g = torch.Generator(device="cpu").manual_seed(m + 3 * n + k)
     a = torch.randn(m, k, generator=g).bfloat16().to(dev)
     w = (torch.randn(n, k, generator=g) / math.sqrt(k)).bfloat16().to(dev)

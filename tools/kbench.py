@@ -90,8 +90,9 @@ def gemm():
             c = torch.zeros(m, n, device=dev)
         variants = [("dp128", "128", None, "0"), ("dp128s4", "1284", None, "0"), ("dp128s5", "1285", None, "0"),
                     ("dp256x128", "2561", None, "0"), ("dp256ring", "256", None, "0"), ("dp256ph", "256", None, "0"),
+                    ("dp128x256ph", "1282", None, "0"),
                     ("sk128x512", "128", "512", "0"), ("sk128x768", "128", "768", "0"), ("sk256", None, None, "1"),
-                    ("auto", None, None, None)]
+                    ("skph", None, None, "0"), ("auto", None, None, None)]
         if os.environ.get("KB_VARIANTS"):
             variants = [v for v in variants if v[0] in os.environ["KB_VARIANTS"].split(",")]
         for label, tile, sk, gm in variants:
@@ -101,7 +102,13 @@ def gemm():
                 else:
                     os.environ[key] = val
             os.environ["RF_GEMM_PHASED"] = "0" if label in ("dp256ring", "sk256") else "1"
-            if label in ("dp256ring", "dp256ph", "sk256") and n % 256:
+            if label == "skph":
+                os.environ["RF_GEMM_SKPH"] = "1"
+            elif label == "auto":
+                os.environ.pop("RF_GEMM_SKPH", None)
+            else:
+                os.environ["RF_GEMM_SKPH"] = "0"
+            if label in ("dp256ring", "dp256ph", "sk256", "skph", "dp128x256ph") and n % 256:
                 continue
             ms = timeit(lambda: ops.gemm(a, w, c, None, epi), reps=10 if k > 8000 else 20)
             print(f"gemm {name:8s} {m}x{n}x{k} {label}: {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF")
@@ -122,10 +129,11 @@ def conv():
             x = split_planes(torch.randn(1, hw, hw, cin, device=dev), conv.cin_pad, f16=f16)
             fl = 2 * hw * hw * cin * cout * 9
             mf = 1 if f16 else 3
-            tiles = ("128", "256", "2561", "auto") if f16 else ("128", "256")
+            tiles = ("128", "256", "256ph", "2561", "auto") if f16 else ("128", "256")
             for t in tiles:
+                os.environ["RF_CONV_PHASED"] = "1" if t == "256ph" else "0"
                 if t != "auto":
-                    os.environ["RF_CONV_TILE"] = t
+                    os.environ["RF_CONV_TILE"] = t.replace("ph", "")
                 ms = timeit(lambda: conv(x, out_f32=True), reps=10)
                 os.environ.pop("RF_CONV_TILE", None)
                 print(f"conv3x3 {'f16 ' if f16 else 'bf16x3'} {cin}->{cout} @{hw} tile={t}: "
