@@ -49,7 +49,7 @@ extern "C" {
 #define RF_ERR_LAUNCH 2
 #define RF_ERR_UNSUPPORTED 3
 
-#define RF_ABI_VERSION 3
+#define RF_ABI_VERSION 4
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -80,19 +80,27 @@ int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, float eps, void
 /* dst[r] = rope(rmsnorm(src[src_rows ? src_rows[r] : r]))  (bf16 -> bf16, may alias when src_rows == NULL)
  * over n_seg consecutive segments of width dim (q and k of one qkv row), each with its own full-width
  * RMSNorm weights norm_w[seg*dim ...] (norm_w may be NULL: no norm); pos may be NULL (no rope).
+ * Segment 0 is additionally multiplied by seg0_scale (1 = none): passing softmax_scale * log2(e) for
+ * the q segment lets rf_attn_fwd run with scale = ln 2 (no per-score multiply).
  * RoPE: head_dim 128, per head the half-split rotation with
  * angle[i] = pos[r / pos_div][i / n_freqs] * freqs[i % n_freqs] for i < 9*n_freqs, else 0. */
 int rf_qk_norm_rope(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, const int32_t* src_rows,
-                    int rows, int dim, int n_heads, int n_seg, const float* norm_w, float eps, const float* pos,
-                    int64_t ld_pos, int pos_div, const float* freqs, int n_freqs, void* stream);
+                    int rows, int dim, int n_heads, int n_seg, const float* norm_w, float eps, float seg0_scale,
+                    const float* pos, int64_t ld_pos, int pos_div, const float* freqs, int n_freqs, void* stream);
 
 /* Variable-length multi-head attention, non-causal, head_dim 128, bf16 in/out, f32 softmax.
- * problems: int32[n_problems][5] = {q_start, q_len, k_start, k_len, v_start} (rows).
- * For every problem p and head h: O[q_start+i, h*128:(h+1)*128] =
+ * problems: int32[n_problems][5] = {q_start, q_len, k_start, k_len, v_start} (rows); k_len >= 1
+ * wherever q_len >= 1.  For every problem p and head h: O[q_start+i, h*128:(h+1)*128] =
  *   softmax(scale * Q_i K_j^T, j < k_len) V_j .
- * n_split > 1 splits every key range over n_split workgroups (for launches that would leave CUs
- * idle): partials go to `workspace` (rf_attn_workspace_bytes(ws_rows, n_heads, n_split) bytes, ws_rows
- * >= every output row + 1) and rf_attn_combine(rows = NULL, n_rows = ws_rows) writes O. */
+ * scale = ln 2 means q already carries softmax_scale * log2(e) (rf_qk_norm_rope seg0_scale): the
+ * scores are then used as exp2 exponents directly.
+ * n_split == 0 (default mode): stream-K kernel, one workgroup per CU over the flattened
+ *   (problem, head, 256-row block, 64-key tile) space; `workspace` = rf_attn_workspace_bytes(0, H, 0)
+ *   bytes, ZEROED before its first use and reused as is afterwards (the kernel re-arms its flags);
+ *   one launch at a time per workspace.  ws_rows is ignored.
+ * n_split >= 1: one workgroup per (problem, head, block, split); for n_split > 1 partials go to
+ *   `workspace` (rf_attn_workspace_bytes(ws_rows, n_heads, n_split) bytes, ws_rows >= every output
+ *   row + 1) and rf_attn_combine(rows = NULL, n_rows = ws_rows) writes O. */
 int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                 void* o, int64_t ldo, const int32_t* problems, int n_problems, int max_q_len, int n_heads,
                 int head_dim, float scale, int n_split, void* workspace, int64_t ws_rows, void* stream);

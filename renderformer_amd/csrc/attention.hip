@@ -36,6 +36,10 @@
 // Workgroups are mapped so that every XCD processes a contiguous range of
 // (problem, head, split, q-block): the q-blocks sharing one K/V stream sit on one
 // XCD and read it from that XCD's L2.
+#include <math.h>
+
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -62,6 +66,10 @@ struct AttnArgs {
     float* part_o;
     float* part_ml;
     int64_t part_rows;
+    // stream-K
+    int n_problems;
+    int* flag;
+    float thr;  // deferred-rescale threshold (log2 units; RF_ATTN_THR, default 8)
 };
 
 RF_DEV int swz_off(int row, int ch) { return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4); }
@@ -385,8 +393,7 @@ constexpr int NST3 = 3;
 
 template <int N>
 RF_DEV void attn_wait_vm() {
-    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 __global__ __launch_bounds__(NW3 * 64, 1) void attn_v3_kernel(AttnArgs p) {
@@ -614,6 +621,401 @@ __global__ __launch_bounds__(NW3 * 64, 1) void attn_v3_kernel(AttnArgs p) {
         }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Stream-K varlen kernel (rf_attn_fwd with n_split == 0, the default).
+//
+// Work decomposition: the launch's (problem, head, 256-row q-block, 64-key tile) space is flattened
+// and every workgroup of a one-per-CU grid takes an equal contiguous range of it, so the CUs finish
+// together whatever the unit count (184 units of 89 tiles on 256 CUs at the bench shape).  A unit
+// cut between workgroups is finished by the workgroup holding its first tile (the "owner", which
+// reaches that tile at the END of its range): every later piece is published as an unnormalised
+// partial (O, m, l in register order, sc1 stores + flag) and folded into the owner's registers
+// before its epilogue.  Q-blocks split each problem's rows evenly (<= 256 rows each).
+//
+// Main loop, per 64-key tile t (8 waves x 32 query rows, one barrier per tile):
+//   * K(t+2) and V(t+1) arrive by LDS-DMA (inline asm, so hipcc does not put a vmcnt(0) in front
+//     of the transposed V reads of the same tile) into 2-deep K and V rings (64 KiB); the loop is
+//     unrolled by 2 so every LDS offset is an immediate.
+//   * S(t+1) = K(t+1) Q^T (v_mfma_f32_32x32x16_bf16, query on the lane) is issued in one block with
+//     the softmax of S(t) and O^T += V(t)^T P(t)^T, so exp/convert VALU work overlaps the MFMAs.
+//   * q arrives pre-scaled by scale*log2(e) (rf_qk_norm_rope seg0_scale) and the QK^T chain starts
+//     from C = -m (the running max), so P = exp2(S) needs no per-score FMA (UNIT); the max is only
+//     re-based (deferred rescale, guide T13) when a row grows by more than 2^8.
+constexpr int NW5 = 8;
+constexpr int QB5 = NW5 * 32;
+constexpr int K5 = 0;                  // K ring: 2 x 16 KiB
+constexpr int V5 = 2 * TILE_BYTES;     // V ring: 2 x 16 KiB
+constexpr int SK5_MAX_GRID = 512;
+constexpr int PIECE_O = QB5 * HD;                // f32, register order
+constexpr int PIECE_FLOATS = PIECE_O + QB5 * 2 * 2;  // + (m, l) per lane
+
+RF_DEV float vmax3(float a, float b, float c) {  // single v_max3_f32 (no canonicalising v_max in front)
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// One 1-KiB LDS-DMA piece: lane l's 16 B land at LDS byte lds + 16 l.  Inline asm so hipcc neither
+// counts it (the loop waits with its own vmcnt) nor guards later ds_read_b64_tr_b16 with vmcnt(0);
+// M0 is compiler-reserved, so it is saved and restored inside the statement (guide §5.7).
+RF_DEV void dma_piece(const bf16_t* g, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
+}
+
+// DBG (diagnostic builds only, RF_ATTN_DBG; results are garbage): 1 = no K/V DMA in the loop,
+// 2 = no top-of-tile wait + barrier, 4 = no PV MFMAs, 8 = no exp2 (P = bf16(S)), 16 = no QK MFMAs
+template <bool UNIT, int DBG = 0>
+__global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
+    __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // 64 KiB
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int half = lane >> 5;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
+    // the second-dispatched half loses VALU arbitration every segment: static priority (guide T5)
+    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+
+    const int nwg = gridDim.x, hw = blockIdx.x;
+    const int xcd = hw & 7, qd = nwg >> 3, rm = nwg & 7;
+    const int wg = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + (hw >> 3);
+
+    int64_t total = 0;
+    for (int i = 0; i < p.n_problems; ++i) {
+        const int32_t* d = p.problems + 5 * i;
+        total += (int64_t)p.n_heads * ((d[1] + QB5 - 1) / QB5) * ((d[3] + KT - 1) / KT);
+    }
+    int64_t it = total * wg / nwg;
+    const int64_t it_end = total * (wg + 1) / nwg;
+
+    const float c = UNIT ? 1.f : p.c;
+    const float inv_c = UNIT ? 1.f : 1.f / p.c;
+    const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;  // ds_read_b64_tr_b16 lane geometry
+    const int qi = wave * 32 + (lane & 31);
+    // LDS image of a K/V tile (guide T10 image (a)): 8-row x 32-column subtiles of 512 B,
+    // off(row, ch) = 2048 (row >> 3) + 512 (ch >> 2) + 64 (row & 7) + 16 ((ch & 3) ^ ((row >> 2) & 3)),
+    // conflict-free for the K ds_read_b128 and the V ds_read_b64_tr_b16 of the 32x32x16 operands, and
+    // every read is one of two lane bases per operand plus an immediate.
+    // DMA: wave w fills row group w (pieces 2w, 2w+1 = column groups {0,1}, {2,3}); lane l writes
+    // 16 B at piece + 16 l = row 8w + ((l >> 2) & 7), physical chunk l & 3 of column group (l >> 5) (+2).
+    const int d_row = 8 * wave + ((lane >> 2) & 7);
+    const int d_ch = 4 * (lane >> 5) + ((lane & 3) ^ ((d_row >> 2) & 3));
+    const int kr = lane & 31;
+    const int kb_even = 2048 * (kr >> 3) + 64 * (kr & 7) + 16 * (half ^ ((kr >> 2) & 3));
+    const int kb_odd = 2048 * (kr >> 3) + 64 * (kr & 7) + 16 * ((2 + half) ^ ((kr >> 2) & 3));
+    const int vb_lo = 64 * (4 * (g >> 1) + qq) + 16 * ((2 * (g & 1) + (pp >> 1)) ^ ((g >> 1) & 3)) + 8 * (pp & 1);
+    const int vb_hi = 64 * (4 * (g >> 1) + qq) + 16 * ((2 * (g & 1) + (pp >> 1)) ^ ((2 + (g >> 1)) & 3)) + 8 * (pp & 1);
+
+    int pi = -1;
+    int64_t base = 0, usz = 0;
+    int q_start = 0, q_len = 0, k_start = 0, k_len = 0, v_start = 0, nqb = 1, nt = 1;
+    while (it < it_end) {
+        while (it >= base + usz) {  // advance to the problem holding tile `it`
+            base += usz;
+            ++pi;
+            const int32_t* d = p.problems + 5 * pi;
+            q_start = d[0];
+            q_len = d[1];
+            k_start = d[2];
+            k_len = d[3];
+            v_start = d[4];
+            nqb = (q_len + QB5 - 1) / QB5;
+            nt = (k_len + KT - 1) / KT;
+            usz = (int64_t)p.n_heads * nqb * nt;
+        }
+        const int64_t rel = it - base;
+        const int unit = (int)(rel / nt);
+        const int kt0 = (int)(rel - (int64_t)unit * nt);
+        const int kt1 = (int)min((int64_t)nt, kt0 + (it_end - it));
+        const int n = kt1 - kt0;
+        const int64_t unit_end = base + (int64_t)(unit + 1) * nt;
+        it += n;
+        const int h = unit / nqb, qb = unit - (unit / nqb) * nqb;
+        const int q0 = (int)((int64_t)qb * q_len / nqb), q1 = (int)((int64_t)(qb + 1) * q_len / nqb);
+        const int hoff = h * HD;
+        const bool active = q0 + wave * 32 < q1;  // wave-uniform: this wave owns at least one row
+
+        attn_wait_vm<0>();
+        __syncthreads();  // the previous piece's LDS readers and stores are done
+
+        bf16x8 qf[8];
+        {
+            const int qrow = q_start + min(q0 + qi, q1 - 1);
+            const bf16_t* src = p.q + (int64_t)qrow * p.ldq + hoff + 8 * half;
+#pragma unroll
+            for (int st = 0; st < 8; ++st) qf[st] = *reinterpret_cast<const bf16x8*>(src + 16 * st);
+        }
+
+        const bf16_t* kp = p.k + (int64_t)(k_start + kt0 * KT + d_row) * p.ldk + hoff + 8 * d_ch;
+        const bf16_t* vp = p.v + (int64_t)(v_start + kt0 * KT + d_row) * p.ldv + hoff + 8 * d_ch;
+        const int64_t kstep = KT * p.ldk, vstep = KT * p.ldv;
+        // tiles are issued in order; rows past k_len (tail tile) re-read row k_len - 1, masked later
+        auto issue = [&](const bf16_t*& src, int64_t ld, int64_t step, int t, uint32_t dst) {
+            const uint32_t d0 = __builtin_amdgcn_readfirstlane(dst + wave * 2048);
+            if ((t + 1) * KT <= k_len) {
+                dma_piece(src, d0);
+                dma_piece(src + 64, d0 + 1024);
+            } else {
+                const int over = t * KT + d_row - (k_len - 1);
+                const bf16_t* a = src - (int64_t)(over > 0 ? over : 0) * ld;
+                dma_piece(a, d0);
+                dma_piece(a + 64, d0 + 1024);
+            }
+            src += step;
+        };
+
+        f32x16 o[4];
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+        float m_run = 0.f, l_run = 0.f;  // m_run in exp2 units, identical in both lane halves
+        // -m in score units: the C operand of the QK^T chains.  Rebuilt from m_run in every phase B, so
+        // S(t+1) issued right after a rescale of tile t still carries the old base: `carry` holds that
+        // difference and the next tile removes it (rare path).
+        f32x16 minit;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) minit[r] = 0.f;
+        float carry = 0.f;
+        bool fresh = true, carried = false;
+
+        auto qk = [&](const int koff, f32x16* s) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int st = 0; st < 8; ++st) {
+                    const bf16x8 a = *reinterpret_cast<const bf16x8*>(smem + koff + (st & 1 ? kb_odd : kb_even) +
+                                                                      8192 * b + 512 * (st >> 1));
+                    s[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[st], st == 0 ? minit : s[b], 0, 0, 0);
+                }
+        };
+
+        issue(kp, p.ldk, kstep, kt0, lds0 + K5);
+        issue(vp, p.ldv, vstep, kt0, lds0 + V5);
+        if (n > 1) {
+            issue(kp, p.ldk, kstep, kt0 + 1, lds0 + K5 + TILE_BYTES);
+            attn_wait_vm<4>();
+        } else {
+            attn_wait_vm<2>();
+        }
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        f32x16 sA[2], sB[2];
+        qk(K5, sA);
+
+        auto body = [&](const int i, auto par_c, f32x16(&s)[2], f32x16(&sn)[2]) {
+            constexpr int PAR = decltype(par_c)::value;
+            const int t = kt0 + i;
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (!(DBG & 2)) {
+                attn_wait_vm<0>();             // K(t+1) and V(t) landed for this wave ...
+                __builtin_amdgcn_s_barrier();  // ... and for every wave; K(t) and V(t-1) are free
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (!(DBG & 1)) {
+                if (i + 2 < n) issue(kp, p.ldk, kstep, t + 2, lds0 + K5 + PAR * TILE_BYTES);
+                if (i + 1 < n) issue(vp, p.ldv, vstep, t + 1, lds0 + V5 + (PAR ^ 1) * TILE_BYTES);
+            }
+            // (a wave with no valid rows computes clamped duplicates: no branch, so no register shuffles)
+
+            if ((t + 1) * KT > k_len) {
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int key = b * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                        s[b][r] = t * KT + key >= k_len ? NEG : s[b][r];
+                    }
+            }
+            float mt = vmax3(s[0][0], s[0][1], s[0][2]);
+#pragma unroll
+            for (int r = 3; r < 15; r += 2) mt = vmax3(mt, s[0][r], s[0][r + 1]);
+            mt = vmax3(mt, s[0][15], s[1][0]);
+#pragma unroll
+            for (int r = 1; r < 15; r += 2) mt = vmax3(mt, s[1][r], s[1][r + 1]);
+            mt = vmax3(mt, s[1][15], s[1][15]);
+            if (fresh || carried || __any(mt * c > p.thr)) {
+                // bring S(t) onto the current base, then re-base the running max on this tile's row max
+                // (exact on a piece's first tile)
+                const float cs = carry * inv_c;
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) s[b][r] -= cs;
+                const float mrow = (__builtin_fmaxf(mt, __shfl_xor(mt, 32, 64)) - cs) * c;
+                const float delta = fresh ? mrow : __builtin_fmaxf(mrow, 0.f);
+                const float alpha = fresh ? 1.f : fast_exp2(-delta);
+                l_run *= alpha;
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+                m_run += delta;
+                const float ds = delta * inv_c;
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) s[b][r] -= ds;
+                carry = delta;
+                carried = __any(delta != 0.f);
+                fresh = false;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+
+            // ---- hand-placed block (sched_barrier walls keep the source order):
+            // phase A: S(t+1) = K(t+1) Q^T as two alternating independent chains, each gap carrying two
+            //          exp2 and one bf16 pack of P(t); K fragments read two MFMAs ahead (3-deep ring).
+            // phase B: O^T += V(t)^T P(t)^T as four alternating chains, V^T fragments (2 transposed
+            //          reads each) two MFMAs ahead; the row-sum adds ride in its gaps.
+            const int koff = K5 + (PAR ^ 1) * TILE_BYTES;
+            const int voff = V5 + PAR * TILE_BYTES;
+            auto kread = [&](int j) {  // QK step j: chain b = j & 1, k-slice st = j >> 1
+                const int b = j & 1, st = j >> 1;
+                return *reinterpret_cast<const bf16x8*>(smem + koff + (st & 1 ? kb_odd : kb_even) + 8192 * b +
+                                                        512 * (st >> 1));
+            };
+            auto vread = [&](int j) {  // PV step j: chain dt = j & 3, key block (b, sp) = j >> 2
+                const int dt = j & 3, b = (j >> 2) >> 1, sp = (j >> 2) & 1;
+                const int imm = voff + 2048 * (4 * b + 2 * sp) + 512 * dt;
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, smem + imm + vb_lo));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, smem + imm + 2048 + vb_hi));
+                return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            };
+            bf16x8 kf[3], vf[3];
+            bf16x8 pf[2][2];
+            float ls[4];
+            kf[0] = kread(0);
+            kf[1] = kread(1);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                if (j + 2 < 16) kf[(j + 2) % 3] = kread(j + 2);
+                if (j == 14) vf[0] = vread(0);
+                if (j == 15) vf[1] = vread(1);
+                const int b = j & 1, st = j >> 1;
+                if constexpr (DBG & 16) {
+                    if (st == 0) sn[b] = minit;
+                    asm volatile("" : "+v"(kf[j % 3]));
+                } else {
+                    sn[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[j % 3], qf[st], st == 0 ? minit : sn[b], 0, 0, 0);
+                }
+                float e[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int x = 2 * j + u;
+                    const float v = s[x >> 4][x & 15];
+                    e[u] = (DBG & 8) ? v : fast_exp2(UNIT ? v : v * c);
+                    ls[x & 3] = j < 2 ? e[u] : ls[x & 3] + e[u];
+                    asm volatile("" : "+v"(ls[x & 3]));  // keep the add in this gap (IR passes sink it)
+                }
+                pf[j >> 3][(j >> 2) & 1][2 * (j & 3)] = (__bf16)e[0];
+                pf[j >> 3][(j >> 2) & 1][2 * (j & 3) + 1] = (__bf16)e[1];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                if (j + 2 < 16) vf[(j + 2) % 3] = vread(j + 2);
+                const int dt = j & 3, b = (j >> 2) >> 1, sp = (j >> 2) & 1;
+                if constexpr (DBG & 4) {
+                    asm volatile("" : "+v"(vf[j % 3]), "+v"(pf[b][sp]));
+                } else {
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[j % 3], pf[b][sp], o[dt], 0, 0, 0);
+                }
+                minit[j] = -m_run * inv_c;
+                asm volatile("" : "+v"(minit[j]));  // one v_mov per PV gap (otherwise hoisted into phase A)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+        };
+        int i = 0;
+        for (; i + 1 < n; i += 2) {
+            body(i, std::integral_constant<int, 0>{}, sA, sB);
+            body(i + 1, std::integral_constant<int, 1>{}, sB, sA);
+        }
+        if (i < n) body(i, std::integral_constant<int, 0>{}, sA, sB);
+
+        // ---- piece epilogue.  Register order: lane owns query (lane & 31), d = dt*32 + 8 gq + 4 half + 0..3
+        float* piece = p.part_o + (int64_t)wg * PIECE_FLOATS;
+        if (kt0 > 0) {
+            // not the unit's first tile: publish the unnormalised partial for the owner (sc1 stores,
+            // every storing wave drains, one lane flags; guide Guideline 16 / MI355X_MICROARCH hand-offs)
+            if (active) {
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(piece, 0, PIECE_FLOATS * 4, 0x00020000);
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int gq = 0; gq < 4; ++gq) {
+                        const f32x4 v4 = {o[dt][4 * gq], o[dt][4 * gq + 1], o[dt][4 * gq + 2], o[dt][4 * gq + 3]};
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v4), rs,
+                                                               (((wave * 16 + dt * 4 + gq) * 64) + lane) * 16, 0, 16);
+                    }
+                const f32x2 ml = {m_run, l_run};
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ml), rs,
+                                                      PIECE_O * 4 + (wave * 64 + lane) * 8, 0, 16);
+            }
+            attn_wait_vm<0>();
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(p.flag + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+        }
+        if (kt1 < nt) {
+            // owner of a cut unit: fold in the partials of the later workgroups that hold its other tiles
+            for (int cw = wg + 1; cw < nwg; ++cw) {
+                const int64_t cs = total * cw / nwg, ce = total * (cw + 1) / nwg;
+                if (cs >= unit_end) break;
+                if (ce == cs) continue;
+                if (tid == 0) {
+                    int spins = 0;
+                    while (__hip_atomic_load(p.flag + cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1 &&
+                           ++spins < (1 << 24))
+                        __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(p.flag + cw, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+                }
+                __syncthreads();
+                if (active) {
+                    const float* src = p.part_o + (int64_t)cw * PIECE_FLOATS;
+                    const f32x2 ml = *reinterpret_cast<const f32x2*>(src + PIECE_O + (wave * 64 + lane) * 2);
+                    const float mx = __builtin_fmaxf(m_run, ml[0]);
+                    const float wa = fast_exp2(m_run - mx), wb = fast_exp2(ml[0] - mx);
+                    l_run = l_run * wa + ml[1] * wb;
+                    m_run = mx;
+#pragma unroll
+                    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                        for (int gq = 0; gq < 4; ++gq) {
+                            const f32x4 v4 = *reinterpret_cast<const f32x4*>(
+                                src + (((wave * 16 + dt * 4 + gq) * 64) + lane) * 4);
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) o[dt][4 * gq + e] = o[dt][4 * gq + e] * wa + v4[e] * wb;
+                        }
+                }
+            }
+        }
+        if (!active) continue;
+        const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+        const int qrow_o = q0 + qi;
+        if (qrow_o < q1) {
+            const float inv = l_tot > 0.f ? 1.0f / l_tot : 0.f;
+            bf16_t* dst = p.o + (int64_t)(q_start + qrow_o) * p.ldo + hoff;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) {
+                    uint2 pk;
+                    pk.x = pack_bf16x2(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
+                    pk.y = pack_bf16x2(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
+                    *reinterpret_cast<uint2*>(dst + dt * 32 + 8 * gq + 4 * half) = pk;
+                }
+        }
+    }
+}
+
 // merge split partials: out = sum_s 2^(m_s - M) O_s / sum_s 2^(m_s - M) l_s   (one wave per (row, head))
 __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restrict__ part_o,
                                                            const float* __restrict__ part_ml, int64_t part_rows,
@@ -643,6 +1045,64 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
 
 constexpr float LOG2E = 1.4426950408889634f;
 
+int cu_count() {  // per-device, queried once
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cache[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cache[dev] = n;
+    }
+    return cache[dev];
+}
+
+int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv, void* o,
+                   int64_t ldo, const int32_t* problems, int n_problems, int n_heads, float scale, void* workspace,
+                   void* stream) {
+    RF_REQUIRE(workspace, "rf_attn_fwd: stream-K mode needs the workspace (rf_attn_workspace_bytes(0, H, 0))");
+    int grid = cu_count();
+    if (const char* env = getenv("RF_ATTN_GRID")) grid = atoi(env);  // tests: force many cut units
+    RF_REQUIRE(grid >= 1 && grid <= SK5_MAX_GRID, "rf_attn_fwd: grid %d out of range", grid);
+    AttnArgs a{};
+    a.q = (const bf16_t*)q;
+    a.k = (const bf16_t*)k;
+    a.v = (const bf16_t*)v;
+    a.o = (bf16_t*)o;
+    a.ldq = ldq;
+    a.ldk = ldk;
+    a.ldv = ldv;
+    a.ldo = ldo;
+    a.problems = problems;
+    a.n_problems = n_problems;
+    a.n_heads = n_heads;
+    a.c = scale * LOG2E;
+    a.part_o = (float*)workspace;
+    a.flag = (int*)(a.part_o + (int64_t)SK5_MAX_GRID * PIECE_FLOATS);
+    a.thr = getenv("RF_ATTN_THR") ? (float)atof(getenv("RF_ATTN_THR")) : RESCALE_LOG2;
+    // q pre-scaled by scale*log2(e) upstream (scale = ln 2): scores are already exp2 exponents
+    const bool unit = fabsf(a.c - 1.0f) < 1e-6f;
+    const int dbg = getenv("RF_ATTN_DBG") ? atoi(getenv("RF_ATTN_DBG")) : 0;
+    const dim3 g(grid), b(NW5 * 64);
+    hipStream_t st = (hipStream_t)stream;
+    switch (unit ? dbg : 0) {  // diagnostic variants (garbage results): ablation timing only
+        case 1: hipLaunchKernelGGL((attn_sk_kernel<true, 1>), g, b, 0, st, a); break;
+        case 2: hipLaunchKernelGGL((attn_sk_kernel<true, 2>), g, b, 0, st, a); break;
+        case 3: hipLaunchKernelGGL((attn_sk_kernel<true, 3>), g, b, 0, st, a); break;
+        case 4: hipLaunchKernelGGL((attn_sk_kernel<true, 4>), g, b, 0, st, a); break;
+        case 8: hipLaunchKernelGGL((attn_sk_kernel<true, 8>), g, b, 0, st, a); break;
+        case 16: hipLaunchKernelGGL((attn_sk_kernel<true, 16>), g, b, 0, st, a); break;
+        case 20: hipLaunchKernelGGL((attn_sk_kernel<true, 20>), g, b, 0, st, a); break;
+        case 11: hipLaunchKernelGGL((attn_sk_kernel<true, 11>), g, b, 0, st, a); break;
+        default:
+            if (unit)
+                hipLaunchKernelGGL((attn_sk_kernel<true, 0>), g, b, 0, st, a);
+            else
+                hipLaunchKernelGGL((attn_sk_kernel<false, 0>), g, b, 0, st, a);
+    }
+    return rf::check_launch("rf_attn_fwd");
+}
+
 }  // namespace
 
 extern "C" int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
@@ -651,11 +1111,13 @@ extern "C" int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ld
     RF_REQUIRE(q && k && v && o && problems, "rf_attn_fwd: null pointer");
     RF_REQUIRE(head_dim == HD, "rf_attn_fwd: head_dim must be 128 (got %d)", head_dim);
     RF_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0, "rf_attn_fwd: strides must be 16-B aligned");
-    RF_REQUIRE(n_split >= 1 && n_split <= 16, "rf_attn_fwd: n_split must be 1..16");
+    RF_REQUIRE(n_split >= 0 && n_split <= 16, "rf_attn_fwd: n_split must be 0..16");
     RF_REQUIRE(n_split == 1 || (workspace && ws_rows > 0), "rf_attn_fwd: split needs a workspace");
     if (n_problems <= 0 || max_q_len <= 0) return RF_OK;
-    static const int kv = getenv("RF_ATTN_KERNEL") ? atoi(getenv("RF_ATTN_KERNEL")) : 3;
-    const int qrows = kv == 2 ? 128 : 256;
+    if (n_split == 0) return attn_sk_launch(q, ldq, k, ldk, v, ldv, o, ldo, problems, n_problems, n_heads, scale,
+                                            workspace, stream);
+    const int kv = getenv("RF_ATTN_KERNEL") ? atoi(getenv("RF_ATTN_KERNEL")) : 3;
+    const int qrows = kv == 2 ? 128 : 256;  // v2: 128 rows per workgroup; v3 (8 x 32): 256
     const int n_qblk = (max_q_len + qrows - 1) / qrows;
     const int64_t total = (int64_t)n_qblk * n_heads * n_split * n_problems;
     RF_REQUIRE(total < (1ll << 31), "rf_attn_fwd: grid too large");
@@ -690,6 +1152,7 @@ extern "C" int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ld
 }
 
 extern "C" int64_t rf_attn_workspace_bytes(int64_t rows, int n_heads, int n_split) {
+    if (n_split == 0) return (int64_t)SK5_MAX_GRID * PIECE_FLOATS * 4 + SK5_MAX_GRID * 4;
     return n_split <= 1 ? 0 : (int64_t)n_split * rows * n_heads * (HD + 2) * (int64_t)sizeof(float);
 }
 

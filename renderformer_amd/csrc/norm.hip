@@ -52,6 +52,7 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(const bf16_t* src, in
                                                            int64_t ld_dst, const int32_t* __restrict__ src_rows,
                                                            int rows, int n_heads, int n_seg,
                                                            const float* __restrict__ norm_w, float eps,
+                                                           float seg0_scale,
                                                            const float* __restrict__ pos, int64_t ld_pos, int pos_div,
                                                            const float* __restrict__ freqs, int n_freqs) {
     const int lane = threadIdx.x & 63;
@@ -79,6 +80,14 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(const bf16_t* src, in
         } else {
 #pragma unroll
             for (int e = 0; e < 8; ++e) wlo[u][e] = whi[u][e] = 1.f;
+        }
+        // segment 0 (q) may carry the softmax scale * log2(e) for the attention kernel; RoPE is linear
+        if (unit < n_heads * 8) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                wlo[u][e] *= seg0_scale;
+                whi[u][e] *= seg0_scale;
+            }
         }
     }
     const int stride = gridDim.x * ROWS_PER_BLOCK;
@@ -211,7 +220,7 @@ extern "C" int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, floa
 
 extern "C" int rf_qk_norm_rope(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, const int32_t* src_rows,
                                int rows, int dim, int n_heads, int n_seg, const float* norm_w, float eps,
-                               const float* pos, int64_t ld_pos, int pos_div, const float* freqs, int n_freqs,
+                               float seg0_scale, const float* pos, int64_t ld_pos, int pos_div, const float* freqs, int n_freqs,
                                void* stream) {
     RF_REQUIRE(src && dst, "rf_qk_norm_rope: null pointer");
     RF_REQUIRE(dim == n_heads * 128 && n_seg >= 1 && n_seg * n_heads * 8 <= MAX_UNITS,
@@ -228,7 +237,7 @@ extern "C" int rf_qk_norm_rope(const void* src, int64_t ld_src, void* dst, int64
     hipStream_t st = (hipStream_t)stream;
 #define RF_QKN(U)                                                                                                 \
     hipLaunchKernelGGL(qk_norm_rope_kernel<U>, grid, dim3(256), 0, st, (const bf16_t*)src, ld_src, (bf16_t*)dst,  \
-                       ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, pos, ld_pos, pos_div, freqs, n_freqs)
+                       ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, seg0_scale, pos, ld_pos, pos_div, freqs, n_freqs)
     if (units <= 64) RF_QKN(1);
     else if (units <= 128) RF_QKN(2);
     else RF_QKN(4);

@@ -298,8 +298,9 @@ class RenderFormer:
             ops.rmsnorm(x, L.query_norm, EPS, h)
             ops.gemm(h, L.w_in, qkv)
             ops.qk_norm_rope(qk_pair, qk_pair, H, L.qk_norm if cfg.view_indep_qk_norm else None, EPS, pos1, W.enc_freqs,
-                             n_seg=2)
-            ops.attention(q, k, v, att, plan.prob1, plan.max_s, H, tag="attn_stage1", max_k_len=plan.max_s)
+                             n_seg=2, q_scale=ops.Q_LOG2_SCALE)
+            ops.attention(q, k, v, att, plan.prob1, plan.max_s, H, tag="attn_stage1", max_k_len=plan.max_s,
+                          q_prescaled=True)
             ops.gemm(att, L.w_out, x, None, ops.EPI_ADD_F32)
             ops.rmsnorm(x, L.ffn_norm, EPS, h)
             ops.gemm(h, L.w13, g, None, ops.EPI_SWIGLU, tag="gemm_w13_stage1")
@@ -329,10 +330,12 @@ class RenderFormer:
             ops.gemm(h, L.wq, q2)
             ops.rmsnorm(ctx, L.kv_norm, EPS, hc)
             ops.gemm(hc, L.wkv, kv)
-            ops.qk_norm_rope(q2, q2, H, L.q_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R)
+            ops.qk_norm_rope(q2, q2, H, L.q_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R,
+                             q_scale=ops.Q_LOG2_SCALE)
             ops.qk_norm_rope(kv[:, :D], kview, H, L.k_norm if qk else None, EPS, pos2, W.dec_freqs,
                              src_rows=plan.kv_src_rows)
-            ops.attention(q2, kview, kv[:, D:], att, plan.prob2, R, H, tag="attn_cross", max_k_len=plan.max_s)
+            ops.attention(q2, kview, kv[:, D:], att, plan.prob2, R, H, tag="attn_cross", max_k_len=plan.max_s,
+                          q_prescaled=True)
             ops.gemm(att, L.wo, x, None, ops.EPI_ADD_F32)
             # (ii) self-attention between ray tokens
             if qkv is not None:
@@ -341,13 +344,13 @@ class RenderFormer:
                 qs, ks, vs = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
                 qks = qkv[:, :2 * D]
                 if swin:
-                    ops.qk_norm_rope(qks, qks, H, L.sqk_norm if qk else None, EPS, n_seg=2)
+                    ops.qk_norm_rope(qks, qks, H, L.sqk_norm if qk else None, EPS, n_seg=2, q_scale=ops.Q_LOG2_SCALE)
                     ops.swin_attention(qs, ks, vs, att, P, plan.hp, plan.wp, 0 if i % 2 == 0 else SWIN_SHIFT, H,
-                                       SWIN_WINDOW)
+                                       SWIN_WINDOW, q_prescaled=True)
                 else:
                     ops.qk_norm_rope(qks, qks, H, L.sqk_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R,
-                                     n_seg=2)
-                    ops.attention(qs, ks, vs, att, plan.prob_self, R, H, max_k_len=R)
+                                     n_seg=2, q_scale=ops.Q_LOG2_SCALE)
+                    ops.attention(qs, ks, vs, att, plan.prob_self, R, H, max_k_len=R, q_prescaled=True)
                 ops.gemm(att, L.ws_out, x, None, ops.EPI_ADD_F32)
             # (iii) FFN
             ops.rmsnorm(x, L.ffn_norm, EPS, h)

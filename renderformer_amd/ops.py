@@ -108,9 +108,10 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor) -> 
 
 def qk_norm_rope(src: torch.Tensor, dst: torch.Tensor, n_heads: int, norm_w: Optional[torch.Tensor], eps: float,
                  pos: Optional[torch.Tensor] = None, freqs: Optional[torch.Tensor] = None, pos_div: int = 1,
-                 src_rows: Optional[torch.Tensor] = None, n_seg: int = 1) -> torch.Tensor:
+                 src_rows: Optional[torch.Tensor] = None, n_seg: int = 1, q_scale: float = 1.0) -> torch.Tensor:
     """dst[r] = rope(rmsnorm(src[src_rows[r]])) over the full width (attention.py:127-141), for n_seg
-    consecutive width-(n_heads*128) segments (q and k of a qkv row) with weights norm_w [n_seg*dim]."""
+    consecutive width-(n_heads*128) segments (q and k of a qkv row) with weights norm_w [n_seg*dim].
+    Segment 0 is also multiplied by q_scale (Q_LOG2_SCALE pre-scales q for attention(scale=LN2))."""
     _dev(src, torch.bfloat16, "src")
     _dev(dst, torch.bfloat16, "dst")
     rows, width = dst.shape
@@ -126,45 +127,54 @@ def qk_norm_rope(src: torch.Tensor, dst: torch.Tensor, n_heads: int, norm_w: Opt
         _dev(pos, torch.float32, "pos")
         _check(pos.shape[1] == 9 and freqs is not None, "qk_norm_rope: pos must be [*, 9] with freqs")
     call("rf_qk_norm_rope", ptr(src), src.stride(0), ptr(dst), dst.stride(0), ptr(src_rows), rows, dim, n_heads,
-         n_seg, ptr(norm_w), eps, ptr(pos), pos.stride(0) if pos is not None else 0, pos_div, ptr(freqs),
+         n_seg, ptr(norm_w), eps, q_scale, ptr(pos), pos.stride(0) if pos is not None else 0, pos_div, ptr(freqs),
          freqs.numel() if freqs is not None else 0, stream())
     return dst
 
 
-ATTN_QBLK = 128 if os.environ.get("RF_ATTN_KERNEL", "3") == "2" else 256  # query rows per rf_attn_fwd workgroup
+ATTN_QBLK = 128 if os.environ.get("RF_ATTN_KERNEL", "3") == "2" else 256  # query rows per legacy workgroup
+LN2 = math.log(2.0)
+# softmax scale * log2(e) for head_dim 128: q pre-multiplied by this (qk_norm_rope q_scale) lets attention run
+# with scale = ln 2, i.e. scores are exp2 exponents and the kernel needs no per-score multiply
+Q_LOG2_SCALE = 1.0 / math.sqrt(128) / LN2
+_ATTN_WS = {}
 
 
-def _auto_split(n_wg: int, kv_tiles: int) -> int:
-    """Split each key range over s workgroups (flash-decoding) to fill the 256 CUs (one workgroup each):
-    minimise rounds(n_wg * s) * (tiles per split + fixed cost of ~3 tiles for prologue/epilogue/combine)."""
-    env = os.environ.get("RF_ATTN_SPLIT")
-    if env:
-        return max(1, int(env))
-    best, best_cost = 1, None
-    for s in range(1, 9):
-        if s > 1 and kv_tiles < 4 * s:
-            break
-        cost = -(-n_wg * s // CUS) * (-(-kv_tiles // s) + 3)
-        if best_cost is None or cost < best_cost:
-            best, best_cost = s, cost
-    return best
+def _attn_workspace(device) -> torch.Tensor:
+    """Stream-K partials + per-workgroup flags, zero-filled once per device (the kernel re-arms the flags)."""
+    key = (device.type, device.index)
+    ws = _ATTN_WS.get(key)
+    if ws is None:
+        nbytes = load().rf_attn_workspace_bytes(0, 1, 0)
+        ws = torch.zeros((nbytes + 3) // 4, dtype=torch.float32, device=device)
+        _ATTN_WS[key] = ws
+    return ws
 
 
 def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int,
               scale: Optional[float] = None, tag: Optional[str] = None, max_k_len: Optional[int] = None,
-              n_split: Optional[int] = None) -> torch.Tensor:
-    """Varlen attention; problems int32 [P, 5] = (q_start, q_len, k_start, k_len, v_start)."""
+              n_split: Optional[int] = None, q_prescaled: bool = False) -> torch.Tensor:
+    """Varlen attention; problems int32 [P, 5] = (q_start, q_len, k_start, k_len, v_start).
+
+    n_split None/0: the stream-K kernel (balanced over the CUs, cut units merged in-kernel);
+    n_split >= 1: the legacy per-unit kernel with flash-decoding splits + rf_attn_combine.
+    q_prescaled: q already carries scale*log2(e) (qk_norm_rope q_scale=Q_LOG2_SCALE)."""
     for t, nme in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
         _dev(t, torch.bfloat16, nme)
     _dev(problems, torch.int32, "problems")
     _check(problems.dim() == 2 and problems.shape[1] == 5, "attention: problems must be [P, 5]")
     hd = q.shape[1] // n_heads
+    if q_prescaled:
+        _check(scale is None, "attention: q_prescaled implies the scale")
+        scale = LN2
     scale = 1.0 / math.sqrt(hd) if scale is None else scale
-    n_wg = -(-max_q_len // ATTN_QBLK) * n_heads * problems.shape[0]
     if n_split is None:
-        n_split = _auto_split(n_wg, -(-(max_k_len or 0) // 64))
+        env = os.environ.get("RF_ATTN_SPLIT")
+        n_split = int(env) if env else 0
     ws, rows = None, out.shape[0]
-    if n_split > 1:
+    if n_split == 0:
+        ws = _attn_workspace(out.device)
+    elif n_split > 1:
         nbytes = load().rf_attn_workspace_bytes(rows, n_heads, n_split)
         ws = torch.empty(nbytes // 4, dtype=torch.float32, device=out.device)
     ev = _t0(tag)
@@ -177,12 +187,12 @@ def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int
 
 
 def swin_attention(q, k, v, out, n_images: int, grid_h: int, grid_w: int, shift: int, n_heads: int,
-                   window: int = 8) -> torch.Tensor:
+                   window: int = 8, q_prescaled: bool = False) -> torch.Tensor:
     for t, nme in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
         _dev(t, torch.bfloat16, nme)
     hd = q.shape[1] // n_heads
     call("rf_swin_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out), out.stride(0),
-         n_images, grid_h, grid_w, window, shift, n_heads, hd, 1.0 / math.sqrt(hd), stream())
+         n_images, grid_h, grid_w, window, shift, n_heads, hd, LN2 if q_prescaled else 1.0 / math.sqrt(hd), stream())
     return out
 
 

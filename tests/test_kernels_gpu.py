@@ -211,8 +211,18 @@ def _ref_attn(q, k, v, H):
     return (torch.softmax(s, -1) @ vh).transpose(0, 1).reshape(lq, H * 128)
 
 
+@pytest.fixture(params=["sk", "sk_grid7", "sk_grid61", "legacy"])
+def attn_mode(request, monkeypatch):
+    """Varlen attention modes: the stream-K kernel on the full grid, on small grids that cut most units
+    into 2-3 pieces merged by their owner (RF_ATTN_GRID), and the legacy per-unit kernel (n_split=1).
+    Returns the n_split to pass."""
+    if request.param.startswith("sk_grid"):
+        monkeypatch.setenv("RF_ATTN_GRID", request.param[len("sk_grid"):])
+    return 1 if request.param == "legacy" else None
+
+
 @pytest.mark.parametrize("lens", [[1], [63], [64, 65], [77, 200, 1], [5649]])
-def test_attention_varlen_self(lens):
+def test_attention_varlen_self(lens, attn_mode):
     ops = _ops()
     H = 2
     D = H * 128
@@ -226,7 +236,7 @@ def test_attention_varlen_self(lens):
     out = torch.zeros(T, D, device=dev, dtype=torch.bfloat16)
     d = qkv.to(dev)
     ops.attention(d[:, :D], d[:, D:2 * D], d[:, 2 * D:], out, torch.tensor(probs, dtype=torch.int32, device=dev),
-                  max(lens), H)
+                  max(lens), H, n_split=attn_mode)
     out = out.float().cpu()
     off = 0
     for n in lens:
@@ -267,7 +277,7 @@ def test_attention_split_kv(n_split):
             off += n
 
 
-def test_attention_cross_shared_v():
+def test_attention_cross_shared_v(attn_mode):
     """Stage-2 form: per-view K rows, V rows shared by the views of a scene."""
     ops = _ops()
     H, D, R = 2, 256, 64
@@ -285,12 +295,79 @@ def test_attention_cross_shared_v():
             p += 1
         voff += s
     out = torch.empty_like(q).to(dev)
-    ops.attention(q.to(dev), kview.to(dev), vsc.to(dev), out, torch.tensor(probs, dtype=torch.int32, device=dev), R, H)
+    ops.attention(q.to(dev), kview.to(dev), vsc.to(dev), out, torch.tensor(probs, dtype=torch.int32, device=dev), R, H,
+                  n_split=attn_mode)
     out = out.float().cpu()
     for pr in probs:
         qs, ql, ks, kl, vs = pr
         ref = _ref_attn(q[qs:qs + ql].float(), kview[ks:ks + kl].float(), vsc[vs:vs + kl].float(), H)
         assert relerr(out[qs:qs + ql], ref) < 6e-3
+
+
+@pytest.mark.parametrize("thr", ["8", "0"])
+@pytest.mark.parametrize("grid", [None, "5", "23"])
+def test_attention_stream_k_prescaled_rescale(thr, grid, monkeypatch):
+    """The model's form: q pre-scaled by scale*log2(e) (scores are exp2 exponents, no per-score multiply),
+    ragged problems with tail tiles, key spikes that force the deferred-rescale branch at chosen tiles
+    (incl. right after a piece boundary), repeated launches on the re-armed workspace.  THR=0 (rescale on
+    every growth) and the shipped THR=8 must both match the fp64 reference (guide rule 26)."""
+    monkeypatch.setenv("RF_ATTN_THR", thr)
+    if grid:
+        monkeypatch.setenv("RF_ATTN_GRID", grid)
+    ops = _ops()
+    H = 4
+    D = H * 128
+    lens = [1000, 129, 700, 65]
+    T = sum(lens)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    qkv = torch.randn(T, 3 * D, generator=g).bfloat16()
+    for r in (5, 640, 960, 1129 + 64, 1129 + 699):  # late large keys: scores jump by >> 2^8 mid-sequence
+        qkv[r, D:2 * D] = (qkv[r, D:2 * D].float() * 6.0).bfloat16()
+    probs, off = [], 0
+    for n in lens:
+        probs.append([off, n, off, n, off])
+        off += n
+    d = qkv.to(dev)
+    qs = (d[:, :D].float() * ops.Q_LOG2_SCALE).bfloat16()
+    pt = torch.tensor(probs, dtype=torch.int32, device=dev)
+    for _ in range(3):
+        out = torch.zeros(T, D, device=dev, dtype=torch.bfloat16)
+        ops.attention(qs, d[:, D:2 * D], d[:, 2 * D:], out, pt, max(lens), H, q_prescaled=True)
+        o = out.float().cpu()
+        off = 0
+        for n in lens:
+            sl = slice(off, off + n)
+            qref = qs[sl].float().cpu() / ops.Q_LOG2_SCALE
+            ref = _ref_attn(qref, qkv[sl, D:2 * D].float(), qkv[sl, 2 * D:].float(), H)
+            assert relerr(o[sl], ref) < 6e-3, (thr, grid, n)
+            off += n
+
+
+def test_attention_stream_k_many_problems():
+    """A batch of scenes of very different lengths (batch_infer form): 24 problems, 8 heads, the
+    flattened space crossing problem boundaries inside workgroup ranges."""
+    ops = _ops()
+    H = 8
+    D = H * 128
+    g = torch.Generator(device="cpu").manual_seed(11)
+    lens = [int(x) for x in torch.randint(1, 700, (24,), generator=g)]
+    T = sum(lens)
+    qkv = torch.randn(T, 3 * D, generator=g).bfloat16()
+    probs, off = [], 0
+    for n in lens:
+        probs.append([off, n, off, n, off])
+        off += n
+    d = qkv.to(dev)
+    out = torch.zeros(T, D, device=dev, dtype=torch.bfloat16)
+    ops.attention(d[:, :D], d[:, D:2 * D], d[:, 2 * D:], out, torch.tensor(probs, dtype=torch.int32, device=dev),
+                  max(lens), H)
+    o = out.float().cpu()
+    off = 0
+    for n in lens:
+        sl = slice(off, off + n)
+        ref = _ref_attn(qkv[sl, :D].float(), qkv[sl, D:2 * D].float(), qkv[sl, 2 * D:].float(), H)
+        assert relerr(o[sl], ref) < 6e-3, n
+        off += n
 
 
 @pytest.mark.parametrize("grid,shift", [(8, 0), (8, 4), (16, 4), (16, 0)])

@@ -38,7 +38,7 @@ def attn_check():
     out = torch.empty(T, D, device=dev, dtype=torch.bfloat16)
     prob = torch.tensor([[0, 1000, 0, 1000, 0], [1000, 333, 1000, 333, 1000]], dtype=torch.int32, device=dev)
     worst = 0.0
-    for sp in (1, 3):
+    for sp in (0, 1, 3):
         ops.attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], out, prob, 1000, H, n_split=sp)
         st = 0
         for n in lens:
@@ -51,22 +51,31 @@ def attn_check():
 
 
 def attn():
+    """stream-K kernel (n_split 0, q pre-scaled as in the model) vs the legacy per-unit kernel with splits."""
     attn_check()
     qkv = (torch.randn(S, 3 * D, device=dev) * 2).bfloat16()
+    qs = (qkv[:, :D].float() * ops.Q_LOG2_SCALE).bfloat16()
     out = torch.empty(S, D, device=dev, dtype=torch.bfloat16)
     prob = torch.tensor([[0, S, 0, S, 0]], dtype=torch.int32, device=dev)
     fl = 4 * S * S * D
-    for sp in (1, 2, 3, 4, 6):
+    ms = timeit(lambda: ops.attention(qs, qkv[:, D:2 * D], qkv[:, 2 * D:], out, prob, S, H, q_prescaled=True))
+    print(f"attn stage1 S={S} stream-K (prescaled q): {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF")
+    ms = timeit(lambda: ops.attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], out, prob, S, H, n_split=0))
+    print(f"attn stage1 S={S} stream-K (scale mult): {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF")
+    for sp in (1, 4):
         ms = timeit(lambda: ops.attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], out, prob, S, H, n_split=sp))
-        print(f"attn stage1 S={S} split={sp}: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF")
+        print(f"attn stage1 S={S} legacy split={sp}: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF")
     q = torch.randn(R, D, device=dev).bfloat16()
+    q2 = (q.float() * ops.Q_LOG2_SCALE).bfloat16()
     kv = torch.randn(S, 2 * D, device=dev).bfloat16()
     prob2 = torch.tensor([[0, R, 0, S, 0]], dtype=torch.int32, device=dev)
     o2 = torch.empty(R, D, device=dev, dtype=torch.bfloat16)
     fl = 4 * R * S * D
-    for sp in (1, 2, 3, 4):
+    ms = timeit(lambda: ops.attention(q2, kv[:, :D], kv[:, D:], o2, prob2, R, H, q_prescaled=True))
+    print(f"attn cross R={R} S={S} stream-K: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF")
+    for sp in (1, 2):
         ms = timeit(lambda: ops.attention(q, kv[:, :D], kv[:, D:], o2, prob2, R, H, n_split=sp))
-        print(f"attn cross R={R} S={S} split={sp}: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF")
+        print(f"attn cross R={R} S={S} legacy split={sp}: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF")
     qkv2 = torch.randn(R, 3 * D, device=dev).bfloat16()
     for sh in (0, 4):
         ms = timeit(lambda: ops.swin_attention(qkv2[:, :D], qkv2[:, D:2 * D], qkv2[:, 2 * D:], o2, 1, 64, 64, sh, H))
