@@ -632,15 +632,20 @@ __global__ __launch_bounds__(NW3 * 64, 1) void attn_v3_kernel(AttnArgs p) {
 // partial (O, m, l in register order, sc1 stores + flag) and folded into the owner's registers
 // before its epilogue.  Q-blocks split each problem's rows evenly (<= 256 rows each).
 //
-// Main loop, per 64-key tile t (8 waves x 32 query rows, one barrier per tile):
-//   * K(t+2) and V(t+1) arrive by LDS-DMA (inline asm, so hipcc does not put a vmcnt(0) in front
-//     of the transposed V reads of the same tile) into 2-deep K and V rings (64 KiB); the loop is
-//     unrolled by 2 so every LDS offset is an immediate.
-//   * S(t+1) = K(t+1) Q^T (v_mfma_f32_32x32x16_bf16, query on the lane) is issued in one block with
-//     the softmax of S(t) and O^T += V(t)^T P(t)^T, so exp/convert VALU work overlaps the MFMAs.
+// Main loop, per 64-key tile t (8 waves x 32 query rows), two half-tile phases split by barriers:
+//   A(t): softmax of S(t) (exp2 / bf16 pack / row sums: the VALU work) woven into
+//         S(t+1) = K(t+1) Q^T (16 v_mfma_f32_32x32x16_bf16, query on the lane);
+//   B(t): O^T += V(t)^T P(t)^T (16 MFMAs, P as the B operand with no lane movement).
+//   Waves 4-7 run one phase behind waves 0-3, so each SIMD pairs A of one wave with B of its partner
+//   (VALU beside MFMA instead of both waves fighting over the same pipe).
+//   * K(t+2) / V(t+1) arrive by LDS-DMA at the top of A(t) / B(t) (inline asm, so hipcc does not
+//     put a vmcnt(0) in front of the transposed V reads) into 2-deep K and V rings (64 KiB), and are
+//     waited for at the end of that phase; the loop is unrolled by 2 so every LDS offset is an
+//     immediate.
 //   * q arrives pre-scaled by scale*log2(e) (rf_qk_norm_rope seg0_scale) and the QK^T chain starts
 //     from C = -m (the running max), so P = exp2(S) needs no per-score FMA (UNIT); the max is only
-//     re-based (deferred rescale, guide T13) when a row grows by more than 2^8.
+//     re-based (deferred rescale, guide T13) when a row grows by more than 2^8, checked at the end of
+//     B(t) on S(t+1) (its row max is taken in B's gaps), after all of P(t) is in O and l.
 constexpr int NW5 = 8;
 constexpr int QB5 = NW5 * 32;
 constexpr int K5 = 0;                  // K ring: 2 x 16 KiB
@@ -649,25 +654,20 @@ constexpr int SK5_MAX_GRID = 512;
 constexpr int PIECE_O = QB5 * HD;                // f32, register order
 constexpr int PIECE_FLOATS = PIECE_O + QB5 * 2 * 2;  // + (m, l) per lane
 
-RF_DEV float vmax3(float a, float b, float c) {  // single v_max3_f32 (no canonicalising v_max in front)
-    float r;
-    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
+RF_DEV float vmax3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }  // v_max3_f32
 
 // One 1-KiB LDS-DMA piece: lane l's 16 B land at LDS byte lds + 16 l.  Inline asm so hipcc neither
-// counts it (the loop waits with its own vmcnt) nor guards later ds_read_b64_tr_b16 with vmcnt(0);
-// M0 is compiler-reserved, so it is saved and restored inside the statement (guide §5.7).
+// counts it (the loop waits with its own vmcnt) nor guards later ds_read_b64_tr_b16 with vmcnt(0).
+// M0 is declared clobbered (hipcc warns: reserved register); the kernel has no other M0 user (checked
+// in the .s: every m0 access is one of these statements), so it is not saved/restored (guide §5.7).
 RF_DEV void dma_piece(const bf16_t* g, uint32_t lds) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(g), "s"(lds)
-                 : "memory");
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
 }
 
 // DBG (diagnostic builds only, RF_ATTN_DBG; results are garbage): 1 = no K/V DMA in the loop,
-// 2 = no top-of-tile wait + barrier, 4 = no PV MFMAs, 8 = no exp2 (P = bf16(S)), 16 = no QK MFMAs
+// 2 = no top-of-tile wait + barrier, 4 = no PV MFMAs, 8 = no exp2 (P = bf16(S)), 16 = no QK MFMAs,
+// 32 = s_memtime stamps per segment (cycles summed over tiles) into the workspace's last piece slot,
+// 64 = no static priority for waves 4-7
 template <bool UNIT, int DBG = 0>
 __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // 64 KiB
@@ -677,8 +677,10 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     const int wave = tid >> 6;
     const int half = lane >> 5;
     const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
-    // the second-dispatched half loses VALU arbitration every segment: static priority (guide T5)
-    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+    const bool late = __builtin_amdgcn_readfirstlane(tid) >= 256;  // waves 4-7 (SIMD partners of 0-3)
+    // the second-dispatched half loses VALU arbitration to its older partner: static priority (guide T5)
+    if constexpr (!(DBG & 64))
+        if (late) __builtin_amdgcn_s_setprio(1);
 
     const int nwg = gridDim.x, hw = blockIdx.x;
     const int xcd = hw & 7, qd = nwg >> 3, rm = nwg & 7;
@@ -713,6 +715,16 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     int pi = -1;
     int64_t base = 0, usz = 0;
     int q_start = 0, q_len = 0, k_start = 0, k_len = 0, v_start = 0, nqb = 1, nt = 1;
+    // DBG & 32: top wait, K DMA issue, mask+max+check, A, seam wait, V DMA issue, B, tiles
+    uint64_t stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t t_prev = 0;
+    auto stamp_at = [&](int k) {
+        if constexpr (DBG & 32) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            stamp[k] += now - t_prev;
+            t_prev = now;
+        }
+    };
     while (it < it_end) {
         while (it >= base + usz) {  // advance to the problem holding tile `it`
             base += usz;
@@ -780,8 +792,9 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         f32x16 minit;
 #pragma unroll
         for (int r = 0; r < 16; ++r) minit[r] = 0.f;
-        float carry = 0.f;
-        bool fresh = true, carried = false;
+
+        float carry = 0.f;     // exp2 units S(t+1) sits above the current base (after a rescale)
+        bool carried = false;  // wave-uniform: some lane has carry != 0
 
         auto qk = [&](const int koff, f32x16* s) {
 #pragma unroll
@@ -793,84 +806,84 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                     s[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[st], st == 0 ? minit : s[b], 0, 0, 0);
                 }
         };
-
-        issue(kp, p.ldk, kstep, kt0, lds0 + K5);
-        issue(vp, p.ldv, vstep, kt0, lds0 + V5);
-        if (n > 1) {
-            issue(kp, p.ldk, kstep, kt0 + 1, lds0 + K5 + TILE_BYTES);
-            attn_wait_vm<4>();
-        } else {
-            attn_wait_vm<2>();
-        }
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        f32x16 sA[2], sB[2];
-        qk(K5, sA);
-
-        auto body = [&](const int i, auto par_c, f32x16(&s)[2], f32x16(&sn)[2]) {
-            constexpr int PAR = decltype(par_c)::value;
-            const int t = kt0 + i;
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (!(DBG & 2)) {
-                attn_wait_vm<0>();             // K(t+1) and V(t) landed for this wave ...
-                __builtin_amdgcn_s_barrier();  // ... and for every wave; K(t) and V(t-1) are free
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (!(DBG & 1)) {
-                if (i + 2 < n) issue(kp, p.ldk, kstep, t + 2, lds0 + K5 + PAR * TILE_BYTES);
-                if (i + 1 < n) issue(vp, p.ldv, vstep, t + 1, lds0 + V5 + (PAR ^ 1) * TILE_BYTES);
-            }
-            // (a wave with no valid rows computes clamped duplicates: no branch, so no register shuffles)
-
+        auto mask_tail = [&](f32x16* sv, int t) {  // keys >= k_len of tile t -> -inf (tail tile only)
             if ((t + 1) * KT > k_len) {
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int key = b * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                        s[b][r] = t * KT + key >= k_len ? NEG : s[b][r];
+                        sv[b][r] = t * KT + key >= k_len ? NEG : sv[b][r];
                     }
             }
-            float mt = vmax3(s[0][0], s[0][1], s[0][2]);
+        };
+        // rare path: bring S onto the current base (minus `carry`), then re-base the running max on its row
+        // max (exactly on a piece's first tile).  Everything accumulated so far (O, l) is at the old base.
+        // minit is rebuilt in every phase B from m_run, so the S issued next (already built on the old
+        // base) is `delta` too high: `carry` records that for the next check.
+        auto rebase = [&](f32x16* sv, float mt, bool fresh) {
+            const float cs = carry * inv_c;
+            const float mrow = (__builtin_fmaxf(mt, __shfl_xor(mt, 32, 64)) - cs) * c;
+            const float delta = fresh ? mrow : __builtin_fmaxf(mrow, 0.f);
+            const float alpha = fresh ? 1.f : fast_exp2(-delta);
+            l_run *= alpha;
 #pragma unroll
-            for (int r = 3; r < 15; r += 2) mt = vmax3(mt, s[0][r], s[0][r + 1]);
-            mt = vmax3(mt, s[0][15], s[1][0]);
+            for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-            for (int r = 1; r < 15; r += 2) mt = vmax3(mt, s[1][r], s[1][r + 1]);
-            mt = vmax3(mt, s[1][15], s[1][15]);
-            if (fresh || carried || __any(mt * c > p.thr)) {
-                // bring S(t) onto the current base, then re-base the running max on this tile's row max
-                // (exact on a piece's first tile)
-                const float cs = carry * inv_c;
+                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+            m_run += delta;
+            const float ds = cs + delta * inv_c;
 #pragma unroll
-                for (int b = 0; b < 2; ++b)
+            for (int b = 0; b < 2; ++b)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) s[b][r] -= cs;
-                const float mrow = (__builtin_fmaxf(mt, __shfl_xor(mt, 32, 64)) - cs) * c;
-                const float delta = fresh ? mrow : __builtin_fmaxf(mrow, 0.f);
-                const float alpha = fresh ? 1.f : fast_exp2(-delta);
-                l_run *= alpha;
+                for (int r = 0; r < 16; ++r) sv[b][r] -= ds;
+            carry = delta;
+            carried = __any(delta != 0.f);
+        };
+
+        issue(kp, p.ldk, kstep, kt0, lds0 + K5);
+        issue(vp, p.ldv, vstep, kt0, lds0 + V5);
+        if (n > 1) issue(kp, p.ldk, kstep, kt0 + 1, lds0 + K5 + TILE_BYTES);
+        attn_wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        f32x16 sA[2], sB[2];
+        qk(K5, sA);  // raw scores of the piece's first tile (base 0)
+        mask_tail(sA, kt0);
+        {
+            float mt = vmax3(sA[0][0], sA[0][1], sA[0][2]);
 #pragma unroll
-                for (int dt = 0; dt < 4; ++dt)
+            for (int r = 3; r < 15; r += 2) mt = vmax3(mt, sA[0][r], sA[0][r + 1]);
+            mt = vmax3(mt, sA[0][15], sA[1][0]);
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-                m_run += delta;
-                const float ds = delta * inv_c;
+            for (int r = 1; r < 15; r += 2) mt = vmax3(mt, sA[1][r], sA[1][r + 1]);
+            mt = vmax3(mt, sA[1][15], sA[1][15]);
+            rebase(sA, mt, true);
+        }
+        carry = 0.f;  // minit is rebuilt below from the new base: S(kt0 + 1) needs no correction
+        carried = false;
 #pragma unroll
-                for (int b = 0; b < 2; ++b)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) s[b][r] -= ds;
-                carry = delta;
-                carried = __any(delta != 0.f);
-                fresh = false;
+        for (int r = 0; r < 16; ++r) minit[r] = -m_run * inv_c;
+        // stagger (guide MI355X_MICROARCH "Two waves per SIMD", item 9): waves 4-7 run half a tile behind,
+        // so on every SIMD one wave's phase A (QK^T + softmax VALU) pairs with its partner's phase B (PV)
+        if (late) __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+
+        // one tile: A(t) = softmax(S(t)) woven into S(t+1) = K(t+1) Q^T; seam; B(t) = PV(t) with the
+        // minit rebuild and the row max of S(t+1) woven in; then the (rare) rescale of S(t+1)
+        auto body = [&](const int i, auto par_c, f32x16(&s)[2], f32x16(&sn)[2]) {
+            constexpr int PAR = decltype(par_c)::value;
+            const int t = kt0 + i;
+            const bool has_next = i + 1 < n;
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (DBG & 32) t_prev = __builtin_amdgcn_s_memtime();
+            if constexpr (!(DBG & 2)) {
+                attn_wait_vm<0>();             // K(t+1) and V(t) landed for this wave ...
+                __builtin_amdgcn_s_barrier();  // ... and for every wave; K(t) and V(t-1) are free
             }
             __builtin_amdgcn_sched_barrier(0);
+            stamp_at(0);
 
-            // ---- hand-placed block (sched_barrier walls keep the source order):
-            // phase A: S(t+1) = K(t+1) Q^T as two alternating independent chains, each gap carrying two
-            //          exp2 and one bf16 pack of P(t); K fragments read two MFMAs ahead (3-deep ring).
-            // phase B: O^T += V(t)^T P(t)^T as four alternating chains, V^T fragments (2 transposed
-            //          reads each) two MFMAs ahead; the row-sum adds ride in its gaps.
             const int koff = K5 + (PAR ^ 1) * TILE_BYTES;
             const int voff = V5 + PAR * TILE_BYTES;
             auto kread = [&](int j) {  // QK step j: chain b = j & 1, k-slice st = j >> 1
@@ -888,14 +901,15 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             bf16x8 kf[3], vf[3];
             bf16x8 pf[2][2];
             float ls[4];
+
+            // ---- phase A: S(t+1) chains b = 0, 1 alternating; each gap: 2 exp2, 2 row-sum adds, 1 bf16 pack
+            // of P(t); K fragments two MFMAs ahead; K(t+2)'s LDS-DMA rides in gap 1
             kf[0] = kread(0);
             kf[1] = kread(1);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 if (j + 2 < 16) kf[(j + 2) % 3] = kread(j + 2);
-                if (j == 14) vf[0] = vread(0);
-                if (j == 15) vf[1] = vread(1);
                 const int b = j & 1, st = j >> 1;
                 if constexpr (DBG & 16) {
                     if (st == 0) sn[b] = minit;
@@ -914,8 +928,27 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 }
                 pf[j >> 3][(j >> 2) & 1][2 * (j & 3)] = (__bf16)e[0];
                 pf[j >> 3][(j >> 2) & 1][2 * (j & 3) + 1] = (__bf16)e[1];
+                if constexpr (!(DBG & 1)) {
+                    if (j == 1 && i + 2 < n) issue(kp, p.ldk, kstep, t + 2, lds0 + K5 + PAR * TILE_BYTES);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
+            stamp_at(1);
+            // ---- half-tile seam: K(t+2) landed for this wave; the partner group switches phase
+            if constexpr (!(DBG & 2)) {
+                attn_wait_vm<0>();
+                __builtin_amdgcn_s_barrier();
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            stamp_at(2);
+            if (has_next) mask_tail(sn, t + 1);
+
+            // ---- phase B: four O chains alternating; V^T fragments two MFMAs ahead; V(t+1)'s LDS-DMA in gap
+            // 1; each gap also rebuilds one register of minit and takes one max3 step over S(t+1)
+            vf[0] = vread(0);
+            vf[1] = vread(1);
+            float mt = 0.f;
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 if (j + 2 < 16) vf[(j + 2) % 3] = vread(j + 2);
@@ -927,9 +960,26 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 }
                 minit[j] = -m_run * inv_c;
                 asm volatile("" : "+v"(minit[j]));  // one v_mov per PV gap (otherwise hoisted into phase A)
+                if (j == 0) {
+                    mt = vmax3(sn[0][0], sn[0][1], sn[0][2]);
+                } else if (j < 15) {
+                    const int x = 2 * j + 1;  // values x, x + 1 of the flattened 32
+                    mt = vmax3(mt, sn[x >> 4][x & 15], sn[(x + 1) >> 4][(x + 1) & 15]);
+                } else {
+                    mt = vmax3(mt, sn[1][15], sn[1][15]);
+                }
+                if constexpr (!(DBG & 1)) {
+                    if (j == 1 && has_next) issue(vp, p.ldv, vstep, t + 1, lds0 + V5 + (PAR ^ 1) * TILE_BYTES);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
             l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+            stamp_at(3);
+            // ---- deferred rescale (guide T13) for S(t+1): P(t) is fully in O and l, so all of it is rescaled
+            if (has_next && (carried || __any(mt * c > p.thr))) rebase(sn, mt, false);
+            __builtin_amdgcn_sched_barrier(0);
+            stamp_at(4);
+            if constexpr (DBG & 32) stamp[7] += 1;
         };
         int i = 0;
         for (; i + 1 < n; i += 2) {
@@ -937,6 +987,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             body(i + 1, std::integral_constant<int, 1>{}, sB, sA);
         }
         if (i < n) body(i, std::integral_constant<int, 0>{}, sA, sB);
+        if (!late) __builtin_amdgcn_s_barrier();  // re-align the groups' barrier counts
 
         // ---- piece epilogue.  Register order: lane owns query (lane & 31), d = dt*32 + 8 gq + 4 half + 0..3
         float* piece = p.part_o + (int64_t)wg * PIECE_FLOATS;
@@ -1012,6 +1063,13 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                     pk.y = pack_bf16x2(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
                     *reinterpret_cast<uint2*>(dst + dt * 32 + 8 * gq + 4 * half) = pk;
                 }
+        }
+    }
+    if constexpr (DBG & 32) {  // diagnostic: [wg][wave][6] u64 in the last piece slot of the workspace
+        if (lane == 0) {
+            uint64_t* dbg = reinterpret_cast<uint64_t*>(p.part_o + (int64_t)(SK5_MAX_GRID - 1) * PIECE_FLOATS);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) dbg[(wg * NW5 + wave) * 8 + k] = stamp[k];
         }
     }
 }
@@ -1094,6 +1152,9 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
         case 16: hipLaunchKernelGGL((attn_sk_kernel<true, 16>), g, b, 0, st, a); break;
         case 20: hipLaunchKernelGGL((attn_sk_kernel<true, 20>), g, b, 0, st, a); break;
         case 11: hipLaunchKernelGGL((attn_sk_kernel<true, 11>), g, b, 0, st, a); break;
+        case 32: hipLaunchKernelGGL((attn_sk_kernel<true, 32>), g, b, 0, st, a); break;
+        case 64: hipLaunchKernelGGL((attn_sk_kernel<true, 64>), g, b, 0, st, a); break;
+        case 96: hipLaunchKernelGGL((attn_sk_kernel<true, 96>), g, b, 0, st, a); break;
         default:
             if (unit)
                 hipLaunchKernelGGL((attn_sk_kernel<true, 0>), g, b, 0, st, a);

@@ -24,22 +24,49 @@ def run():
     ops.attention(qs, qkv[:, D:2 * D], qkv[:, 2 * D:], out, prob, S, H, q_prescaled=True)
 
 
+if len(sys.argv) > 1 and sys.argv[1] == "stamps":
+    os.environ["RF_ATTN_DBG"] = sys.argv[2] if len(sys.argv) > 2 else "32"
+    for _ in range(30):
+        run()
+    torch.cuda.synchronize()
+    ws = ops._attn_workspace(out.device)
+    piece = (ws.numel() - 512) // 512
+    st = ws[511 * piece:511 * piece + 256 * 8 * 16].view(torch.int64).view(256, 8, 8).cpu().double()
+    tiles = st[..., 7].clamp_min(1)
+    names = ["top wait", "A (+K DMA)", "seam wait", "B (+V DMA, max)", "check", "-", "-"]
+    for grp, sl in (("waves 0-3", slice(0, 4)), ("waves 4-7", slice(4, 8))):
+        per = (st[:, sl, :7] / tiles[:, sl, None]).mean(dim=(0, 1))
+        print(grp, "cycles/tile:", ", ".join(f"{n} {v:.0f}" for n, v in zip(names, per.tolist())),
+              f"| total {per.sum():.0f}", flush=True)
+    sys.exit(0)
 if len(sys.argv) > 1 and sys.argv[1] == "pmc":
     for _ in range(int(sys.argv[2]) if len(sys.argv) > 2 else 5):
         run()
     torch.cuda.synchronize()
     sys.exit(0)
 fl = 4 * S * S * D
-for dbg in ("0", "1", "2", "3", "4", "8", "16", "20", "11", "0"):
+VARIANTS = os.environ.get("ABL", "0,64,1,2,4,8,16,20").split(",")
+
+
+def timed(dbg, reps=20):
     os.environ["RF_ATTN_DBG"] = dbg
-    for _ in range(3):
-        run()
+    run()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(20):
+    for _ in range(reps):
         run()
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / 20
-    print(f"dbg={dbg:>2}: {ms*1e3:7.1f} us  {fl/ms/1e9:7.1f} TF(equiv)", flush=True)
+    return e0.elapsed_time(e1) / reps
+
+
+for _ in range(30):  # clocks settle
+    timed("0", 5)
+res = {v: [] for v in VARIANTS}
+for rnd in range(3):  # interleaved rounds, median (guide rule 24)
+    for v in VARIANTS:
+        res[v].append(timed(v))
+for v in VARIANTS:
+    ms = sorted(res[v])[1]
+    print(f"dbg={v:>3}: {ms*1e3:7.1f} us  {fl/ms/1e9:7.1f} TF(equiv)  (min {min(res[v])*1e3:.1f})", flush=True)

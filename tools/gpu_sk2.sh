@@ -1,0 +1,10 @@
+# attention tests + ablation timing (quick loop for attention kernel work).  usage: bash tools/gpu_sk2.sh <tag>
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${1:-sk}
+mkdir -p $O
+cd $R
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "attention or swin" -x -q --timeout 120 --timeout-method thread > $O/t_attn.log 2>&1
+timeout -k 10 200 python tools/attn_ablate.py > $O/ablate.log 2>&1
+timeout -k 10 200 python tools/kbench.py attn > $O/kb_attn.log 2>&1
+echo done
