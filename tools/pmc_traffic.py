@@ -13,13 +13,23 @@ import sys
 from collections import defaultdict
 
 
+ATTN_CYCLE = (14, 10)  # bench frame: 14 stage-1 then 10 cross-attention launches of attn_sk_kernel
+
+
 def load(path, counter):
+    """Average per (kernel, grid); the stream-K attention launches all have grid = #CUs, so they are split
+    into stage-1 / cross by their position in the per-frame launch sequence."""
     per = defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter:
-            continue
-        key = (r["Kernel_Name"], int(r["Grid_Size"]) // max(1, int(r["Workgroup_Size"])))
-        per[key].append(float(r["Counter_Value"]) * 1024.0)
+    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    n_attn = 0
+    for r in rows:
+        name = r["Kernel_Name"]
+        grid = int(r["Grid_Size"]) // max(1, int(r["Workgroup_Size"]))
+        if "attn_sk_kernel" in name:
+            name += " [stage-1]" if n_attn % sum(ATTN_CYCLE) < ATTN_CYCLE[0] else " [cross]"
+            n_attn += 1
+        per[(name, grid)].append(float(r["Counter_Value"]) * 1024.0)
     return per
 
 
@@ -38,6 +48,13 @@ def main():
               f"wr {r['write_bytes_per_launch']/1e6:9.2f}) n={r['launches']:4d} grid={r['grid']:6d} {r['kernel'][:90]}")
     if len(sys.argv) > 3:
         json.dump(rows, open(sys.argv[3], "w"), indent=1)
+    st1 = [r for r in rows if "[stage-1]" in r["kernel"]]
+    if st1:
+        json.dump({"kernel": st1[0]["kernel"], "hbm_bytes_per_launch": st1[0]["hbm_bytes_per_launch"],
+                   "read_bytes_per_launch": st1[0]["read_bytes_per_launch"],
+                   "write_bytes_per_launch": st1[0]["write_bytes_per_launch"], "launches": st1[0]["launches"],
+                   "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --profile (separate runs)"},
+                  open("profiles/attn_stage1_traffic.json", "w"), indent=1)
 
 
 if __name__ == "__main__":
