@@ -26,6 +26,7 @@
 #include <cmath>
 #include <math.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "common.h"
 
@@ -1076,6 +1077,15 @@ bool skph(int m, int n, int k) {
 
 extern "C" int64_t rf_gemm_workspace_bytes(void) { return SK_WS_BYTES; }
 
+namespace rf {
+int blaslt_gemm(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int m, int n, int k,
+                int mode, const float* bias, void* workspace, int64_t ws_bytes, void* stream);
+bool gemm_engine_forced() {
+    const char* be = getenv("RF_GEMM_BACKEND");
+    return be && strcmp(be, "hip") == 0;
+}
+}  // namespace rf
+
 extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
                             const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
                             void* stream) {
@@ -1088,6 +1098,13 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
     RF_REQUIRE(epilogue >= RF_EPI_BF16 && epilogue <= RF_EPI_SWIGLU, "rf_gemm_bf16: bad epilogue %d", epilogue);
     RF_REQUIRE(ldc >= (epilogue == RF_EPI_SWIGLU ? n / 2 : n) && ldc % 4 == 0, "rf_gemm_bf16: ldc too small/unaligned");
     RF_REQUIRE(((uintptr_t)c & 7) == 0, "rf_gemm_bf16: output must be 8-B aligned");
+    // plain epilogues (bf16 out, fp32 out + bias, fp32 residual accumulate) go to hipBLASLt, which is
+    // faster on every plain projection shape of the path (tools/kbench.py); RF_GEMM_BACKEND=hip keeps them
+    // on the engine below.  The fused epilogues (SwiGLU) are engine-only.
+    if (epilogue != RF_EPI_SWIGLU && (epilogue == RF_EPI_F32 || !bias) && !rf::gemm_engine_forced()) {
+        const int r = rf::blaslt_gemm(a, lda, w, ldw, c, ldc, m, n, k, epilogue, bias, workspace, ws_bytes, stream);
+        if (r != -1) return r;
+    }
     EngineArgs p{};
     p.a = (const bf16_t*)a;
     p.lda = lda;

@@ -31,9 +31,13 @@ def relerr(a, b):
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
+@pytest.mark.parametrize("backend", ["auto", "hip"])
 @pytest.mark.parametrize("m,n,k", [(1, 128, 64), (77, 256, 128), (333, 384, 192), (5649, 1024, 1024),
-                                   (1000, 128, 13312), (4096, 3072, 1024)])
-def test_gemm_f32_bf16(m, n, k):
+                                   (1000, 128, 13312), (4096, 3072, 1024), (5649, 1024, 4096)])
+def test_gemm_f32_bf16(m, n, k, backend, monkeypatch):
+    """Plain epilogues on both backends: hipBLASLt (auto; bf16 out, fp32 + bias, fp32 accumulate) and the
+    hand-written engine (RF_GEMM_BACKEND=hip), against fp64."""
+    monkeypatch.setenv("RF_GEMM_BACKEND", backend)
     ops = _ops()
     g = torch.Generator(device="cpu").manual_seed(m * 7 + n)
     a = torch.randn(m, k, generator=g).bfloat16().to(dev)
@@ -57,7 +61,8 @@ def test_gemm_f32_bf16(m, n, k):
                                    (5649, 1024, 4096), (4096, 3072, 1024)])
 def test_gemm_stream_k(monkeypatch, grid, m, n, k):
     """Stream-K split (forced grid sizes, incl. an odd one where a tile spans 3+ blocks, and the 256x256-tile
-    variant over 256 blocks) vs fp64, every epilogue."""
+    variant over 256 blocks) vs fp64, every epilogue (engine backend)."""
+    monkeypatch.setenv("RF_GEMM_BACKEND", "hip")
     ops = _ops()
     if grid in ("sk256", "skph"):
         if n % 256 or (grid == "skph" and k % 64):
@@ -94,7 +99,8 @@ def test_gemm_stream_k(monkeypatch, grid, m, n, k):
                                    (4096, 1024, 4096), (2000, 768, 320)])
 def test_gemm_256_tiles(monkeypatch, tile, m, n, k):
     """The 256-wide tiles: the phased BK=64 loop at 256x256 and 128x256 and the ring engine's 256x256, forced on
-    every shape (ragged M, one to three K-tiles, long K), every epilogue, against fp64."""
+    every shape (ragged M, one to three K-tiles, long K), every epilogue, against fp64 (engine backend)."""
+    monkeypatch.setenv("RF_GEMM_BACKEND", "hip")
     ops = _ops()
     monkeypatch.setenv("RF_GEMM_TILE", "1282" if tile == "128x256ph" else "256")
     monkeypatch.setenv("RF_GEMM_PHASED", "0" if tile == "256ring" else "1")

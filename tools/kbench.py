@@ -97,7 +97,7 @@ def gemm():
             c = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
         else:
             c = torch.zeros(m, n, device=dev)
-        variants = [("dp128", "128", None, "0"), ("dp128s4", "1284", None, "0"), ("dp128s5", "1285", None, "0"),
+        variants = [("blaslt", None, None, None), ("dp128", "128", None, "0"), ("dp128s4", "1284", None, "0"), ("dp128s5", "1285", None, "0"),
                     ("dp256x128", "2561", None, "0"), ("dp256ring", "256", None, "0"), ("dp256ph", "256", None, "0"),
                     ("dp128x256ph", "1282", None, "0"),
                     ("sk128x512", "128", "512", "0"), ("sk128x768", "128", "768", "0"), ("sk256", None, None, "1"),
@@ -105,6 +105,9 @@ def gemm():
         if os.environ.get("KB_VARIANTS"):
             variants = [v for v in variants if v[0] in os.environ["KB_VARIANTS"].split(",")]
         for label, tile, sk, gm in variants:
+            os.environ["RF_GEMM_BACKEND"] = "auto" if label == "blaslt" else "hip"
+            if label == "blaslt" and epi == ops.EPI_SWIGLU:
+                continue
             for key, val in (("RF_GEMM_TILE", tile), ("RF_GEMM_SK", sk), ("RF_GEMM_SK256", gm)):
                 if val is None:
                     os.environ.pop(key, None)
