@@ -48,7 +48,8 @@ constexpr int HD = 128;
 constexpr int KT = 64;                   // keys per tile
 constexpr int TILE_BYTES = KT * HD * 2;  // 16 KiB
 constexpr float NEG = -1.0e30f;
-constexpr float RESCALE_LOG2 = 8.0f;
+constexpr float RESCALE_LOG2 = 8.0f;  // legacy kernels: row-max growth (log2 units) that forces a rescale
+constexpr float SUM_THR_LOG2 = 12.0f;  // stream-K kernel: half-row tile sum (log2) that forces a rescale
 
 struct AttnArgs {
     const bf16_t* q;
@@ -643,9 +644,10 @@ __global__ __launch_bounds__(NW3 * 64, 1) void attn_v3_kernel(AttnArgs p) {
 //     waited for at the end of that phase; the loop is unrolled by 2 so every LDS offset is an
 //     immediate.
 //   * q arrives pre-scaled by scale*log2(e) (rf_qk_norm_rope seg0_scale) and the QK^T chain starts
-//     from C = -m (the running max), so P = exp2(S) needs no per-score FMA (UNIT); the max is only
-//     re-based (deferred rescale, guide T13) when a row grows by more than 2^8, checked at the end of
-//     B(t) on S(t+1) (its row max is taken in B's gaps), after all of P(t) is in O and l.
+//     from C = -m (the running max), so P = exp2(S) needs no per-score FMA (UNIT) and no per-tile row
+//     max: the running max (exact on a piece's first tile) is only re-based (deferred rescale, guide
+//     T13) when a half-row sum of P(t) exceeds 2^12 (which bounds every P by 2^12), checked at the seam
+//     after A(t); that tile's P is then recomputed on the new base.
 constexpr int NW5 = 8;
 constexpr int QB5 = NW5 * 32;
 constexpr int K5 = 0;                  // K ring: 2 x 16 KiB
@@ -696,6 +698,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
 
     const float c = UNIT ? 1.f : p.c;
     const float inv_c = UNIT ? 1.f : 1.f / p.c;
+    const float sum_thr = exp2f(p.thr);  // half-row sum of one tile's P above which the running max moves
     const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;  // ds_read_b64_tr_b16 lane geometry
     const int qi = wave * 32 + (lane & 31);
     // LDS image of a K/V tile (guide T10 image (a)): 8-row x 32-column subtiles of 512 B,
@@ -717,7 +720,11 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     int q_start = 0, q_len = 0, k_start = 0, k_len = 0, v_start = 0, nqb = 1, nt = 1;
     // DBG & 32: top wait, K DMA issue, mask+max+check, A, seam wait, V DMA issue, B, tiles
     uint64_t stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t t_prev = 0;
+    uint64_t t_prev = 0, clk0 = 0, ref0 = 0;
+    if constexpr (DBG & 32) {
+        clk0 = __builtin_amdgcn_s_memtime();
+        ref0 = __builtin_amdgcn_s_memrealtime();
+    }
     auto stamp_at = [&](int k) {
         if constexpr (DBG & 32) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
@@ -786,15 +793,12 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
         float m_run = 0.f, l_run = 0.f;  // m_run in exp2 units, identical in both lane halves
-        // -m in score units: the C operand of the QK^T chains.  Rebuilt from m_run in every phase B, so
-        // S(t+1) issued right after a rescale of tile t still carries the old base: `carry` holds that
-        // difference and the next tile removes it (rare path).
+        // -m in score units: the C operand of the QK^T chains, rebuilt from m_run in every phase B (a
+        // rescale at the seam also shifts the S(t+1) already issued on the old base).
         f32x16 minit;
 #pragma unroll
         for (int r = 0; r < 16; ++r) minit[r] = 0.f;
 
-        float carry = 0.f;     // exp2 units S(t+1) sits above the current base (after a rescale)
-        bool carried = false;  // wave-uniform: some lane has carry != 0
 
         auto qk = [&](const int koff, f32x16* s) {
 #pragma unroll
@@ -817,13 +821,21 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                     }
             }
         };
-        // rare path: bring S onto the current base (minus `carry`), then re-base the running max on its row
-        // max (exactly on a piece's first tile).  Everything accumulated so far (O, l) is at the old base.
-        // minit is rebuilt in every phase B from m_run, so the S issued next (already built on the old
-        // base) is `delta` too high: `carry` records that for the next check.
-        auto rebase = [&](f32x16* sv, float mt, bool fresh) {
-            const float cs = carry * inv_c;
-            const float mrow = (__builtin_fmaxf(mt, __shfl_xor(mt, 32, 64)) - cs) * c;
+        auto row_max = [&](const f32x16* sv) {
+            float mt = vmax3(sv[0][0], sv[0][1], sv[0][2]);
+#pragma unroll
+            for (int r = 3; r < 15; r += 2) mt = vmax3(mt, sv[0][r], sv[0][r + 1]);
+            mt = vmax3(mt, sv[0][15], sv[1][0]);
+#pragma unroll
+            for (int r = 1; r < 15; r += 2) mt = vmax3(mt, sv[1][r], sv[1][r + 1]);
+            return vmax3(mt, sv[1][15], sv[1][15]);
+        };
+        // rare path: re-base the running max on S's row max (exactly on a piece's first tile).  Everything
+        // accumulated so far (O, l) is at the old base and is scaled by alpha; S (and S2, the next tile's
+        // scores, already issued on the old base) move with the base.
+        auto rebase = [&](f32x16* sv, f32x16* sv2, bool fresh) {
+            const float mt = row_max(sv);
+            const float mrow = __builtin_fmaxf(mt, __shfl_xor(mt, 32, 64)) * c;
             const float delta = fresh ? mrow : __builtin_fmaxf(mrow, 0.f);
             const float alpha = fresh ? 1.f : fast_exp2(-delta);
             l_run *= alpha;
@@ -832,13 +844,14 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
             m_run += delta;
-            const float ds = cs + delta * inv_c;
+            const float ds = delta * inv_c;
 #pragma unroll
             for (int b = 0; b < 2; ++b)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) sv[b][r] -= ds;
-            carry = delta;
-            carried = __any(delta != 0.f);
+                for (int r = 0; r < 16; ++r) {
+                    sv[b][r] -= ds;
+                    if (sv2) sv2[b][r] -= ds;
+                }
         };
 
         issue(kp, p.ldk, kstep, kt0, lds0 + K5);
@@ -850,18 +863,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         f32x16 sA[2], sB[2];
         qk(K5, sA);  // raw scores of the piece's first tile (base 0)
         mask_tail(sA, kt0);
-        {
-            float mt = vmax3(sA[0][0], sA[0][1], sA[0][2]);
-#pragma unroll
-            for (int r = 3; r < 15; r += 2) mt = vmax3(mt, sA[0][r], sA[0][r + 1]);
-            mt = vmax3(mt, sA[0][15], sA[1][0]);
-#pragma unroll
-            for (int r = 1; r < 15; r += 2) mt = vmax3(mt, sA[1][r], sA[1][r + 1]);
-            mt = vmax3(mt, sA[1][15], sA[1][15]);
-            rebase(sA, mt, true);
-        }
-        carry = 0.f;  // minit is rebuilt below from the new base: S(kt0 + 1) needs no correction
-        carried = false;
+        rebase(sA, nullptr, true);
 #pragma unroll
         for (int r = 0; r < 16; ++r) minit[r] = -m_run * inv_c;
         // stagger (guide MI355X_MICROARCH "Two waves per SIMD", item 9): waves 4-7 run half a tile behind,
@@ -875,6 +877,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             constexpr int PAR = decltype(par_c)::value;
             const int t = kt0 + i;
             const bool has_next = i + 1 < n;
+            (void)has_next;
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (DBG & 32) t_prev = __builtin_amdgcn_s_memtime();
             if constexpr (!(DBG & 2)) {
@@ -904,6 +907,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
 
             // ---- phase A: S(t+1) chains b = 0, 1 alternating; each gap: 2 exp2, 2 row-sum adds, 1 bf16 pack
             // of P(t); K fragments two MFMAs ahead; K(t+2)'s LDS-DMA rides in gap 1
+            if (i > 0) mask_tail(s, t);  // (tile kt0 was masked in the prologue)
             kf[0] = kread(0);
             kf[1] = kread(1);
             __builtin_amdgcn_sched_barrier(0);
@@ -933,6 +937,23 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
+            // ---- overflow check (deferred rescale, guide T13): a half-row sum <= 2^thr bounds every P(t) by
+            // 2^thr, so the running max only moves (rare) when some sum exceeds it; P(t) is then recomputed
+            // on the new base and S(t+1), issued on the old one, is shifted with it
+            float l_tile = (ls[0] + ls[1]) + (ls[2] + ls[3]);
+            if (__any(l_tile > sum_thr)) {
+                rebase(s, sn, false);
+                l_tile = 0.f;
+#pragma unroll
+                for (int x = 0; x < 32; ++x) {
+                    const float v = s[x >> 4][x & 15];
+                    const float e = fast_exp2(UNIT ? v : v * c);
+                    l_tile += e;
+                    pf[x >> 4][(x >> 3) & 1][x & 7] = (__bf16)e;
+                }
+            }
+            l_run += l_tile;
+            __builtin_amdgcn_sched_barrier(0);
             stamp_at(1);
             // ---- half-tile seam: K(t+2) landed for this wave; the partner group switches phase
             if constexpr (!(DBG & 2)) {
@@ -941,13 +962,11 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             }
             __builtin_amdgcn_sched_barrier(0);
             stamp_at(2);
-            if (has_next) mask_tail(sn, t + 1);
 
             // ---- phase B: four O chains alternating; V^T fragments two MFMAs ahead; V(t+1)'s LDS-DMA in gap
-            // 1; each gap also rebuilds one register of minit and takes one max3 step over S(t+1)
+            // 1; each gap also rebuilds one register of minit (the C operand of the next QK^T chains)
             vf[0] = vread(0);
             vf[1] = vread(1);
-            float mt = 0.f;
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
@@ -960,25 +979,12 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 }
                 minit[j] = -m_run * inv_c;
                 asm volatile("" : "+v"(minit[j]));  // one v_mov per PV gap (otherwise hoisted into phase A)
-                if (j == 0) {
-                    mt = vmax3(sn[0][0], sn[0][1], sn[0][2]);
-                } else if (j < 15) {
-                    const int x = 2 * j + 1;  // values x, x + 1 of the flattened 32
-                    mt = vmax3(mt, sn[x >> 4][x & 15], sn[(x + 1) >> 4][(x + 1) & 15]);
-                } else {
-                    mt = vmax3(mt, sn[1][15], sn[1][15]);
-                }
                 if constexpr (!(DBG & 1)) {
                     if (j == 1 && has_next) issue(vp, p.ldv, vstep, t + 1, lds0 + V5 + (PAR ^ 1) * TILE_BYTES);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
-            l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
             stamp_at(3);
-            // ---- deferred rescale (guide T13) for S(t+1): P(t) is fully in O and l, so all of it is rescaled
-            if (has_next && (carried || __any(mt * c > p.thr))) rebase(sn, mt, false);
-            __builtin_amdgcn_sched_barrier(0);
-            stamp_at(4);
             if constexpr (DBG & 32) stamp[7] += 1;
         };
         int i = 0;
@@ -1065,7 +1071,10 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 }
         }
     }
-    if constexpr (DBG & 32) {  // diagnostic: [wg][wave][6] u64 in the last piece slot of the workspace
+    if constexpr (DBG & 32) {  // diagnostic: [wg][wave][8] u64 in the last piece slot of the workspace;
+        // slots 4 / 5 hold the wave's shader-clock and 100-MHz reference-clock spans (in-kernel clock)
+        stamp[4] = __builtin_amdgcn_s_memtime() - clk0;
+        stamp[5] = __builtin_amdgcn_s_memrealtime() - ref0;
         if (lane == 0) {
             uint64_t* dbg = reinterpret_cast<uint64_t*>(p.part_o + (int64_t)(SK5_MAX_GRID - 1) * PIECE_FLOATS);
 #pragma unroll
@@ -1137,7 +1146,7 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
     a.c = scale * LOG2E;
     a.part_o = (float*)workspace;
     a.flag = (int*)(a.part_o + (int64_t)SK5_MAX_GRID * PIECE_FLOATS);
-    a.thr = getenv("RF_ATTN_THR") ? (float)atof(getenv("RF_ATTN_THR")) : RESCALE_LOG2;
+    a.thr = getenv("RF_ATTN_THR") ? (float)atof(getenv("RF_ATTN_THR")) : SUM_THR_LOG2;
     // q pre-scaled by scale*log2(e) upstream (scale = ln 2): scores are already exp2 exponents
     const bool unit = fabsf(a.c - 1.0f) < 1e-6f;
     const int dbg = getenv("RF_ATTN_DBG") ? atoi(getenv("RF_ATTN_DBG")) : 0;

@@ -33,9 +33,11 @@ if len(sys.argv) > 1 and sys.argv[1] == "stamps":
     piece = (ws.numel() - 512) // 512
     st = ws[511 * piece:511 * piece + 256 * 8 * 16].view(torch.int64).view(256, 8, 8).cpu().double()
     tiles = st[..., 7].clamp_min(1)
-    names = ["top wait", "A (+K DMA)", "seam wait", "B (+V DMA, max)", "check", "-", "-"]
+    names = ["top wait", "A (+K DMA, check)", "seam wait", "B (+V DMA)"]
+    clk = (st[..., 4] / st[..., 5].clamp_min(1)).median() * 100.0
+    print(f"in-kernel shader clock (s_memtime / s_memrealtime x 100 MHz, median over waves): {clk:.0f} MHz")
     for grp, sl in (("waves 0-3", slice(0, 4)), ("waves 4-7", slice(4, 8))):
-        per = (st[:, sl, :7] / tiles[:, sl, None]).mean(dim=(0, 1))
+        per = (st[:, sl, :4] / tiles[:, sl, None]).mean(dim=(0, 1))
         print(grp, "cycles/tile:", ", ".join(f"{n} {v:.0f}" for n, v in zip(names, per.tolist())),
               f"| total {per.sum():.0f}", flush=True)
     sys.exit(0)

@@ -3,5 +3,5 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-st}
 mkdir -p $O
 cd $R
-timeout -k 10 120 python tools/attn_ablate.py stamps > $O/stamps.log 2>&1
+timeout -k 10 120 python tools/attn_ablate.py stamps 32 > $O/stamps.log 2>&1
 echo done
