@@ -60,6 +60,7 @@ struct EngineArgs {
     int m, n, k;
     // gathered A (convolution): NHWC plane [img][hi][wi][cin_pad]
     int hi, wi, cin_pad, ho, wo, kw, stride, pad;
+    uint64_t cin_m, kw_m;  // magic multipliers: x / cin_pad == (x * cin_m) >> 32 (x < 2^16), same for kw
     const bf16_t* zero;
     // epilogue
     void* c;
@@ -81,6 +82,13 @@ struct EngineArgs {
     int sk_epoch;
     int group_m;  // tile raster: groups of group_m m-tiles, n fastest within a group (host-chosen)
 };
+
+// x / d for 0 <= x < 2^16 and 1 <= d < 2^16 as one 64-bit multiply: m = 2^32 / d + 1 (the error of
+// x * m / 2^32 is below x / 2^32 < 1 / d, so the floor is exact); replaces runtime integer divisions
+// (~30 scalar instructions each) in the gathered-convolution staging
+RF_DEV int udiv_m(int x, uint64_t m) { return (int)(((uint64_t)(uint32_t)x * m) >> 32); }
+inline uint64_t udiv_magic(int d) { return (1ull << 32) / (uint64_t)d + 1; }
+
 
 // Tile raster.  Each XCD runs a contiguous range of tile ids (see the remap in engine_kernel); with
 // groups of group_m m-tiles walked n-fastest, that range is a ~group_m x (range/group_m) rectangle of
@@ -168,9 +176,9 @@ RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
         const int k0 = kt * BK;
         int cb = k0, ky = 0, kx = 0;
         if constexpr (GATHER) {
-            const int tap = k0 / p.cin_pad;
+            const int tap = udiv_m(k0, p.cin_m);
             cb = k0 - tap * p.cin_pad;
-            ky = tap / p.kw;
+            ky = udiv_m(tap, p.kw_m);
             kx = tap - ky * p.kw;
         }
 #pragma unroll
@@ -597,8 +605,8 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
             const bf16_t* g = src[r] + k0 + ch * 8;
             if constexpr (GATHER) {
                 if (is_a) {
-                    const int tap = k0 / p.cin_pad, cb = k0 - tap * p.cin_pad;
-                    const int ky = tap / p.kw, kx = tap - ky * p.kw;
+                    const int tap = udiv_m(k0, p.cin_m), cb = k0 - tap * p.cin_pad;
+                    const int ky = udiv_m(tap, p.kw_m), kx = tap - ky * p.kw;
                     const int iy = gy[r] + ky, ix = gx[r] + kx;
                     const bool ok = gi[r] >= 0 && iy >= 0 && iy < p.hi && ix >= 0 && ix < p.wi;
                     g = ok ? p.a + (((int64_t)gi[r] * p.hi + iy) * p.wi + ix) * p.cin_pad + cb + ch * 8 : p.zero;
@@ -915,6 +923,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
 // Tile configurations.  T128: 128x128, 4 waves of 64x64, 3-stage ring (48 KiB / 96 KiB LDS).
 // T256: 256x256, 8 waves of 128x64, 4-stage ring (128 KiB).  T256x128: 8 waves of 64x64, bf16x3 3-stage (144 KiB).
 using T128 = Tile<128, 128, 2, 2, 3>;
+using T128w8 = Tile<128, 128, 2, 4, 3>;  // 8 waves of 64x32: two waves per SIMD at one block per CU
 using T256 = Tile<256, 256, 2, 4, 4>;
 using T256x128 = Tile<256, 128, 4, 2, 3>;
 using T256x64 = Tile<256, 64, 4, 1, 4>;  // fp16 convolutions with <= 64 output channels (DPT output_conv2)
@@ -1159,11 +1168,16 @@ static int conv_f16_dp(EngineArgs& p, void* stream, const char* what) {
     const int t = env ? atoi(env) : 0;
     if (p.n == 64) return launch<T256x64, E_CONV, P_F16, GATHER>(p, stream, what);
     if (t == 128) return launch<T128, E_CONV, P_F16, GATHER>(p, stream, what);
+    if (t == 1288) return launch<T128w8, E_CONV, P_F16, GATHER>(p, stream, what);
     if (p.n % 256 == 0 && (t == 256 || (!t && ((p.m + 255) / 256) * (p.n / 256) >= 256)))
         return (getenv("RF_CONV_PHASED") && atoi(getenv("RF_CONV_PHASED")) && use_phased(p.n, p.k))
                    ? launch_phased<E_CONV, P_F16, GATHER, 256>(p, stream, what)
                    : launch<T256, E_CONV, P_F16, GATHER>(p, stream, what);
     if (t == 2561) return launch<T256x128, E_CONV, P_F16, GATHER>(p, stream, what);
+    // up to two 128x128 tiles per CU: the 8-wave tile (two waves per SIMD) hides the gathered staging's
+    // latency (128^2 DPT level: 52 -> 41 us); with more tiles the 4-wave tile's extra blocks do that
+    const int64_t tiles = (int64_t)((p.m + 127) / 128) * (p.n / 128);
+    if (t != 128 && tiles <= 512) return launch<T128w8, E_CONV, P_F16, GATHER>(p, stream, what);
     return launch<T128, E_CONV, P_F16, GATHER>(p, stream, what);
 }
 
@@ -1175,6 +1189,10 @@ static int conv_dispatch(EngineArgs& p, bool gather, bool big, int64_t sk_grid_n
     }
     if (sk_grid_n) {
         sk_setup(p, workspace);
+        // fp16 convolutions stream-K over the 8-wave 128x128 tile (64^2 / 32^2 DPT levels: 1.6x / 2.1x)
+        if (NT == P_F16 && !(getenv("RF_CONV_SKW8") && atoi(getenv("RF_CONV_SKW8")) == 0))
+            return gather ? launch_sk<T128w8, E_CONV, NT, true>(p, (int)sk_grid_n, stream, what)
+                          : launch_sk<T128w8, E_CONV, NT, false>(p, (int)sk_grid_n, stream, what);
         return gather ? launch_sk<T128, E_CONV, NT, true>(p, (int)sk_grid_n, stream, what)
                       : launch_sk<T128, E_CONV, NT, false>(p, (int)sk_grid_n, stream, what);
     }
@@ -1252,13 +1270,16 @@ extern "C" int rf_conv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img,
     p.hi = hi;
     p.wi = wi;
     p.cin_pad = cin_pad;
+    p.cin_m = udiv_magic(cin_pad);
     p.ho = (hi + 2 * pad - kh) / stride + 1;
     p.wo = (wi + 2 * pad - kw) / stride + 1;
     p.kw = kw;
+    p.kw_m = udiv_magic(kw);
     p.stride = stride;
     p.pad = pad;
     p.m = n_img * p.ho * p.wo;
     p.k = kh * kw * cin_pad;
+    RF_REQUIRE(p.k < 65536, "conv: kh*kw*cin_pad = %d must be < 65536", p.k);
     p.ldw = p.k;
     return conv_common(p, 3, true, w_hi, w_lo, cout, cout_pad, out, bias, res1, res2, p_hi, p_lo, p_ld, flags, w_fin,
                        b_fin, n_fin, elu_alpha, workspace, ws_bytes, stream, "rf_conv2d_bf16x3");
@@ -1278,13 +1299,16 @@ extern "C" int rf_conv2d_f16(const void* in, int n_img, int hi, int wi, int cin_
     p.hi = hi;
     p.wi = wi;
     p.cin_pad = cin_pad;
+    p.cin_m = udiv_magic(cin_pad);
     p.ho = (hi + 2 * pad - kh) / stride + 1;
     p.wo = (wi + 2 * pad - kw) / stride + 1;
     p.kw = kw;
+    p.kw_m = udiv_magic(kw);
     p.stride = stride;
     p.pad = pad;
     p.m = n_img * p.ho * p.wo;
     p.k = kh * kw * cin_pad;
+    RF_REQUIRE(p.k < 65536, "conv: kh*kw*cin_pad = %d must be < 65536", p.k);
     p.ldw = p.k;
     return conv_common(p, P_F16, true, w, nullptr, cout, cout_pad, out, bias, res1, res2, p_out, nullptr, p_ld, flags,
                        w_fin, b_fin, n_fin, elu_alpha, workspace, ws_bytes, stream, "rf_conv2d_f16");

@@ -135,16 +135,18 @@ def gemm():
 
 def conv():
     from renderformer_amd.dpt import _Conv, split_planes
-    for f16 in (True, False):
-        for cin, cout, hw in [(256, 256, 256), (256, 128, 512), (256, 256, 128), (128, 256, 256), (128, 32, 512)]:
+    for f16 in (True,) if os.environ.get("KB_F16_ONLY") else (True, False):
+        for cin, cout, hw in [(256, 256, 256), (256, 128, 512), (256, 256, 128), (256, 256, 64), (256, 256, 32),
+                              (128, 256, 256), (128, 32, 512)]:
             conv = _Conv(torch.randn(cout, cin, 3, 3) / 48, torch.randn(cout), dev, f16=f16)
             x = split_planes(torch.randn(1, hw, hw, cin, device=dev), conv.cin_pad, f16=f16)
             fl = 2 * hw * hw * cin * cout * 9
             mf = 1 if f16 else 3
-            tiles = ("128", "256", "256ph", "2561", "auto") if f16 else ("128", "256")
+            tiles = ("128", "1288", "256", "2561", "auto4w", "auto") if f16 else ("128", "256")
             for t in tiles:
                 os.environ["RF_CONV_PHASED"] = "1" if t == "256ph" else "0"
-                if t != "auto":
+                os.environ["RF_CONV_SKW8"] = "0" if t == "auto4w" else "1"
+                if not t.startswith("auto"):
                     os.environ["RF_CONV_TILE"] = t.replace("ph", "")
                 ms = timeit(lambda: conv(x, out_f32=True), reps=10)
                 os.environ.pop("RF_CONV_TILE", None)
