@@ -21,6 +21,11 @@
  *                      (attention.py:205-271, 316-370), with the roll done as index math
  *   rf_texture_pack    rendering_pipeline.py:67-68 (in-place log10 encode) + renderformer.py:145-147
  *                      flatten, with flash_attn.bert_padding.unpad_input-style compaction
+ *   rf_texture_scan / rf_texture_linear  the texture encoder Linear (renderformer.py:145-147, 49) on
+ *                      to_h5-format textures (scene_processor/to_h5.py:41-66: per-channel constant x fixed
+ *                      patch mask) as a C-wide product with mask-summed weights, proven per call on the
+ *                      device; rf_texture_pack_if / rf_gemm_bf16_if run the general path only when the
+ *                      proof fails (device-side flag, no host round trip)
  *   rf_vn_encode       NeRFEncoding (nerf_encoding.py:63-84) on vertex normals, renderformer.py:139
  *   rf_ray_tokens      RayGenerator (ray_generator.py:13-50) + patchify rearrange (view_transformer.py:104-105)
  *   rf_patchify_rays   the patchify rearrange alone, for RenderFormer.forward callers (renderformer.py:171)
@@ -49,7 +54,7 @@ extern "C" {
 #define RF_ERR_LAUNCH 2
 #define RF_ERR_UNSUPPORTED 3
 
-#define RF_ABI_VERSION 4
+#define RF_ABI_VERSION 5
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -72,6 +77,11 @@ int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c
                  const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
                  void* stream);
 int64_t rf_gemm_workspace_bytes(void);
+/* rf_gemm_bf16 on the HIP engine that does nothing unless *flag != 0 (read on the device when the launch
+ * runs); stream-ordered after whatever wrote the flag. */
+int rf_gemm_bf16_if(const int* flag, const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
+                    const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
+                    void* stream);
 
 /* out(bf16)[r, :] = x[r, :] * rsqrt(mean(x^2) + eps) * weight ; x f32. */
 int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, float eps, void* out, int64_t ldo,
@@ -119,6 +129,21 @@ int rf_swin_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, con
  * encoded IN PLACE for every row; rows with dst_row[r] >= 0 are written as bf16 to out[dst_row[r]]. */
 int rf_texture_pack(float* texture, int64_t n_rows, int channels, int patch_elems, int log_channels,
                     const int32_t* dst_row, void* out, int64_t ldo, void* stream);
+/* rf_texture_pack that does nothing unless *flag != 0. */
+int rf_texture_pack_if(const int* flag, float* texture, int64_t n_rows, int channels, int patch_elems,
+                       int log_channels, const int32_t* dst_row, void* out, int64_t ldo, void* stream);
+/* One pass over texture f32 [n_rows, channels, 1024] (32x32 patches, channels <= 32): zeroes *flag, then
+ * log10(x+1)-encodes channels >= channels-log_channels IN PLACE for every row (as rf_texture_pack), and for
+ * rows with dst_row[r] >= 0 writes coef[dst_row[r]*ldc + c] = the row's channel-c constant and sets
+ * *flag = 1 unless every texel equals that constant inside the to_h5 patch mask {(i, j): i + j <= 32}
+ * (row-major i, j) and 0 outside it (exact compares; NaN fails). */
+int rf_texture_scan(float* texture, int64_t n_rows, int channels, int patch_elems, int log_channels,
+                    const int32_t* dst_row, float* coef, int64_t ldc, int* flag, void* stream);
+/* When *flag == 0: out f32 [rows, n] = bias + coef[rows, channels] * wsum[channels, n], with
+ * wsum[c, o] = sum over the patch mask of W[o, c*1024 + e] (the texture Linear on scanned rows);
+ * no-op otherwise.  channels <= 16, n % 4 == 0, 16-B aligned out/wsum/bias (bias may be NULL). */
+int rf_texture_linear(const float* coef, int64_t ldc, int rows, int channels, const float* wsum,
+                      const float* bias, float* out, int64_t ldo, int n, const int* flag, void* stream);
 
 /* NeRF encoding (include_input) of vn f32 [n_rows, 9] into bf16 out[dst_row[r], 0:ldo] (zero padded). */
 int rf_vn_encode(const float* vn, int64_t n_rows, const int32_t* dst_row, int n_freqs, void* out,

@@ -29,6 +29,10 @@ SIGNATURES = {
     "rf_attn_combine": [_P, _L, _I, _I, _P, _I, _P, _L, _P],
     "rf_swin_attn_fwd": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _I, _I, _F, _P],
     "rf_texture_pack": [_P, _L, _I, _I, _I, _P, _P, _L, _P],
+    "rf_texture_pack_if": [_P, _P, _L, _I, _I, _I, _P, _P, _L, _P],
+    "rf_texture_scan": [_P, _L, _I, _I, _I, _P, _P, _L, _P, _P],
+    "rf_texture_linear": [_P, _L, _I, _I, _P, _P, _P, _L, _I, _P, _P],
+    "rf_gemm_bf16_if": [_P, _P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _L, _P],
     "rf_vn_encode": [_P, _L, _P, _I, _P, _L, _P],
     "rf_ray_tokens": [_P, _P, _I, _I, _I, _P, _P, _P],
     "rf_patchify_rays": [_P, _I, _I, _I, _P, _P],

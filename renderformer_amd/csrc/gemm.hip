@@ -81,7 +81,11 @@ struct EngineArgs {
     int* sk_flag;
     int sk_epoch;
     int group_m;  // tile raster: groups of group_m m-tiles, n fastest within a group (host-chosen)
+    const int* gate;  // optional device flag: the launch is a no-op unless *gate != 0 (rf_gemm_bf16_if)
 };
+
+// uniform early exit of a gated launch (every block reads the same flag, so a stream-K grid exits whole)
+RF_DEV bool gated_off(const EngineArgs& p) { return p.gate && *p.gate == 0; }
 
 // x / d for 0 <= x < 2^16 and 1 <= d < 2^16 as one 64-bit multiply: m = 2^32 / d + 1 (the error of
 // x * m / 2^32 is below x / 2^32 < 1 / d, so the floor is exact); replaces runtime integer divisions
@@ -747,6 +751,7 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
 template <int BM, int EPI, int NTERM, bool GATHER>
 __global__ __launch_bounds__(512, 1) void phased_kernel(EngineArgs p) {
     __shared__ __attribute__((aligned(16))) char smem[ph::Cfg<BM>::LDS];
+    if (gated_off(p)) return;
     const int tiles_m = (p.m + BM - 1) / BM;
     const int nwg = gridDim.x;
     const int hw = blockIdx.x;
@@ -766,6 +771,7 @@ template <int EPI, int NTERM>
 __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
     constexpr int TI = 8, TJ = 4, BM = 256, TS = BM * ph::BN;
     __shared__ __attribute__((aligned(16))) char smem[ph::Cfg<BM>::LDS];
+    if (gated_off(p)) return;
     const int tiles_m = (p.m + BM - 1) / BM, tiles_n = p.n / ph::BN;
     const int nwg = gridDim.x;
     const int hw = blockIdx.x;
@@ -841,6 +847,7 @@ template <class C, int EPI, int NTERM, bool GATHER, bool SK>
 __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
     constexpr int BM = C::BM, BN = C::BN, TI = C::TI, TJ = C::TJ;
     __shared__ __attribute__((aligned(16))) char smem[C::STAGES * stage_bytes<C, NTERM>()];
+    if (gated_off(p)) return;
 
     const int tiles_m = (p.m + BM - 1) / BM;
     const int nwg = gridDim.x;
@@ -1095,9 +1102,9 @@ bool gemm_engine_forced() {
 }
 }  // namespace rf
 
-extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
-                            const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
-                            void* stream) {
+static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
+                     const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
+                     void* stream, const int* gate) {
     RF_REQUIRE(a && w && c, "rf_gemm_bf16: null pointer");
     RF_REQUIRE(m > 0 && n > 0 && k > 0, "rf_gemm_bf16: empty problem m=%d n=%d k=%d", m, n, k);
     RF_REQUIRE(k % BK == 0, "rf_gemm_bf16: K=%d must be a multiple of %d", k, BK);
@@ -1110,7 +1117,7 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
     // plain epilogues (bf16 out, fp32 out + bias, fp32 residual accumulate) go to hipBLASLt, which is
     // faster on every plain projection shape of the path (tools/kbench.py); RF_GEMM_BACKEND=hip keeps them
     // on the engine below.  The fused epilogues (SwiGLU) are engine-only.
-    if (epilogue != RF_EPI_SWIGLU && (epilogue == RF_EPI_F32 || !bias) && !rf::gemm_engine_forced()) {
+    if (!gate && epilogue != RF_EPI_SWIGLU && (epilogue == RF_EPI_F32 || !bias) && !rf::gemm_engine_forced()) {
         const int r = rf::blaslt_gemm(a, lda, w, ldw, c, ldc, m, n, k, epilogue, bias, workspace, ws_bytes, stream);
         if (r != -1) return r;
     }
@@ -1125,6 +1132,7 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
     p.c = c;
     p.ldc = ldc;
     p.bias = bias;
+    p.gate = gate;
     if (workspace && ws_bytes >= SK_WS_BYTES && skph(m, n, k)) {
         sk_setup(p, workspace);
         switch (epilogue) {
@@ -1157,6 +1165,19 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
         }
     }
     return run_dp(pick_cfg(m, n, k), p, epilogue, stream);
+}
+
+extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
+                            const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
+                            void* stream) {
+    return gemm_bf16(a, lda, w, ldw, c, ldc, bias, m, n, k, epilogue, workspace, ws_bytes, stream, nullptr);
+}
+
+extern "C" int rf_gemm_bf16_if(const int* flag, const void* a, int64_t lda, const void* w, int64_t ldw, void* c,
+                               int64_t ldc, const float* bias, int m, int n, int k, int epilogue, void* workspace,
+                               int64_t ws_bytes, void* stream) {
+    RF_REQUIRE(flag, "rf_gemm_bf16_if: null flag");
+    return gemm_bf16(a, lda, w, ldw, c, ldc, bias, m, n, k, epilogue, workspace, ws_bytes, stream, flag);
 }
 
 // fp16 convolutions (one MFMA per product): the 256x256 tile when the filter bank is a multiple of 256

@@ -15,7 +15,8 @@ namespace {
 // + renderformer.py:145-147 flatten to [N, C*P*P], compacted to valid rows, bf16.
 __global__ __launch_bounds__(256) void texture_pack_kernel(float* __restrict__ tex, int channels, int patch_elems,
                                                            int log_from, const int32_t* __restrict__ dst_row,
-                                                           bf16_t* __restrict__ out, int64_t ldo) {
+                                                           bf16_t* __restrict__ out, int64_t ldo, const int* gate) {
+    if (gate && *gate == 0) return;
     const int64_t r = blockIdx.x;
     const int n4 = channels * patch_elems / 4;
     float4* row = reinterpret_cast<float4*>(tex + r * (int64_t)channels * patch_elems);
@@ -35,6 +36,91 @@ __global__ __launch_bounds__(256) void texture_pack_kernel(float* __restrict__ t
             pk.x = pack_bf16x2(v.x, v.y);
             pk.y = pack_bf16x2(v.z, v.w);
             *reinterpret_cast<uint2*>(o + i * 4) = pk;
+        }
+    }
+}
+
+// Texture encoder fast path.  Every texture written by scene_processor/to_h5.py:41-66 is, per triangle and
+// channel, one constant times the fixed patch mask {(i, j) : i + j <= 32} of the 32x32 patch, so the
+// texture Linear(C*1024 -> D) of renderformer.py:145-147 reduces exactly to a C-wide product with the
+// mask-summed weights.  The scan proves that form for every valid row (exact float
+// compares after the in-place log encode; NaN fails) and raises *flag otherwise; the consumers are gated
+// on the flag on the device, so no host round trip decides the path.
+constexpr int TEX_SIDE = 32;  // to_h5.py:41
+
+RF_DEV bool tex_in_mask(int e) { return (e >> 5) + (e & 31) <= TEX_SIDE; }
+
+// one block per texture row (all n_rows rows are log-encoded, like rendering_pipeline.py:67-68); thread t
+// owns texels 4t..4t+3 of every channel (patch row t >> 3)
+__global__ __launch_bounds__(256) void texture_scan_kernel(float* __restrict__ tex, int channels, int log_from,
+                                                           const int32_t* __restrict__ dst_row,
+                                                           float* __restrict__ coef, int64_t ldc, int* flag) {
+    const int64_t r = blockIdx.x;
+    const int t = threadIdx.x;
+    float* base = tex + r * (int64_t)channels * (TEX_SIDE * TEX_SIDE);
+    __shared__ float c_raw[32];
+    if (t < channels) c_raw[t] = base[t * TEX_SIDE * TEX_SIDE];  // texel (0, 0): inside the mask
+    __syncthreads();  // read before any thread rewrites it in place
+    const int e0 = 4 * t;
+    const bool m0 = tex_in_mask(e0), m1 = tex_in_mask(e0 + 1), m2 = tex_in_mask(e0 + 2), m3 = tex_in_mask(e0 + 3);
+    bool ok = true;
+    for (int ch = 0; ch < channels; ++ch) {
+        float4* p4 = reinterpret_cast<float4*>(base + ch * TEX_SIDE * TEX_SIDE) + t;
+        float4 v = *p4;
+        float c = c_raw[ch];
+        if (ch >= log_from) {
+            v.x = log10f(v.x + 1.0f);
+            v.y = log10f(v.y + 1.0f);
+            v.z = log10f(v.z + 1.0f);
+            v.w = log10f(v.w + 1.0f);
+            *p4 = v;
+            c = log10f(c + 1.0f);  // the same op on the same input as texel (0, 0) above: bit-identical
+        }
+        ok = ok && v.x == (m0 ? c : 0.f) && v.y == (m1 ? c : 0.f) && v.z == (m2 ? c : 0.f) && v.w == (m3 ? c : 0.f);
+    }
+    const int d = dst_row ? dst_row[r] : (int)r;
+    if (d < 0) return;  // block-uniform: padded rows are only log-encoded
+    if (!__syncthreads_and(ok) && t == 0) *flag = 1;
+    if (t < channels) {
+        const float c = c_raw[t];
+        coef[(int64_t)d * ldc + t] = t >= log_from ? log10f(c + 1.0f) : c;
+    }
+}
+
+// out[r, o] = bias[o] + sum_c coef[r, c] * wsum[c, o]   (fast path; no-op when *flag != 0).  Thread t keeps
+// columns 4t..4t+3 of wsum (<= 16 channels) in registers for TL_ROWS rows; the rows' coefficients go
+// through LDS, so wsum is read once per block (not once per row).
+constexpr int TL_ROWS = 16, TL_MAXC = 16;
+__global__ __launch_bounds__(256) void texture_linear_kernel(const float* __restrict__ coef, int64_t ldc, int rows,
+                                                             int channels, const float* __restrict__ wsum,
+                                                             const float* __restrict__ bias, float* __restrict__ out,
+                                                             int64_t ldo, int n, const int* flag) {
+    if (*flag != 0) return;
+    __shared__ float cs[TL_ROWS][TL_MAXC];
+    const int r0 = blockIdx.x * TL_ROWS;
+    const int t = threadIdx.x;
+    {
+        const int rr = t / TL_MAXC, c = t % TL_MAXC;
+        cs[rr][c] = (r0 + rr < rows && c < channels) ? coef[(int64_t)(r0 + rr) * ldc + c] : 0.f;
+    }
+    __syncthreads();
+    for (int o = 4 * t; o < n; o += 1024) {
+        float4 w[TL_MAXC];
+#pragma unroll
+        for (int c = 0; c < TL_MAXC; ++c)
+            w[c] = c < channels ? *reinterpret_cast<const float4*>(wsum + (int64_t)c * n + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 b4 = bias ? *reinterpret_cast<const float4*>(bias + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int rr = 0; rr < TL_ROWS && r0 + rr < rows; ++rr) {
+            float4 acc = b4;
+#pragma unroll
+            for (int c = 0; c < TL_MAXC; ++c) {
+                const float k = cs[rr][c];
+                acc.x = fmaf(k, w[c].x, acc.x);
+                acc.y = fmaf(k, w[c].y, acc.y);
+                acc.z = fmaf(k, w[c].z, acc.z);
+                acc.w = fmaf(k, w[c].w, acc.w);
+            }
+            *reinterpret_cast<float4*>(out + (int64_t)(r0 + rr) * ldo + o) = acc;
         }
     }
 }
@@ -119,13 +205,13 @@ __global__ __launch_bounds__(256) void patchify_rays_kernel(const float* __restr
 // ----------------------------------------------------------------------------- RoPE positions
 // trans_to_cam_coord (transform.py:24-27: p -> R^T p - R^T t) and process_tri_vpos_list
 // (renderformer.py:111-122: register rows = masked mean position, averaged over the 3 vertices).
-__global__ __launch_bounds__(256) void scene_pos_kernel(const float* __restrict__ tris,
+__global__ __launch_bounds__(1024) void scene_pos_kernel(const float* __restrict__ tris,
                                                         const int32_t* __restrict__ valid_idx,
                                                         const int32_t* __restrict__ scene_off,
                                                         const float* __restrict__ c2w, int n_views, int n_reg,
                                                         float* __restrict__ pos_out,
                                                         const int32_t* __restrict__ set_off) {
-    __shared__ float red[256 / 64][9];
+    __shared__ float red[1024 / 64][9];
     const int set = blockIdx.x;
     const int scene = c2w ? set / n_views : set;
     const int t0 = scene_off[scene], n = scene_off[scene + 1] - t0;
@@ -165,7 +251,12 @@ __global__ __launch_bounds__(256) void scene_pos_kernel(const float* __restrict_
     if (threadIdx.x < n_reg * 9) {
         const float wgt = 1.0f / ((float)n + 1e-5f);
         float tot[9];
-        for (int c = 0; c < 9; ++c) tot[c] = (red[0][c] + red[1][c] + red[2][c] + red[3][c]) * wgt;
+        for (int c = 0; c < 9; ++c) {
+            float sum = 0.f;
+#pragma unroll
+            for (int w = 0; w < 1024 / 64; ++w) sum += red[w][c];
+            tot[c] = sum * wgt;
+        }
         const int k = threadIdx.x % 3;
         const float ctr = (tot[k] + tot[3 + k] + tot[6 + k]) / 3.0f;
         pos_out[(int64_t)set_off[set] * 9 + threadIdx.x] = ctr;
@@ -198,8 +289,52 @@ extern "C" int rf_texture_pack(float* texture, int64_t n_rows, int channels, int
     RF_REQUIRE(n_rows < (1ll << 31), "rf_texture_pack: too many rows");
     if (n_rows <= 0) return RF_OK;
     hipLaunchKernelGGL(texture_pack_kernel, dim3((unsigned)n_rows), dim3(256), 0, (hipStream_t)stream, texture,
-                       channels, patch_elems, channels - log_channels, dst_row, (bf16_t*)out, ldo);
+                       channels, patch_elems, channels - log_channels, dst_row, (bf16_t*)out, ldo, nullptr);
     return rf::check_launch("rf_texture_pack");
+}
+
+extern "C" int rf_texture_pack_if(const int* flag, float* texture, int64_t n_rows, int channels, int patch_elems,
+                                  int log_channels, const int32_t* dst_row, void* out, int64_t ldo, void* stream) {
+    RF_REQUIRE(flag && texture && out, "rf_texture_pack_if: null pointer");
+    RF_REQUIRE(patch_elems % 4 == 0 && ((uintptr_t)texture & 15) == 0, "rf_texture_pack_if: need 16-B aligned rows");
+    RF_REQUIRE(ldo >= (int64_t)channels * patch_elems && ldo % 4 == 0, "rf_texture_pack_if: bad ldo");
+    RF_REQUIRE(n_rows < (1ll << 31), "rf_texture_pack_if: too many rows");
+    if (n_rows <= 0) return RF_OK;
+    hipLaunchKernelGGL(texture_pack_kernel, dim3((unsigned)n_rows), dim3(256), 0, (hipStream_t)stream, texture,
+                       channels, patch_elems, channels - log_channels, dst_row, (bf16_t*)out, ldo, flag);
+    return rf::check_launch("rf_texture_pack_if");
+}
+
+extern "C" int rf_texture_scan(float* texture, int64_t n_rows, int channels, int patch_elems, int log_channels,
+                               const int32_t* dst_row, float* coef, int64_t ldc, int* flag, void* stream) {
+    RF_REQUIRE(texture && coef && flag, "rf_texture_scan: null pointer");
+    RF_REQUIRE(patch_elems == TEX_SIDE * TEX_SIDE, "rf_texture_scan: patch_elems must be %d", TEX_SIDE * TEX_SIDE);
+    RF_REQUIRE(channels >= 1 && channels <= 32 && ldc >= channels, "rf_texture_scan: bad channels/ldc");
+    RF_REQUIRE(log_channels >= 0 && log_channels <= channels, "rf_texture_scan: bad log_channels");
+    RF_REQUIRE(((uintptr_t)texture & 15) == 0, "rf_texture_scan: texture must be 16-B aligned");
+    RF_REQUIRE(n_rows < (1ll << 31), "rf_texture_scan: too many rows");
+    if (hipMemsetAsync(flag, 0, sizeof(int), (hipStream_t)stream) != hipSuccess) {
+        rf::set_error("rf_texture_scan: flag reset failed");
+        return RF_ERR_LAUNCH;
+    }
+    if (n_rows <= 0) return RF_OK;
+    hipLaunchKernelGGL(texture_scan_kernel, dim3((unsigned)n_rows), dim3(256), 0, (hipStream_t)stream, texture,
+                       channels, channels - log_channels, dst_row, coef, ldc, flag);
+    return rf::check_launch("rf_texture_scan");
+}
+
+extern "C" int rf_texture_linear(const float* coef, int64_t ldc, int rows, int channels, const float* wsum,
+                                 const float* bias, float* out, int64_t ldo, int n, const int* flag, void* stream) {
+    RF_REQUIRE(coef && wsum && out && flag, "rf_texture_linear: null pointer");
+    RF_REQUIRE(n % 4 == 0 && ldo % 4 == 0 && ldo >= n && ldc >= channels, "rf_texture_linear: bad n/ldo/ldc");
+    RF_REQUIRE(channels >= 1 && channels <= TL_MAXC, "rf_texture_linear: channels must be in [1, %d]", TL_MAXC);
+    RF_REQUIRE(((uintptr_t)out & 15) == 0 && ((uintptr_t)wsum & 15) == 0 && (!bias || ((uintptr_t)bias & 15) == 0),
+               "rf_texture_linear: out/wsum/bias must be 16-B aligned");
+    if (rows <= 0) return RF_OK;
+    hipLaunchKernelGGL(texture_linear_kernel, dim3((unsigned)((rows + TL_ROWS - 1) / TL_ROWS)), dim3(256), 0,
+                       (hipStream_t)stream,
+                       coef, ldc, rows, channels, wsum, bias, out, ldo, n, flag);
+    return rf::check_launch("rf_texture_linear");
 }
 
 extern "C" int rf_vn_encode(const float* vn, int64_t n_rows, const int32_t* dst_row, int n_freqs, void* out,
@@ -238,7 +373,7 @@ extern "C" int rf_scene_pos(const float* tris, const int32_t* valid_idx, const i
     RF_REQUIRE(n_reg * 9 <= 256, "rf_scene_pos: too many register tokens");
     const int sets = c2w ? n_scenes * n_views : n_scenes;
     if (sets <= 0) return RF_OK;
-    hipLaunchKernelGGL(scene_pos_kernel, dim3(sets), dim3(256), 0, (hipStream_t)stream, tris, valid_idx, scene_off,
+    hipLaunchKernelGGL(scene_pos_kernel, dim3(sets), dim3(1024), 0, (hipStream_t)stream, tris, valid_idx, scene_off,
                        c2w, n_views, n_reg, pos_out, set_off);
     return rf::check_launch("rf_scene_pos");
 }

@@ -65,6 +65,16 @@ class _DeviceWeights:
         self.vn_norm = _f32(sd["vn_encoder_norm.weight"], device)
         self.tex_w = _bf16(sd["texture_encoder.weight"], device)
         self.tex_b = _f32(sd["texture_encoder.bias"], device)
+        # texture fast path (prologue.hip rf_texture_scan): the encoder weights summed over the to_h5 patch
+        # mask {(i, j): i + j <= 32} per channel, [C, D] f32 (from the f32 checkpoint weights, in f64)
+        tw = sd["texture_encoder.weight"]
+        self.tex_wsum = None
+        if cfg.texture_encode_patch_size == 32 and tw.shape[1] == cfg.texture_channels * 1024:
+            i, j = torch.meshgrid(torch.arange(32), torch.arange(32), indexing="ij")
+            mask = (i + j <= 32).double().reshape(1, 1, 1024)
+            ws = (tw.detach().double().reshape(d, cfg.texture_channels, 1024) * mask).sum(-1)
+            self.tex_wsum = _f32(ws.t(), device)
+        self.tex_flag = torch.zeros(1, dtype=torch.int32, device=device)
         self.tex_norm = _f32(sd["texture_encoder_norm.weight"], device)
         self.enc_freqs = _f32(sd["transformer.rope_emb.freqs"], device)
         self.enc = []
@@ -198,6 +208,9 @@ class RenderFormer:
         self._sd = state_dict if state_dict is not None else synthetic_state_dict(cfg, seed)
         check_state_dict(cfg, self._sd, strict=state_dict is None)
         self._device = torch.device("cpu")
+        # texture encoder fast path for to_h5-format textures (proven per call on the device; RF_TEX_FAST=0
+        # forces the general pack + GEMM path)
+        self._tex_fast = os.environ.get("RF_TEX_FAST", "1") != "0"
         self._w: Optional[_DeviceWeights] = None
         self._plans: Dict = {}
         self.skip_token_num = cfg.num_register_tokens
@@ -268,14 +281,28 @@ class RenderFormer:
         cfg, W, dev = self.config, self._w, self._device
         D = cfg.latent_dim
         kt = cfg.texture_channels * cfg.texture_encode_patch_size ** 2
+        log_ch = 3 if log_encode else 0
         tex_in = torch.empty(plan.T_tri, kt, dtype=torch.bfloat16, device=dev)
-        ops.texture_pack(texture, 3 if log_encode else 0, plan.dst_row, tex_in)
+        tex_lin = torch.empty(plan.T_tri, D, dtype=torch.float32, device=dev)
+        fast = (self._tex_fast and plan.T_tri > 0 and W.tex_wsum is not None and texture.dim() == 5
+                and tuple(texture.shape[2:]) == (cfg.texture_channels, 32, 32))
+        if fast:
+            # to_h5-format textures: one scan proves the per-channel-constant form and
+            # the C-wide product replaces the K=13,312 GEMM; the general path below it runs only when the
+            # scan's device flag says some row is not of that form
+            coef = torch.empty(plan.T_tri, 16, dtype=torch.float32, device=dev)
+            ops.texture_scan(texture, log_ch, plan.dst_row, coef, W.tex_flag)
+            ops.texture_linear(coef, W.tex_wsum, W.tex_b, tex_lin, W.tex_flag)
+            ops.texture_pack_if(W.tex_flag, texture, 0, plan.dst_row, tex_in)
+            ops.gemm(tex_in, W.tex_w, tex_lin, W.tex_b, ops.EPI_F32, flag=W.tex_flag)
+        else:
+            ops.texture_pack(texture, log_ch, plan.dst_row, tex_in)
+            if plan.T_tri:
+                ops.gemm(tex_in, W.tex_w, tex_lin, W.tex_b, ops.EPI_F32)
         vn_in = torch.empty(plan.T_tri, W.vn_k, dtype=torch.bfloat16, device=dev)
         ops.vn_encode(vns, plan.dst_row, cfg.vn_pe_num_freqs, vn_in)
-        tex_lin = torch.empty(plan.T_tri, D, dtype=torch.float32, device=dev)
         vn_lin = torch.empty(plan.T_tri, D, dtype=torch.float32, device=dev)
         if plan.T_tri:
-            ops.gemm(tex_in, W.tex_w, tex_lin, W.tex_b, ops.EPI_F32)
             ops.gemm(vn_in, W.vn_w, vn_lin, W.vn_b, ops.EPI_F32)
         x = torch.empty(plan.T1, D, dtype=torch.float32, device=dev)
         ops.embed(x, plan.tri_rows, plan.T_tri, W.tri_token, 1, tex_lin, W.tex_norm, ops.FLT_EPS, vn_lin, W.vn_norm,

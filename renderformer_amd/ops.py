@@ -77,8 +77,9 @@ def _gemm_workspace(device) -> torch.Tensor:
 
 
 def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias: Optional[torch.Tensor] = None,
-         epilogue: int = EPI_BF16, tag: Optional[str] = None) -> torch.Tensor:
-    """out (epilogue)= a @ w.T ; a [M,K] bf16, w [N,K] bf16."""
+         epilogue: int = EPI_BF16, tag: Optional[str] = None, flag: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out (epilogue)= a @ w.T ; a [M,K] bf16, w [N,K] bf16.  With ``flag`` (int32 device scalar) the HIP engine
+    runs it and the launch is a no-op unless the flag is non-zero when it runs (rf_gemm_bf16_if)."""
     _dev(a, torch.bfloat16, "a")
     _dev(w, torch.bfloat16, "w")
     m, k = a.shape
@@ -92,8 +93,13 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias: Optional[tor
         _dev(bias, torch.float32, "bias")
     ws = _gemm_workspace(a.device)
     ev = _t0(tag)
-    call("rf_gemm_bf16", ptr(a), a.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), ptr(bias), m, n, k,
-         epilogue, ptr(ws), ws.numel(), stream())
+    if flag is None:
+        call("rf_gemm_bf16", ptr(a), a.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), ptr(bias), m, n, k,
+             epilogue, ptr(ws), ws.numel(), stream())
+    else:
+        _dev(flag, torch.int32, "flag")
+        call("rf_gemm_bf16_if", ptr(flag), ptr(a), a.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0),
+             ptr(bias), m, n, k, epilogue, ptr(ws), ws.numel(), stream())
     _t1(ev)
     return out
 
@@ -202,6 +208,51 @@ def texture_pack(texture: torch.Tensor, log_channels: int, dst_row: torch.Tensor
     b, n, c = texture.shape[:3]
     pe = texture[0, 0, 0].numel() if texture.dim() > 3 else 1
     call("rf_texture_pack", ptr(texture), b * n, c, pe, log_channels, ptr(dst_row), ptr(out), out.stride(0), stream())
+    return out
+
+
+def texture_pack_if(flag: torch.Tensor, texture: torch.Tensor, log_channels: int, dst_row: torch.Tensor,
+                    out: torch.Tensor):
+    """texture_pack that runs only when the device flag is non-zero (the general texture path)."""
+    _dev(flag, torch.int32, "flag")
+    _dev(texture, torch.float32, "texture")
+    _check(texture.is_contiguous(), "texture must be contiguous")
+    b, n, c = texture.shape[:3]
+    pe = texture[0, 0, 0].numel() if texture.dim() > 3 else 1
+    call("rf_texture_pack_if", ptr(flag), ptr(texture), b * n, c, pe, log_channels, ptr(dst_row), ptr(out),
+         out.stride(0), stream())
+    return out
+
+
+def texture_scan(texture: torch.Tensor, log_channels: int, dst_row: torch.Tensor, coef: torch.Tensor,
+                 flag: torch.Tensor):
+    """In-place log encode + per-row channel constants of to_h5-format textures; flag = 1 if any valid row is
+    not of that form (rf_texture_scan)."""
+    _dev(texture, torch.float32, "texture")
+    _dev(coef, torch.float32, "coef")
+    _dev(flag, torch.int32, "flag")
+    _check(texture.is_contiguous() and texture.dim() == 5 and tuple(texture.shape[3:]) == (32, 32),
+           "texture_scan: texture must be contiguous [B, N, C, 32, 32]")
+    b, n, c = texture.shape[:3]
+    call("rf_texture_scan", ptr(texture), b * n, c, 32 * 32, log_channels, ptr(dst_row), ptr(coef), coef.stride(0),
+         ptr(flag), stream())
+    return coef
+
+
+def texture_linear(coef: torch.Tensor, wsum: torch.Tensor, bias: Optional[torch.Tensor], out: torch.Tensor,
+                   flag: torch.Tensor):
+    """out = bias + coef @ wsum when the device flag is 0 (rf_texture_linear)."""
+    _dev(coef, torch.float32, "coef")
+    _dev(wsum, torch.float32, "wsum")
+    _dev(out, torch.float32, "out")
+    _dev(flag, torch.int32, "flag")
+    ch, n = wsum.shape
+    _check(coef.shape[1] >= ch and out.shape == (coef.shape[0], n) and wsum.is_contiguous(),
+           "texture_linear: shape mismatch")
+    if bias is not None:
+        _dev(bias, torch.float32, "bias")
+    call("rf_texture_linear", ptr(coef), coef.stride(0), out.shape[0], ch, ptr(wsum), ptr(bias), ptr(out),
+         out.stride(0), n, ptr(flag), stream())
     return out
 
 

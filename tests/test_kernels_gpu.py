@@ -611,3 +611,107 @@ def test_conv_stream_k_matches_data_parallel(monkeypatch, final, prec):
         assert relerr(a.cpu(), ref) < 2e-5
         # fp16 planes: a last-bit fp32 difference from the other K split can flip one fp16 rounding
         assert relerr(_planes_value(pa), _planes_value(pb)) < (1e-4 if f16 else 1e-6)
+
+
+# ----------------------------------------------------------------------------- texture encoder fast path
+def _to_h5_texture(b, n, c, seed):
+    from renderformer_amd.scenes import texture_mask
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    const = torch.rand(b, n, c, generator=g) * 4
+    return const[..., None, None] * torch.from_numpy(texture_mask(32)).float()
+
+
+@pytest.mark.parametrize("log_ch", [0, 3])
+def test_texture_scan(log_ch):
+    """rf_texture_scan: in-place log encode identical to rf_texture_pack's, per-row constants, and the flag
+    raised exactly when a VALID row leaves the to_h5 form (padded rows are only log-encoded)."""
+    ops = _ops()
+    b, n, c = 2, 37, 13
+    tex = _to_h5_texture(b, n, c, 5)
+    mask = torch.ones(b, n, dtype=torch.bool)
+    mask[1, 30:] = False
+    dst = torch.full((b * n,), -1, dtype=torch.int32)
+    dst[mask.reshape(-1)] = torch.arange(int(mask.sum()), dtype=torch.int32)
+    dst = dst.to(dev)
+    t_valid = int(mask.sum())
+
+    def scan(t):
+        t = t.clone().to(dev)
+        coef = torch.full((t_valid, 16), -7.0, device=dev)
+        flag = torch.full((1,), 5, dtype=torch.int32, device=dev)
+        ops.texture_scan(t, log_ch, dst, coef, flag)
+        return t.cpu(), coef.cpu(), int(flag.item())
+
+    got, coef, flag = scan(tex)
+    ref = tex.clone().to(dev)
+    ops.texture_pack(ref, log_ch, dst, torch.empty(t_valid, c * 1024, dtype=torch.bfloat16, device=dev))
+    assert flag == 0
+    assert torch.equal(got, ref.cpu())  # same in-place encode, bit for bit
+    exp = got[..., 0, 0].reshape(b * n, c)[mask.reshape(-1)]
+    assert torch.equal(coef[:, :c], exp)
+    assert torch.all(coef[:, c:] == -7.0)
+    bad = tex.clone()
+    bad[1, 4, 11, 31, 2] = 0.5  # outside the mask (31 + 2 > 32), valid row
+    assert scan(bad)[2] == 1
+    bad = tex.clone()
+    bad[0, 7, 3, 31, 1] += 0.5  # inside the mask (31 + 1 <= 32), valid row
+    assert scan(bad)[2] == 1
+    pad_only = tex.clone()
+    pad_only[1, 33, 0, 3, 3] += 1.0  # padded row: not checked
+    assert scan(pad_only)[2] == 0
+    nan = tex.clone()
+    nan[0, 0, 5, 0, 0] = float("nan")
+    assert scan(nan)[2] == 1
+
+
+def test_texture_linear_and_gates():
+    """rf_texture_linear == bias + coef @ wsum when the flag is 0 and a no-op otherwise; rf_gemm_bf16_if and
+    rf_texture_pack_if run only when the flag is set."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(3)
+    rows, c, d = 300, 13, 1024
+    coef = torch.randn(rows, 16, generator=g).to(dev)
+    wsum = torch.randn(c, d, generator=g).to(dev)
+    bias = torch.randn(d, generator=g).to(dev)
+    out = torch.full((rows, d), 9.0, device=dev)
+    flag = torch.ones(1, dtype=torch.int32, device=dev)
+    ops.texture_linear(coef, wsum, bias, out, flag)
+    assert torch.all(out == 9.0)
+    flag.zero_()
+    ops.texture_linear(coef, wsum, bias, out, flag)
+    ref = bias.double() + coef[:, :c].double() @ wsum.double()
+    assert relerr(out, ref) < 1e-6
+
+    a = torch.randn(333, 1024, generator=g).bfloat16().to(dev)
+    w = (torch.randn(1024, 1024, generator=g) / 32).bfloat16().to(dev)
+    o = torch.full((333, 1024), 9.0, device=dev)
+    ops.gemm(a, w, o, bias, ops.EPI_F32, flag=flag)
+    tex = _to_h5_texture(1, 20, 13, 1).to(dev)
+    dst = torch.arange(20, dtype=torch.int32, device=dev)
+    packed = torch.zeros(20, 13 * 1024, dtype=torch.bfloat16, device=dev)
+    ops.texture_pack_if(flag, tex, 0, dst, packed)
+    torch.cuda.synchronize()
+    assert torch.all(o == 9.0) and torch.all(packed == 0)
+    flag.fill_(1)
+    ops.gemm(a, w, o, bias, ops.EPI_F32, flag=flag)
+    assert relerr(o, a.double() @ w.double().t() + bias.double()) < 1e-5
+    ops.texture_pack_if(flag, tex, 0, dst, packed)
+    assert torch.equal(packed, tex.reshape(20, -1).bfloat16())
+
+
+def test_texture_embedding_fast_vs_general(monkeypatch):
+    """The model's texture embedding on the fast path vs the general pack + GEMM path (bf16 operands)."""
+    from renderformer_amd import RenderFormer
+    from golden_util import load_case
+    cfg, sd, inp, res, z = load_case("tiny_swin")
+    m = RenderFormer(cfg, sd).to("cuda")
+    mask = inp["mask"].cuda()
+    plan = m._plan(mask, 1, res)
+    vns = inp["vn"].reshape(mask.shape[0], -1, 9).cuda()
+    outs = {}
+    for fast in ("1", "0"):
+        monkeypatch.setenv("RF_TEX_FAST", fast)
+        m._tex_fast = fast == "1"
+        outs[fast] = m._embed_triangles(plan, inp["texture"].clone().cuda(), vns, True).cpu()
+    assert int(m._w.tex_flag.item()) == 0
+    assert relerr(outs["1"], outs["0"]) < 2e-3

@@ -31,6 +31,7 @@ def test_pipeline_matches_reference(name, dpt):
     err = rel_l2(out.cpu(), z["hdr"])
     print(f"{name} (DPT {dpt}): rel L2 {err:.3e}")
     assert err < HDR_TOL
+    assert int(pipe.model._w.tex_flag.item()) == 0  # to_h5-format textures: the texture fast path ran
     # in-place log encoding side effect (rendering_pipeline.py:67-68)
     assert torch.allclose(tex[:, :, 10, 0, 0].cpu(), torch.from_numpy(z["texture_after_ch10"]), rtol=1e-6, atol=1e-6)
 
@@ -81,3 +82,27 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(L, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(L.HipLibraryError):
         L.load()
+
+
+@pytest.mark.parametrize("mode", ["general", "perturbed"])
+def test_texture_paths_match_reference(mode, monkeypatch):
+    """The texture encoder's to_h5 fast path is proven per call on the device: forcing the general pack+GEMM
+    path (RF_TEX_FAST=0), or feeding a texture that is NOT of the to_h5 form (one texel moved, which must
+    raise the scan's flag and route through the gated general path), still matches the oracle."""
+    cfg, sd, inp, res, z = load_case("tiny_swin")
+    tex = inp["texture"].clone()
+    if mode == "general":
+        monkeypatch.setenv("RF_TEX_FAST", "0")
+    else:
+        tex[0, 3, 2, 5, 7] += 0.25  # diffuse channel 2 of triangle 3: no longer constant x mask
+    ref = rf_ref.render(sd, cfg, inp["triangles"], tex.clone(), inp["mask"], inp["vn"], inp["c2w"], inp["fov"],
+                        resolution=res)
+    pipe = _pipeline(cfg, sd)
+    d = {k: v.cuda() for k, v in inp.items()}
+    out = pipe(d["triangles"], tex.cuda(), d["mask"], d["vn"], d["c2w"], d["fov"], resolution=res,
+               torch_dtype=torch.bfloat16)
+    err = rel_l2(out.cpu(), ref)
+    print(f"texture {mode}: rel L2 {err:.3e}")
+    assert err < HDR_TOL
+    if mode == "perturbed":
+        assert int(pipe.model._w.tex_flag.item()) == 1  # the scan rejected the fast path

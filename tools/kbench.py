@@ -142,7 +142,7 @@ def conv():
             x = split_planes(torch.randn(1, hw, hw, cin, device=dev), conv.cin_pad, f16=f16)
             fl = 2 * hw * hw * cin * cout * 9
             mf = 1 if f16 else 3
-            tiles = ("128", "1288", "256", "2561", "auto4w", "auto") if f16 else ("128", "256")
+            tiles = os.environ.get("KB_CONV_TILES", "128,1288,256,2561,auto4w,auto").split(",") if f16 else ("128", "256")
             for t in tiles:
                 os.environ["RF_CONV_PHASED"] = "1" if t == "256ph" else "0"
                 os.environ["RF_CONV_SKW8"] = "0" if t == "auto4w" else "1"
@@ -152,6 +152,15 @@ def conv():
                 os.environ.pop("RF_CONV_TILE", None)
                 print(f"conv3x3 {'f16 ' if f16 else 'bf16x3'} {cin}->{cout} @{hw} tile={t}: "
                       f"{ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF(algorithmic)  {mf*fl/ms/1e9:7.1f} TF(MFMA issued)")
+            if f16 and os.environ.get("KB_CONV_GEMM"):  # the same M, N, K as a plain bf16 GEMM (no gather)
+                a = torch.randn(hw * hw, 9 * cin, device=dev).bfloat16()
+                w = torch.randn(cout, 9 * cin, device=dev).bfloat16()
+                c = torch.empty(hw * hw, cout, device=dev)
+                for be in ("hip", "auto"):
+                    os.environ["RF_GEMM_BACKEND"] = be
+                    ms = timeit(lambda: ops.gemm(a, w, c, None, ops.EPI_F32), reps=10)
+                    print(f"  plain GEMM {hw*hw}x{cout}x{9*cin} [{be}]: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF")
+                os.environ.pop("RF_GEMM_BACKEND", None)
 
 
 if __name__ == "__main__":
