@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -30,7 +32,60 @@ struct Plan {
 
 std::mutex g_mu;
 std::map<int, hipblasLtHandle_t> g_handles;
-std::map<std::tuple<int, int, int, int, int64_t, int64_t, int64_t, int, bool>, Plan> g_plans;
+std::map<std::tuple<int, int, int, int, int64_t, int64_t, int64_t, int, bool, int>, Plan> g_plans;
+
+// RF_BLASLT_ALGO=i (tuning/diagnostics, tools/kbench.py blaslt): use the i-th heuristic candidate instead
+// of the first
+int algo_choice() {
+    const char* e = getenv("RF_BLASLT_ALGO");
+    return e ? atoi(e) : 0;
+}
+
+// One-time tuning of a bf16-output plan (the QKV / Q / KV projections): hipBLASLt's first heuristic pick
+// is up to 15 % off the best of its top candidates on the path's shapes (tools/kbench.py blaslt), so the
+// first call per shape times TUNE_CANDIDATES of them on the caller's buffers (beta = 0: the output is
+// rewritten by the real call that follows) and keeps the fastest.  This synchronises the stream once per
+// shape; RF_BLASLT_TUNE=0 disables it, and it is skipped while the stream is being captured.  The
+// residual-accumulate plans (beta = 1) are never tuned: their output is live (and the first pick was the
+// fastest on every path shape).
+constexpr int TUNE_CANDIDATES = 8;
+
+bool tune_enabled(hipStream_t stream) {
+    const char* e = getenv("RF_BLASLT_TUNE");
+    if (e && atoi(e) == 0) return false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+    return true;
+}
+
+int fastest(hipblasLtHandle_t h, const Plan& pl, const hipblasLtMatmulHeuristicResult_t* res, int found,
+            const void* w, const void* a, void* c, uint64_t wmax, void* workspace, hipStream_t stream) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return 0;
+    const float alpha = 1.0f, beta = 0.0f;
+    int best = 0;
+    float best_ms = 1e30f;
+    for (int i = 0; i < found; ++i) {
+        if (res[i].workspaceSize > wmax) continue;
+        auto run = [&]() {
+            return hipblasLtMatmul(h, pl.desc, &alpha, w, pl.la, a, pl.lb, &beta, c, pl.lc, c, pl.lc, &res[i].algo,
+                                   workspace, res[i].workspaceSize, stream) == HIPBLAS_STATUS_SUCCESS;
+        };
+        if (!run()) continue;  // warm-up (and validity)
+        bool ok = hipEventRecord(e0, stream) == hipSuccess;
+        for (int r = 0; r < 4 && ok; ++r) ok = run();
+        ok = ok && hipEventRecord(e1, stream) == hipSuccess;
+        float ms = 0.f;
+        if (!ok || hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
+        if (ms < best_ms) {
+            best_ms = ms;
+            best = i;
+        }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return best;
+}
 
 hipblasLtHandle_t handle_for(int dev) {
     auto it = g_handles.find(dev);
@@ -54,7 +109,8 @@ int blaslt_gemm(const void* a, int64_t lda, const void* w, int64_t ldw, void* c,
     std::lock_guard<std::mutex> lock(g_mu);
     hipblasLtHandle_t h = handle_for(dev);
     if (!h) return -1;
-    const auto key = std::make_tuple(dev, m, n, k, lda, ldw, ldc, mode, bias != nullptr);
+    const int choice = algo_choice();
+    const auto key = std::make_tuple(dev, m, n, k, lda, ldw, ldc, mode, bias != nullptr, choice);
     auto it = g_plans.find(key);
     if (it == g_plans.end()) {
         Plan pl;
@@ -81,14 +137,18 @@ int blaslt_gemm(const void* a, int64_t lda, const void* w, int64_t ldw, void* c,
         uint64_t wmax = workspace ? (uint64_t)ws_bytes : 0;
         good = good && hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wmax,
                                                              sizeof(wmax)) == HIPBLAS_STATUS_SUCCESS;
-        hipblasLtMatmulHeuristicResult_t res[1];
+        hipblasLtMatmulHeuristicResult_t res[32];
         int found = 0;
-        good = good && hipblasLtMatmulAlgoGetHeuristic(h, pl.desc, pl.la, pl.lb, pl.lc, pl.lc, pref, 1, res, &found) ==
-                           HIPBLAS_STATUS_SUCCESS;
+        const bool tune = choice == 0 && mode == RF_EPI_BF16 && tune_enabled((hipStream_t)stream);
+        const int want = tune ? TUNE_CANDIDATES : std::min(choice + 1, 32);
+        good = good && hipblasLtMatmulAlgoGetHeuristic(h, pl.desc, pl.la, pl.lb, pl.lc, pl.lc, pref, want, res,
+                                                       &found) == HIPBLAS_STATUS_SUCCESS;
         if (pref) hipblasLtMatmulPreferenceDestroy(pref);
         if (good && found > 0) {
-            pl.algo = res[0].algo;
-            pl.ws = res[0].workspaceSize;
+            int i = std::max(0, std::min(choice, found - 1));
+            if (tune && found > 1) i = fastest(h, pl, res, found, w, a, c, wmax, workspace, (hipStream_t)stream);
+            pl.algo = res[i].algo;
+            pl.ws = res[i].workspaceSize;
             pl.ok = pl.ws <= wmax;
         }
         it = g_plans.emplace(key, pl).first;

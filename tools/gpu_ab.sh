@@ -1,6 +1,11 @@
-# A/B: current library vs renderformer_amd/lib/librfhip_old.so on the same box (kbench $1)
+# A/B of one env switch on the full bench in one call: bash tools/gpu_ab.sh <tag> "<envA>" "<envB>"
 set -e
-mkdir -p gpurun_out
-timeout -k 10 300 python tools/kbench.py ${1:-gemm} > gpurun_out/kb_A.log 2>&1
-RF_LIB=$PWD/renderformer_amd/lib/librfhip_old.so timeout -k 10 300 python tools/kbench.py ${1:-gemm} > gpurun_out/kb_B.log 2>&1
-timeout -k 10 300 python tools/kbench.py ${1:-gemm} > gpurun_out/kb_A2.log 2>&1
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${1:-ab}
+mkdir -p $O
+cd $R
+for i in 1 2; do
+env $2 timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_a$i.json 2> $O/bench_a.err
+env $3 timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_b$i.json 2> $O/bench_b.err
+done
+echo done

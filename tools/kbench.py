@@ -133,6 +133,28 @@ def gemm():
     print(f"torch/hipBLASLt 8192^3 reference: {2*8192**3/ms/1e9:7.1f} TF")
 
 
+def blaslt():
+    """hipBLASLt heuristic candidates 0..15 (RF_BLASLT_ALGO) on the frame's plain projection shapes."""
+    shapes = [("s1 qkv", S, 3 * D, D, ops.EPI_BF16), ("s1 out", S, D, D, ops.EPI_ADD_F32),
+              ("s1 w2", S, D, F, ops.EPI_ADD_F32), ("s2 q", R, D, D, ops.EPI_BF16), ("s2 kv", S, 2 * D, D, ops.EPI_BF16),
+              ("s2 qkv", R, 3 * D, D, ops.EPI_BF16), ("s2 out", R, D, D, ops.EPI_ADD_F32),
+              ("s2 w2", R, D, F, ops.EPI_ADD_F32)]
+    os.environ["RF_GEMM_BACKEND"] = "auto"
+    for name, m, n, k, epi in shapes:
+        a = torch.randn(m, k, device=dev).bfloat16()
+        w = (torch.randn(n, k, device=dev) / math.sqrt(k)).bfloat16()
+        c = (torch.empty(m, n, device=dev, dtype=torch.bfloat16) if epi == ops.EPI_BF16 else torch.zeros(m, n, device=dev))
+        res = []
+        for i in range(int(os.environ.get("KB_ALGOS", "16"))):
+            os.environ["RF_BLASLT_ALGO"] = str(i)
+            ms = timeit(lambda: ops.gemm(a, w, c, None, epi), reps=20)
+            res.append(ms)
+        os.environ.pop("RF_BLASLT_ALGO", None)
+        best = min(range(len(res)), key=lambda i: res[i])
+        print(f"blaslt {name:7s} {m}x{n}x{k}: algo0 {res[0]*1e3:6.1f} us, best algo{best} {res[best]*1e3:6.1f} us "
+              f"({2*m*n*k/res[best]/1e9:6.1f} TF)  all: " + " ".join(f"{r*1e3:.1f}" for r in res), flush=True)
+
+
 def conv():
     from renderformer_amd.dpt import _Conv, split_planes
     for f16 in (True,) if os.environ.get("KB_F16_ONLY") else (True, False):
@@ -165,6 +187,6 @@ def conv():
 
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
-    for name, fn in (("attn", attn), ("gemm", gemm), ("conv", conv)):
+    for name, fn in (("attn", attn), ("gemm", gemm), ("conv", conv), ("blaslt", blaslt)):
         if what in (name, "all"):
             fn()
