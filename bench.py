@@ -123,18 +123,22 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    ops.TIMER = ops.KernelTimer(DOMINANT)
+    # HIP events bracket the dominant kernel's launches in the LAST timed step only: each event pair adds
+    # ~11 us of queue time around its launch (profiles/r1: 14 x 11.4 us per frame when every step was timed)
+    timer = ops.KernelTimer(DOMINANT)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if i == args.steps - 1:
+            ops.TIMER = timer
         out = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    timer, ops.TIMER = ops.TIMER, None
+    ops.TIMER = None
     elapsed = max_over_ranks(elapsed, device=dev)
     if not torch.isfinite(out).all():
         raise RuntimeError("non-finite output")
@@ -144,7 +148,7 @@ def main():
     fps = total_frames / elapsed
     fl = frame_flops(cfg, args.tris, args.res, args.views)
     durs = timer.durations_ms()
-    per_step_launches = len(durs) // max(1, args.steps)
+    per_step_launches = len(durs)  # one timed step
     kern_ms = statistics.mean(durs) if durs else float("nan")
     s_len = args.tris + cfg.num_register_tokens
     kern_flops = 4 * s_len * s_len * cfg.latent_dim * args.scenes  # QK^T + PV per launch (all heads, all scenes)

@@ -211,6 +211,7 @@ class RenderFormer:
         # texture encoder fast path for to_h5-format textures (proven per call on the device; RF_TEX_FAST=0
         # forces the general pack + GEMM path)
         self._tex_fast = os.environ.get("RF_TEX_FAST", "1") != "0"
+        self._last_plan = None
         self._w: Optional[_DeviceWeights] = None
         self._plans: Dict = {}
         self.skip_token_num = cfg.num_register_tokens
@@ -267,6 +268,12 @@ class RenderFormer:
         _load_lib()
 
     def _plan(self, mask, V, res):
+        # same mask tensor object, unmodified since the last call (torch's version counter): reuse that plan
+        # without reading the mask back (the host sync below stalls the queue at the start of every frame).
+        # The reference is held, so the object (and its storage) cannot be recycled under the same id.
+        last = self._last_plan
+        if last is not None and last[0] is mask and last[1] == (mask._version, V, res):
+            return last[2]
         key = (tuple(mask.shape), mask.sum(1).cpu().numpy().tobytes(), mask.cpu().numpy().tobytes(), V, res)
         plan = self._plans.get(key)
         if plan is None:
@@ -274,6 +281,7 @@ class RenderFormer:
                 self._plans.clear()
             plan = _build_plan(mask, V, res, self.config.patch_size, self.config.num_register_tokens, self._device)
             self._plans[key] = plan
+        self._last_plan = (mask, (mask._version, V, res), plan)
         return plan
 
     # ------------------------------------------------------------------ stages

@@ -106,3 +106,23 @@ def test_texture_paths_match_reference(mode, monkeypatch):
     assert err < HDR_TOL
     if mode == "perturbed":
         assert int(pipe.model._w.tex_flag.item()) == 1  # the scan rejected the fast path
+
+
+def test_plan_cache_follows_in_place_mask_edits():
+    """The per-call plan is reused only for the same, unmodified mask tensor: an in-place edit of the mask
+    must produce the same image as a fresh tensor with the edited content."""
+    from renderformer_amd.scenes import batch_scenes, synthetic_scene
+    cfg, sd, _, _, _ = load_case("tiny_swin")
+    pipe = _pipeline(cfg, sd)
+    b = {k: v.cuda() for k, v in batch_scenes([synthetic_scene(60, 1, seed=5)], padding_length=64).items()
+         if k != "tex_channels"}
+
+    def run(mask):
+        return pipe(b["triangles"], b["texture"].clone(), mask, b["vn"], b["c2w"], b["fov"], resolution=64).cpu()
+
+    mask = b["mask"].clone()
+    run(mask)
+    mask[0, 40:] = False  # in place: same object, new version
+    got = run(mask)
+    ref = run(mask.clone())
+    assert rel_l2(got, ref) < 1e-6
