@@ -4,6 +4,7 @@
 // All are HBM-bound streaming kernels: one wave64 per row, fp32 reductions with
 // xor-shuffles, 8-16 B per lane accesses where the layout allows.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -34,6 +35,36 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
         pk.x = pack_bf16x2(v.x * inv * g.x, v.y * inv * g.y);
         pk.y = pack_bf16x2(v.z * inv * g.z, v.w * inv * g.w);
         *reinterpret_cast<uint2*>(orow + c) = pk;
+    }
+}
+
+// dim = 256 * NV: the whole row and its weights are loaded up front (NV float4 per lane each, all in
+// flight at once), so a row costs one memory round trip instead of one per 256 columns plus a re-read
+template <int NV>
+__global__ __launch_bounds__(256) void rmsnorm_v_kernel(const float* __restrict__ x, int64_t ldx,
+                                                        const float* __restrict__ w, float eps,
+                                                        bf16_t* __restrict__ out, int64_t ldo, int rows) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float* xr = x + (int64_t)row * ldx + 4 * lane;
+    float4 v[NV], g[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = *reinterpret_cast<const float4*>(xr + 256 * i);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) g[i] = *reinterpret_cast<const float4*>(w + 4 * lane + 256 * i);
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) ss += v[i].x * v[i].x + v[i].y * v[i].y + v[i].z * v[i].z + v[i].w * v[i].w;
+    ss = wave_sum(ss);
+    const float inv = 1.0f / sqrtf(ss / (float)(256 * NV) + eps);
+    bf16_t* orow = out + (int64_t)row * ldo + 4 * lane;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        uint2 pk;
+        pk.x = pack_bf16x2(v[i].x * inv * g[i].x, v[i].y * inv * g[i].y);
+        pk.y = pack_bf16x2(v[i].z * inv * g[i].z, v[i].w * inv * g[i].w);
+        *reinterpret_cast<uint2*>(orow + 256 * i) = pk;
     }
 }
 
@@ -94,6 +125,9 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(const bf16_t* src, in
     for (int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6); row < rows; row += stride) {
         const int srow = src_rows ? src_rows[row] : row;
         const bf16_t* s = src + (int64_t)srow * ld_src;
+        // RoPE angle inputs are loaded with the row (one round trip), the sincos waits for them
+        float ang = 0.f;
+        if (pos && lane < 9 * n_freqs) ang = pos[(int64_t)(row / pos_div) * ld_pos + lane / n_freqs] * freqs[lane % n_freqs];
         u32x4 lo[UPL], hi[UPL];
         float ss[UPL];
 #pragma unroll
@@ -132,11 +166,8 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(const bf16_t* src, in
             }
         }
         float my_c = 1.f, my_s = 0.f;
-        if (pos && lane < 9 * n_freqs) {
-            // hardware sin/cos: ~1e-6 absolute, far below the bf16 rounding of the rotated output
-            const float* pr = pos + (int64_t)(row / pos_div) * ld_pos;
-            __sincosf(pr[lane / n_freqs] * freqs[lane % n_freqs], &my_s, &my_c);
-        }
+        // hardware sin/cos: ~1e-6 absolute, far below the bf16 rounding of the rotated output
+        if (pos && lane < 9 * n_freqs) __sincosf(ang, &my_s, &my_c);
         // every unit of this lane has chunk index j = lane & 7 (64 is a multiple of 8)
         float cs[8], sn[8];
 #pragma unroll
@@ -213,8 +244,19 @@ extern "C" int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, floa
     RF_REQUIRE(x && weight && out, "rf_rmsnorm: null pointer");
     RF_REQUIRE(dim % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0, "rf_rmsnorm: dim/ld must be multiples of 4");
     if (rows <= 0) return RF_OK;
-    hipLaunchKernelGGL(rmsnorm_kernel, dim3((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), dim3(256), 0,
-                       (hipStream_t)stream, x, ldx, weight, eps, (bf16_t*)out, ldo, rows, dim);
+    const dim3 grid((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK);
+    hipStream_t st = (hipStream_t)stream;
+    const bool al = ((uintptr_t)x & 15) == 0 && ((uintptr_t)weight & 15) == 0 && ((uintptr_t)out & 7) == 0;
+    static const bool generic = getenv("RF_RMSNORM_GENERIC") && atoi(getenv("RF_RMSNORM_GENERIC"));  // A/B only
+    switch (al && !generic && dim % 256 == 0 ? dim / 256 : 0) {
+        case 2: hipLaunchKernelGGL(rmsnorm_v_kernel<2>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
+        case 3: hipLaunchKernelGGL(rmsnorm_v_kernel<3>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
+        case 4: hipLaunchKernelGGL(rmsnorm_v_kernel<4>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
+        case 6: hipLaunchKernelGGL(rmsnorm_v_kernel<6>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
+        case 8: hipLaunchKernelGGL(rmsnorm_v_kernel<8>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
+        default:
+            hipLaunchKernelGGL(rmsnorm_kernel, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows, dim);
+    }
     return rf::check_launch("rf_rmsnorm");
 }
 

@@ -155,6 +155,24 @@ def blaslt():
               f"({2*m*n*k/res[best]/1e9:6.1f} TF)  all: " + " ".join(f"{r*1e3:.1f}" for r in res), flush=True)
 
 
+def norms():
+    """Row kernels at the frame's shapes: RMSNorm (f32 -> bf16) and q/k norm + RoPE (bf16 in place)."""
+    for rows in (S, R):
+        x = torch.randn(rows, D, device=dev)
+        w = torch.rand(D, device=dev)
+        o = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+        ms = timeit(lambda: ops.rmsnorm(x, w, 1e-6, o), reps=50)
+        print(f"rmsnorm {rows}x{D}: {ms*1e3:6.1f} us  {rows*D*6/ms/1e9:6.0f} GB/s", flush=True)
+    freqs = torch.rand(6, device=dev)
+    for name, rows, seg in (("s1 qk", S, 2), ("s2 q", R, 1)):
+        qkv = torch.randn(rows, 3 * D, device=dev).bfloat16()
+        pair = qkv[:, :seg * D]
+        nw = torch.rand(seg * D, device=dev)
+        pos = torch.randn(rows, 9, device=dev)
+        ms = timeit(lambda: ops.qk_norm_rope(pair, pair, H, nw, 1e-6, pos, freqs, n_seg=seg), reps=50)
+        print(f"qk_norm_rope {name} {rows}x{seg*D}: {ms*1e3:6.1f} us  {rows*seg*D*4/ms/1e9:6.0f} GB/s", flush=True)
+
+
 def conv():
     from renderformer_amd.dpt import _Conv, split_planes
     for f16 in (True,) if os.environ.get("KB_F16_ONLY") else (True, False):
@@ -187,6 +205,6 @@ def conv():
 
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
-    for name, fn in (("attn", attn), ("gemm", gemm), ("conv", conv), ("blaslt", blaslt)):
+    for name, fn in (("attn", attn), ("gemm", gemm), ("conv", conv), ("blaslt", blaslt), ("norms", norms)):
         if what in (name, "all"):
             fn()
