@@ -82,6 +82,7 @@ struct EngineArgs {
     int sk_epoch;
     int group_m;  // tile raster: groups of group_m m-tiles, n fastest within a group (host-chosen)
     const int* gate;  // optional device flag: the launch is a no-op unless *gate != 0 (rf_gemm_bf16_if)
+    int halo_lg;      // halo-tiled 3x3 convolution: log2 of the tile width in pixels (halo_kernel)
 };
 
 // uniform early exit of a gated launch (every block reads the same flag, so a stream-K grid exits whole)
@@ -114,6 +115,7 @@ RF_DEV float silu(float x) { return x / (1.0f + expf(-x)); }
 template <int N>
 RF_DEV void wait_vm() {
     if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -927,6 +929,167 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Halo-tiled 3x3 convolution (stride 1, pad 1, fp16 operands).  The im2col gather of engine_mainloop
+// stages every input pixel once per tap (9x the input through L2 -> LDS per output tile); here an output
+// tile of BM pixels is a TH x TW block of one image (TW = min(BM, wo), rows of m stay contiguous, so the
+// epilogue is unchanged) and, per 32-channel chunk, its (TH+2) x (TW+2) input halo is staged ONCE and
+// read by all nine taps at a per-tap row offset (3x the tile's pixels at TH = 1, 2x at TH = 2).  K runs
+// chunk-major, tap-minor: W rows (tap * cin_pad + chunk * 32) stream through a 3-stage ring as before;
+// the next chunk's halo is issued at the chunk's first tap into the other of two halo buffers and drained
+// (vmcnt(0) + barrier) before the step that first reads it.
+template <class C>
+struct Halo {
+    static constexpr int ROWS = (3 * (C::BM + 2) + 15) / 16 * 16;  // >= (TH+2)(TW+2) for every TW | BM, TW >= 16
+    static constexpr int BYTES = ROWS * 64;
+    static constexpr int PIECES = ROWS / 16;
+    static constexpr int PPW = (PIECES + C::NWAVE - 1) / C::NWAVE;  // halo pieces per wave
+    static constexpr int BST = 3;                                   // W ring stages
+    static constexpr int LDS = 2 * BYTES + BST * C::B_BYTES;
+};
+
+template <class C>
+RF_DEV void halo_mainloop(const EngineArgs& p, char* smem, int m0, int n0, f32x4 (&acc)[C::TI][C::TJ]) {
+    using H = Halo<C>;
+    constexpr int TI = C::TI, TJ = C::TJ, PB = C::PB, S = H::BST;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave / C::WGN, wn = wave % C::WGN;
+    const int lg = p.halo_lg, tw = 1 << lg, hw2 = tw + 2;
+    const int hr_n = ((C::BM >> lg) + 2) * hw2;  // halo rows in use
+    const int per_img = p.ho * p.wo;
+    const int img = m0 / per_img, rem = m0 - img * per_img;
+    const int y0 = rem / p.wo, x0 = rem - y0 * p.wo;
+
+    // halo staging: slot t of this wave is piece wave + NWAVE t (16 rows x 64 B); lane -> (row, chunk)
+    int hpix[H::PPW];
+#pragma unroll
+    for (int t = 0; t < H::PPW; ++t) {
+        const int hr = (wave + C::NWAVE * t) * 16 + (lane >> 2);
+        int pix = -1;
+        if (hr < hr_n) {
+            const int hy = hr / hw2, hx = hr - hy * hw2;
+            const int iy = y0 + hy - 1, ix = x0 + hx - 1;
+            if (iy >= 0 && iy < p.hi && ix >= 0 && ix < p.wi) pix = (img * p.hi + iy) * p.wi + ix;
+        }
+        hpix[t] = pix;
+    }
+    int brow[PB], blc[PB];
+#pragma unroll
+    for (int pc = 0; pc < PB; ++pc) {
+        brow[pc] = (wave * PB + pc) * 16 + (lane >> 2);
+        blc[pc] = (lane & 3) ^ ((brow[pc] >> 1) & 3);
+    }
+    auto issue_halo = [&](int chunk, int buf) {
+#pragma unroll
+        for (int t = 0; t < H::PPW; ++t) {
+            const int piece = wave + C::NWAVE * t;
+            if (piece < H::PIECES) {
+                const int hch = (lane & 3) ^ (((piece * 16 + (lane >> 2)) >> 1) & 3);
+                const bf16_t* src = hpix[t] >= 0 ? p.a + (int64_t)hpix[t] * p.cin_pad + chunk * BK + hch * 8 : p.zero;
+                __builtin_amdgcn_global_load_lds(GLB_PTR(void, src), LDS_PTR(void, smem + buf * H::BYTES + piece * 1024),
+                                                 16, 0, 0);
+            }
+        }
+    };
+    auto issue_w = [&](int kt, int stage) {
+        const int chunk = kt / 9, tap = kt - 9 * chunk;
+        const int k0 = tap * p.cin_pad + chunk * BK;
+        char* st = smem + 2 * H::BYTES + stage * C::B_BYTES;
+#pragma unroll
+        for (int pc = 0; pc < PB; ++pc) {
+            const int piece = wave * PB + pc;
+            const int64_t woff = (int64_t)(n0 + brow[pc]) * p.ldw + k0 + blc[pc] * 8;
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, p.w + woff), LDS_PTR(void, st + piece * 1024), 16, 0, 0);
+        }
+    };
+
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nch = p.cin_pad / BK, nk = 9 * nch;
+    const int frag_row = lane & 15, frag_ch = lane >> 4;
+    // halo row of fragment i's output row r at tap (0, 0): r + 2 (r / TW)
+    auto base_hr = [&](int i) {
+        const int r = wm * C::MW + i * 16 + frag_row;
+        return r + ((r >> lg) << 1);
+    };
+    struct Frags {
+        bf16x8 a[TI], w[TJ];
+    };
+    auto load_frags = [&](int kt, Frags& f) {
+        const int chunk = kt / 9, tap = kt - 9 * chunk;
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        const char* hb = smem + (chunk & 1) * H::BYTES;
+        const int toff = ky * hw2 + kx;
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+            f.a[i] = *reinterpret_cast<const bf16x8*>(hb + lds_off(base_hr(i) + toff, frag_ch));
+        const char* st = smem + 2 * H::BYTES + (kt % S) * C::B_BYTES;
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+            f.w[j] = *reinterpret_cast<const bf16x8*>(st + lds_off(wn * C::NWD + j * 16 + frag_row, frag_ch));
+    };
+    auto mma = [&](const Frags& f) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, f.w[j]),
+                                                                   __builtin_bit_cast(f16x8, f.a[i]), acc[i][j], 0, 0, 0);
+    };
+    // W tile kt+1 landed (over-waiting when halo pieces are among the younger DMAs is safe)
+    auto wait_w = [&](int younger) {
+        if (younger >= 1) wait_vm<PB>();
+        else wait_vm<0>();
+    };
+
+    issue_halo(0, 0);
+#pragma unroll
+    for (int st = 0; st < S; ++st) issue_w(st, st);
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    Frags f0, f1;
+    load_frags(0, f0);
+    auto step = [&](int kt, Frags& cur, Frags& nxt) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's fragment reads of `cur` are complete
+        if (kt + 1 < nk) {
+            if ((kt + 1) % 9 == 0) wait_vm<0>();  // tile kt+1 starts a chunk: its halo (and all W) landed
+            else wait_w(std::min(S - 2, nk - 2 - kt));
+        }
+        __builtin_amdgcn_s_barrier();  // every wave's DMA landed and every wave's reads of tile kt are done
+        __builtin_amdgcn_sched_barrier(0);
+        const int chunk = kt / 9;
+        if (kt - 9 * chunk == 0 && chunk + 1 < nch) issue_halo(chunk + 1, (chunk + 1) & 1);
+        if (kt + S < nk) issue_w(kt + S, kt % S);
+        if (kt + 1 < nk) load_frags(kt + 1, nxt);
+        mma(cur);
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+        step(kt, f0, f1);
+        if (kt + 1 < nk) step(kt + 1, f1, f0);
+    }
+}
+
+template <class C, int EPI>
+__global__ __launch_bounds__(C::THREADS, C::BM == 256 ? 1 : 2) void halo_kernel(EngineArgs p) {
+    __shared__ __attribute__((aligned(16))) char smem[Halo<C>::LDS];
+    if (gated_off(p)) return;
+    const int tiles_m = p.m / C::BM;
+    const int nwg = gridDim.x;
+    const int hw = blockIdx.x;
+    const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
+    int tm, tn;
+    tile_coords(wg, tiles_m, p.n / C::BN, p.group_m, tm, tn);
+    f32x4 acc[C::TI][C::TJ];
+    halo_mainloop<C>(p, smem, tm * C::BM, tn * C::BN, acc);
+    engine_epilogue<C, EPI>(p, tm * C::BM, tn * C::BN, acc);
+}
+
 // Tile configurations.  T128: 128x128, 4 waves of 64x64, 3-stage ring (48 KiB / 96 KiB LDS).
 // T256: 256x256, 8 waves of 128x64, 4-stage ring (128 KiB).  T256x128: 8 waves of 64x64, bf16x3 3-stage (144 KiB).
 using T128 = Tile<128, 128, 2, 2, 3>;
@@ -952,6 +1115,43 @@ int launch(EngineArgs a, void* stream, const char* what) {
     hipLaunchKernelGGL((engine_kernel<C, EPI, NTERM, GATHER, false>), dim3(nwg), dim3(C::THREADS), 0, (hipStream_t)stream,
                        a);
     return rf::check_launch(what);
+}
+
+// the halo kernel serves this convolution: 3x3, stride 1, pad 1, whole tiles of TW | wo (power of 2) x TH
+template <class C>
+bool halo_ok(EngineArgs& a) {
+    if (a.kw != 3 || a.k != 9 * a.cin_pad || a.stride != 1 || a.pad != 1 || a.ho != a.hi || a.wo != a.wi) return false;
+    if (a.cin_pad % BK || a.m % C::BM || (a.ho * a.wo) % C::BM) return false;
+    const int tw = std::min(C::BM, a.wo);
+    if (tw < 16 || (tw & (tw - 1)) || a.wo % tw || C::BM % tw) return false;
+    const int th = C::BM / tw;
+    if (a.ho % th || (th + 2) * (tw + 2) > Halo<C>::ROWS) return false;
+    a.halo_lg = __builtin_ctz(tw);
+    return true;
+}
+
+template <class C, int EPI>
+int launch_halo(EngineArgs a, void* stream, const char* what) {
+    const int tiles_m = a.m / C::BM, tiles_n = a.n / C::BN;
+    const int nwg = tiles_n * tiles_m;
+    a.group_m = pick_group_m(tiles_m, tiles_n, C::BM, C::BN, (nwg + 7) / 8);
+    hipLaunchKernelGGL((halo_kernel<C, EPI>), dim3(nwg), dim3(C::THREADS), 0, (hipStream_t)stream, a);
+    return rf::check_launch(what);
+}
+
+// the engine's data-parallel conv launch, or the halo kernel when it serves the shape
+// Measured (tools/kbench.py conv, RF_CONV_HALO): the halo kernel wins on the 4-wave 128x128 tile at large
+// grids (512^2 output_conv1, 256 -> 128: 293 -> 251 us), where the gathered A re-reads dominate; on the
+// 8-wave tiles it loses (128^2: 45 -> 49 us; 256^2 256x256: 123 -> 258 us, the tile spills), so by
+// default only T128 uses it (RF_CONV_HALO=1: every tile that can, 0: none).
+template <class C, int NTERM, bool GATHER>
+int launch_conv(EngineArgs& a, void* stream, const char* what) {
+    if constexpr (GATHER && NTERM == P_F16) {
+        const char* env = getenv("RF_CONV_HALO");
+        const bool want = env ? atoi(env) != 0 : (C::BM == 128 && C::NWAVE == 4);
+        if (want && halo_ok<C>(a)) return launch_halo<C, E_CONV>(a, stream, what);
+    }
+    return launch<C, E_CONV, NTERM, GATHER>(a, stream, what);
 }
 
 constexpr int SK_MAX_GRID = 768;                                  // 3 blocks of T128 per CU
@@ -1188,18 +1388,18 @@ static int conv_f16_dp(EngineArgs& p, void* stream, const char* what) {
     const char* env = getenv("RF_CONV_TILE");
     const int t = env ? atoi(env) : 0;
     if (p.n == 64) return launch<T256x64, E_CONV, P_F16, GATHER>(p, stream, what);
-    if (t == 128) return launch<T128, E_CONV, P_F16, GATHER>(p, stream, what);
-    if (t == 1288) return launch<T128w8, E_CONV, P_F16, GATHER>(p, stream, what);
+    if (t == 128) return launch_conv<T128, P_F16, GATHER>(p, stream, what);
+    if (t == 1288) return launch_conv<T128w8, P_F16, GATHER>(p, stream, what);
     if (p.n % 256 == 0 && (t == 256 || (!t && ((p.m + 255) / 256) * (p.n / 256) >= 256)))
         return (getenv("RF_CONV_PHASED") && atoi(getenv("RF_CONV_PHASED")) && use_phased(p.n, p.k))
                    ? launch_phased<E_CONV, P_F16, GATHER, 256>(p, stream, what)
-                   : launch<T256, E_CONV, P_F16, GATHER>(p, stream, what);
+                   : launch_conv<T256, P_F16, GATHER>(p, stream, what);
     if (t == 2561) return launch<T256x128, E_CONV, P_F16, GATHER>(p, stream, what);
     // up to two 128x128 tiles per CU: the 8-wave tile (two waves per SIMD) hides the gathered staging's
     // latency (128^2 DPT level: 52 -> 41 us); with more tiles the 4-wave tile's extra blocks do that
     const int64_t tiles = (int64_t)((p.m + 127) / 128) * (p.n / 128);
-    if (t != 128 && tiles <= 512) return launch<T128w8, E_CONV, P_F16, GATHER>(p, stream, what);
-    return launch<T128, E_CONV, P_F16, GATHER>(p, stream, what);
+    if (t != 128 && tiles <= 512) return launch_conv<T128w8, P_F16, GATHER>(p, stream, what);
+    return launch_conv<T128, P_F16, GATHER>(p, stream, what);
 }
 
 template <int NT>

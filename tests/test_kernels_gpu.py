@@ -514,6 +514,34 @@ def test_conv_matches_fp64(cin, cout, k, stride, hw, prec, tile, monkeypatch):
         assert (pl.hi[..., cout:] == 0).all() and (f16 or (pl.lo[..., cout:] == 0).all())
 
 
+@pytest.mark.parametrize("tile", ["128", "1288", "256"])
+@pytest.mark.parametrize("cin,cout,hw", [(256, 256, 32), (64, 128, 64), (32, 256, 16), (128, 128, 128),
+                                         (64, 256, 256)])
+def test_conv_halo(cin, cout, hw, tile, monkeypatch):
+    """Halo-tiled 3x3 convolution (RF_CONV_HALO=1) on every tile that takes it: tiles of whole image rows
+    (TW = wo) and of partial rows (TW = BM), two images, fused bias + 2 residuals + SiLU planes."""
+    if tile == "256" and cout % 256:
+        pytest.skip("256x256 tile needs 256 output channels")
+    monkeypatch.setenv("RF_CONV_HALO", "1")
+    monkeypatch.setenv("RF_CONV_TILE", tile)
+    monkeypatch.setenv("RF_CONV_SK", "0")
+    from renderformer_amd.dpt import _Conv, split_planes
+    g = torch.Generator(device="cpu").manual_seed(cin * hw + cout)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(cin * 9)
+    b = torch.randn(cout, generator=g)
+    x = torch.randn(2, cin, hw, hw, generator=g)
+    conv = _Conv(w, b, dev, f16=True)
+    xn = x.permute(0, 2, 3, 1).contiguous().to(dev)
+    r1 = torch.randn(2, hw, hw, cout, generator=g)
+    r2 = torch.randn(2, hw, hw, cout, generator=g)
+    out, pl = conv(split_planes(xn, conv.cin_pad, silu=True, f16=True), res1=r1.to(dev), res2=r2.to(dev),
+                   out_f32=True, planes_ld=cout, planes_silu=True)
+    sx = _q(F.silu(x.double()).float(), "f16")
+    ref = F.conv2d(sx, _q(w, "f16"), b.double(), padding=1).permute(0, 2, 3, 1) + r1 + r2
+    assert relerr(out.cpu(), ref) < 2e-5
+    assert relerr(_planes_value(pl)[..., :cout].cpu(), F.silu(ref)) < 1e-3
+
+
 @pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("cin,cout,k", [(128, 128, 4), (256, 256, 2), (16, 16, 4), (32, 32, 2)])
 def test_deconv(cin, cout, k, prec):
