@@ -10,6 +10,13 @@ Under `torch.distributed.run` (one process per GPU) every rank renders its longe
 processing-time share of the scenes (renderformer_amd.parallel.assign_units on the FLOP
 model); no data crosses ranks.  `--save_video` needs an mp4 encoder (imageio/ffmpeg) that
 the image lacks: frames are written as PNGs and the video step is skipped with a notice.
+
+The data path is pipelined: loader threads decode and collate the next batches into
+pinned host memory (texture kept fp16 as stored, widened on the device) while batch i renders, the
+host-to-device copy runs on a side stream that the compute stream waits on, results come back on
+another side stream, and writer threads encode and write the EXR/PNG files — the GPU only waits for
+the HDF5 decode when that is slower than a batch.  RF_BATCH_INLINE=1 runs every step
+inline on the main thread.
 """
 from __future__ import annotations
 
@@ -18,6 +25,7 @@ import glob
 import os
 import re
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import torch
@@ -32,11 +40,12 @@ def natural_key(path: str):
     return [int(t) if t.isdigit() else t.lower() for t in re.split(r"(\d+)", path)]
 
 
-def load_scene(path: str, padding_length=None) -> dict:
-    """`TriangleRenderH5Dataset.__getitem__` (batch_infer.py:27-58)."""
+def load_scene(path: str, padding_length=None, texture_dtype=torch.float32) -> dict:
+    """`TriangleRenderH5Dataset.__getitem__` (batch_infer.py:27-58).  texture_dtype=float16 keeps the file's
+    fp16 texture (half the host bytes; the pipelined path widens it on the device)."""
     with File(path) as f:
         tri = torch.from_numpy(np.array(f["triangles"])).float()
-        tex = torch.from_numpy(np.array(f["texture"])).float()
+        tex = torch.from_numpy(np.array(f["texture"])).to(texture_dtype)
         vn = torch.from_numpy(np.array(f["vn"])).float()
         c2w = torch.from_numpy(np.array(f["c2w"]).astype(np.float32))
         fov = torch.from_numpy(np.array(f["fov"]).astype(np.float32))
@@ -63,12 +72,100 @@ def collate(items):
     return {k: torch.stack([it[k] for it in items]) for k in keys}
 
 
+LOADERS = 3  # batches decoded ahead (threads)
+WRITERS = 4  # image encode/write threads
+
+
+def _load_batch(files, idx, padding_length, pin):
+    items = [load_scene(files[i], padding_length, torch.float16 if pin else torch.float32) for i in idx]
+    host = collate(items)
+    if pin:
+        host = {k: v.pin_memory() for k, v in host.items()}
+    return items, host
+
+
+def render_batches(pipeline, files, batches, args, pipelined=True):
+    """Yield (items, hdr images on the host) per batch, in order.  Pipelined: loader thread -> pinned batch
+    -> side-stream H2D -> render on the current stream -> side-stream D2H into pinned memory; batch i is
+    yielded (and its files written by the caller) while batch i+1 renders and batch i+2 loads."""
+    dev = pipeline.device
+    kw = dict(resolution=args.resolution, torch_dtype=PRECISION[args.precision])
+
+    def render(batch):
+        tex = batch["texture"]
+        if tex.dtype != torch.float32:  # fp16 from the file, widened on the device (exact)
+            tex = tex.float()
+        return pipeline(triangles=batch["triangles"], texture=tex, mask=batch["mask"], vn=batch["vn"],
+                        c2w=batch["c2w"], fov=batch["fov"].unsqueeze(-1), **kw)
+
+    if not pipelined or dev.type != "cuda":
+        for idx in batches:
+            items, host = _load_batch(files, idx, args.padding_length, False)
+            yield items, render({k: v.to(dev) for k, v in host.items()}).cpu()
+        return
+    # HDF5 decode (zlib releases the GIL) runs LOADERS batches ahead on a thread pool, consumed in order
+    pool = ThreadPoolExecutor(max_workers=LOADERS)
+    ahead = [pool.submit(_load_batch, files, idx, args.padding_length, True) for idx in batches[:LOADERS]]
+    nxt_batch = len(ahead)
+
+    class _Loaded:
+        def get(self):
+            nonlocal nxt_batch
+            if not ahead:
+                pool.shutdown(wait=False)
+                return None
+            fut = ahead.pop(0)
+            if nxt_batch < len(batches):
+                ahead.append(pool.submit(_load_batch, files, batches[nxt_batch], args.padding_length, True))
+                nxt_batch += 1
+            try:
+                return fut.result()
+            except BaseException as e:  # surfaced on the main thread
+                return e
+
+    loaded = _Loaded()
+    h2d = torch.cuda.Stream(device=dev)
+    d2h = torch.cuda.Stream(device=dev)
+    compute = torch.cuda.current_stream(dev)
+    pending = None  # (items, pinned host images, their copy event, pinned inputs) of the previous batch
+    while True:
+        got = loaded.get()
+        if isinstance(got, BaseException):
+            raise got
+        nxt = None
+        if got is not None:
+            items, host = got
+            with torch.cuda.stream(h2d):
+                batch = {k: v.to(dev, non_blocking=True) for k, v in host.items()}
+            compute.wait_stream(h2d)
+            for v in batch.values():  # allocated on the copy stream, used on the compute stream
+                v.record_stream(compute)
+            imgs = render(batch)
+            # the result goes back on its own stream right behind this batch, not behind the next one
+            d2h.wait_stream(compute)
+            with torch.cuda.stream(d2h):
+                out = torch.empty(imgs.shape, dtype=imgs.dtype, pin_memory=True)
+                out.copy_(imgs, non_blocking=True)
+                copied = torch.cuda.Event()
+                copied.record(d2h)
+            imgs.record_stream(d2h)
+            nxt = (items, out, copied, host)  # `host` (pinned inputs) lives until this batch is yielded
+        if pending is not None:  # batch i is handed out while batch i+1 renders
+            p_items, p_out, p_copied, _ = pending
+            p_copied.synchronize()
+            yield p_items, p_out
+        if nxt is None:
+            return
+        pending = nxt
+
+
 def main(argv=None):
     parser = argparse.ArgumentParser(description="Batch inference using triangle radiosity transformer model (MI355X)")
     parser.add_argument("--h5_folder", type=str, required=True)
     parser.add_argument("--batch_size", type=int, default=8)
     parser.add_argument("--padding_length", type=int, default=None)
-    parser.add_argument("--num_workers", type=int, default=0, help="accepted for compatibility; loading is inline")
+    parser.add_argument("--num_workers", type=int, default=0,
+                        help="accepted for compatibility (loading always runs in one background thread)")
     parser.add_argument("--output_dir", type=str, default=None)
     parser.add_argument("--save_video", action="store_true", default=True)
     add_common_args(parser)
@@ -93,17 +190,23 @@ def main(argv=None):
     output_dir = args.output_dir if args.output_dir is not None else args.h5_folder
     os.makedirs(output_dir, exist_ok=True)
     dev = pipeline.device
+    batches = [mine[b0:b0 + args.batch_size] for b0 in range(0, len(mine), args.batch_size)]
     n_frames = 0
-    for b0 in range(0, len(mine), args.batch_size):
-        items = [load_scene(files[i], args.padding_length) for i in mine[b0:b0 + args.batch_size]]
-        batch = {k: v.to(dev) for k, v in collate(items).items()}
-        imgs = pipeline(triangles=batch["triangles"], texture=batch["texture"], mask=batch["mask"], vn=batch["vn"],
-                        c2w=batch["c2w"], fov=batch["fov"].unsqueeze(-1), resolution=args.resolution,
-                        torch_dtype=PRECISION[args.precision])
+    inline = os.environ.get("RF_BATCH_INLINE", "0") != "0"
+    writers = None if inline else ThreadPoolExecutor(max_workers=WRITERS)
+    pending = []
+    for items, imgs in render_batches(pipeline, files, batches, args, pipelined=not inline):
         for i, it in enumerate(items):
             base = os.path.splitext(os.path.basename(it["file_path"]))[0]
-            save_views(imgs[i], output_dir, base)
+            if writers is None:
+                save_views(imgs[i], output_dir, base)
+            else:  # EXR/PNG encode + write off the render loop (zlib releases the GIL)
+                pending.append(writers.submit(save_views, imgs[i], output_dir, base))
             n_frames += imgs.shape[1]
+    if writers is not None:
+        for f in pending:
+            f.result()  # re-raises a writer's error
+        writers.shutdown()
     print(f"Output saved to: {output_dir} ({n_frames} frames on rank {rank}/{world})")
     if args.save_video:
         print("video.mp4 not written: no mp4 encoder in this environment (frames are saved as PNG)")
