@@ -658,6 +658,19 @@ constexpr int PIECE_FLOATS = PIECE_O + QB5 * 2 * 2;  // + (m, l) per lane
 
 RF_DEV float vmax3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }  // v_max3_f32
 
+// two f32 -> one packed bf16x2 (RNE, as the (__bf16) cast), pinned where it is written (volatile asm)
+RF_DEV uint32_t cvt_pk_bf16(float lo, float hi) {
+    uint32_t r;
+    asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+    return r;
+}
+// dword w (0..3) of an MFMA bf16x8 operand
+RF_DEV void set_pk(bf16x8& f, int w, uint32_t v) {
+    u32x4 u = __builtin_bit_cast(u32x4, f);
+    u[w] = v;
+    f = __builtin_bit_cast(bf16x8, u);
+}
+
 // One 1-KiB LDS-DMA piece: lane l's 16 B land at LDS byte lds + 16 l.  Inline asm so hipcc neither
 // counts it (the loop waits with its own vmcnt) nor guards later ds_read_b64_tr_b16 with vmcnt(0).
 // M0 is declared clobbered (hipcc warns: reserved register); the kernel has no other M0 user (checked
@@ -672,6 +685,14 @@ RF_DEV void dma_piece(const bf16_t* g, uint32_t lds) {
 // 64 = no static priority for waves 4-7
 template <bool UNIT, int DBG = 0>
 __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
+    // SPLIT: half of each tile's softmax (keys 32-63) moves from phase A (QK^T, VALU-heavy) into the first
+    // half of phase B (PV, VALU-light), balancing the two phases that share each SIMD; DBG & 128 = unsplit
+    constexpr bool SPLIT = (DBG & 128) != 0;  // measured: no gain (the per-tile total stays ~3,200 cycles)
+    // CVT_PIN: the bf16 packs of P are inline-asm v_cvt_pk_bf16_f32 in their MFMA gaps (hipcc otherwise
+    // sinks all 16 of them into one VALU burst after the last QK^T MFMA); DBG & 256 = compiler casts
+    constexpr bool CVT_PIN = !(DBG & 256);
+    constexpr auto x_blk = [](int x) { return x >> 4; };
+    constexpr auto x_sp = [](int x) { return (x >> 3) & 1; };
     __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // 64 KiB
 
     const int tid = threadIdx.x;
@@ -906,7 +927,8 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             float ls[4];
 
             // ---- phase A: S(t+1) chains b = 0, 1 alternating; each gap: 2 exp2, 2 row-sum adds, 1 bf16 pack
-            // of P(t); K fragments two MFMAs ahead; K(t+2)'s LDS-DMA rides in gap 1
+            // of P(t) (SPLIT: the first 8 gaps, keys 0-31 of the tile; keys 32-63 go to phase B); K fragments
+            // two MFMAs ahead; K(t+2)'s LDS-DMA rides in gap 1
             if (i > 0) mask_tail(s, t);  // (tile kt0 was masked in the prologue)
             kf[0] = kread(0);
             kf[1] = kread(1);
@@ -921,31 +943,40 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 } else {
                     sn[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[j % 3], qf[st], st == 0 ? minit : sn[b], 0, 0, 0);
                 }
-                float e[2];
+                if (!SPLIT || j < 8) {
+                    float e[2];
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const int x = 2 * j + u;
-                    const float v = s[x >> 4][x & 15];
-                    e[u] = (DBG & 8) ? v : fast_exp2(UNIT ? v : v * c);
-                    ls[x & 3] = j < 2 ? e[u] : ls[x & 3] + e[u];
-                    asm volatile("" : "+v"(ls[x & 3]));  // keep the add in this gap (IR passes sink it)
+                    for (int u = 0; u < 2; ++u) {
+                        const int x = 2 * j + u;
+                        const float v = s[x >> 4][x & 15];
+                        e[u] = (DBG & 8) ? v : fast_exp2(UNIT ? v : v * c);
+                        ls[x & 3] = j < 2 ? e[u] : ls[x & 3] + e[u];
+                        asm volatile("" : "+v"(ls[x & 3]));  // keep the add in this gap (IR passes sink it)
+                    }
+                    if constexpr (CVT_PIN) {
+                        set_pk(pf[j >> 3][(j >> 2) & 1], j & 3, cvt_pk_bf16(e[0], e[1]));
+                    } else {
+                        pf[j >> 3][(j >> 2) & 1][2 * (j & 3)] = (__bf16)e[0];
+                        pf[j >> 3][(j >> 2) & 1][2 * (j & 3) + 1] = (__bf16)e[1];
+                    }
                 }
-                pf[j >> 3][(j >> 2) & 1][2 * (j & 3)] = (__bf16)e[0];
-                pf[j >> 3][(j >> 2) & 1][2 * (j & 3) + 1] = (__bf16)e[1];
                 if constexpr (!(DBG & 1)) {
                     if (j == 1 && i + 2 < n) issue(kp, p.ldk, kstep, t + 2, lds0 + K5 + PAR * TILE_BYTES);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
             // ---- overflow check (deferred rescale, guide T13): a half-row sum <= 2^thr bounds every P(t) by
-            // 2^thr, so the running max only moves (rare) when some sum exceeds it; P(t) is then recomputed
-            // on the new base and S(t+1), issued on the old one, is shifted with it
+            // 2^thr, so the running max only moves (rare) when some sum exceeds it; the P(t) not yet in O is
+            // then recomputed on the new base and S(t+1), issued on the old one, is shifted with it.  SPLIT:
+            // checked per 32-key half (here for keys 0-31, in phase B for 32-63: O and l then already hold keys
+            // 0-31 on the old base and are scaled with everything else).
+            constexpr int XA = SPLIT ? 16 : 32;  // P values produced in phase A
             float l_tile = (ls[0] + ls[1]) + (ls[2] + ls[3]);
             if (__any(l_tile > sum_thr)) {
                 rebase(s, sn, false);
                 l_tile = 0.f;
 #pragma unroll
-                for (int x = 0; x < 32; ++x) {
+                for (int x = 0; x < XA; ++x) {
                     const float v = s[x >> 4][x & 15];
                     const float e = fast_exp2(UNIT ? v : v * c);
                     l_tile += e;
@@ -964,21 +995,64 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             stamp_at(2);
 
             // ---- phase B: four O chains alternating; V^T fragments two MFMAs ahead; V(t+1)'s LDS-DMA in gap
-            // 1; each gap also rebuilds one register of minit (the C operand of the next QK^T chains)
+            // 1.  SPLIT: gaps 0-7 (PV of keys 0-31) produce P for keys 32-63, checked before gap 8; gaps 8-15
+            // rebuild minit (the C operand of the next QK^T chains), two registers each.  Unsplit: one minit
+            // register per gap.
             vf[0] = vread(0);
             vf[1] = vread(1);
             __builtin_amdgcn_sched_barrier(0);
+            float l2 = 0.f;
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 if (j + 2 < 16) vf[(j + 2) % 3] = vread(j + 2);
                 const int dt = j & 3, b = (j >> 2) >> 1, sp = (j >> 2) & 1;
+                if (SPLIT && j == 8) {
+                    l2 = (ls[0] + ls[1]) + (ls[2] + ls[3]);
+                    if (__any(l2 > sum_thr)) {
+                        rebase(s, sn, false);
+                        l2 = 0.f;
+#pragma unroll
+                        for (int x = 16; x < 32; ++x) {
+                            const float v = s[x >> 4][x & 15];
+                            const float e = fast_exp2(UNIT ? v : v * c);
+                            l2 += e;
+                            pf[x >> 4][(x >> 3) & 1][x & 7] = (__bf16)e;
+                        }
+                    }
+                    l_run += l2;
+                }
                 if constexpr (DBG & 4) {
                     asm volatile("" : "+v"(vf[j % 3]), "+v"(pf[b][sp]));
                 } else {
                     o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[j % 3], pf[b][sp], o[dt], 0, 0, 0);
                 }
-                minit[j] = -m_run * inv_c;
-                asm volatile("" : "+v"(minit[j]));  // one v_mov per PV gap (otherwise hoisted into phase A)
+                if (SPLIT && j < 8) {
+                    float e[2];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int x = 16 + 2 * j + u;
+                        const float v = s[x >> 4][x & 15];
+                        e[u] = (DBG & 8) ? v : fast_exp2(UNIT ? v : v * c);
+                        ls[x & 3] = j < 2 ? e[u] : ls[x & 3] + e[u];
+                        asm volatile("" : "+v"(ls[x & 3]));
+                    }
+                    if constexpr (CVT_PIN) {
+                        set_pk(pf[x_blk(16 + 2 * j)][x_sp(16 + 2 * j)], j & 3, cvt_pk_bf16(e[0], e[1]));
+                    } else {
+                        pf[x_blk(16 + 2 * j)][x_sp(16 + 2 * j)][(2 * j) & 7] = (__bf16)e[0];
+                        pf[x_blk(16 + 2 * j)][x_sp(16 + 2 * j)][(2 * j + 1) & 7] = (__bf16)e[1];
+                    }
+                } else if (SPLIT) {
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int r = 2 * (j - 8) + u;
+                        minit[r] = -m_run * inv_c;
+                        asm volatile("" : "+v"(minit[r]));  // keep the v_mov in this gap
+                    }
+                } else {
+                    minit[j] = -m_run * inv_c;
+                    asm volatile("" : "+v"(minit[j]));  // one v_mov per PV gap (otherwise hoisted into phase A)
+                }
                 if constexpr (!(DBG & 1)) {
                     if (j == 1 && has_next) issue(vp, p.ldv, vstep, t + 1, lds0 + V5 + (PAR ^ 1) * TILE_BYTES);
                 }
@@ -1164,6 +1238,11 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
         case 32: hipLaunchKernelGGL((attn_sk_kernel<true, 32>), g, b, 0, st, a); break;
         case 64: hipLaunchKernelGGL((attn_sk_kernel<true, 64>), g, b, 0, st, a); break;
         case 96: hipLaunchKernelGGL((attn_sk_kernel<true, 96>), g, b, 0, st, a); break;
+        case 128: hipLaunchKernelGGL((attn_sk_kernel<true, 128>), g, b, 0, st, a); break;
+        case 160: hipLaunchKernelGGL((attn_sk_kernel<true, 160>), g, b, 0, st, a); break;
+        case 256: hipLaunchKernelGGL((attn_sk_kernel<true, 256>), g, b, 0, st, a); break;
+        case 288: hipLaunchKernelGGL((attn_sk_kernel<true, 288>), g, b, 0, st, a); break;
+        case 384: hipLaunchKernelGGL((attn_sk_kernel<true, 384>), g, b, 0, st, a); break;
         default:
             if (unit)
                 hipLaunchKernelGGL((attn_sk_kernel<true, 0>), g, b, 0, st, a);
