@@ -52,6 +52,13 @@ RF_DEV float wave_max(float v) {
 
 RF_DEV void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// silu(x) = x / (1 + e^-x) on the hardware exp2 and reciprocal (~1 ulp each; every caller rounds the result
+// to bf16/fp16 or adds it into an fp32 stream right after): 4 VALU ops instead of libm expf + an IEEE
+// division (~25).  In the SwiGLU / conv epilogues the precise form cost 15 us of an 80 us GEMM.
+RF_DEV float silu(float x) {
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
+
 // ------------------------------------------------------------------------- host side
 namespace rf {
 void set_error(const char* fmt, ...);

@@ -11,7 +11,6 @@
 
 namespace {
 
-RF_DEV float silu(float x) { return x / (1.0f + expf(-x)); }
 
 RF_DEV void store_split4(bf16_t* p_hi, bf16_t* p_lo, int64_t off, float4 v, bool act) {
     float x[4] = {v.x, v.y, v.z, v.w};

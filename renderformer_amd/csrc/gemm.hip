@@ -110,7 +110,6 @@ RF_DEV void tile_coords(int tile, int tiles_m, int tiles_n, int group_m, int& tm
 
 RF_DEV int lds_off(int row, int ch) { return row * 64 + ((ch ^ ((row >> 1) & 3)) << 4); }
 
-RF_DEV float silu(float x) { return x / (1.0f + expf(-x)); }
 
 template <int N>
 RF_DEV void wait_vm() {
@@ -1282,13 +1281,16 @@ bool sk256(int m, int n, int k) {
     return false;  // the ring engine's 256x256 stream-K: superseded by the phased one, kept for A/B
 }
 
-// Phased 256x256 stream-K over one block per CU (RF_GEMM_SKPH=1).  Off by default: its partial-tile
-// fix-up costs ~5-10 us per block, and the 128x256 phased tile beat it on every bench shape measured
-// (texture GEMM 5633x1024x13312: 170 us vs 212 us).
+// Phased 256x256 stream-K over one block per CU (RF_GEMM_SKPH=1/0 forces it on/off).  With partial tiles
+// its fix-up costs ~5-10 us per block, and the 128x256 phased tile beat it on every such shape measured
+// (texture GEMM 5633x1024x13312: 170 us vs 212 us); when the tile count is a multiple of the 256-block
+// grid every block runs whole tiles back to back (no fix-up) and it beats the data-parallel launch
+// (stage-2 W13 4096x8192x1024: 68 vs 72.5 us), so that case is the default.
 bool skph(int m, int n, int k) {
     if (!use_phased(n, k)) return false;
-    const char* env = getenv("RF_GEMM_SKPH");
-    return env && atoi(env) != 0;
+    if (const char* env = getenv("RF_GEMM_SKPH")) return atoi(env) != 0;
+    const int64_t tiles = (int64_t)((m + 255) / 256) * (n / 256);
+    return n % 256 == 0 && tiles >= 512 && tiles % 256 == 0;
 }
 
 extern "C" int64_t rf_gemm_workspace_bytes(void) { return SK_WS_BYTES; }
