@@ -38,48 +38,48 @@ RF_DEV void store_split4(bf16_t* p_hi, bf16_t* p_lo, int64_t off, float4 v, bool
     *reinterpret_cast<uint2*>(p_lo + off) = make_uint2(l[0], l[1]);
 }
 
-__global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ x, int64_t rows, int c, int64_t ldx,
+__global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ x, int rows, int c, int64_t ldx,
                                                     bf16_t* __restrict__ p_hi, bf16_t* __restrict__ p_lo, int p_ld,
                                                     int act) {
     const int c4 = c / 4;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // rows * c4 < 2^31 (host check)
     if (i >= rows * c4) return;
-    const int64_t r = i / c4;
-    const int cc = (int)(i % c4) * 4;
+    const int r32 = i / c4;
+    const int64_t r = r32;
+    const int cc = (i - r32 * c4) * 4;
     store_split4(p_hi, p_lo, r * p_ld + cc, *reinterpret_cast<const float4*>(x + r * ldx + cc), act);
 }
 
-// bilinear, align_corners=True (torch upsample_bilinear2d); scale passed from the host
+// bilinear, align_corners=True (torch upsample_bilinear2d); scale passed from the host.  One block row per
+// output image row (blockIdx.y = img * ho + oy, uniform), threads over (ox, 4-channel group) with 32-bit
+// index math (the flat 64-bit div/mod chain cost more than the memory traffic)
 __global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                        bf16_t* __restrict__ p_hi, bf16_t* __restrict__ p_lo, int p_ld,
-                                                       int n_img, int hi, int wi, int c, int ho, int wo, float sh,
-                                                       float sw) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int c4n = c / 4;
-    const int64_t total = (int64_t)n_img * ho * wo * c4n;
-    if (idx >= total) return;
-    const int cc = (int)(idx % c4n) * 4;
-    const int64_t pix = idx / c4n;
-    const int ox = (int)(pix % wo);
-    const int64_t t = pix / wo;
-    const int oy = (int)(t % ho);
-    const int img = (int)(t / ho);
+                                                       int hi, int wi, int c, int ho, int wo, float sh, float sw) {
+    const int c4n = c >> 2;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= wo * c4n) return;
+    const int row = blockIdx.y;  // img * ho + oy
+    const int img = row / ho, oy = row - img * ho;
+    const int ox = i / c4n;
+    const int cc = (i - ox * c4n) * 4;
     const float fy = sh * (float)oy, fx = sw * (float)ox;
     const int y0 = (int)fy, x0 = (int)fx;
     const int y1 = y0 + (y0 < hi - 1 ? 1 : 0), x1 = x0 + (x0 < wi - 1 ? 1 : 0);
     const float ly1 = fy - (float)y0, lx1 = fx - (float)x0;
     const float ly0 = 1.0f - ly1, lx0 = 1.0f - lx1;
     const float* base = in + (int64_t)img * hi * wi * c + cc;
-    const float4 a = *reinterpret_cast<const float4*>(base + ((int64_t)y0 * wi + x0) * c);
-    const float4 b = *reinterpret_cast<const float4*>(base + ((int64_t)y0 * wi + x1) * c);
-    const float4 d = *reinterpret_cast<const float4*>(base + ((int64_t)y1 * wi + x0) * c);
-    const float4 e = *reinterpret_cast<const float4*>(base + ((int64_t)y1 * wi + x1) * c);
+    const float4 a = *reinterpret_cast<const float4*>(base + (int64_t)(y0 * wi + x0) * c);
+    const float4 b = *reinterpret_cast<const float4*>(base + (int64_t)(y0 * wi + x1) * c);
+    const float4 d = *reinterpret_cast<const float4*>(base + (int64_t)(y1 * wi + x0) * c);
+    const float4 e = *reinterpret_cast<const float4*>(base + (int64_t)(y1 * wi + x1) * c);
     float4 r;
     r.x = ly0 * (lx0 * a.x + lx1 * b.x) + ly1 * (lx0 * d.x + lx1 * e.x);
     r.y = ly0 * (lx0 * a.y + lx1 * b.y) + ly1 * (lx0 * d.y + lx1 * e.y);
     r.z = ly0 * (lx0 * a.z + lx1 * b.z) + ly1 * (lx0 * d.z + lx1 * e.z);
     r.w = ly0 * (lx0 * a.w + lx1 * b.w) + ly1 * (lx0 * d.w + lx1 * e.w);
-    if (out) *reinterpret_cast<float4*>(out + idx * 4) = r;
+    const int64_t pix = (int64_t)row * wo + ox;
+    if (out) *reinterpret_cast<float4*>(out + pix * c + cc) = r;
     if (p_hi) store_split4(p_hi, p_lo, pix * p_ld + cc, r, false);
 }
 
@@ -91,7 +91,8 @@ extern "C" int rf_split_planes(const float* x, int64_t rows, int c, int64_t ldx,
     RF_REQUIRE(c % 4 == 0 && ldx % 4 == 0 && p_ld % 4 == 0 && p_ld >= c, "rf_split_planes: bad widths");
     const int64_t n = rows * (c / 4);
     if (n <= 0) return RF_OK;
-    hipLaunchKernelGGL(split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, rows, c,
+    RF_REQUIRE(n < (1ll << 31) - 256, "rf_split_planes: too many elements");
+    hipLaunchKernelGGL(split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, (int)rows, c,
                        ldx, (bf16_t*)p_hi, (bf16_t*)p_lo, p_ld, silu_act);
     return rf::check_launch("rf_split_planes");
 }
@@ -102,10 +103,13 @@ extern "C" int rf_upsample_bilinear(const float* in, int n_img, int hi, int wi, 
     RF_REQUIRE(c % 4 == 0 && (!p_hi || (p_ld % 4 == 0 && p_ld >= c)), "rf_upsample_bilinear: bad widths");
     const int64_t total = (int64_t)n_img * ho * wo * (c / 4);
     if (total <= 0) return RF_OK;
+    RF_REQUIRE((int64_t)wo * (c / 4) < (1 << 30) && (int64_t)n_img * ho < 65536 && (int64_t)hi * wi < (1 << 30),
+               "rf_upsample_bilinear: image too large");
     // scale computed on the host with IEEE float division, as aten's area_pixel_compute_scale<float>
     const float sh = ho > 1 ? (float)(hi - 1) / (float)(ho - 1) : 0.f;
     const float sw = wo > 1 ? (float)(wi - 1) / (float)(wo - 1) : 0.f;
-    hipLaunchKernelGGL(upsample_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, in,
-                       out, (bf16_t*)p_hi, (bf16_t*)p_lo, p_ld, n_img, hi, wi, c, ho, wo, sh, sw);
+    const dim3 grid((unsigned)((wo * (c / 4) + 255) / 256), (unsigned)(n_img * ho));
+    hipLaunchKernelGGL(upsample_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, out, (bf16_t*)p_hi,
+                       (bf16_t*)p_lo, p_ld, hi, wi, c, ho, wo, sh, sw);
     return rf::check_launch("rf_upsample_bilinear");
 }
