@@ -58,6 +58,10 @@ RF_DEV void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 RF_DEV float silu(float x) {
     return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
 }
+// libm expf + IEEE division.  Kept for the convolution epilogue: with the short form the 256x256 conv
+// kernel's register allocation changes and its main loop spills (6 scratch ops per K-step instead of 1:
+// 114 -> 186 us at the 256^2 DPT level), which costs far more than the epilogue saves.
+RF_DEV float silu_precise(float x) { return x / (1.0f + expf(-x)); }
 
 // ------------------------------------------------------------------------- host side
 namespace rf {

@@ -352,7 +352,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                     const int col = cbase + j * 16 + cq + e;
                     const float b = (p.bias && col < p.cout) ? p.bias[col] : 0.f;
 #pragma unroll
-                    for (int i = 0; i < TI; ++i) act[i][j][e] = col < p.cout ? silu(acc[i][j][e] + b) : 0.f;
+                    for (int i = 0; i < TI; ++i) act[i][j][e] = col < p.cout ? silu_precise(acc[i][j][e] + b) : 0.f;
                 }
             for (int f = 0; f < p.n_fin; ++f) {
                 float wf[TJ][4];
@@ -434,7 +434,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                 for (int e = 0; e < 4; ++e) {
                     if (p.bias) v[e] += p.bias[co + e];
                     v[e] = (v[e] + rr1[e]) + rr2[e];
-                    if (p.flags & RF_CONV_SILU_OUT) v[e] = silu(v[e]);
+                    if (p.flags & RF_CONV_SILU_OUT) v[e] = silu_precise(v[e]);
                 }
                 if (p.c)
                     *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + pix * p.cout + co) =
@@ -443,7 +443,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                     float a[4] = {v[0], v[1], v[2], v[3]};
                     if (p.flags & RF_CONV_PLANE_SILU) {
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) a[e] = silu(a[e]);
+                        for (int e = 0; e < 4; ++e) a[e] = silu_precise(a[e]);
                     }
                     *reinterpret_cast<uint2*>(p.p_hi + pix * p.p_ld + co) = make_uint2(pack_f16x2(a[0], a[1]),
                                                                                        pack_f16x2(a[2], a[3]));
@@ -453,8 +453,8 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                     for (int e = 0; e < 2; ++e) {
                         float a0 = v[2 * e], a1 = v[2 * e + 1];
                         if (p.flags & RF_CONV_PLANE_SILU) {
-                            a0 = silu(a0);
-                            a1 = silu(a1);
+                            a0 = silu_precise(a0);
+                            a1 = silu_precise(a1);
                         }
                         const bf16_t h0 = f32_to_bf16(a0), h1 = f32_to_bf16(a1);
                         h[e] = (uint32_t)h0 | ((uint32_t)h1 << 16);
