@@ -118,6 +118,18 @@ class _DeviceWeights:
             L.w2 = _bf16(sd[p + "ffn.w2.weight"], device)
             L.ffn_norm = _f32(sd[p + "ffn_norm.weight"], device)
             self.dec.append(L)
+        # Cross-attention K/V of every decoder layer in ONE GEMM (their input, the stage-1 output, is the same
+        # for all layers): RMSNorm(ctx) W^T = (ctx * inv_rms) (W diag(g))^T, so each layer's kv_norm weight g
+        # is folded into its K/V rows (in f32, then rounded to bf16) and ctx is normalised once with unit
+        # weights; layer i reads columns [2D i, 2D (i+1)) of the [T1, L*2D] result.
+        wkv_all = []
+        for i in range(cfg.view_transformer_n_layers):
+            p = f"{vt}transformer.layers.{i}."
+            a = p + "multihead_attn."
+            w = torch.cat([sd[a + "k_proj.weight"], sd[a + "v_proj.weight"]], 0).float()
+            wkv_all.append(w * sd[p + "kv_norm.weight"].float()[None, :])
+        self.wkv_all = _bf16(torch.cat(wkv_all, 0), device)
+        self.ctx_unit = torch.ones(self.wkv_all.shape[1], dtype=torch.float32, device=device)
         self.dpt = DPTHead(sd, vt + "out_dpt", device, precision=dpt_precision)
 
 
@@ -353,7 +365,15 @@ class RenderFormer:
         att = torch.empty(T2, D, dtype=torch.bfloat16, device=dev)
         g = torch.empty(T2, F, dtype=torch.bfloat16, device=dev)
         hc = torch.empty(plan.T1, ctx.shape[1], dtype=torch.bfloat16, device=dev)
-        kv = torch.empty(plan.T1, 2 * D, dtype=torch.bfloat16, device=dev)
+        n_dec = len(W.dec)
+        # all layers' K/V in one GEMM (see _DeviceWeights.wkv_all) unless RF_KV_BATCH=0 or it would exceed 4 GiB
+        kv_batch = (os.environ.get("RF_KV_BATCH", "1") != "0" and plan.T1 * n_dec * 2 * D * 2 <= (4 << 30))
+        if kv_batch:
+            ops.rmsnorm(ctx, W.ctx_unit, EPS, hc)
+            kv_all = torch.empty(plan.T1, n_dec * 2 * D, dtype=torch.bfloat16, device=dev)
+            ops.gemm(hc, W.wkv_all, kv_all)
+        else:
+            kv = torch.empty(plan.T1, 2 * D, dtype=torch.bfloat16, device=dev)
         kview = torch.empty(plan.T_kv, D, dtype=torch.bfloat16, device=dev)
         qkv = torch.empty(T2, 3 * D, dtype=torch.bfloat16, device=dev) if cfg.view_transformer_include_self_attn else None
         swin = cfg.view_transformer_use_swin_attn
@@ -363,8 +383,11 @@ class RenderFormer:
             # (i) cross-attention: K/V projections once per scene, K rotated per view
             ops.rmsnorm(x, L.query_norm, EPS, h)
             ops.gemm(h, L.wq, q2)
-            ops.rmsnorm(ctx, L.kv_norm, EPS, hc)
-            ops.gemm(hc, L.wkv, kv)
+            if kv_batch:
+                kv = kv_all[:, 2 * D * i:2 * D * (i + 1)]
+            else:
+                ops.rmsnorm(ctx, L.kv_norm, EPS, hc)
+                ops.gemm(hc, L.wkv, kv)
             ops.qk_norm_rope(q2, q2, H, L.q_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R,
                              q_scale=ops.Q_LOG2_SCALE)
             ops.qk_norm_rope(kv[:, :D], kview, H, L.k_norm if qk else None, EPS, pos2, W.dec_freqs,
