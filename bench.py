@@ -168,7 +168,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {
-                "workload": f"{args.config}-proxy cbox-sized scene N={args.tris}, {args.res}x{args.res}, "
+                "workload": f"{'large-proxy' if args.config == 'large' else args.config} cbox-sized scene N={args.tris}, {args.res}x{args.res}, "
                             f"{args.views} view(s) x {args.scenes} scene(s) per rank per step",
                 "model": "renderformer-v1.1-swin-large" if args.config == "large" else args.config,
                 "model_shape": f"D={cfg.latent_dim} H={cfg.num_heads} L1={cfg.num_layers} "
