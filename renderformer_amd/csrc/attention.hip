@@ -1131,17 +1131,35 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         if (!active) continue;
         const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
         const int qrow_o = q0 + qi;
-        if (qrow_o < q1) {
+        if (qrow_o < q1) {  // (lanes l and l + 32 hold the same query row: both store or neither)
             const float inv = l_tot > 0.f ? 1.0f / l_tot : 0.f;
             bf16_t* dst = p.o + (int64_t)(q_start + qrow_o) * p.ldo + hoff;
+            // row-per-lane store widened to 16 B (guide T21): column group k = 4 dt + gq is split across the
+            // halves (lane l: columns 8k..8k+3, lane l+32: 8k+4..8k+7); one v_permlane32_swap per dword of
+            // the pair (k, k+1) gives the lower half columns 8k..8k+7 and the upper half 8k+8..8k+15
+            if constexpr (DBG & 512) {  // A/B: the unwidened 8-B stores
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int gq = 0; gq < 4; ++gq) {
+                        uint2 pk;
+                        pk.x = pack_bf16x2(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
+                        pk.y = pack_bf16x2(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
+                        *reinterpret_cast<uint2*>(dst + dt * 32 + 8 * gq + 4 * half) = pk;
+                    }
+                continue;
+            }
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-                for (int gq = 0; gq < 4; ++gq) {
-                    uint2 pk;
-                    pk.x = pack_bf16x2(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
-                    pk.y = pack_bf16x2(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
-                    *reinterpret_cast<uint2*>(dst + dt * 32 + 8 * gq + 4 * half) = pk;
+                for (int gq = 0; gq < 4; gq += 2) {
+                    uint32_t a0 = pack_bf16x2(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
+                    uint32_t a1 = pack_bf16x2(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
+                    uint32_t b0 = pack_bf16x2(o[dt][4 * gq + 4] * inv, o[dt][4 * gq + 5] * inv);
+                    uint32_t b1 = pack_bf16x2(o[dt][4 * gq + 6] * inv, o[dt][4 * gq + 7] * inv);
+                    const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+                    const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+                    *reinterpret_cast<uint4*>(dst + dt * 32 + 8 * gq + 8 * half) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
                 }
         }
     }
@@ -1243,6 +1261,7 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
         case 256: hipLaunchKernelGGL((attn_sk_kernel<true, 256>), g, b, 0, st, a); break;
         case 288: hipLaunchKernelGGL((attn_sk_kernel<true, 288>), g, b, 0, st, a); break;
         case 384: hipLaunchKernelGGL((attn_sk_kernel<true, 384>), g, b, 0, st, a); break;
+        case 512: hipLaunchKernelGGL((attn_sk_kernel<true, 512>), g, b, 0, st, a); break;
         default:
             if (unit)
                 hipLaunchKernelGGL((attn_sk_kernel<true, 0>), g, b, 0, st, a);
