@@ -877,8 +877,14 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
 
         issue(kp, p.ldk, kstep, kt0, lds0 + K5);
         issue(vp, p.ldv, vstep, kt0, lds0 + V5);
-        if (n > 1) issue(kp, p.ldk, kstep, kt0 + 1, lds0 + K5 + TILE_BYTES);
-        attn_wait_vm<0>();
+        // the first QK^T needs Q and K(t0) only: V(t0) and K(t0+1) (2 DMA pieces each, the youngest
+        // vector-memory ops) keep landing under it (guide T20: wait at the first consumer)
+        if (n > 1) {
+            issue(kp, p.ldk, kstep, kt0 + 1, lds0 + K5 + TILE_BYTES);
+            attn_wait_vm<4>();
+        } else {
+            attn_wait_vm<2>();
+        }
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         f32x16 sA[2], sB[2];
