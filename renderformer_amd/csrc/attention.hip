@@ -754,6 +754,8 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         }
     };
     while (it < it_end) {
+        uint64_t t_piece = 0;  // DBG & 32: piece prologue cycles -> stamp[6]
+        if constexpr (DBG & 32) t_piece = __builtin_amdgcn_s_memtime();
         while (it >= base + usz) {  // advance to the problem holding tile `it`
             base += usz;
             ++pi;
@@ -897,6 +899,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         // so on every SIMD one wave's phase A (QK^T + softmax VALU) pairs with its partner's phase B (PV)
         if (late) __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (DBG & 32) stamp[6] += __builtin_amdgcn_s_memtime() - t_piece;
 
         // one tile: A(t) = softmax(S(t)) woven into S(t+1) = K(t+1) Q^T; seam; B(t) = PV(t) with the
         // minit rebuild and the row max of S(t+1) woven in; then the (rare) rescale of S(t+1)

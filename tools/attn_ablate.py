@@ -36,6 +36,11 @@ if len(sys.argv) > 1 and sys.argv[1] == "stamps":
     names = ["top wait", "A (+K DMA, check)", "seam wait", "B (+V DMA)"]
     clk = (st[..., 4] / st[..., 5].clamp_min(1)).median() * 100.0
     print(f"in-kernel shader clock (s_memtime / s_memrealtime x 100 MHz, median over waves): {clk:.0f} MHz")
+    tot = st[..., 4].mean()
+    loop = st[..., :4].sum(-1).mean()
+    pro = st[..., 6].mean()
+    print(f"per wave (mean): total {tot:.0f} cycles = loop {loop:.0f} + piece prologues {pro:.0f} + "
+          f"epilogues/merge/other {tot - loop - pro:.0f}; tiles {st[..., 7].mean():.1f}")
     for grp, sl in (("waves 0-3", slice(0, 4)), ("waves 4-7", slice(4, 8))):
         per = (st[:, sl, :4] / tiles[:, sl, None]).mean(dim=(0, 1))
         print(grp, "cycles/tile:", ", ".join(f"{n} {v:.0f}" for n, v in zip(names, per.tolist())),
