@@ -223,12 +223,19 @@ class DPTHead:
             return upsample(y32, *size, out_f32=False, planes_ld=self.out1.cin_pad, f16=self.f16)[1]
         return upsample(y32, *size)[0]
 
+    def tap_planes(self, i: int, t: torch.Tensor, n_img: int, hp: int, wp: int) -> Planes:
+        """Decoder tap i (fp32 patch rows [n_img*hp*wp, C], view_transformer.py:85) -> the operand planes of
+        act_postprocess[i]'s 1x1 projection.  Taken when the decoder produces the tap, so the residual
+        stream is never cloned (4 x 33.6 MB of copy traffic per 512^2 frame at D = 1024)."""
+        return split_planes(t.view(n_img, hp, wp, t.shape[-1]), self.projects[i].cin_pad, f16=self.f16)
+
     @torch.no_grad()
-    def __call__(self, taps: List[torch.Tensor], n_img: int, hp: int, wp: int, patch: int, elu_alpha: float,
+    def __call__(self, taps: List, n_img: int, hp: int, wp: int, patch: int, elu_alpha: float,
                  log_decode: bool, channels_last: bool) -> torch.Tensor:
+        """taps: the four decoder outputs, as fp32 rows or as their tap_planes()."""
         layers = []
         for i, t in enumerate(taps):
-            x = split_planes(t.view(n_img, hp, wp, t.shape[-1]), self.projects[i].cin_pad, f16=self.f16)
+            x = t if isinstance(t, Planes) else self.tap_planes(i, t, n_img, hp, wp)
             nxt = self.resize[i] if i in self.resize else self.rn[i]
             _, x = self.projects[i](x, planes_ld=nxt.cin_pad)
             if i in self.resize:

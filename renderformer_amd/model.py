@@ -414,8 +414,8 @@ class RenderFormer:
             ops.rmsnorm(x, L.ffn_norm, EPS, h)
             ops.gemm(h, L.w13, g, None, ops.EPI_SWIGLU)
             ops.gemm(g, L.w2, x, None, ops.EPI_ADD_F32)
-            if i in outl:
-                taps.append(x.clone())
+            if i in outl:  # straight into the DPT projection's operand planes (no fp32 copy of x)
+                taps.append(W.dpt.tap_planes(len(taps), x, P, plan.hp, plan.wp))
         return taps
 
     def _ray_embed(self, plan: _Plan, ray_in: torch.Tensor):
