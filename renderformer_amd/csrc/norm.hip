@@ -202,6 +202,125 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(const bf16_t* src, in
     }
 }
 
+// One row per wave, no row loop (like rmsnorm_v_kernel): the row's q/k chunks are issued first, then the
+// RoPE position and the norm weights, so every load of a wave is in flight in one round trip and the
+// grid holds all rows at once (stage 1: 5,649 rows = 5,652 waves, 5.5 per SIMD).
+template <int UPL>
+__global__ __launch_bounds__(256) void qk_norm_rope_row_kernel(const bf16_t* src, int64_t ld_src, bf16_t* dst,
+                                                               int64_t ld_dst, const int32_t* __restrict__ src_rows,
+                                                               int rows, int n_heads, int n_seg,
+                                                               const float* __restrict__ norm_w, float eps,
+                                                               float seg0_scale,
+                                                               const float* __restrict__ pos, int64_t ld_pos,
+                                                               int pos_div, const float* __restrict__ freqs,
+                                                               int n_freqs) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int upsg = n_heads * 8;
+    const int units = n_seg * upsg;
+    const int dim = n_heads * 128;
+    const int srow = src_rows ? src_rows[row] : row;
+    const bf16_t* s = src + (int64_t)srow * ld_src;
+    int col[UPL];
+    u32x4 lo[UPL], hi[UPL];
+#pragma unroll
+    for (int u = 0; u < UPL; ++u) {
+        const int unit = lane + 64 * u;
+        col[u] = (unit / upsg) * dim + ((unit % upsg) >> 3) * 128 + 8 * (unit & 7);
+        if (unit < units) {
+            lo[u] = *reinterpret_cast<const u32x4*>(s + col[u]);
+            hi[u] = *reinterpret_cast<const u32x4*>(s + col[u] + 64);
+        }
+    }
+    float ang = 0.f;
+    if (pos && lane < 9 * n_freqs) ang = pos[(int64_t)(row / pos_div) * ld_pos + lane / n_freqs] * freqs[lane % n_freqs];
+    float4 wl[UPL][2], wh[UPL][2];
+#pragma unroll
+    for (int u = 0; u < UPL; ++u) {
+        if (norm_w && lane + 64 * u < units) {
+            const float4* pl = reinterpret_cast<const float4*>(norm_w + col[u]);
+            const float4* ph = reinterpret_cast<const float4*>(norm_w + col[u] + 64);
+            wl[u][0] = pl[0];
+            wl[u][1] = pl[1];
+            wh[u][0] = ph[0];
+            wh[u][1] = ph[1];
+        } else {
+            wl[u][0] = wl[u][1] = wh[u][0] = wh[u][1] = make_float4(1.f, 1.f, 1.f, 1.f);
+        }
+    }
+    float ss[UPL];
+#pragma unroll
+    for (int u = 0; u < UPL; ++u) {
+        ss[u] = 0.f;
+        if (lane + 64 * u < units) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float a0 = __uint_as_float(lo[u][e] << 16), a1 = __uint_as_float(lo[u][e] & 0xffff0000u);
+                const float b0 = __uint_as_float(hi[u][e] << 16), b1 = __uint_as_float(hi[u][e] & 0xffff0000u);
+                ss[u] += a0 * a0 + a1 * a1 + b0 * b0 + b1 * b1;
+            }
+        }
+    }
+    float inv[UPL];
+#pragma unroll
+    for (int u = 0; u < UPL; ++u) inv[u] = 1.f;
+    if (norm_w) {
+        for (int sg = 0; sg < n_seg; ++sg) {
+            float part = 0.f;
+#pragma unroll
+            for (int u = 0; u < UPL; ++u) {
+                const int unit = lane + 64 * u;
+                part += (unit < units && unit / upsg == sg) ? ss[u] : 0.f;
+            }
+            const float iv = 1.0f / sqrtf(wave_sum(part) / (float)dim + eps);
+#pragma unroll
+            for (int u = 0; u < UPL; ++u)
+                if ((lane + 64 * u) / upsg == sg) inv[u] = iv;
+        }
+    }
+    // segment 0 (q) carries seg0_scale (RoPE is linear): folded into the row scale
+#pragma unroll
+    for (int u = 0; u < UPL; ++u)
+        if (lane + 64 * u < upsg) inv[u] *= seg0_scale;
+    float my_c = 1.f, my_s = 0.f;
+    if (pos && lane < 9 * n_freqs) __sincosf(ang, &my_s, &my_c);
+    float cs[8], sn[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        cs[k] = pos ? __shfl(my_c, 8 * (lane & 7) + k, 64) : 1.f;
+        sn[k] = pos ? __shfl(my_s, 8 * (lane & 7) + k, 64) : 0.f;
+    }
+    bf16_t* d = dst + (int64_t)row * ld_dst;
+#pragma unroll
+    for (int u = 0; u < UPL; ++u) {
+        if (lane + 64 * u < units) {
+            const float wlo[8] = {wl[u][0].x, wl[u][0].y, wl[u][0].z, wl[u][0].w,
+                                  wl[u][1].x, wl[u][1].y, wl[u][1].z, wl[u][1].w};
+            const float whi[8] = {wh[u][0].x, wh[u][0].y, wh[u][0].z, wh[u][0].w,
+                                  wh[u][1].x, wh[u][1].y, wh[u][1].z, wh[u][1].w};
+            u32x4 olo, ohi;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float ra[2], rb[2];
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const int i = 2 * e + t;
+                    const float a = (t ? __uint_as_float(lo[u][e] & 0xffff0000u) : __uint_as_float(lo[u][e] << 16));
+                    const float b = (t ? __uint_as_float(hi[u][e] & 0xffff0000u) : __uint_as_float(hi[u][e] << 16));
+                    const float x0 = a * inv[u] * wlo[i], x1 = b * inv[u] * whi[i];
+                    ra[t] = x0 * cs[i] - x1 * sn[i];  // rotate_half_hf: (-x2, x1)
+                    rb[t] = x1 * cs[i] + x0 * sn[i];
+                }
+                olo[e] = pack_bf16x2(ra[0], ra[1]);
+                ohi[e] = pack_bf16x2(rb[0], rb[1]);
+            }
+            *reinterpret_cast<u32x4*>(d + col[u]) = olo;
+            *reinterpret_cast<u32x4*>(d + col[u] + 64) = ohi;
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------- embedding assembly
 __global__ __launch_bounds__(256) void embed_kernel(float* __restrict__ out, int64_t ldo,
                                                     const int32_t* __restrict__ out_rows, int rows, int dim,
@@ -274,12 +393,19 @@ extern "C" int rf_qk_norm_rope(const void* src, int64_t ld_src, void* dst, int64
     if (rows <= 0) return RF_OK;
     RF_REQUIRE(!norm_w || ((uintptr_t)norm_w & 15) == 0, "rf_qk_norm_rope: norm weights must be 16-B aligned");
     const int blocks = (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
-    const dim3 grid(blocks < 2048 ? blocks : 2048);
+    static const bool loop = getenv("RF_QKN_LOOP") && atoi(getenv("RF_QKN_LOOP"));  // A/B only
+    const dim3 grid(loop && blocks > 2048 ? 2048 : blocks);
     const int units = n_seg * n_heads * 8;
     hipStream_t st = (hipStream_t)stream;
 #define RF_QKN(U)                                                                                                 \
-    hipLaunchKernelGGL(qk_norm_rope_kernel<U>, grid, dim3(256), 0, st, (const bf16_t*)src, ld_src, (bf16_t*)dst,  \
-                       ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, seg0_scale, pos, ld_pos, pos_div, freqs, n_freqs)
+    if (loop)                                                                                                     \
+        hipLaunchKernelGGL(qk_norm_rope_kernel<U>, grid, dim3(256), 0, st, (const bf16_t*)src, ld_src,            \
+                           (bf16_t*)dst, ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, seg0_scale, pos,    \
+                           ld_pos, pos_div, freqs, n_freqs);                                                      \
+    else                                                                                                          \
+        hipLaunchKernelGGL(qk_norm_rope_row_kernel<U>, grid, dim3(256), 0, st, (const bf16_t*)src, ld_src,        \
+                           (bf16_t*)dst, ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, seg0_scale, pos,    \
+                           ld_pos, pos_div, freqs, n_freqs)
     if (units <= 64) RF_QKN(1);
     else if (units <= 128) RF_QKN(2);
     else RF_QKN(4);
