@@ -356,6 +356,59 @@ __global__ __launch_bounds__(256) void embed_kernel(float* __restrict__ out, int
     }
 }
 
+// dim = 256 * NV, 16-B aligned rows: both encoder outputs and the base token row are loaded whole up front
+// (NV float4 per lane each, one memory round trip per row), then normed and summed in registers
+template <int NV>
+__global__ __launch_bounds__(256) void embed_v_kernel(float* __restrict__ out, int64_t ldo,
+                                                      const int32_t* __restrict__ out_rows, int rows,
+                                                      const float* __restrict__ base, int base_rows,
+                                                      const float* __restrict__ in0, int64_t ld0,
+                                                      const float* __restrict__ w0, float eps0,
+                                                      const float* __restrict__ in1, int64_t ld1,
+                                                      const float* __restrict__ w1, float eps1) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int orow = out_rows ? out_rows[row] : row;
+    float4 a[NV], b[NV], t[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        a[i] = in0 ? reinterpret_cast<const float4*>(in0 + (int64_t)row * ld0)[lane + 64 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        b[i] = in1 ? reinterpret_cast<const float4*>(in1 + (int64_t)row * ld1)[lane + 64 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        t[i] = base ? reinterpret_cast<const float4*>(base + (int64_t)(row % base_rows) * (256 * NV))[lane + 64 * i]
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        s0 += a[i].x * a[i].x + a[i].y * a[i].y + a[i].z * a[i].z + a[i].w * a[i].w;
+        s1 += b[i].x * b[i].x + b[i].y * b[i].y + b[i].z * b[i].z + b[i].w * b[i].w;
+    }
+    s0 = in0 ? 1.0f / sqrtf(wave_sum(s0) / (float)(256 * NV) + eps0) : 0.f;
+    s1 = in1 ? 1.0f / sqrtf(wave_sum(s1) / (float)(256 * NV) + eps1) : 0.f;
+    float4* o = reinterpret_cast<float4*>(out + (int64_t)orow * ldo);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        // same association as the reference: (token + tex_emb) + vn_emb (renderformer.py:158)
+        float4 v = t[i];
+        if (in0) {
+            const float4 g = reinterpret_cast<const float4*>(w0)[lane + 64 * i];
+            v.x = v.x + a[i].x * s0 * g.x;
+            v.y = v.y + a[i].y * s0 * g.y;
+            v.z = v.z + a[i].z * s0 * g.z;
+            v.w = v.w + a[i].w * s0 * g.w;
+        }
+        if (in1) {
+            const float4 g = reinterpret_cast<const float4*>(w1)[lane + 64 * i];
+            v.x = v.x + b[i].x * s1 * g.x;
+            v.y = v.y + b[i].y * s1 * g.y;
+            v.z = v.z + b[i].z * s1 * g.z;
+            v.w = v.w + b[i].w * s1 * g.w;
+        }
+        o[lane + 64 * i] = v;
+    }
+}
+
 }  // namespace
 
 extern "C" int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, float eps, void* out, int64_t ldo,
@@ -420,8 +473,23 @@ extern "C" int rf_embed(float* out, int64_t ldo, const int32_t* out_rows, int ro
     RF_REQUIRE((!in0 || w0) && (!in1 || w1), "rf_embed: input without norm weight");
     RF_REQUIRE(!base || base_rows > 0, "rf_embed: base_rows must be > 0");
     if (rows <= 0) return RF_OK;
-    hipLaunchKernelGGL(embed_kernel, dim3((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), dim3(256), 0,
-                       (hipStream_t)stream, out, ldo, out_rows, rows, dim, base, base_rows, in0, ld0, w0, eps0, in1,
-                       ld1, w1, eps1);
+    const dim3 grid((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK);
+    hipStream_t st = (hipStream_t)stream;
+    auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    const bool vec = dim % 256 == 0 && ldo % 4 == 0 && ld0 % 4 == 0 && ld1 % 4 == 0 && al(out) && al(base) &&
+                     al(in0) && al(w0) && al(in1) && al(w1);
+#define RF_EMB(NV)                                                                                                \
+    hipLaunchKernelGGL(embed_v_kernel<NV>, grid, dim3(256), 0, st, out, ldo, out_rows, rows, base, base_rows, in0, \
+                       ld0, w0, eps0, in1, ld1, w1, eps1)
+    switch (vec ? dim / 256 : 0) {
+        case 3: RF_EMB(3); break;
+        case 4: RF_EMB(4); break;
+        case 6: RF_EMB(6); break;
+        case 8: RF_EMB(8); break;
+        default:
+            hipLaunchKernelGGL(embed_kernel, grid, dim3(256), 0, st, out, ldo, out_rows, rows, dim, base, base_rows,
+                               in0, ld0, w0, eps0, in1, ld1, w1, eps1);
+    }
+#undef RF_EMB
     return rf::check_launch("rf_embed");
 }
