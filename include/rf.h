@@ -101,6 +101,17 @@ int rf_qk_norm_rope(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, 
                     int rows, int dim, int n_heads, int n_seg, const float* norm_w, float eps, float seg0_scale,
                     const float* pos, int64_t ld_pos, int pos_div, const float* freqs, int n_freqs, void* stream);
 
+/* rf_qk_norm_rope over n_groups column groups of the same rows in one launch: group g reads
+ * src + g*src_gstride, writes dst + g*dst_gstride (elements) and uses norm_w + g*w_gstride; the rows,
+ * src_rows and RoPE positions are shared.  The decoder's cross-attention keys of every layer
+ * (attention.py:127-141 applied to the k projection of each decoder layer, with that layer's k_norm)
+ * are rotated this way in one pass over the batched K/V projection.  Offsets must keep 16-B alignment. */
+int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t src_gstride, void* dst, int64_t ld_dst,
+                           int64_t dst_gstride, const int32_t* src_rows, int rows, int dim, int n_heads, int n_seg,
+                           int n_groups, const float* norm_w, int64_t w_gstride, float eps, float seg0_scale,
+                           const float* pos, int64_t ld_pos, int pos_div, const float* freqs, int n_freqs,
+                           void* stream);
+
 /* Variable-length multi-head attention, non-causal, head_dim 128, bf16 in/out, f32 softmax.
  * problems: int32[n_problems][5] = {q_start, q_len, k_start, k_len, v_start} (rows); k_len >= 1
  * wherever q_len >= 1.  For every problem p and head h: O[q_start+i, h*128:(h+1)*128] =

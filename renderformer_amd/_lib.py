@@ -25,6 +25,8 @@ SIGNATURES = {
     "rf_gemm_bf16": [_P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _L, _P],
     "rf_rmsnorm": [_P, _L, _P, _F, _P, _L, _I, _I, _P],
     "rf_qk_norm_rope": [_P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _F, _F, _P, _L, _I, _P, _I, _P],
+    "rf_qk_norm_rope_groups": [_P, _L, _L, _P, _L, _L, _P, _I, _I, _I, _I, _I, _P, _L, _F, _F, _P, _L, _I, _P, _I,
+                               _P],
     "rf_attn_fwd": [_P, _L, _P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _F, _I, _P, _L, _P],
     "rf_attn_combine": [_P, _L, _I, _I, _P, _I, _P, _L, _P],
     "rf_swin_attn_fwd": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _I, _I, _F, _P],

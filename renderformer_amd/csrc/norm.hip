@@ -213,10 +213,15 @@ __global__ __launch_bounds__(256) void qk_norm_rope_row_kernel(const bf16_t* src
                                                                float seg0_scale,
                                                                const float* __restrict__ pos, int64_t ld_pos,
                                                                int pos_div, const float* __restrict__ freqs,
-                                                               int n_freqs) {
+                                                               int n_freqs, int64_t src_gstride, int64_t dst_gstride,
+                                                               int w_gstride) {
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
     if (row >= rows) return;
+    // group blockIdx.y: its own column block of src/dst and its own norm weights (same rows, same RoPE)
+    src += blockIdx.y * src_gstride;
+    dst += blockIdx.y * dst_gstride;
+    if (norm_w) norm_w += blockIdx.y * w_gstride;
     const int upsg = n_heads * 8;
     const int units = n_seg * upsg;
     const int dim = n_heads * 128;
@@ -432,38 +437,60 @@ extern "C" int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, floa
     return rf::check_launch("rf_rmsnorm");
 }
 
-extern "C" int rf_qk_norm_rope(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, const int32_t* src_rows,
-                               int rows, int dim, int n_heads, int n_seg, const float* norm_w, float eps,
-                               float seg0_scale, const float* pos, int64_t ld_pos, int pos_div, const float* freqs, int n_freqs,
-                               void* stream) {
+extern "C" int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t src_gstride, void* dst, int64_t ld_dst,
+                                      int64_t dst_gstride, const int32_t* src_rows, int rows, int dim, int n_heads,
+                                      int n_seg, int n_groups, const float* norm_w, int64_t w_gstride, float eps,
+                                      float seg0_scale, const float* pos, int64_t ld_pos, int pos_div,
+                                      const float* freqs, int n_freqs, void* stream) {
     RF_REQUIRE(src && dst, "rf_qk_norm_rope: null pointer");
     RF_REQUIRE(dim == n_heads * 128 && n_seg >= 1 && n_seg * n_heads * 8 <= MAX_UNITS,
                "rf_qk_norm_rope: need head_dim 128 and n_seg*n_heads <= %d", MAX_UNITS / 8);
     RF_REQUIRE(ld_src % 8 == 0 && ld_dst % 8 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0,
                "rf_qk_norm_rope: rows must be 16-B aligned");
+    RF_REQUIRE(n_groups >= 1 && n_groups <= 65535 && src_gstride % 8 == 0 && dst_gstride % 8 == 0 && w_gstride % 4 == 0,
+               "rf_qk_norm_rope: bad group count/strides (16-B aligned group offsets)");
     RF_REQUIRE(!pos || (freqs && n_freqs > 0 && 9 * n_freqs <= 64 && pos_div > 0),
                "rf_qk_norm_rope: rope needs freqs with 9*n_freqs <= 64");
     if (rows <= 0) return RF_OK;
     RF_REQUIRE(!norm_w || ((uintptr_t)norm_w & 15) == 0, "rf_qk_norm_rope: norm weights must be 16-B aligned");
     const int blocks = (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
     static const bool loop = getenv("RF_QKN_LOOP") && atoi(getenv("RF_QKN_LOOP"));  // A/B only
-    const dim3 grid(loop && blocks > 2048 ? 2048 : blocks);
     const int units = n_seg * n_heads * 8;
     hipStream_t st = (hipStream_t)stream;
+    if (loop) {  // the grid-stride kernel, one launch per group
+        const dim3 grid(blocks > 2048 ? 2048 : blocks);
+        for (int g = 0; g < n_groups; ++g) {
+            const bf16_t* s = (const bf16_t*)src + g * src_gstride;
+            bf16_t* d = (bf16_t*)dst + g * dst_gstride;
+            const float* w = norm_w ? norm_w + g * w_gstride : nullptr;
+#define RF_QKL(U)                                                                                                 \
+    hipLaunchKernelGGL(qk_norm_rope_kernel<U>, grid, dim3(256), 0, st, s, ld_src, d, ld_dst, src_rows, rows,      \
+                       n_heads, n_seg, w, eps, seg0_scale, pos, ld_pos, pos_div, freqs, n_freqs)
+            if (units <= 64) RF_QKL(1);
+            else if (units <= 128) RF_QKL(2);
+            else RF_QKL(4);
+#undef RF_QKL
+        }
+        return rf::check_launch("rf_qk_norm_rope");
+    }
+    const dim3 grid(blocks, n_groups);
 #define RF_QKN(U)                                                                                                 \
-    if (loop)                                                                                                     \
-        hipLaunchKernelGGL(qk_norm_rope_kernel<U>, grid, dim3(256), 0, st, (const bf16_t*)src, ld_src,            \
-                           (bf16_t*)dst, ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, seg0_scale, pos,    \
-                           ld_pos, pos_div, freqs, n_freqs);                                                      \
-    else                                                                                                          \
-        hipLaunchKernelGGL(qk_norm_rope_row_kernel<U>, grid, dim3(256), 0, st, (const bf16_t*)src, ld_src,        \
-                           (bf16_t*)dst, ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, seg0_scale, pos,    \
-                           ld_pos, pos_div, freqs, n_freqs)
+    hipLaunchKernelGGL(qk_norm_rope_row_kernel<U>, grid, dim3(256), 0, st, (const bf16_t*)src, ld_src, (bf16_t*)dst, \
+                       ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, seg0_scale, pos, ld_pos, pos_div, freqs, \
+                       n_freqs, src_gstride, dst_gstride, (int)w_gstride)
     if (units <= 64) RF_QKN(1);
     else if (units <= 128) RF_QKN(2);
     else RF_QKN(4);
 #undef RF_QKN
     return rf::check_launch("rf_qk_norm_rope");
+}
+
+extern "C" int rf_qk_norm_rope(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, const int32_t* src_rows,
+                               int rows, int dim, int n_heads, int n_seg, const float* norm_w, float eps,
+                               float seg0_scale, const float* pos, int64_t ld_pos, int pos_div, const float* freqs, int n_freqs,
+                               void* stream) {
+    return rf_qk_norm_rope_groups(src, ld_src, 0, dst, ld_dst, 0, src_rows, rows, dim, n_heads, n_seg, 1, norm_w, 0, eps,
+                                  seg0_scale, pos, ld_pos, pos_div, freqs, n_freqs, stream);
 }
 
 extern "C" int rf_embed(float* out, int64_t ldo, const int32_t* out_rows, int rows, int dim, const float* base,

@@ -129,6 +129,9 @@ class _DeviceWeights:
             w = torch.cat([sd[a + "k_proj.weight"], sd[a + "v_proj.weight"]], 0).float()
             wkv_all.append(w * sd[p + "kv_norm.weight"].float()[None, :])
         self.wkv_all = _bf16(torch.cat(wkv_all, 0), device)
+        # every layer's k_norm weight, for the one-launch key rotation of all layers (ops.qk_norm_rope_groups)
+        self.k_norm_all = _f32(torch.cat([sd[f"{vt}transformer.layers.{i}.multihead_attn.k_norm.weight"]
+                                          for i in range(cfg.view_transformer_n_layers)]), device)
         self.ctx_unit = torch.ones(self.wkv_all.shape[1], dtype=torch.float32, device=device)
         self.dpt = DPTHead(sd, vt + "out_dpt", device, precision=dpt_precision)
 
@@ -374,7 +377,16 @@ class RenderFormer:
             ops.gemm(hc, W.wkv_all, kv_all)
         else:
             kv = torch.empty(plan.T1, 2 * D, dtype=torch.bfloat16, device=dev)
-        kview = torch.empty(plan.T_kv, D, dtype=torch.bfloat16, device=dev)
+        # (the rotated keys of all layers are kept when they fit in 4 GiB: T_kv grows with the view count)
+        k_batch = kv_batch and os.environ.get("RF_K_BATCH", "1") != "0" and plan.T_kv * n_dec * D * 2 <= (4 << 30)
+        if k_batch:
+            # keys of all layers normed + rotated in one launch: layer i's K is the D columns at 2*D*i of kv_all,
+            # its rotated copy the D columns at D*i of kview_all
+            kview_all = torch.empty(plan.T_kv, n_dec * D, dtype=torch.bfloat16, device=dev)
+            ops.qk_norm_rope_groups(kv_all, 2 * D, kview_all, D, n_dec, H, W.k_norm_all if qk else None, EPS, pos2,
+                                    W.dec_freqs, src_rows=plan.kv_src_rows)
+        else:
+            kview = torch.empty(plan.T_kv, D, dtype=torch.bfloat16, device=dev)
         qkv = torch.empty(T2, 3 * D, dtype=torch.bfloat16, device=dev) if cfg.view_transformer_include_self_attn else None
         swin = cfg.view_transformer_use_swin_attn
         taps = []
@@ -388,10 +400,13 @@ class RenderFormer:
             else:
                 ops.rmsnorm(ctx, L.kv_norm, EPS, hc)
                 ops.gemm(hc, L.wkv, kv)
+            if k_batch:
+                kview = kview_all[:, D * i:D * (i + 1)]
             ops.qk_norm_rope(q2, q2, H, L.q_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R,
                              q_scale=ops.Q_LOG2_SCALE)
-            ops.qk_norm_rope(kv[:, :D], kview, H, L.k_norm if qk else None, EPS, pos2, W.dec_freqs,
-                             src_rows=plan.kv_src_rows)
+            if not k_batch:
+                ops.qk_norm_rope(kv[:, :D], kview, H, L.k_norm if qk else None, EPS, pos2, W.dec_freqs,
+                                 src_rows=plan.kv_src_rows)
             ops.attention(q2, kview, kv[:, D:], att, plan.prob2, R, H, tag="attn_cross", max_k_len=plan.max_s,
                           q_prescaled=True)
             ops.gemm(att, L.wo, x, None, ops.EPI_ADD_F32)

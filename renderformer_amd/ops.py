@@ -138,6 +138,34 @@ def qk_norm_rope(src: torch.Tensor, dst: torch.Tensor, n_heads: int, norm_w: Opt
     return dst
 
 
+def qk_norm_rope_groups(src: torch.Tensor, src_gstride: int, dst: torch.Tensor, dst_gstride: int, n_groups: int,
+                        n_heads: int, norm_w: Optional[torch.Tensor], eps: float, pos: Optional[torch.Tensor] = None,
+                        freqs: Optional[torch.Tensor] = None, src_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """qk_norm_rope (one segment) on n_groups column groups in one launch: group g maps the width-
+    (n_heads*128) block at column g*src_gstride of src to column g*dst_gstride of dst with norm weights
+    norm_w[g*dim:(g+1)*dim].  src/dst are the full row matrices holding every group."""
+    _dev(src, torch.bfloat16, "src")
+    _dev(dst, torch.bfloat16, "dst")
+    dim = n_heads * 128
+    rows = dst.shape[0]
+    _check(n_groups >= 1 and (n_groups - 1) * src_gstride + dim <= src.shape[1]
+           and (n_groups - 1) * dst_gstride + dim <= dst.shape[1], "qk_norm_rope_groups: groups exceed the width")
+    if src_rows is None:
+        _check(src.shape[0] == rows, "qk_norm_rope_groups: row mismatch")
+    else:
+        _dev(src_rows, torch.int32, "src_rows")
+        _check(src_rows.numel() == rows, "qk_norm_rope_groups: src_rows size")
+    if norm_w is not None:
+        _check(norm_w.numel() == n_groups * dim, "qk_norm_rope_groups: norm weight size")
+    if pos is not None:
+        _dev(pos, torch.float32, "pos")
+        _check(pos.shape[1] == 9 and freqs is not None, "qk_norm_rope_groups: pos must be [*, 9] with freqs")
+    call("rf_qk_norm_rope_groups", ptr(src), src.stride(0), src_gstride, ptr(dst), dst.stride(0), dst_gstride,
+         ptr(src_rows), rows, dim, n_heads, 1, n_groups, ptr(norm_w), dim, eps, 1.0, ptr(pos),
+         pos.stride(0) if pos is not None else 0, 1, ptr(freqs), freqs.numel() if freqs is not None else 0, stream())
+    return dst
+
+
 ATTN_QBLK = 128 if os.environ.get("RF_ATTN_KERNEL", "3") == "2" else 256  # query rows per legacy workgroup
 LN2 = math.log(2.0)
 # softmax scale * log2(e) for head_dim 128: q pre-multiplied by this (qk_norm_rope q_scale) lets attention run

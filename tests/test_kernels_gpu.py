@@ -208,6 +208,33 @@ def test_qk_norm_rope_two_segments():
     assert torch.equal(s[:, 2 * D:].cpu(), src[:, 2 * D:])
 
 
+@pytest.mark.parametrize("with_norm", [True, False])
+def test_qk_norm_rope_groups_equals_per_group(with_norm):
+    """One launch over the keys of every decoder layer (the K columns at stride 2D of the batched K/V
+    projection, gathered per view) is bit-identical to one launch per layer, and matches the oracle."""
+    ops = _ops()
+    T, H, G = 131, 8, 3
+    D = H * 128
+    kv = torch.randn(T, G * 2 * D).bfloat16().to(dev)
+    w = (torch.rand(G * D) + 0.5).to(dev) if with_norm else None
+    rows = torch.tensor(list(range(T)) + list(range(0, T, 2)), dtype=torch.int32)  # two views of one scene
+    pos = (torch.rand(rows.numel(), 9) * 2 - 1).to(dev)
+    freqs = (2 ** torch.linspace(0, math.log2(5), 6)).to(dev)
+    out = torch.empty(rows.numel(), G * D, device=dev, dtype=torch.bfloat16)
+    ops.qk_norm_rope_groups(kv, 2 * D, out, D, G, H, w, 1e-6, pos, freqs, src_rows=rows.to(dev))
+    cos, sin = rf_ref.rope_cos_sin(pos.cpu()[None], freqs.cpu(), 128)
+    for g in range(G):
+        one = torch.empty(rows.numel(), D, device=dev, dtype=torch.bfloat16)
+        wg = w[g * D:(g + 1) * D] if with_norm else None
+        ops.qk_norm_rope(kv[:, 2 * D * g:2 * D * g + D], one, H, wg, 1e-6, pos, freqs, src_rows=rows.to(dev))
+        assert torch.equal(out[:, g * D:(g + 1) * D], one)
+        x = kv[:, 2 * D * g:2 * D * g + D].float().cpu()[rows.long()]
+        if with_norm:
+            x = F.rms_norm(x, (D,), wg.cpu(), 1e-6)
+        ref = rf_ref.rope_apply(x.view(1, -1, H, 128).transpose(1, 2), cos, sin).transpose(1, 2).reshape(-1, D)
+        assert relerr(out[:, g * D:(g + 1) * D].float().cpu(), ref) < 4e-3
+
+
 def _ref_attn(q, k, v, H):
     lq, lk = q.shape[0], k.shape[0]
     qh = q.double().view(lq, H, 128).transpose(0, 1)
