@@ -1389,7 +1389,9 @@ template <bool GATHER>
 static int conv_f16_dp(EngineArgs& p, void* stream, const char* what) {
     const char* env = getenv("RF_CONV_TILE");
     const int t = env ? atoi(env) : 0;
-    if (p.n == 64) return launch<T256x64, E_CONV, P_F16, GATHER>(p, stream, what);
+    // (RF_CONV_HALO=1 runs it halo-tiled: 90 -> 140 us at 512^2, 128 -> 32; a 128x64 tile at two blocks per
+    // CU measured the same 90 us with or without the halo, so the gathered 256x64 launch stays the default)
+    if (p.n == 64) return launch_conv<T256x64, P_F16, GATHER>(p, stream, what);
     if (t == 128) return launch_conv<T128, P_F16, GATHER>(p, stream, what);
     if (t == 1288) return launch_conv<T128w8, P_F16, GATHER>(p, stream, what);
     if (p.n % 256 == 0 && (t == 256 || (!t && ((p.m + 255) / 256) * (p.n / 256) >= 256)))

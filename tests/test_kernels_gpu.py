@@ -541,14 +541,17 @@ def test_conv_matches_fp64(cin, cout, k, stride, hw, prec, tile, monkeypatch):
         assert (pl.hi[..., cout:] == 0).all() and (f16 or (pl.lo[..., cout:] == 0).all())
 
 
-@pytest.mark.parametrize("tile", ["128", "1288", "256"])
+@pytest.mark.parametrize("tile", ["128", "1288", "256", "64"])
 @pytest.mark.parametrize("cin,cout,hw", [(256, 256, 32), (64, 128, 64), (32, 256, 16), (128, 128, 128),
-                                         (64, 256, 256)])
+                                         (64, 256, 256), (128, 32, 64), (64, 32, 256)])
 def test_conv_halo(cin, cout, hw, tile, monkeypatch):
     """Halo-tiled 3x3 convolution (RF_CONV_HALO=1) on every tile that takes it: tiles of whole image rows
-    (TW = wo) and of partial rows (TW = BM), two images, fused bias + 2 residuals + SiLU planes."""
+    (TW = wo) and of partial rows (TW = BM), two images, fused bias + 2 residuals + SiLU planes.  Tile "64"
+    is the 256x64 tile every filter bank of <= 64 channels takes (DPT output_conv2)."""
     if tile == "256" and cout % 256:
         pytest.skip("256x256 tile needs 256 output channels")
+    if (tile == "64") != (cout <= 64):
+        pytest.skip("the 256x64 tile serves exactly the filter banks of <= 64 channels")
     monkeypatch.setenv("RF_CONV_HALO", "1")
     monkeypatch.setenv("RF_CONV_TILE", tile)
     monkeypatch.setenv("RF_CONV_SK", "0")
