@@ -67,8 +67,9 @@ _GEMM_WS = {}
 
 
 def _gemm_workspace(device) -> torch.Tensor:
-    """Stream-K partial tiles + flags: one zero-filled buffer per device, reused by every GEMM (one stream)."""
-    key = (device.type, device.index)
+    """Stream-K partial tiles + flags: one zero-filled buffer per (device, stream), reused by every GEMM on
+    that stream, so renders on concurrent streams never share partials or flags."""
+    key = (device.type, device.index, torch.cuda.current_stream(device).cuda_stream)
     ws = _GEMM_WS.get(key)
     if ws is None:
         ws = torch.zeros(int(load().rf_gemm_workspace_bytes()), dtype=torch.uint8, device=device)
@@ -175,8 +176,9 @@ _ATTN_WS = {}
 
 
 def _attn_workspace(device) -> torch.Tensor:
-    """Stream-K partials + per-workgroup flags, zero-filled once per device (the kernel re-arms the flags)."""
-    key = (device.type, device.index)
+    """Stream-K partials + per-workgroup flags, zero-filled once per (device, stream) (the kernel re-arms the
+    flags; rf.h allows one launch at a time per workspace, so concurrent streams each get their own)."""
+    key = (device.type, device.index, torch.cuda.current_stream(device).cuda_stream)
     ws = _ATTN_WS.get(key)
     if ws is None:
         nbytes = load().rf_attn_workspace_bytes(0, 1, 0)
