@@ -83,6 +83,59 @@ __global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__
     if (p_hi) store_split4(p_hi, p_lo, pix * p_ld + cc, r, false);
 }
 
+// The same with 8 channels per thread (c % 8 == 0): 16-B fp16 plane stores and half the index math per
+// output element; the arithmetic per channel is identical, so results are bit-identical to upsample_kernel
+__global__ __launch_bounds__(256) void upsample8_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                        bf16_t* __restrict__ p_hi, bf16_t* __restrict__ p_lo, int p_ld,
+                                                        int hi, int wi, int c, int ho, int wo, float sh, float sw) {
+    const int c8n = c >> 3;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= wo * c8n) return;
+    const int row = blockIdx.y;  // img * ho + oy
+    const int img = row / ho, oy = row - img * ho;
+    const int ox = i / c8n;
+    const int cc = (i - ox * c8n) * 8;
+    const float fy = sh * (float)oy, fx = sw * (float)ox;
+    const int y0 = (int)fy, x0 = (int)fx;
+    const int y1 = y0 + (y0 < hi - 1 ? 1 : 0), x1 = x0 + (x0 < wi - 1 ? 1 : 0);
+    const float ly1 = fy - (float)y0, lx1 = fx - (float)x0;
+    const float ly0 = 1.0f - ly1, lx0 = 1.0f - lx1;
+    const float* base = in + (int64_t)img * hi * wi * c + cc;
+    const float4* pa = reinterpret_cast<const float4*>(base + (int64_t)(y0 * wi + x0) * c);
+    const float4* pb = reinterpret_cast<const float4*>(base + (int64_t)(y0 * wi + x1) * c);
+    const float4* pd = reinterpret_cast<const float4*>(base + (int64_t)(y1 * wi + x0) * c);
+    const float4* pe = reinterpret_cast<const float4*>(base + (int64_t)(y1 * wi + x1) * c);
+    float4 a[2], b[2], d[2], e[2], r[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        a[h] = pa[h];
+        b[h] = pb[h];
+        d[h] = pd[h];
+        e[h] = pe[h];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        r[h].x = ly0 * (lx0 * a[h].x + lx1 * b[h].x) + ly1 * (lx0 * d[h].x + lx1 * e[h].x);
+        r[h].y = ly0 * (lx0 * a[h].y + lx1 * b[h].y) + ly1 * (lx0 * d[h].y + lx1 * e[h].y);
+        r[h].z = ly0 * (lx0 * a[h].z + lx1 * b[h].z) + ly1 * (lx0 * d[h].z + lx1 * e[h].z);
+        r[h].w = ly0 * (lx0 * a[h].w + lx1 * b[h].w) + ly1 * (lx0 * d[h].w + lx1 * e[h].w);
+    }
+    const int64_t pix = (int64_t)row * wo + ox;
+    if (out) {
+        float4* o = reinterpret_cast<float4*>(out + pix * c + cc);
+        o[0] = r[0];
+        o[1] = r[1];
+    }
+    if (p_hi && !p_lo) {
+        *reinterpret_cast<uint4*>(p_hi + pix * p_ld + cc) =
+            make_uint4(pack_f16x2(r[0].x, r[0].y), pack_f16x2(r[0].z, r[0].w), pack_f16x2(r[1].x, r[1].y),
+                       pack_f16x2(r[1].z, r[1].w));
+    } else if (p_hi) {
+        store_split4(p_hi, p_lo, pix * p_ld + cc, r[0], false);
+        store_split4(p_hi, p_lo, pix * p_ld + cc + 4, r[1], false);
+    }
+}
+
 }  // namespace
 
 extern "C" int rf_split_planes(const float* x, int64_t rows, int c, int64_t ldx, void* p_hi, void* p_lo, int p_ld,
@@ -108,8 +161,15 @@ extern "C" int rf_upsample_bilinear(const float* in, int n_img, int hi, int wi, 
     // scale computed on the host with IEEE float division, as aten's area_pixel_compute_scale<float>
     const float sh = ho > 1 ? (float)(hi - 1) / (float)(ho - 1) : 0.f;
     const float sw = wo > 1 ? (float)(wi - 1) / (float)(wo - 1) : 0.f;
-    const dim3 grid((unsigned)((wo * (c / 4) + 255) / 256), (unsigned)(n_img * ho));
-    hipLaunchKernelGGL(upsample_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, out, (bf16_t*)p_hi,
-                       (bf16_t*)p_lo, p_ld, hi, wi, c, ho, wo, sh, sw);
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (c % 8 == 0 && (!p_hi || p_ld % 8 == 0) && al16(in) && al16(out) && al16(p_hi) && al16(p_lo)) {
+        const dim3 grid((unsigned)((wo * (c / 8) + 255) / 256), (unsigned)(n_img * ho));
+        hipLaunchKernelGGL(upsample8_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, out, (bf16_t*)p_hi,
+                           (bf16_t*)p_lo, p_ld, hi, wi, c, ho, wo, sh, sw);
+    } else {
+        const dim3 grid((unsigned)((wo * (c / 4) + 255) / 256), (unsigned)(n_img * ho));
+        hipLaunchKernelGGL(upsample_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, out, (bf16_t*)p_hi,
+                           (bf16_t*)p_lo, p_ld, hi, wi, c, ho, wo, sh, sw);
+    }
     return rf::check_launch("rf_upsample_bilinear");
 }

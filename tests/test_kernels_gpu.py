@@ -591,19 +591,23 @@ def test_deconv(cin, cout, k, prec):
 
 
 @pytest.mark.parametrize("prec", PRECS)
+@pytest.mark.parametrize("c", [12, 16])  # 4- and 8-channel-per-thread kernels
 @pytest.mark.parametrize("hi,ho", [(8, 16), (16, 32), (32, 64), (7, 13)])
-def test_upsample_bilinear_align_corners(hi, ho, prec):
+def test_upsample_bilinear_align_corners(hi, ho, c, prec):
     from renderformer_amd.dpt import upsample
     f16 = prec == "f16"
-    x = torch.randn(2, 12, hi, hi)
+    x = torch.randn(2, c, hi, hi)
     out, pl = upsample(x.permute(0, 2, 3, 1).contiguous().to(dev), ho, ho, planes_ld=32, f16=f16)
     ref = F.interpolate(x, size=(ho, ho), mode="bilinear", align_corners=True).permute(0, 2, 3, 1)
     assert torch.allclose(out.cpu(), ref, atol=1e-5, rtol=1e-5)
     if f16:
-        assert torch.equal(pl.hi[..., :12].cpu(), out.cpu().half())  # RNE fp16 of the fp32 value
-        assert (pl.hi[..., 12:] == 0).all()
+        assert torch.equal(pl.hi[..., :c].cpu(), out.cpu().half())  # RNE fp16 of the fp32 value
+        assert (pl.hi[..., c:] == 0).all()
     else:
-        assert torch.allclose(_planes_value(pl)[..., :12].cpu(), ref, atol=1e-5, rtol=1e-5)
+        assert torch.allclose(_planes_value(pl)[..., :c].cpu(), ref, atol=1e-5, rtol=1e-5)
+    # plane-only output (the DPT's last upsample) equals the planes written alongside the fp32 output
+    out2, pl2 = upsample(x.permute(0, 2, 3, 1).contiguous().to(dev), ho, ho, out_f32=False, planes_ld=32, f16=f16)
+    assert out2 is None and torch.equal(pl2.hi, pl.hi) and (f16 or torch.equal(pl2.lo, pl.lo))
 
 
 @pytest.mark.parametrize("prec", PRECS)
