@@ -12,7 +12,7 @@ model); no data crosses ranks.  `--save_video` needs an mp4 encoder (imageio/ffm
 the image lacks: frames are written as PNGs and the video step is skipped with a notice.
 
 The data path is pipelined: loader threads decode and collate the next batches into
-pinned host memory (texture kept fp16 as stored, widened on the device) while batch i renders, the
+pinned host memory (texture kept in the dtype the file stores, widened on the device) while batch i renders, the
 host-to-device copy runs on a side stream that the compute stream waits on, results come back on
 another side stream, and writer threads encode and write the EXR/PNG files — the GPU only waits for
 the HDF5 decode when that is slower than a batch.  RF_BATCH_INLINE=1 runs every step
@@ -41,11 +41,14 @@ def natural_key(path: str):
 
 
 def load_scene(path: str, padding_length=None, texture_dtype=torch.float32) -> dict:
-    """`TriangleRenderH5Dataset.__getitem__` (batch_infer.py:27-58).  texture_dtype=float16 keeps the file's
-    fp16 texture (half the host bytes; the pipelined path widens it on the device)."""
+    """`TriangleRenderH5Dataset.__getitem__` (batch_infer.py:27-58).  texture_dtype=None keeps the dtype the
+    file stores (to_h5 writes fp16: half the host bytes; the pipelined path widens it to fp32 on the device,
+    the same conversion the inline path does on the host)."""
     with File(path) as f:
         tri = torch.from_numpy(np.array(f["triangles"])).float()
-        tex = torch.from_numpy(np.array(f["texture"])).to(texture_dtype)
+        tex = torch.from_numpy(np.array(f["texture"]))
+        if texture_dtype is not None:
+            tex = tex.to(texture_dtype)
         vn = torch.from_numpy(np.array(f["vn"])).float()
         c2w = torch.from_numpy(np.array(f["c2w"]).astype(np.float32))
         fov = torch.from_numpy(np.array(f["fov"]).astype(np.float32))
@@ -77,7 +80,7 @@ WRITERS = 4  # image encode/write threads
 
 
 def _load_batch(files, idx, padding_length, pin):
-    items = [load_scene(files[i], padding_length, torch.float16 if pin else torch.float32) for i in idx]
+    items = [load_scene(files[i], padding_length, None if pin else torch.float32) for i in idx]
     host = collate(items)
     if pin:
         host = {k: v.pin_memory() for k, v in host.items()}
@@ -93,7 +96,7 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
 
     def render(batch):
         tex = batch["texture"]
-        if tex.dtype != torch.float32:  # fp16 from the file, widened on the device (exact)
+        if tex.dtype != torch.float32:  # the file's dtype, widened on the device like the inline path's host cast
             tex = tex.float()
         return pipeline(triangles=batch["triangles"], texture=tex, mask=batch["mask"], vn=batch["vn"],
                         c2w=batch["c2w"], fov=batch["fov"].unsqueeze(-1), **kw)

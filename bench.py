@@ -1,59 +1,107 @@
 """Headline benchmark: rendered frames/s at 512x512, RenderFormer-V1.1-swin-large (proxy shape), cbox.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cbox|c4|c5] ...
 
-One step = one full render of one synthetic cbox-sized scene (N = 5,633 triangles,
-SURVEY §8d) and one view at 512x512 through the drop-in pipeline: texture/vn
-encoders, stage 1 (14 layers), ray tokens, stage 2 (10 layers, Swin), DPT, HDR
-decode.  Inputs are resident in HBM before the timed region.  With N > 1 (one
-process per GPU under torch.distributed.run) every rank renders its own scene each
-step (weak scaling over the embarrassingly parallel (scene, view) dimension, no
-data-path collective); the reported value is frames of all ranks / max-over-ranks time.
+Workloads (all synthetic, seeded, inputs resident in HBM before the timed region):
 
-The JSON line carries a roofline object for the dominant kernel, timed with HIP
-events around each of its launches inside the timed region, and a CPU baseline:
-the oracle restatement of the reference (oracle/rf_ref.py, PyTorch CPU fp32) on a
-bounded sample of the same workload, rank 0 at N = 1 only.
+* ``cbox`` (default, BASELINE config 2; weak scaling): one step = every rank renders ``--scenes`` cbox-sized
+  scenes (N = 5,633 triangles) x ``--views`` views at 512x512 through the drop-in pipeline (texture/vn
+  encoders, stage 1 (14 layers), ray tokens, stage 2 (10 layers, Swin), DPT, HDR decode); with N > 1 ranks
+  the finished HDR frames are all-gathered to every rank over RCCL (xGMI) inside the timed region.
+* ``c4`` (BASELINE config 4; strong scaling): one step = 64 scenes, triangle counts cycling through the 16
+  example scenes (examples/*.json), assigned to ranks by longest-processing-time on the FLOP model
+  (parallel.assign_units), frames all-gathered.
+* ``c5`` (BASELINE config 5's shape; strong scaling): one step = ONE scene with ``--views`` views (default 24)
+  at ``--res`` (default 1024), the views split across ranks (parallel.shard_views; stage 1 recomputed on each
+  rank), frames all-gathered.
+
+Multi-GPU: one process per GPU.  Under ``torch.distributed.run`` the env (RANK/WORLD_SIZE/...) is read and
+``--gpus`` must equal WORLD_SIZE; run directly with ``--gpus N > 1`` this script starts
+``torch.distributed.run --nproc-per-node N`` itself (before any GPU call) and exits with its status.
+
+The JSON line carries a roofline object for the dominant kernel (stage-1 attention), timed with HIP events
+around each of its launches in the last timed step, the parity of the last GPU frame against the reference
+(the committed reference-generated fixture when the workload is that fixture's, and the oracle frame of the
+CPU baseline), and the CPU baseline itself: the oracle restatement of the reference (oracle/rf_ref.py,
+PyTorch CPU fp32) on a bounded sample of the same workload, rank 0 at N = 1 only.
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "rendered frames/sec at 512×512, renderformer-v1.1-swin-large, 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
 DOMINANT = "attn_stage1"   # largest single kernel family by time in the rocprof summary (profiles/)
+FIXTURE = ("large", 5633, 512, 1, 1, 1)  # tests/golden/large_cbox_r512.npz: config, N, res, views, scenes, seed
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=["cbox", "c4", "c5"], default="cbox")
     ap.add_argument("--config", default="large")
     ap.add_argument("--tris", type=int, default=5633)
-    ap.add_argument("--res", type=int, default=512)
-    ap.add_argument("--views", type=int, default=1)
-    ap.add_argument("--scenes", type=int, default=1, help="scenes per rank per step")
+    ap.add_argument("--res", type=int, default=None, help="default 512 (1024 for c5)")
+    ap.add_argument("--views", type=int, default=None, help="default 1 (24 for c5)")
+    ap.add_argument("--scenes", type=int, default=1, help="cbox: scenes per rank per step; c4: scenes per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=2)
+    ap.add_argument("--cpu-frames", type=int, default=3)
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no cpu baseline)")
-    return ap.parse_args()
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo: CPU-side tests)")
+    ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (1-GPU rehearsal)")
+    ap.add_argument("--dump", default=None, help="rank 0 saves the gathered frames of the last step (.npy)")
+    a = ap.parse_args(argv)
+    if a.res is None:
+        a.res = 1024 if a.workload == "c5" else 512
+    if a.views is None:
+        a.views = 24 if a.workload == "c5" else 1
+    if a.workload == "c4" and a.scenes == 1:
+        a.scenes = 64
+    return a
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """--gpus N > 1 without a torch.distributed.run environment: start one process per GPU as a child
+    (this process has not touched the GPU) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(cfg, sd, batch, res, frames):
-    """Reference CPU path (oracle restatement, fp32) on this host's cores: median of `frames` after 1 warm-up."""
+    """Reference CPU path (oracle restatement, fp32) on this host's cores: median of `frames` after 1 warm-up,
+    with the per-stage split of the same frames.  Returns (record, last oracle frame)."""
     from oracle import rf_ref
     threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     try:  # honour a cgroup CPU quota (the GPU box exposes 256 CPUs but grants 16)
@@ -63,60 +111,126 @@ def cpu_baseline(cfg, sd, batch, res, frames):
     except Exception:
         pass
     torch.set_num_threads(threads)
-    times = []
+    times, splits, out = [], [], None
     for i in range(frames + 1):
         tex = batch["texture"].clone()
+        rf_ref.STAMPS = st = {}
         t0 = time.perf_counter()
-        rf_ref.render(sd, cfg, batch["triangles"], tex, batch["mask"], batch["vn"], batch["c2w"], batch["fov"], res)
+        out = rf_ref.render(sd, cfg, batch["triangles"], tex, batch["mask"], batch["vn"], batch["c2w"], batch["fov"],
+                            res)
+        t1 = time.perf_counter()
+        rf_ref.STAMPS = None
         if i > 0:
-            times.append(time.perf_counter() - t0)
+            times.append(t1 - t0)
+            splits.append({"prologue+stage1": st["stage1_end"] - t0, "stage2": st["stage2_end"] - st["stage1_end"],
+                           "dpt+decode": t1 - st["stage2_end"]})
     t = statistics.median(times)
-    return {"value": round(1.0 / t, 5), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{frames} frame(s) of the same workload (median after 1 warm-up), oracle/rf_ref.py fp32, "
-                      f"torch {torch.__version__}, {threads} threads", "s_per_frame": round(t, 3)}
+    split = {k: round(statistics.median(s[k] for s in splits), 3) for k in splits[0]}
+    n_frames = int(batch["c2w"].shape[0] * batch["c2w"].shape[1])
+    rec = {"value": round(n_frames / t, 5), "unit": "frames/s", "cores": threads, "kind": "port",
+           "sample": f"{frames} render(s) of the same workload ({n_frames} frame(s) each; median after 1 warm-up), "
+                     f"oracle/rf_ref.py fp32, torch {torch.__version__}, {threads} threads",
+           "cpu_model": cpu_model(), "s_per_frame": round(t / n_frames, 3), "s_per_stage": split}
+    return rec, out
+
+
+def fixture_parity(args, frame):
+    """rel L2 of the GPU frame against the reference-generated fixture when the workload is the fixture's."""
+    if (args.config, args.tris, args.res, args.views, args.scenes, 1) != FIXTURE or args.workload != "cbox":
+        return None
+    path = os.path.join(REPO, "tests", "golden", "large_cbox_r512.npz")
+    if not os.path.exists(path):
+        return None
+    import numpy as np
+    ref = torch.from_numpy(np.load(path)["hdr"]).double()
+    got = frame.detach().double().cpu().reshape(ref.shape)
+    return float((got - ref).norm() / ref.norm())
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args)
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    dev_index = 0 if args.same_device else local
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     from renderformer_amd import RenderFormer, RenderFormerRenderingPipeline, ops
     from renderformer_amd.config import named_config
     from renderformer_amd.flops import frame_flops
-    from renderformer_amd.parallel import max_over_ranks
-    from renderformer_amd.scenes import batch_scenes, synthetic_scene
+    from renderformer_amd.parallel import assign_units, gather_frames, max_over_ranks, scene_cost, shard_views
+    from renderformer_amd.scenes import EXAMPLE_SCENE_TRIS, batch_scenes, synthetic_scene
     from renderformer_amd.weights import synthetic_state_dict
 
     cfg = named_config(args.config)
     sd = synthetic_state_dict(cfg, seed=0)
     pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd)).to(dev)
-    scenes = [synthetic_scene(args.tris, args.views, seed=1 + rank * args.scenes + i) for i in range(args.scenes)]
-    host = batch_scenes(scenes)
-    batch = {k: v.to(dev) for k, v in host.items() if k != "tex_channels"}
-    tex0 = batch["texture"][:, :, -3:].clone()
+
+    # ---- the units of one step: (batch tensors on the device, global frame ids)
+    if args.workload == "cbox":
+        scenes = [synthetic_scene(args.tris, args.views, seed=1 + rank * args.scenes + i) for i in range(args.scenes)]
+        hosts = [batch_scenes(scenes)]
+        n_per_rank = args.scenes * args.views
+        ids = [list(range(rank * n_per_rank, (rank + 1) * n_per_rank))]
+        n_frames_step = n_per_rank * world
+        scaling = "weak"
+    elif args.workload == "c4":
+        counts = [EXAMPLE_SCENE_TRIS[i % len(EXAMPLE_SCENE_TRIS)] for i in range(args.scenes)]
+        costs = [scene_cost(cfg, n, args.views, args.res) for n in counts]
+        mine = assign_units(costs, world)[rank]
+        hosts = [batch_scenes([synthetic_scene(counts[i], args.views, seed=100 + i)]) for i in mine]
+        ids = [[i * args.views + v for v in range(args.views)] for i in mine]
+        n_frames_step = args.scenes * args.views
+        scaling = "strong"
+    else:  # c5
+        sc = synthetic_scene(args.tris, args.views, seed=1)
+        vr = shard_views(args.views, world)[rank]
+        sc.c2w, sc.fov = sc.c2w[vr.start:vr.stop], sc.fov[vr.start:vr.stop]
+        hosts = [batch_scenes([sc])] if len(vr) else []
+        ids = [list(vr)] if len(vr) else []
+        n_frames_step = args.views
+        scaling = "strong"
+    batches = [{k: v.to(dev) for k, v in h.items() if k != "tex_channels"} for h in hosts]
+    tex0 = [b["texture"][:, :, -3:].clone() for b in batches]
     # the pipeline log-encodes the 3 emission channels in place (reference semantics): every step gets a
     # fresh input texture staged in HBM before the timed region (or, past 32 GiB of copies, the emission
-    # channels are restored inside the step)
+    # channels are restored inside the step, which is then timed with that copy)
     n_in = args.warmup + args.steps
-    staged = ([batch["texture"].clone() for _ in range(n_in)]
-              if n_in * batch["texture"].numel() * 4 <= (32 << 30) else None)
+    tex_bytes = sum(b["texture"].numel() * 4 for b in batches)
+    staged = ([[b["texture"].clone() for b in batches] for _ in range(n_in)] if n_in * tex_bytes <= (32 << 30)
+              else None)
     calls = [0]
+    chans = 4 if cfg.include_alpha else 3
+    frame_shape = (args.res, args.res, chans)
 
     def step():
-        if staged is not None:
-            tex = staged[calls[0] % n_in]
-        else:
-            tex = batch["texture"]
-            tex[:, :, -3:].copy_(tex0)
+        frames = []
+        for j, b in enumerate(batches):
+            if staged is not None:
+                tex = staged[calls[0] % n_in][j]
+            else:
+                tex = b["texture"]
+                tex[:, :, -3:].copy_(tex0[j])
+            out = pipe(b["triangles"], tex, b["mask"], b["vn"], b["c2w"], b["fov"], resolution=args.res,
+                       torch_dtype=torch.bfloat16)
+            frames.append(out.reshape(-1, *frame_shape))
         calls[0] += 1
-        return pipe(batch["triangles"], tex, batch["mask"], batch["vn"], batch["c2w"], batch["fov"],
-                    resolution=args.res, torch_dtype=torch.bfloat16)
+        local = torch.cat(frames) if frames else torch.empty((0,) + frame_shape, device=dev)
+        if world > 1:  # finished frames to every rank (RCCL all_gather over xGMI)
+            return gather_frames(local, [i for u in ids for i in u], n_frames_step)
+        return local
 
     for _ in range(args.warmup):
         step()
@@ -139,69 +253,98 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ops.TIMER = None
-    elapsed = max_over_ranks(elapsed, device=dev)
+    elapsed = max_over_ranks(elapsed, device=dev if args.backend == "nccl" else None)
     if not torch.isfinite(out).all():
         raise RuntimeError("non-finite output")
 
-    frames_per_step = args.scenes * args.views
-    total_frames = frames_per_step * args.steps * world
+    total_frames = n_frames_step * args.steps
     fps = total_frames / elapsed
-    fl = frame_flops(cfg, args.tris, args.res, args.views)
+    if args.workload == "cbox":
+        fl_frame = frame_flops(cfg, args.tris, args.res, args.views)["total"] / args.views
+        fl_step = fl_frame * n_frames_step
+    elif args.workload == "c4":
+        fl_step = sum(frame_flops(cfg, EXAMPLE_SCENE_TRIS[i % len(EXAMPLE_SCENE_TRIS)], args.res, args.views)["total"]
+                      for i in range(args.scenes))
+    else:
+        fl_step = frame_flops(cfg, args.tris, args.res, args.views)["total"] * world  # stage 1 on every rank
     durs = timer.durations_ms()
     per_step_launches = len(durs)  # one timed step
     kern_ms = statistics.mean(durs) if durs else float("nan")
-    s_len = args.tris + cfg.num_register_tokens
-    kern_flops = 4 * s_len * s_len * cfg.latent_dim * args.scenes  # QK^T + PV per launch (all heads, all scenes)
-    achieved = kern_flops / (kern_ms * 1e-3) / 1e12
+    s_len = (args.tris if args.workload != "c4" else EXAMPLE_SCENE_TRIS[0]) + cfg.num_register_tokens
+    scenes_per_launch = args.scenes if args.workload == "cbox" else 1
+    kern_flops = 4 * s_len * s_len * cfg.latent_dim * scenes_per_launch  # QK^T + PV per launch
+    if args.workload == "c4":  # launches differ in S: use the mean algorithmic FLOP of this rank's scenes
+        ss = [int(b["mask"].sum()) + cfg.num_register_tokens for b in batches]
+        kern_flops = 4 * cfg.latent_dim * statistics.mean(s * s for s in ss) if ss else 0
+    achieved = kern_flops / (kern_ms * 1e-3) / 1e12 if durs else float("nan")
     traffic = None
     tpath = os.path.join(REPO, "profiles", "attn_stage1_traffic.json")
-    if os.path.exists(tpath):
+    if os.path.exists(tpath) and args.workload == "cbox" and args.scenes == 1:
         try:
             traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
             traffic = None if traffic is None else int(traffic)
         except Exception:
             traffic = None
 
+    if args.dump and rank == 0:
+        import numpy as np
+        np.save(args.dump, out.cpu().numpy())
     if rank == 0:
+        wl = {"cbox": f"cbox-sized scene N={args.tris}, {args.res}x{args.res}, {args.views} view(s) x {args.scenes} "
+                      f"scene(s) per rank per step",
+              "c4": f"{args.scenes} scenes per step (N cycling through the 16 example scenes' counts), {args.res}x"
+                    f"{args.res}, {args.views} view(s) each, LPT-sharded over ranks",
+              "c5": f"one scene N={args.tris}, {args.views} views at {args.res}x{args.res} per step, views split "
+                    f"over ranks (stage 1 on every rank)"}[args.workload]
         rec = {
             "metric": METRIC, "value": round(fps, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "scaling": scaling, "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {
-                "workload": f"{'large-proxy' if args.config == 'large' else args.config} cbox-sized scene N={args.tris}, {args.res}x{args.res}, "
-                            f"{args.views} view(s) x {args.scenes} scene(s) per rank per step",
+                "workload": f"{'large-proxy' if args.config == 'large' else args.config} {wl}",
                 "model": "renderformer-v1.1-swin-large" if args.config == "large" else args.config,
                 "model_shape": f"D={cfg.latent_dim} H={cfg.num_heads} L1={cfg.num_layers} "
                                f"L2={cfg.view_transformer_n_layers} F={cfg.dim_feedforward} swin="
                                f"{cfg.view_transformer_use_swin_attn} dpt={cfg.dpt_features}/{cfg.dpt_out_channels}",
-                "global_batch": frames_per_step * world, "seq_len": s_len, "res": args.res,
-                "parallelism": f"dp{world}", "weights": "synthetic seed 0 (no checkpoint offline)",
+                "global_batch": n_frames_step, "seq_len": s_len, "res": args.res,
+                "parallelism": f"dp{world}" + ("" if args.workload != "c5" else " (views)"),
+                "gather": "RCCL all_gather of the HDR frames" if world > 1 and args.backend == "nccl" else
+                          (f"{args.backend} all_gather" if world > 1 else "none (1 rank)"),
+                "weights": "synthetic seed 0 (no checkpoint offline)",
                 "precision": "bf16 MFMA operands, fp32 accumulate/softmax/residual; DPT fp16 operands, fp32 accumulate",
             },
             "frame": {
-                "gflop_per_frame": round(fl["total"] / args.views / 1e9, 1),
-                "tflops_effective": round(fl["total"] / args.views * fps / world / 1e12, 1),
-                "mfma_frac_bf16_peak": round(fl["total"] / args.views * fps / world / 1e12 / PEAK_BF16_TFLOPS, 4),
+                "gflop_per_step": round(fl_step / 1e9, 1),
+                "tflops_effective": round(fl_step * args.steps / elapsed / world / 1e12, 1),
+                "mfma_frac_bf16_peak": round(fl_step * args.steps / elapsed / world / 1e12 / PEAK_BF16_TFLOPS, 4),
             },
             "roofline": {
                 "kernel": "rf_attn_fwd — stage-1 triangle self-attention (attn_sk_kernel: stream-K, in-kernel merge)",
                 "bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                "traffic_source": "profiles/attn_stage1_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE pass)"
+                if traffic is not None else None,
                 "avg_launch_ms": round(kern_ms, 4), "launches_per_step": per_step_launches,
                 "algorithmic_flop_per_launch": kern_flops,
                 # Q, K, V read once + O written once (bf16); traffic above this = K/V re-reads + split partials
-                "algorithmic_bytes_per_launch": 4 * s_len * cfg.latent_dim * 2 * args.scenes,
+                "algorithmic_bytes_per_launch": 4 * s_len * cfg.latent_dim * 2 * scenes_per_launch,
             },
+            "parity": {"vs_reference_fixture_rel_l2": None, "vs_oracle_rel_l2": None},
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu_baseline and not args.profile:
-            cpu_batch = {k: v for k, v in host.items() if k != "tex_channels"}
-            sd_cpu = sd
-            rec["cpu_baseline"] = cpu_baseline(cfg, sd_cpu, cpu_batch, args.res, args.cpu_frames)
+        if args.workload == "cbox":
+            fp = fixture_parity(args, out[:n_per_rank])
+            rec["parity"]["vs_reference_fixture_rel_l2"] = None if fp is None else float(f"{fp:.3e}")
+        if world == 1 and args.workload == "cbox" and not args.no_cpu_baseline and not args.profile:
+            cpu_batch = {k: v for k, v in hosts[0].items() if k != "tex_channels"}
+            rec["cpu_baseline"], ref = cpu_baseline(cfg, sd, cpu_batch, args.res, args.cpu_frames)
+            got = out.detach().double().cpu().reshape(ref.shape)
+            rec["parity"]["vs_oracle_rel_l2"] = float(f"{float((got - ref.double()).norm() / ref.double().norm()):.3e}")
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

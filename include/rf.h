@@ -53,8 +53,9 @@ extern "C" {
 #define RF_ERR_INVALID 1
 #define RF_ERR_LAUNCH 2
 #define RF_ERR_UNSUPPORTED 3
+#define RF_ERR_DEVICE 4       /* an earlier launch reported a device-side error (see rf_device_error) */
 
-#define RF_ABI_VERSION 5
+#define RF_ABI_VERSION 6
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -65,6 +66,15 @@ extern "C" {
 
 const char* rf_last_error(void);
 int rf_abi_version(void);
+
+/* Device-side error word.  A stream-K owner (GEMM or attention) whose partner's partial does not arrive within
+ * the spin bound (env RF_SPIN_LIMIT polls, default 2^24) stores a non-zero code into a host-mapped word instead
+ * of failing silently; from then on every entry point returns RF_ERR_DEVICE (checked without a device sync)
+ * until rf_clear_device_error(); the outputs of the reporting launch are invalid and the stream-K workspaces
+ * must be re-zeroed.  rf_debug_raise_device_error launches a kernel that stores `code` (tests). */
+int rf_device_error(void);
+int rf_clear_device_error(void);
+int rf_debug_raise_device_error(int code, void* stream);
 
 /* workspace / ws_bytes of the GEMM and convolution entry points: optional (NULL = one block per
  * output tile), rf_gemm_workspace_bytes() bytes, zero-filled once when allocated, used by one stream at a

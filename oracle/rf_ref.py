@@ -296,7 +296,9 @@ def view_transformer(sd, cfg, cam_o, rays_d, tri_tokens, tri_pos, mask, taps: Op
             taps[f"dec{i}"] = x
         if i in out_layers:
             feats.append(x)
+    _stamp("stage2_end")
     img = dpt_head(sd, vt + ".out_dpt", feats, hp, wp, pt)
+    _stamp("dpt_end")
     if taps is not None:
         taps["dpt"] = img
     return F.elu(img, alpha=1e-3)
@@ -304,10 +306,12 @@ def view_transformer(sd, cfg, cam_o, rays_d, tri_tokens, tri_pos, mask, taps: Op
 
 def model_forward(sd, cfg, tri_pos, tex, mask, vns, rays_o, rays_d, tri_pos_view, taps=None):
     """renderformer.py:171-206."""
+    _stamp("start")
     seq, mask_p, pos = construct_seq(sd, cfg, tri_pos, tex, mask, vns)
     if taps is not None:
         taps["seq0"] = seq
     seq = encoder(sd, cfg, seq, mask_p, pos, taps)
+    _stamp("stage1_end")
     b, v = rays_o.shape[:2]
     seq = seq.repeat_interleave(v, dim=0)
     rays_o = rays_o.reshape(-1, *rays_o.shape[2:])
@@ -321,6 +325,15 @@ def model_forward(sd, cfg, tri_pos, tex, mask, vns, rays_o, rays_d, tri_pos_view
 
 
 # ----------------------------------------------------------------------------- pipeline
+STAMPS: Optional[dict] = None  # bench.py's cpu_baseline sets a dict here to time the stages of one frame
+
+
+def _stamp(name: str) -> None:
+    if STAMPS is not None:
+        import time
+        STAMPS[name] = time.perf_counter()
+
+
 def cam_transform(c2w: Tensor, tris: Tensor) -> Tensor:
     """transform.py:7-27 via roma.Rigid: p_cam = R^T p + (-R^T t)."""
     r = c2w[..., :3, :3]

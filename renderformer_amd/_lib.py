@@ -49,7 +49,11 @@ SIGNATURES = {
     "rf_deconv2d_f16": [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P, _I, _P, _L, _P],
     "rf_split_planes": [_P, _L, _I, _L, _P, _P, _I, _I, _P],
     "rf_upsample_bilinear": [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _I, _P],
+    "rf_device_error": [],
+    "rf_clear_device_error": [],
+    "rf_debug_raise_device_error": [_I, _P],
 }
+RF_ERR_DEVICE = 4
 
 _lock = threading.Lock()
 _lib = None
@@ -57,6 +61,11 @@ _lib = None
 
 class HipLibraryError(RuntimeError):
     pass
+
+
+class DeviceError(RuntimeError):
+    """A kernel reported a device-side failure (a stream-K hand-off that timed out): the outputs of that launch
+    are invalid; rf_clear_device_error() + fresh workspaces recover."""
 
 
 def load(require_device: bool = True):
@@ -92,6 +101,8 @@ def call(name: str, *args) -> None:
         msg = lib.rf_last_error().decode(errors="replace")
         if rc == 1:
             raise ValueError(msg)
+        if rc == RF_ERR_DEVICE:
+            raise DeviceError(f"{name}: {msg}")
         raise RuntimeError(f"{name} failed ({rc}): {msg}")
 
 
@@ -99,5 +110,7 @@ def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
 
 
-def stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+def stream(device=None) -> int:
+    """Current stream of `device` (default: the current device; the model wraps every render in a
+    torch.cuda.device guard for its own device, so its launches never land on another device's stream)."""
+    return torch.cuda.current_stream(device).cuda_stream

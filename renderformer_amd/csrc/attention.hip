@@ -71,6 +71,8 @@ struct AttnArgs {
     int n_problems;
     int* flag;
     float thr;  // deferred-rescale threshold (log2 units; RF_ATTN_THR, default 8)
+    int* err;   // device error word (rf::device_error_word): stream-K hand-off timeouts
+    int spin;   // stream-K hand-off spin bound (polls)
 };
 
 RF_DEV int swz_off(int row, int ch) { return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4); }
@@ -1111,8 +1113,9 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 if (tid == 0) {
                     int spins = 0;
                     while (__hip_atomic_load(p.flag + cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1 &&
-                           ++spins < (1 << 24))
+                           ++spins < p.spin)
                         __builtin_amdgcn_s_sleep(1);
+                    if (spins >= p.spin) report_device_error(p.err, RF_DEVERR_SK_ATTN);  // never silent
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __hip_atomic_store(p.flag + cw, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
@@ -1248,6 +1251,8 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
     a.part_o = (float*)workspace;
     a.flag = (int*)(a.part_o + (int64_t)SK5_MAX_GRID * PIECE_FLOATS);
     a.thr = getenv("RF_ATTN_THR") ? (float)atof(getenv("RF_ATTN_THR")) : SUM_THR_LOG2;
+    a.err = rf::device_error_word();
+    a.spin = rf::spin_limit();
     // q pre-scaled by scale*log2(e) upstream (scale = ln 2): scores are already exp2 exponents
     const bool unit = fabsf(a.c - 1.0f) < 1e-6f;
     const int dbg = getenv("RF_ATTN_DBG") ? atoi(getenv("RF_ATTN_DBG")) : 0;

@@ -2,8 +2,12 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 
-#include "../../include/rf.h"
+#include <mutex>
+
+#include "common.h"
 
 namespace rf {
 static thread_local char g_err[512] = "";
@@ -15,15 +19,78 @@ void set_error(const char* fmt, ...) {
     va_end(ap);
 }
 
+// one mapped, portable host word for the process: kernels on any device store error codes into it, the host
+// reads it with a plain load (no device sync)
+static volatile int* g_dev_err_host = nullptr;
+static int* g_dev_err_dev = nullptr;
+static std::once_flag g_dev_err_once;
+
+int* device_error_word() {
+    std::call_once(g_dev_err_once, [] {
+        void* h = nullptr;
+        if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess)
+            return;
+        memset(h, 0, 64);
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return;
+        g_dev_err_host = (volatile int*)h;
+        g_dev_err_dev = (int*)d;
+    });
+    return g_dev_err_dev;
+}
+
+int spin_limit() {
+    static const int lim = [] {
+        const char* e = getenv("RF_SPIN_LIMIT");
+        return e ? atoi(e) : (1 << 24);
+    }();
+    return lim;
+}
+
 int check_launch(const char* what) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("%s: launch failed: %s", what, hipGetErrorString(e));
         return RF_ERR_LAUNCH;
     }
+    if (g_dev_err_host && *g_dev_err_host != 0) {
+        set_error("%s: an earlier launch reported device error %d (%s); its outputs are invalid and the stream-K "
+                  "workspaces must be re-zeroed (rf_clear_device_error)", what, *g_dev_err_host,
+                  *g_dev_err_host == RF_DEVERR_SK_GEMM ? "GEMM stream-K partial not published within the spin bound"
+                  : *g_dev_err_host == RF_DEVERR_SK_ATTN ? "attention stream-K partial not published within the spin "
+                                                            "bound" : "debug");
+        return RF_ERR_DEVICE;
+    }
     return RF_OK;
 }
+
+__global__ void raise_error_kernel(int* err, int code) {
+    if (threadIdx.x == 0) report_device_error(err, code);
+}
 }  // namespace rf
+
+extern "C" int rf_device_error(void) {
+    rf::device_error_word();
+    return rf::g_dev_err_host ? *rf::g_dev_err_host : 0;
+}
+
+extern "C" int rf_clear_device_error(void) {
+    rf::device_error_word();
+    if (rf::g_dev_err_host) *rf::g_dev_err_host = 0;
+    return RF_OK;
+}
+
+extern "C" int rf_debug_raise_device_error(int code, void* stream) {
+    int* w = rf::device_error_word();
+    RF_REQUIRE(w, "rf_debug_raise_device_error: no mapped error word");
+    hipLaunchKernelGGL(rf::raise_error_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, w, code);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        rf::set_error("rf_debug_raise_device_error: launch failed: %s", hipGetErrorString(e));
+        return RF_ERR_LAUNCH;
+    }
+    return RF_OK;
+}
 
 extern "C" const char* rf_last_error(void) { return rf::g_err; }
 extern "C" int rf_abi_version(void) { return RF_ABI_VERSION; }

@@ -63,10 +63,21 @@ RF_DEV float silu(float x) {
 // 114 -> 186 us at the 256^2 DPT level), which costs far more than the epilogue saves.
 RF_DEV float silu_precise(float x) { return x / (1.0f + expf(-x)); }
 
+// Device-side error word (host-pinned, mapped): a stream-K owner whose partial never arrived within the
+// spin bound stores a code here instead of failing silently; every later entry point returns
+// RF_ERR_DEVICE until rf_clear_device_error().  A vector (per-lane address) system-scope store.
+RF_DEV void report_device_error(int* err, int code) {
+    if (err) __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#define RF_DEVERR_SK_GEMM 1
+#define RF_DEVERR_SK_ATTN 2
+
 // ------------------------------------------------------------------------- host side
 namespace rf {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+int* device_error_word();  // device pointer of the mapped error word (nullptr if it could not be allocated)
+int spin_limit();          // stream-K hand-off spin bound (RF_SPIN_LIMIT, default 2^24 polls)
 }  // namespace rf
 
 #define RF_REQUIRE(cond, ...)                          \

@@ -83,6 +83,8 @@ struct EngineArgs {
     int group_m;  // tile raster: groups of group_m m-tiles, n fastest within a group (host-chosen)
     const int* gate;  // optional device flag: the launch is a no-op unless *gate != 0 (rf_gemm_bf16_if)
     int halo_lg;      // halo-tiled 3x3 convolution: log2 of the tile width in pixels (halo_kernel)
+    int* err;         // device error word (rf::device_error_word): stream-K hand-off timeouts
+    int spin;         // stream-K hand-off spin bound (polls)
 };
 
 // uniform early exit of a gated launch (every block reads the same flag, so a stream-K grid exits whole)
@@ -814,8 +816,9 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
                     if (threadIdx.x == 0) {
                         int spins = 0;
                         while (__hip_atomic_load(p.sk_flag + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.sk_epoch &&
-                               ++spins < (1 << 24))
+                               ++spins < p.spin)
                             __builtin_amdgcn_s_sleep(1);
+                        if (spins >= p.spin) report_device_error(p.err, RF_DEVERR_SK_GEMM);  // never silent
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     }
@@ -901,8 +904,9 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
                         if (threadIdx.x == 0) {
                             int spins = 0;
                             while (__hip_atomic_load(p.sk_flag + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.sk_epoch &&
-                                   ++spins < (1 << 24))
+                                   ++spins < p.spin)
                                 __builtin_amdgcn_s_sleep(1);
+                            if (spins >= p.spin) report_device_error(p.err, RF_DEVERR_SK_GEMM);  // never silent
                             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // ONE acquire after the match
                             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         }
@@ -1172,6 +1176,8 @@ void sk_setup(EngineArgs& p, void* workspace) {
     p.sk_part = (float*)workspace;
     p.sk_flag = (int*)(p.sk_part + SK_PART_FLOATS);
     p.sk_epoch = ++g_sk_epoch;
+    p.err = rf::device_error_word();
+    p.spin = rf::spin_limit();
 }
 
 

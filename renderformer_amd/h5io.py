@@ -563,12 +563,13 @@ class _Writer:
 SCENE_KEYS = ("triangles", "vn", "texture", "c2w", "fov")
 
 
-def write_scene(path: str, triangles, vn, texture, c2w, fov) -> None:
-    """The datasets and dtypes of `scene_processor/to_h5.py:87-92` (gzip level 9)."""
+def write_scene(path: str, triangles, vn, texture, c2w, fov, texture_dtype=np.float16) -> None:
+    """The datasets and dtypes of `scene_processor/to_h5.py:87-92` (gzip level 9); texture_dtype=np.float32
+    writes the texture as other producers may (the readers keep whatever dtype the file holds)."""
     write_datasets(path, {
         "triangles": np.asarray(triangles, dtype=np.float32),
         "vn": np.asarray(vn, dtype=np.float32),
-        "texture": np.asarray(texture, dtype=np.float16),
+        "texture": np.asarray(texture, dtype=texture_dtype),
         "c2w": np.asarray(c2w, dtype=np.float32),
         "fov": np.asarray(fov, dtype=np.float32),
     })

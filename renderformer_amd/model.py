@@ -205,6 +205,26 @@ def _build_plan(mask: torch.Tensor, V: int, res: int, patch: int, n_reg: int, de
                  prob1=dev(prob1).view(-1, 5), prob2=dev(prob2).view(-1, 5), prob_self=dev(prob_self).view(-1, 5))
 
 
+def _hf_cache_snapshot(model_id: str) -> Optional[str]:
+    """Newest snapshot directory of a hub model id in the local Hugging Face cache that holds config.json and
+    model.safetensors (the files PyTorchModelHubMixin downloads), or None."""
+    if "/" not in model_id:
+        return None
+    roots = [os.environ.get("HF_HUB_CACHE"), os.environ.get("HUGGINGFACE_HUB_CACHE"),
+             os.path.join(os.environ["HF_HOME"], "hub") if os.environ.get("HF_HOME") else None,
+             os.path.join(os.path.expanduser("~"), ".cache", "huggingface", "hub")]
+    name = "models--" + model_id.replace("/", "--")
+    for root in roots:
+        base = os.path.join(root, name, "snapshots") if root else None
+        if not base or not os.path.isdir(base):
+            continue
+        snaps = sorted((os.path.join(base, d) for d in os.listdir(base)), key=os.path.getmtime, reverse=True)
+        for d in snaps:
+            if os.path.exists(os.path.join(d, "config.json")) and os.path.exists(os.path.join(d, "model.safetensors")):
+                return d
+    return None
+
+
 class RenderFormer:
     """Drop-in for renderformer.models.renderformer.RenderFormer (inference only)."""
 
@@ -235,12 +255,18 @@ class RenderFormer:
     @classmethod
     def from_pretrained(cls, model_id: str, synthetic_seed: Optional[int] = None, dpt_precision: Optional[str] = None,
                         **_):
-        """Local snapshot dir (config.json + model.safetensors) or, with synthetic_seed, a named config
-        with deterministic random weights.  Remote hub downloads are not supported (no network)."""
-        if os.path.isdir(model_id):
-            return cls(named_config(model_id), load_snapshot(model_id), dpt_precision=dpt_precision)
+        """PyTorchModelHubMixin.from_pretrained (renderformer.py:13) without the network: ``model_id`` is a local
+        snapshot directory (config.json + model.safetensors), or a hub id ("microsoft/renderformer-v1.1-swin-
+        large") found in the local Hugging Face cache; with ``synthetic_seed`` (or env RF_SYNTHETIC_SEED) a hub
+        id or architecture name that is not cached gets deterministic random weights of that architecture."""
+        snap = model_id if os.path.isdir(model_id) else _hf_cache_snapshot(model_id)
+        if snap is not None:
+            return cls(named_config(snap), load_snapshot(snap), dpt_precision=dpt_precision)
+        if synthetic_seed is None and os.environ.get("RF_SYNTHETIC_SEED"):
+            synthetic_seed = int(os.environ["RF_SYNTHETIC_SEED"])
         if synthetic_seed is None:
-            raise FileNotFoundError(f"{model_id!r} is not a local snapshot directory; pass synthetic_seed= for "
+            raise FileNotFoundError(f"{model_id!r} is neither a local snapshot directory nor in the local Hugging Face "
+                                    "cache (no network here); pass synthetic_seed= (or set RF_SYNTHETIC_SEED) for "
                                     "random-init weights of the named architecture")
         return cls(named_config(model_id), seed=synthetic_seed, dpt_precision=dpt_precision)
 
@@ -248,7 +274,8 @@ class RenderFormer:
         check_state_dict(self.config, sd, strict=strict)
         self._sd = {k: v.detach().float().cpu() for k, v in sd.items()}
         if self._w is not None:
-            self._w = _DeviceWeights(self.config, self._sd, self._device, self.dpt_precision)
+            with torch.cuda.device(self._device):
+                self._w = _DeviceWeights(self.config, self._sd, self._device, self.dpt_precision)
         return self
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
@@ -265,7 +292,8 @@ class RenderFormer:
         if device.index is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self._device = device
-        self._w = _DeviceWeights(self.config, self._sd, device, self.dpt_precision)
+        with torch.cuda.device(device):
+            self._w = _DeviceWeights(self.config, self._sd, device, self.dpt_precision)
         return self
 
     cuda = lambda self, i=None: self.to("cuda" if i is None else f"cuda:{i}")  # noqa: E731
@@ -453,8 +481,15 @@ class RenderFormer:
     def render_views(self, triangles, texture, mask, vn, c2w, fov, resolution: int, log_encode: bool = True,
                      timings: Optional[dict] = None) -> torch.Tensor:
         """Pipeline fast path: rays, camera transform and positions are generated on the device.
-        Returns [B, V, res, res, C] linear HDR (log-decoded unless use_ldr)."""
+        Returns [B, V, res, res, C] linear HDR (log-decoded unless use_ldr).
+
+        Every launch goes to the current stream of the MODEL's device, whatever device is current in the
+        caller (the reference's own infer.py places the model on cuda:1, infer.py:43)."""
         self._require()
+        with torch.cuda.device(self._device):
+            return self._render_views(triangles, texture, mask, vn, c2w, fov, resolution, log_encode)
+
+    def _render_views(self, triangles, texture, mask, vn, c2w, fov, resolution, log_encode):
         cfg, dev = self.config, self._device
         B, V = c2w.shape[:2]
         for t, n in ((triangles, "triangles"), (texture, "texture"), (mask, "mask"), (vn, "vn"), (c2w, "c2w"),
@@ -489,6 +524,10 @@ class RenderFormer:
                 tf32_view_tf=False):
         """Reference signature (renderformer.py:171-206).  Returns ELU'd log-space images [B, V, C, H, W]."""
         self._require()
+        with torch.cuda.device(self._device):
+            return self._forward(tri_vpos_list, texture_patch_list, valid_mask, vns, rays_o, rays_d, tri_vpos_view_tf)
+
+    def _forward(self, tri_vpos_list, texture_patch_list, valid_mask, vns, rays_o, rays_d, tri_vpos_view_tf):
         cfg, dev = self.config, self._device
         B, V = rays_o.shape[:2]
         res = rays_d.shape[2]

@@ -22,6 +22,7 @@ from __future__ import annotations
 import json
 import os
 import sys
+import time
 import warnings
 
 import numpy as np
@@ -36,10 +37,12 @@ warnings.filterwarnings("ignore")
 
 import torch  # noqa: E402
 
-from renderformer_amd.config import RenderFormerConfig  # noqa: E402
+from renderformer_amd.config import LARGE_PROXY, RenderFormerConfig  # noqa: E402
 from renderformer_amd.scenes import batch_scenes, synthetic_scene  # noqa: E402
 from renderformer_amd.weights import synthetic_state_dict  # noqa: E402
 
+LARGE = LARGE_PROXY.to_dict()
+BASE = {}
 TINY = dict(latent_dim=256, num_layers=2, num_heads=2, dim_feedforward=512, view_transformer_latent_dim=256,
             view_transformer_ffn_hidden_dim=512, view_transformer_n_heads=2, view_transformer_n_layers=4,
             dpt_features=32, dpt_out_channels=[16, 32, 64, 128])
@@ -56,7 +59,16 @@ CASES = {
                         dpt_out_channels=[128, 256, 512, 1024]), [100], None, 1, 64, 3, 14, False),
     "cbox_base": (dict(num_layers=2, view_transformer_n_layers=4, view_transformer_use_swin_attn=True),
                   [5633], None, 1, 64, 4, 15, False),
+    # BASELINE.json configs at their own sizes (full depth).  Weight seed 0 and scene seed 1 are bench.py's
+    # headline workload, so bench's frame can be checked against this fixture too.
+    "large_cbox_r512": (LARGE, [5633], None, 1, 512, 0, 1, False),       # config 2
+    "large_bunny_r512": (LARGE, [6209], None, 1, 512, 0, 2, False),      # config 3 (cbox-bunny N)
+    "base_cbox_r256": (BASE, [5633], None, 1, 256, 0, 3, False),         # config 1 shape (v1-base, full depth)
+    "large_cbox_r1024_v4": (LARGE, [5633], None, 4, 1024, 0, 4, False),  # config 5 shape, 4 views of 1 scene
 }
+# 1024^2 x 4 views is 50 MB of fp32 HDR: such fixtures keep every SUB-th pixel row and column (plus the
+# full-image sum and sum of squares), the GPU test compares the same sample
+HDR_SUB = {"large_cbox_r1024_v4": 4}
 
 
 def weight_checksums(sd):
@@ -79,9 +91,13 @@ def run_case(name, over, ntris, pad, nv, res, wseed, sseed, taps):
     scenes = [synthetic_scene(n, nv, seed=sseed + i) for i, n in enumerate(ntris)]
     batch = batch_scenes(scenes, padding_length=pad)
     tex = batch["texture"].clone()
+    t0 = time.time()
 
     got = {}
     hooks = []
+    if not taps:  # size-independent signature of stage 1 at production sequence length
+        hooks.append(model.transformer.register_forward_hook(
+            lambda m, a, o: got.__setitem__("enc_rownorm", o.norm(dim=-1).clone())))
     if taps:
         hooks.append(model.transformer.register_forward_pre_hook(lambda m, a: got.__setitem__("seq0", a[0].clone())))
         hooks.append(model.transformer.register_forward_hook(lambda m, a, o: got.__setitem__("enc_out", o.clone())))
@@ -103,22 +119,20 @@ def run_case(name, over, ntris, pad, nv, res, wseed, sseed, taps):
         triangles=batch["triangles"].numpy(), vn=batch["vn"].numpy(), tex_channels=batch["tex_channels"].numpy(),
         mask=batch["mask"].numpy(), c2w=batch["c2w"].numpy(), fov=batch["fov"].numpy(),
         texture_after_ch10=tex[:, :, 10, 0, 0].numpy(),
-        hdr=out.numpy().astype(np.float32),
     )
+    sub = HDR_SUB.get(name)
+    if sub:
+        o64 = out.double()
+        rec.update(hdr_sub=out[:, :, ::sub, ::sub].numpy().astype(np.float32), hdr_sub_stride=np.int64(sub),
+                   hdr_shape=np.array(out.shape), hdr_sum=np.float64(o64.sum()), hdr_sumsq=np.float64((o64 ** 2).sum()))
+    else:
+        rec["hdr"] = out.numpy().astype(np.float32)
     for k, v in got.items():
-        rec["tap_" + k] = v.numpy().astype(np.float32)
-    if not taps:
-        # size-independent signature of stage 1 at production sequence length
-        with torch.no_grad():
-            enc = {}
-            h = model.transformer.register_forward_hook(lambda m, a, o: enc.__setitem__("o", o))
-            pipe.render(batch["triangles"], batch["texture"].clone(), batch["mask"], batch["vn"], batch["c2w"],
-                        batch["fov"], resolution=res, torch_dtype=torch.float32)
-            h.remove()
-            rec["enc_rownorm"] = enc["o"].norm(dim=-1).numpy().astype(np.float32)
+        key = k if k == "enc_rownorm" else "tap_" + k
+        rec[key] = v.numpy().astype(np.float32)
     path = os.path.join(HERE, f"{name}.npz")
     np.savez_compressed(path, **rec)
-    print(f"{name}: hdr {tuple(out.shape)} range [{out.min():.3g}, {out.max():.3g}] -> {os.path.getsize(path)/1e6:.2f} MB")
+    print(f"{name}: {time.time() - t0:.1f} s, hdr {tuple(out.shape)} range [{out.min():.3g}, {out.max():.3g}] -> {os.path.getsize(path)/1e6:.2f} MB")
 
 
 def op_level():
@@ -155,7 +169,8 @@ def op_level():
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count() or 8)
     only = sys.argv[1:]
-    op_level()
+    if not only:
+        op_level()
     for name, args in CASES.items():
         if not only or name in only:
             run_case(name, *args)

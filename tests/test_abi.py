@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load(require_device=False)
     for fn in header_functions():
         assert hasattr(lib, fn), fn
-    assert lib.rf_abi_version() == 5
+    assert lib.rf_abi_version() == 6
     # every int-returning entry point has a ctypes signature in the binding
     assert set(_lib.SIGNATURES) == set(header_functions()) - {"rf_last_error", "rf_abi_version",
                                                                "rf_attn_workspace_bytes", "rf_gemm_workspace_bytes"}
@@ -45,3 +45,22 @@ def test_invalid_arguments_raise_value_error_without_device():
     rc = lib.rf_attn_fwd(ctypes.c_void_p(16), 256, ctypes.c_void_p(16), 256, ctypes.c_void_p(16), 256,
                          ctypes.c_void_p(16), 256, ctypes.c_void_p(16), 1, 10, 2, 64, 1.0, 1, None, 0, None)
     assert rc == 1 and b"head_dim" in lib.rf_last_error()
+
+
+@pytest.mark.gpu
+def test_device_error_word_surfaces_on_next_call():
+    """A device-side error (here raised on purpose by a debug kernel; in production a stream-K owner whose
+    partner never published) makes the next entry point fail loudly, without a device sync, until cleared."""
+    import torch
+    from renderformer_amd import _lib, ops
+    lib = _lib.load()
+    assert lib.rf_device_error() == 0
+    _lib.call("rf_debug_raise_device_error", 7, _lib.stream())
+    torch.cuda.synchronize()
+    assert lib.rf_device_error() == 7
+    x = torch.randn(4, 256, device="cuda")
+    out = torch.empty(4, 256, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(_lib.DeviceError, match="device error 7"):
+        ops.rmsnorm(x, torch.ones(256, device="cuda"), 1e-6, out)
+    lib.rf_clear_device_error()
+    ops.rmsnorm(x, torch.ones(256, device="cuda"), 1e-6, out)  # clean again

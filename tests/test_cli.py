@@ -56,7 +56,7 @@ def test_cli_rejects_unavailable_tone_mapper(tmp_path):
         infer.main(["--h5_file", str(tmp_path / "x.h5"), "--tone_mapper", "agx", "--model_id", "x"])
 
 
-def _snapshot_and_scene(tmp_path):
+def _snapshot_and_scene(tmp_path, tex_dtype=np.float16):
     """tiny_swin golden: local snapshot dir (config.json + model.safetensors) + its scene 0 (valid triangles
     only; the reference output is padding-invariant) as an HDF5 file."""
     from safetensors.torch import save_file
@@ -69,8 +69,8 @@ def _snapshot_and_scene(tmp_path):
     h5 = tmp_path / "scenes" / "tiny.h5"
     h5.parent.mkdir()
     h5io.write_scene(str(h5), inp["triangles"][0].numpy()[m], inp["vn"][0].numpy()[m],
-                     inp["texture"][0].numpy()[m].astype(np.float16), inp["c2w"][0].numpy(),
-                     inp["fov"][0].numpy().reshape(-1))
+                     inp["texture"][0].numpy()[m].astype(tex_dtype), inp["c2w"][0].numpy(),
+                     inp["fov"][0].numpy().reshape(-1), texture_dtype=tex_dtype)
     return snap, h5, res, z
 
 
@@ -104,12 +104,29 @@ def test_batch_infer_cli(tmp_path):
     assert rel_l2(a, z["hdr"][0, 0]) < 1e-3
 
 
-@pytest.mark.gpu
-def test_batch_infer_pipelined_matches_inline(tmp_path, monkeypatch):
-    """The pipelined data path (loader thread, pinned H2D/D2H side streams) writes the same images as the
-    inline loop, over several batches (3 scenes, batch size 1: every overlap case)."""
+def test_load_scene_keeps_file_texture_dtype(tmp_path):
+    """The pipelined loader keeps the texture dtype the file stores (fp16 from to_h5, fp32 from other writers):
+    an fp32 texture must not be rounded through fp16 on the way to the device."""
     import batch_infer
-    snap, h5, res, z = _snapshot_and_scene(tmp_path)
+    rng = np.random.default_rng(3)
+    for dt in (np.float16, np.float32):
+        p = str(tmp_path / f"s_{np.dtype(dt).name}.h5")
+        tex = (rng.random((4, 13, 32, 32)) * 3).astype(dt)
+        h5io.write_scene(p, rng.random((4, 3, 3)), rng.random((4, 3, 3)), tex, rng.random((1, 4, 4)), [40.0],
+                         texture_dtype=dt)
+        kept = batch_infer.load_scene(p, texture_dtype=None)["texture"]
+        assert kept.dtype == torch.from_numpy(tex).dtype
+        np.testing.assert_array_equal(kept.numpy(), tex)
+        np.testing.assert_array_equal(batch_infer.load_scene(p)["texture"].numpy(), tex.astype(np.float32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tex_dtype", [np.float16, np.float32])
+def test_batch_infer_pipelined_matches_inline(tmp_path, monkeypatch, tex_dtype):
+    """The pipelined data path (loader thread, pinned H2D/D2H side streams) writes the same images as the
+    inline loop, over several batches (3 scenes, batch size 1: every overlap case), for fp16 and fp32 files."""
+    import batch_infer
+    snap, h5, res, z = _snapshot_and_scene(tmp_path, tex_dtype)
     for i in (2, 3):
         os.link(h5, h5.parent / f"tiny{i}.h5")
     outs = {}

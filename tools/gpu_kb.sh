@@ -1,3 +1,8 @@
+# kernel micro-benchmarks: bash tools/gpu_kb.sh <tag> <kbench mode> (env KB_* passed through)
 set -e
-mkdir -p gpurun_out
-timeout -k 10 300 python tools/kbench.py ${1:-gemm} > gpurun_out/kb_${1:-gemm}.log 2>&1
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${1:-kb}
+mkdir -p $O
+cd $R
+timeout -k 10 600 python -u tools/kbench.py ${2:-gemm} > $O/kb.log 2>&1
+echo done

@@ -88,7 +88,9 @@ def gemm():
               ("s2 q", R, D, D, ops.EPI_BF16), ("s2 kv", S, 2 * D, D, ops.EPI_BF16),
               ("s2 w13", R, 2 * F, D, ops.EPI_SWIGLU), ("s2 w2", R, D, F, ops.EPI_ADD_F32),
               ("tex", 5633, D, 13312, ops.EPI_F32), ("sq8k", 8192, 8192, 8192, ops.EPI_BF16),
-              ("s1 w13bf", S, 2 * F, D, ops.EPI_BF16), ("s2 w13bf", R, 2 * F, D, ops.EPI_BF16)]
+              ("s1 w13bf", S, 2 * F, D, ops.EPI_BF16), ("s2 w13bf", R, 2 * F, D, ops.EPI_BF16),
+              ("s2 qkv", R, 3 * D, D, ops.EPI_BF16), ("s2 out", R, D, D, ops.EPI_ADD_F32),
+              ("kvall", S, 20 * D, D, ops.EPI_BF16), ("ray", R, D, 192, ops.EPI_F32), ("vn", 5633, D, 128, ops.EPI_F32)]
     if os.environ.get("KB_SHAPES"):
         shapes = [x for x in shapes if x[0] in os.environ["KB_SHAPES"].split(",")]
     for name, m, n, k, epi in shapes:
