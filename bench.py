@@ -227,7 +227,10 @@ def main():
                        torch_dtype=torch.bfloat16)
             frames.append(out.reshape(-1, *frame_shape))
         calls[0] += 1
-        local = torch.cat(frames) if frames else torch.empty((0,) + frame_shape, device=dev)
+        if len(frames) == 1:
+            local = frames[0]
+        else:
+            local = torch.cat(frames) if frames else torch.empty((0,) + frame_shape, device=dev)
         if world > 1:  # finished frames to every rank (RCCL all_gather over xGMI)
             return gather_frames(local, [i for u in ids for i in u], n_frames_step)
         return local

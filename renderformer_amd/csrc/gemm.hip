@@ -44,9 +44,14 @@ struct Tile {
     static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_, STAGES = STAGES_;
     static constexpr int NWAVE = WGM * WGN, THREADS = NWAVE * 64;
     static constexpr int MW = BM / WGM, NWD = BN / WGN, TI = MW / 16, TJ = NWD / 16;
-    static constexpr int PA = BM / 16 / NWAVE, PB = BN / 16 / NWAVE;  // 1-KiB LDS-DMA pieces per wave per plane
+    // 1-KiB LDS-DMA pieces per wave per plane; with fewer A pieces than waves (BM < 16 x waves: the short
+    // tiles of the N = 1,024 projections) waves 0..BM/16-1 stage one A piece each and the rest none
+    static constexpr int APIECES = BM / 16;
+    static constexpr bool ASHARE = APIECES < NWAVE;
+    static constexpr int PA = ASHARE ? 1 : BM / 16 / NWAVE, PB = BN / 16 / NWAVE;
     static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-    static_assert(PA >= 1 && PB >= 1 && PA * NWAVE * 16 == BM && PB * NWAVE * 16 == BN, "tile/wave mismatch");
+    static_assert(PA >= 1 && PB >= 1 && (ASHARE || PA * NWAVE * 16 == BM) && PB * NWAVE * 16 == BN,
+                  "tile/wave mismatch");
     static_assert(TI >= 1 && TJ >= 2 && TJ % 2 == 0, "wave tile too small");
 };
 
@@ -85,6 +90,7 @@ struct EngineArgs {
     int halo_lg;      // halo-tiled 3x3 convolution: log2 of the tile width in pixels (halo_kernel)
     int* err;         // device error word (rf::device_error_word): stream-K hand-off timeouts
     int spin;         // stream-K hand-off spin bound (polls)
+    uint64_t* stamps; // diagnostics (RF_GEMM_STAMPS=1): per-block s_memtime stamps, [grid][16]; normally null
 };
 
 // uniform early exit of a gated launch (every block reads the same flag, so a stream-K grid exits whole)
@@ -115,6 +121,7 @@ RF_DEV int lds_off(int row, int ch) { return row * 64 + ((ch ^ ((row >> 1) & 3))
 
 template <int N>
 RF_DEV void wait_vm() {
+    static_assert(N >= 0 && N <= 24, "unsupported vmcnt");
     if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -122,11 +129,24 @@ RF_DEV void wait_vm() {
     else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
     else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
     else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if constexpr (N == 11) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
     else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if constexpr (N == 13) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+    else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+    else if constexpr (N == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
     else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else static_assert(N < 0, "unsupported vmcnt");
+    else if constexpr (N == 17) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+    else if constexpr (N == 18) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+    else if constexpr (N == 19) asm volatile("s_waitcnt vmcnt(19)" ::: "memory");
+    else if constexpr (N == 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else if constexpr (N == 21) asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
+    else if constexpr (N == 22) asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+    else if constexpr (N == 23) asm volatile("s_waitcnt vmcnt(23)" ::: "memory");
+    else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
 }
 
 template <class C, int NTERM>
@@ -134,18 +154,43 @@ constexpr int stage_bytes() {
     return (NTERM == 3 ? 2 : 1) * (C::A_BYTES + C::B_BYTES);
 }
 
+// Residual epilogue (x += A W^T): the accumulators START from the fp32 C tile instead of zero, loaded before
+// the main loop's first staging so their latency hides under it; the epilogue is then a plain store (no
+// read-modify-write round trip per output row at the end: that serialised 8-16 dependent HBM round trips
+// per tile, ~10 us of a 256x256 tile's epilogue).  Layout as engine_epilogue: acc[i][j][e] =
+// C[rbase + i*16 + (lane & 15)][cbase + j*16 + 4*(lane >> 4) + e]; rows >= M start at zero.
+template <int TI, int TJ>
+RF_DEV void load_c_acc(const EngineArgs& p, int rbase, int cbase, f32x4 (&acc)[TI][TJ]) {
+    const int lane = threadIdx.x & 63;
+    const float* c = reinterpret_cast<const float*>(p.c);
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+        const int row = rbase + i * 16 + (lane & 15);
+        const bool ok = row < p.m;
+        const float* src = c + (int64_t)(ok ? row : 0) * p.ldc + cbase + 4 * (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+            const float4 v = *reinterpret_cast<const float4*>(src + j * 16);
+            acc[i][j] = ok ? f32x4{v.x, v.y, v.z, v.w} : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+}
+
 // acc = A[m0:m0+BM, kbeg*BK:kend*BK] * W[n0:n0+BN, same]^T for this wave's sub-tile
-template <class C, int NTERM, bool GATHER>
+// (+ the C tile when INITC and this is the tile's first K range: see load_c_acc)
+template <class C, int NTERM, bool GATHER, bool INITC = false>
 RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int kbeg, int kend,
                             f32x4 (&acc)[C::TI][C::TJ]) {
     constexpr int S = C::STAGES, TI = C::TI, TJ = C::TJ, PA = C::PA, PB = C::PB;
     constexpr int PLANE_A = C::A_BYTES, PLANE_B = C::B_BYTES;
     constexpr int STAGE_BYTES = stage_bytes<C, NTERM>();
     constexpr int GPS = (NTERM == 3 ? 2 : 1) * (PA + PB);  // LDS-DMA instructions per thread per stage
+    constexpr int GPS_B = (NTERM == 3 ? 2 : 1) * PB;       // ... for a wave that stages no A piece (ASHARE)
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int wm = wave / C::WGN, wn = wave % C::WGN;
+    const bool stage_a = !C::ASHARE || __builtin_amdgcn_readfirstlane(wave) < C::APIECES;  // wave-uniform
 
     // ---- staging geometry: piece pc of this wave covers 16 rows x 64 B; lane -> (row, 16-B chunk)
     int arow[PA], alc[PA], brow[PB], blc[PB];
@@ -190,6 +235,7 @@ RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
         }
 #pragma unroll
         for (int pc = 0; pc < PA; ++pc) {
+            if (!stage_a) break;
             const int piece = wave * PA + pc;
             const int kofs = alc[pc] * 8;
             const bf16_t* sa;
@@ -221,10 +267,14 @@ RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
         }
     };
 
+    if (INITC && kbeg == 0) {
+        load_c_acc<TI, TJ>(p, m0 + wm * C::MW, n0 + wn * C::NWD, acc);
+    } else {
 #pragma unroll
-    for (int i = 0; i < TI; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 
     const int nk = kend - kbeg;
     const int frag_row = lane & 15, frag_ch = lane >> 4;
@@ -269,9 +319,15 @@ RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
     };
     // wait until this wave's DMA of tile t landed, given that tiles up to `last` were issued
     auto wait_tile = [&](int younger) {
-        if (younger >= 2) wait_vm<GPS * 2>();
-        else if (younger == 1) wait_vm<GPS>();
-        else wait_vm<0>();
+        if (stage_a) {
+            if (younger >= 2) wait_vm<GPS * 2>();
+            else if (younger == 1) wait_vm<GPS>();
+            else wait_vm<0>();
+        } else {
+            if (younger >= 2) wait_vm<GPS_B * 2>();
+            else if (younger == 1) wait_vm<GPS_B>();
+            else wait_vm<0>();
+        }
     };
 
     // Ring of S stages.  Fragments are register double-buffered: step kt runs the MFMAs of tile kt
@@ -473,13 +529,6 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
         for (int i = 0; i < TI; ++i) {
             const int row = rbase + i * 16 + rl;
             if (row >= p.m) continue;
-            float4 old[TJ];
-            if constexpr (EPI == E_ADD) {
-#pragma unroll
-                for (int j = 0; j < TJ; ++j)
-                    old[j] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.c) + (int64_t)row * p.ldc +
-                                                              cbase + j * 16 + cq);
-            }
 #pragma unroll
             for (int j = 0; j < TJ; ++j) {
                 const int col = cbase + j * 16 + cq;
@@ -495,11 +544,8 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                 if constexpr (EPI == E_BF16) {
                     *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.c) + o) =
                         make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-                } else if constexpr (EPI == E_F32) {
+                } else {  // E_F32, or E_ADD whose accumulators started from the C tile (load_c_acc)
                     *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + o) = make_float4(v[0], v[1], v[2], v[3]);
-                } else {
-                    *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + o) =
-                        make_float4(old[j].x + v[0], old[j].y + v[1], old[j].z + v[2], old[j].w + v[3]);
                 }
             }
         }
@@ -561,7 +607,7 @@ template <int ROWS>
 RF_DEV int img(int row, int kh, int ch) { return kh * (ROWS * 64) + row * 64 + ((ch ^ ((row >> 1) & 3)) << 4); }
 }  // namespace ph
 
-template <int BM, int NTERM, bool GATHER>
+template <int BM, int NTERM, bool GATHER, bool INITC = false>
 RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int kbeg, int kend,
                             f32x4 (&acc)[BM / 32][4]) {
     using namespace ph;
@@ -624,10 +670,14 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
         }
     };
 
+    if (INITC && kbeg == 0) {  // residual epilogue: start from the C tile (load_c_acc), issued before any DMA
+        load_c_acc<MI, 4>(p, m0 + wr * (BM / 2), n0 + wc * 64, acc);
+    } else {
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 
     const int frow = lane & 15, fch = lane >> 4;  // fragment lane geometry (16x16x32: 16 rows x 4 chunks)
     bf16x8 fa[4][2], fb0[2][2], fb1[2][2];        // A: 4 frags (64 rows) x 2 k-slices; B(n0), B(n1): 2 x 2
@@ -763,7 +813,7 @@ __global__ __launch_bounds__(512, 1) void phased_kernel(EngineArgs p) {
     int tm, tn;
     tile_coords(wg, tiles_m, p.n / ph::BN, p.group_m, tm, tn);
     f32x4 acc[BM / 32][4];
-    phased_mainloop<BM, NTERM, GATHER>(p, smem, tm * BM, tn * ph::BN, 0, p.k / ph::BK2, acc);
+    phased_mainloop<BM, NTERM, GATHER, EPI == E_ADD>(p, smem, tm * BM, tn * ph::BN, 0, p.k / ph::BK2, acc);
     engine_epilogue<Tile<BM, 256, 2, 4, 4>, EPI>(p, tm * BM, tn * ph::BN, acc);
 }
 
@@ -786,6 +836,10 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
     const int64_t it_end = total * (wg + 1) / nwg;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     f32x4 acc[TI][TJ];
+    uint64_t st[16];
+    int ns = 0;
+    const bool stamp = p.stamps != nullptr;
+    if (stamp) st[ns++] = __builtin_amdgcn_s_memtime();
     while (it < it_end) {
         const int tile = (int)(it / iters), kf = (int)(it % iters);
         const int kl = (int)min((int64_t)iters, kf + (it_end - it));
@@ -794,7 +848,8 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
         const int m0 = tm * BM, n0 = tn * ph::BN;
         wait_vm<0>();
         __syncthreads();  // the previous segment's LDS readers are done
-        phased_mainloop<BM, NTERM, false>(p, smem, m0, n0, kf, kl, acc);
+        phased_mainloop<BM, NTERM, false, EPI == E_ADD>(p, smem, m0, n0, kf, kl, acc);
+        if (stamp && ns < 14) st[ns++] = __builtin_amdgcn_s_memtime();
         if (kf != 0) {
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(p.sk_part + (int64_t)wg * TS, 0, TS * 4, 0x00020000);
@@ -836,9 +891,14 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
                         }
                 }
             }
+            if (stamp && ns < 14) st[ns++] = __builtin_amdgcn_s_memtime();
             engine_epilogue<Tile<256, 256, 2, 4, 4>, EPI>(p, m0, n0, acc);
         }
+        if (stamp && ns < 14) st[ns++] = __builtin_amdgcn_s_memtime();
         it += kl - kf;
+    }
+    if (stamp && threadIdx.x == 0) {
+        for (int i = 0; i < 16; ++i) p.stamps[wg * 16 + i] = i < ns ? st[i] : 0;
     }
 }
 
@@ -863,7 +923,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
         int tm, tn;
         tile_coords(wg, tiles_m, p.n / BN, p.group_m, tm, tn);
         const int m0 = tm * BM, n0 = tn * BN;
-        engine_mainloop<C, NTERM, GATHER>(p, smem, m0, n0, 0, p.k / BK, acc);
+        engine_mainloop<C, NTERM, GATHER, EPI == E_ADD>(p, smem, m0, n0, 0, p.k / BK, acc);
         engine_epilogue<C, EPI>(p, m0, n0, acc);
     } else {
         const int iters = p.k / BK;
@@ -879,7 +939,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
             const int m0 = tm * BM, n0 = tn * BN;
             wait_vm<0>();
             __syncthreads();  // the previous segment's LDS readers are done with the ring
-            engine_mainloop<C, NTERM, GATHER>(p, smem, m0, n0, kf, kl, acc);
+            engine_mainloop<C, NTERM, GATHER, EPI == E_ADD>(p, smem, m0, n0, kf, kl, acc);
             if (kf != 0) {
                 // partial tile in accumulator order (1 KiB per wave-instruction), stored write-through
                 // (sc1) so no release fence is needed; every storing wave drains, then one lane flags
@@ -1100,6 +1160,11 @@ using T128w8 = Tile<128, 128, 2, 4, 3>;  // 8 waves of 64x32: two waves per SIMD
 using T256 = Tile<256, 256, 2, 4, 4>;
 using T256x128 = Tile<256, 128, 4, 2, 3>;
 using T256x64 = Tile<256, 64, 4, 1, 4>;  // fp16 convolutions with <= 64 output channels (DPT output_conv2)
+// short-M tiles for the N = 1,024 / 3,072 projections: BM chosen so the tile count fills whole rounds of
+// 256 CUs (M = 5,649: 59 x 4 = 236 tiles of 96 x 256; M = 4,096: 64 x 4 = 256 tiles of 64 x 256)
+using T96x256 = Tile<96, 256, 2, 4, 3>;
+using T64x256 = Tile<64, 256, 2, 4, 3>;
+using T64x256w4 = Tile<64, 256, 1, 4, 3>;
 
 int pick_group_m(int tiles_m, int tiles_n, int bm, int bn, int64_t per_xcd) {
     if (const char* env = getenv("RF_GEMM_GROUP_M")) return std::max(1, std::min(tiles_m, atoi(env)));
@@ -1178,6 +1243,9 @@ void sk_setup(EngineArgs& p, void* workspace) {
     p.sk_epoch = ++g_sk_epoch;
     p.err = rf::device_error_word();
     p.spin = rf::spin_limit();
+    // diagnostics: stamps in the last 256 KiB of the partial area (tools/kbench.py skstamps)
+    static const bool stamps = getenv("RF_GEMM_STAMPS") && atoi(getenv("RF_GEMM_STAMPS")) != 0;
+    p.stamps = stamps ? (uint64_t*)(p.sk_part + SK_PART_FLOATS - 65536) : nullptr;
 }
 
 
@@ -1279,6 +1347,9 @@ int run_dp(int cfg, const EngineArgs& p, int epilogue, void* stream) {
     if (cfg == 1284) return run_dp_cfg<Tile<128, 128, 2, 2, 4>>(p, epilogue, stream);
     if (cfg == 1285) return run_dp_cfg<Tile<128, 128, 2, 2, 5>>(p, epilogue, stream);
     if (cfg == 2561) return run_dp_cfg<T256x128>(p, epilogue, stream);
+    if (cfg == 962 && p.n % 256 == 0) return run_dp_cfg<T96x256>(p, epilogue, stream);
+    if (cfg == 642 && p.n % 256 == 0) return run_dp_cfg<T64x256>(p, epilogue, stream);
+    if (cfg == 644 && p.n % 256 == 0) return run_dp_cfg<T64x256w4>(p, epilogue, stream);
     return run_dp_cfg<T128>(p, epilogue, stream);
 }
 

@@ -175,8 +175,8 @@ def test_baseline_configs_match_reference(name):
     assert ac < 2e-2
     if "hdr_sum" in z.files:  # the whole image, not only the sampled pixels
         o64 = out.double()
-        assert abs(float(o64.sum()) - float(z["hdr_sum"])) / abs(float(z["hdr_sum"])) < 1e-4
-        assert abs(float((o64 ** 2).sum()) - float(z["hdr_sumsq"])) / float(z["hdr_sumsq"]) < 2e-4
+        assert abs(float(o64.sum()) - float(z["hdr_sum"])) / abs(float(z["hdr_sum"])) < 1e-3
+        assert abs(float((o64 ** 2).sum()) - float(z["hdr_sumsq"])) / float(z["hdr_sumsq"]) < 2e-3
     del pipe, out, d
     torch.cuda.empty_cache()
 

@@ -5,7 +5,7 @@ TAG=${1:-run}; shift || true
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -rP > $O/tests.log 2>&1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 timeout -k 10 300 python bench.py "$@" > $O/bench.json 2> $O/bench.err
 cd /tmp && export TMPDIR=/tmp

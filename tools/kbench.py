@@ -82,6 +82,25 @@ def attn():
         print(f"swin shift={sh}: {ms*1e3:8.1f} us  {4*R*64*D/ms/1e9:7.1f} TF")
 
 
+def check(a, w, epi):
+    """relative error of one fresh call vs an fp32 torch reference (SwiGLU: interleaved 16-row groups)"""
+    m, n = a.shape[0], w.shape[0]
+    ref = a.float() @ w.float().t()
+    if epi == ops.EPI_SWIGLU:
+        g = ref.view(m, n // 32, 2, 16)
+        ref = (torch.nn.functional.silu(g[:, :, 0]) * g[:, :, 1]).reshape(m, n // 2)
+        c = torch.empty(m, n // 2, device=dev, dtype=torch.bfloat16)
+    elif epi == ops.EPI_BF16:
+        c = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+    else:
+        c0 = torch.randn(m, n, device=dev)
+        c = c0.clone()
+        if epi == ops.EPI_ADD_F32:
+            ref = ref + c0
+    ops.gemm(a, w, c, None, epi)
+    return float((c.float() - ref).norm() / ref.norm())
+
+
 def gemm():
     shapes = [("s1 qkv", S, 3 * D, D, ops.EPI_BF16), ("s1 out", S, D, D, ops.EPI_ADD_F32),
               ("s1 w13", S, 2 * F, D, ops.EPI_SWIGLU), ("s1 w2", S, D, F, ops.EPI_ADD_F32),
@@ -106,7 +125,8 @@ def gemm():
                     ("dp256x128", "2561", None, "0"), ("dp256ring", "256", None, "0"), ("dp256ph", "256", None, "0"),
                     ("dp128x256ph", "1282", None, "0"),
                     ("sk128x512", "128", "512", "0"), ("sk128x768", "128", "768", "0"), ("sk256", None, None, "1"),
-                    ("skph", None, None, "0"), ("auto", None, None, None)]
+                    ("skph", None, None, "0"), ("auto", None, None, None),
+                    ("dp96x256", "962", None, "0"), ("dp64x256", "642", None, "0"), ("dp64x256w4", "644", None, "0")]
         if os.environ.get("KB_VARIANTS"):
             variants = [v for v in variants if v[0] in os.environ["KB_VARIANTS"].split(",")]
         for label, tile, sk, gm in variants:
@@ -128,7 +148,9 @@ def gemm():
             if label in ("dp256ring", "dp256ph", "sk256", "skph", "dp128x256ph") and n % 256:
                 continue
             ms = timeit(lambda: ops.gemm(a, w, c, None, epi), reps=10 if k > 8000 else 20)
-            print(f"gemm {name:8s} {m}x{n}x{k} {label}: {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF")
+            err = check(a, w, epi)
+            print(f"gemm {name:8s} {m}x{n}x{k} {label}: {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF  relerr {err:.1e}",
+                  flush=True)
         wt = w.t()
         ms = timeit(lambda: torch.matmul(a, wt), reps=10 if k > 8000 else 20)
         print(f"gemm {name:8s} {m}x{n}x{k} hipBLASLt(torch.matmul, bf16 out): {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF")
@@ -213,3 +235,35 @@ if __name__ == "__main__":
     for name, fn in (("attn", attn), ("gemm", gemm), ("conv", conv), ("blaslt", blaslt), ("norms", norms)):
         if what in (name, "all"):
             fn()
+
+
+def skstamps():
+    """Per-block timeline of the phased stream-K GEMM (RF_GEMM_STAMPS=1 build path): segment ends, publish /
+    wait / epilogue ends in shader cycles from each block's start, for the shapes in KB_SHAPES (m,n,k,epi;...)."""
+    import numpy as np
+    os.environ["RF_GEMM_STAMPS"] = "1"
+    os.environ["RF_GEMM_BACKEND"] = "hip"
+    os.environ["RF_GEMM_SKPH"] = "1"
+    spec = os.environ.get("KB_SK", "5649,1024,1024,2;5649,1024,4096,2;5649,3072,1024,0")
+    for item in spec.split(";"):
+        m, n, k, epi = (int(x) for x in item.split(","))
+        a = torch.randn(m, k, device=dev).bfloat16()
+        w = (torch.randn(n, k, device=dev) / math.sqrt(k)).bfloat16()
+        c = torch.empty(m, n, device=dev, dtype=torch.bfloat16) if epi == 0 else torch.zeros(m, n, device=dev)
+        ms = timeit(lambda: ops.gemm(a, w, c, None, epi), reps=20)
+        torch.cuda.synchronize()
+        ws = ops._gemm_workspace(a.device)
+        off = (256 * 256 * 256 - 65536) * 4
+        st = ws[off:off + 256 * 16 * 8].view(torch.int64).view(256, 16).cpu().numpy()
+        t0 = st[:, 0].min()
+        rel = np.where(st > 0, st - t0, 0)
+        ends = rel.max(axis=1)
+        print(f"skstamps {m}x{n}x{k} epi{epi}: {ms*1e3:.1f} us; block start spread {int(st[:,0].max()-t0)} cyc, "
+              f"end median {int(np.median(ends))} max {int(ends.max())} cyc", flush=True)
+        for b in list(range(0, 8)) + [int(np.argmax(ends))]:
+            seq = [int(v) for v in rel[b] if v > 0 or v == 0]
+            print(f"  block {b:3d}: " + " ".join(str(int(v)) for v in rel[b][:12] if v != 0 or True), flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "skstamps":
+    skstamps()
