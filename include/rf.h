@@ -80,9 +80,9 @@ int rf_debug_raise_device_error(int code, void* stream);
  * output tile), rf_gemm_workspace_bytes() bytes, zero-filled once when allocated, used by one stream at a
  * time; with it, launches whose output tiles cannot fill the CUs split the K loop stream-K style. */
 /* C[M,N] (epilogue) A[M,K] * W[N,K]^T ; A, W bf16; K % 32 == 0, N % 128 == 0, 16-B aligned rows.
- * Plain epilogues run on hipBLASLt (RF_GEMM_BACKEND=hip: the HIP engine); the first bf16-output call per
- * shape times hipBLASLt's top candidates once on the caller's buffers, synchronising the stream that one
- * time (RF_BLASLT_TUNE=0: no tuning, no sync).
+ * Every epilogue runs on the hand-written MFMA engine (gemm.hip; no vendor GEMM library is linked): the
+ * tile shape (256x256 / 128x256 / 96x256 / 64x256 phased, 96x256 / 128x128 ring) is chosen per shape by a
+ * measured cost model; RF_EPI_ADD_F32 accumulators start from the C tile (no read-modify-write epilogue).
  * workspace (optional, NULL = data-parallel tiles only): rf_gemm_workspace_bytes() bytes, zero-filled once
  * when allocated, used by one stream at a time; it enables the stream-K split for GEMMs whose tile count
  * would leave CUs idle. */

@@ -573,7 +573,9 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
 namespace ph {
 constexpr int BN = 256, BK2 = 64;
 constexpr int REGION = 16384;  // 128 rows x 64 k x 2 B
-// BM = 256: regions RA0, RA1, RB0, RB1; BM = 128 (wave tile 64 x 64): RA, RB0, RB1
+// BM = 256: regions RA0, RA1, RB0, RB1; BM = 128 (wave tile 64 x 64): RA, RB0, RB1.  BM = 96 / 64 (wave tile
+// 48 / 32 x 64; the short tiles of the N = 1,024 projections): the same three regions with a BM-row RA that
+// only waves 0..BM/16-1 stage (the others skip it and count fewer LDS-DMA in their waits)
 template <int BM>
 struct Cfg {
     static constexpr int NREG = BM == 256 ? 4 : 3;
@@ -583,6 +585,8 @@ struct Cfg {
     static constexpr int LDS = 2 * TILE;
     static constexpr int MI = BM / 32;  // 16-row M fragments per wave
     static constexpr int GLDS = 2 * NREG;  // LDS-DMA per lane per K-tile
+    static constexpr int FA = BM == 256 ? 4 : BM / 32;  // A fragments per wave per phase (rows / 16)
+    static_assert(BM == 256 || BM == 128 || BM == 96 || BM == 64, "phased tile height");
 };
 // tile row of region row j (0..127); runs of 16 consecutive j map to 16 consecutive rows
 template <int BM>
@@ -614,10 +618,13 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
     using G = Cfg<BM>;
     constexpr int NREG = G::NREG, NA = G::NA, MI = G::MI;
     static_assert(NTERM == 1 || NTERM == P_F16, "phased loop: single-term operands");
+    constexpr int FA = G::FA;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int wr = wave >> 2, wc = wave & 3;
     const int nk = kend - kbeg;  // K-tiles of this call; local tile t is global K-tile kbeg + t
+    // BM < 128: only waves 0..BM/16-1 stage the A region (wave-uniform)
+    const bool has_a = BM >= 128 || __builtin_amdgcn_readfirstlane(wave) < BM / 16;
 
     // ---- DMA geometry: wave w fills region rows 16 w .. 16 w + 15 (both k-halves) of each region
     const int jrow = 16 * wave + (lane >> 2);
@@ -649,6 +656,7 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
     // issue region r of K-tile kt into buffer kt & 1 (2 LDS-DMA per lane: the two 32-deep k-halves)
     auto issue = [&](int kt, int r) {
         const bool is_a = r < NA;
+        if (is_a && !has_a) return;
         char* base = smem + (kt & 1) * G::TILE + (is_a ? 0 : G::A_IMG);
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) {
@@ -680,10 +688,10 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
     }
 
     const int frow = lane & 15, fch = lane >> 4;  // fragment lane geometry (16x16x32: 16 rows x 4 chunks)
-    bf16x8 fa[4][2], fb0[2][2], fb1[2][2];        // A: 4 frags (64 rows) x 2 k-slices; B(n0), B(n1): 2 x 2
+    bf16x8 fa[FA][2], fb0[2][2], fb1[2][2];       // A: FA frags (16 FA rows) x 2 k-slices; B(n0), B(n1): 2 x 2
     auto read_a = [&](const char* buf, int mi) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < FA; ++i)
 #pragma unroll
             for (int s = 0; s < 2; ++s)
                 fa[i][s] = *reinterpret_cast<const bf16x8*>(buf + img<BM>(wr * (BM / 2) + mi * 64 + i * 16 + frow, s, fch));
@@ -700,10 +708,10 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < FA; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    f32x4& c = acc[mi * 4 + i][ni * 2 + j];
+                    f32x4& c = acc[mi * FA + i][ni * 2 + j];
                     if constexpr (NTERM == P_F16)
                         c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[j][s]),
                                                                    __builtin_bit_cast(f16x8, fa[i][s]), c, 0, 0, 0);
@@ -731,7 +739,8 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
     if (nk > 1) {
 #pragma unroll
         for (int r = 0; r < (BM == 256 ? NREG : 2); ++r) issue(1, r);
-        wait_vm<AHEAD>();
+        if (has_a) wait_vm<AHEAD>();
+        else wait_vm<AHEAD - 2>();  // (BM < 128, no RA: RB0 of tile 1 only)
     } else {
         wait_vm<0>();
     }
@@ -789,7 +798,8 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
             if (pf) {
                 issue(t + 2, 0);
                 issue(t + 2, 1);
-                wait_vm<4>();
+                if (has_a) wait_vm<4>();
+                else wait_vm<2>();
             } else {
                 wait_vm<0>();
             }
@@ -1267,24 +1277,42 @@ int sk_grid(int m, int n, int k) {
     return grid;
 }
 
-// Tile choice: the 256x256 tile halves the L2 traffic per FLOP but needs enough tiles to fill
-// 256 CUs (one 512-thread block per CU); smaller problems keep the 128x128 tile (2-3 blocks per CU).
+// Tile choice by a measured cost model (tools/kbench.py gemm, profiles/r2_*): a launch of T tiles on 256 CUs
+// (x slots blocks per CU) takes ceil(T / (256 slots)) rounds, each `fixed + per_k * K / 1024` us.  Per config:
+//   256  phased 256x256          6.7 + 24.3   (best per FLOP; needs >= ~1 round of tiles)
+//   1282 phased 128x256          5.6 + 14.6
+//   963  phased  96x256          8.0 + 11.1   (M = 5,649, N = 1,024: 236 tiles = one round)
+//   643  phased  64x256          8.0 + 10.6   (M = 4,096, N = 1,024: 256 tiles = one round)
+//   962  ring    96x256          7.5 + 14.0
+//   128  ring   128x128          5.0 + 12.2 at <= 256 tiles (one block per CU), 9.0 + 14.5 per 512 (two)
+// The residual epilogue (C += ...) reads its C tile up front (load_c_acc); all configs pay it alike.
 int pick_cfg(int m, int n, int k) {
     if (const char* env = getenv("RF_GEMM_TILE")) return atoi(env);
     const char* ph = getenv("RF_GEMM_PHASED");
-    if (n % 256 == 0 && k % 64 == 0 && (!ph || atoi(ph) != 0)) {
-        // whole-tile rounds x measured time per round (kbench, K = 1024-13312), relative units: 256x256 phased
-        // 1.1 per 256 tiles, 128x256 phased 0.65 per 256 tiles, 128x128 ring 0.52 for <= 256 tiles (one block
-        // per CU) else 0.85 per 512 (two blocks per CU)
-        const int64_t t256 = (int64_t)(n / 256) * ((m + 255) / 256), t1282 = (int64_t)(n / 256) * ((m + 127) / 128);
-        const int64_t t128 = (int64_t)(n / 128) * ((m + 127) / 128);
-        const double c256 = 1.1 * ((t256 + 255) / 256), c1282 = 0.65 * ((t1282 + 255) / 256),
-                     c128 = t128 <= 256 ? 0.52 : 0.85 * ((t128 + 511) / 512);
-        if (c256 <= c1282 && c256 <= c128) return 256;
-        return c1282 <= c128 ? 1282 : 128;
+    const bool phased = n % 256 == 0 && k % 64 == 0 && (!ph || atoi(ph) != 0);
+    const double kk = k / 1024.0;
+    auto cost = [&](int bm, int bn, int slots, double fixed, double per_k) {
+        const int64_t tiles = (int64_t)((m + bm - 1) / bm) * (n / bn);
+        const int64_t rounds = (tiles + 256 * slots - 1) / (256 * slots);
+        return rounds * (fixed + per_k * kk);
+    };
+    int best = 128;
+    const int64_t t128 = (int64_t)((m + 127) / 128) * (n / 128);
+    double best_c = t128 <= 256 ? cost(128, 128, 1, 5.0, 12.2) : cost(128, 128, 2, 9.0, 14.5);
+    auto consider = [&](int cfg, double c) {
+        if (c < best_c) {
+            best_c = c;
+            best = cfg;
+        }
+    };
+    if (n % 256 == 0) consider(962, cost(96, 256, 1, 7.5, 14.0));
+    if (phased) {
+        consider(256, cost(256, 256, 1, 6.7, 24.3));
+        consider(1282, cost(128, 256, 1, 5.6, 14.6));
+        consider(963, cost(96, 256, 1, 8.0, 11.1));
+        consider(643, cost(64, 256, 1, 8.0, 10.6));
     }
-    if (n % 256 == 0 && (n / 256) * ((m + 255) / 256) >= 2 * 256) return 256;
-    return 128;
+    return best;
 }
 
 __device__ __attribute__((aligned(16))) bf16_t g_zero_row[64];  // stays zero: source of padded conv taps
@@ -1349,6 +1377,22 @@ int run_dp(int cfg, const EngineArgs& p, int epilogue, void* stream) {
     if (cfg == 2561) return run_dp_cfg<T256x128>(p, epilogue, stream);
     if (cfg == 962 && p.n % 256 == 0) return run_dp_cfg<T96x256>(p, epilogue, stream);
     if (cfg == 642 && p.n % 256 == 0) return run_dp_cfg<T64x256>(p, epilogue, stream);
+    if (cfg == 963 && use_phased(p.n, p.k)) {  // phased 96x256
+        switch (epilogue) {
+            case RF_EPI_BF16: return launch_phased<E_BF16, 1, false, 96>(p, stream, "rf_gemm_bf16");
+            case RF_EPI_F32: return launch_phased<E_F32, 1, false, 96>(p, stream, "rf_gemm_bf16");
+            case RF_EPI_ADD_F32: return launch_phased<E_ADD, 1, false, 96>(p, stream, "rf_gemm_bf16");
+            default: return launch_phased<E_SWIGLU, 1, false, 96>(p, stream, "rf_gemm_bf16");
+        }
+    }
+    if (cfg == 643 && use_phased(p.n, p.k)) {  // phased 64x256
+        switch (epilogue) {
+            case RF_EPI_BF16: return launch_phased<E_BF16, 1, false, 64>(p, stream, "rf_gemm_bf16");
+            case RF_EPI_F32: return launch_phased<E_F32, 1, false, 64>(p, stream, "rf_gemm_bf16");
+            case RF_EPI_ADD_F32: return launch_phased<E_ADD, 1, false, 64>(p, stream, "rf_gemm_bf16");
+            default: return launch_phased<E_SWIGLU, 1, false, 64>(p, stream, "rf_gemm_bf16");
+        }
+    }
     if (cfg == 644 && p.n % 256 == 0) return run_dp_cfg<T64x256w4>(p, epilogue, stream);
     return run_dp_cfg<T128>(p, epilogue, stream);
 }
@@ -1372,15 +1416,6 @@ bool skph(int m, int n, int k) {
 
 extern "C" int64_t rf_gemm_workspace_bytes(void) { return SK_WS_BYTES; }
 
-namespace rf {
-int blaslt_gemm(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int m, int n, int k,
-                int mode, const float* bias, void* workspace, int64_t ws_bytes, void* stream);
-bool gemm_engine_forced() {
-    const char* be = getenv("RF_GEMM_BACKEND");
-    return be && strcmp(be, "hip") == 0;
-}
-}  // namespace rf
-
 static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
                      const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
                      void* stream, const int* gate) {
@@ -1393,13 +1428,6 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
     RF_REQUIRE(epilogue >= RF_EPI_BF16 && epilogue <= RF_EPI_SWIGLU, "rf_gemm_bf16: bad epilogue %d", epilogue);
     RF_REQUIRE(ldc >= (epilogue == RF_EPI_SWIGLU ? n / 2 : n) && ldc % 4 == 0, "rf_gemm_bf16: ldc too small/unaligned");
     RF_REQUIRE(((uintptr_t)c & 7) == 0, "rf_gemm_bf16: output must be 8-B aligned");
-    // plain epilogues (bf16 out, fp32 out + bias, fp32 residual accumulate) go to hipBLASLt, which is
-    // faster on every plain projection shape of the path (tools/kbench.py); RF_GEMM_BACKEND=hip keeps them
-    // on the engine below.  The fused epilogues (SwiGLU) are engine-only.
-    if (!gate && epilogue != RF_EPI_SWIGLU && (epilogue == RF_EPI_F32 || !bias) && !rf::gemm_engine_forced()) {
-        const int r = rf::blaslt_gemm(a, lda, w, ldw, c, ldc, m, n, k, epilogue, bias, workspace, ws_bytes, stream);
-        if (r != -1) return r;
-    }
     EngineArgs p{};
     p.a = (const bf16_t*)a;
     p.lda = lda;

@@ -31,13 +31,12 @@ def relerr(a, b):
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("backend", ["auto", "hip"])
 @pytest.mark.parametrize("m,n,k", [(1, 128, 64), (77, 256, 128), (333, 384, 192), (5649, 1024, 1024),
-                                   (1000, 128, 13312), (4096, 3072, 1024), (5649, 1024, 4096)])
-def test_gemm_f32_bf16(m, n, k, backend, monkeypatch):
-    """Plain epilogues on both backends: hipBLASLt (auto; bf16 out, fp32 + bias, fp32 accumulate) and the
-    hand-written engine (RF_GEMM_BACKEND=hip), against fp64."""
-    monkeypatch.setenv("RF_GEMM_BACKEND", backend)
+                                   (1000, 128, 13312), (4096, 3072, 1024), (5649, 1024, 4096), (4096, 1024, 4096),
+                                   (5649, 3072, 1024), (5649, 20480, 1024)])
+def test_gemm_f32_bf16(m, n, k):
+    """Plain epilogues (bf16 out, fp32 + bias, fp32 residual accumulate) on the hand-written engine with the
+    tile the cost model picks for the shape (the path's projection shapes included), against fp64."""
     ops = _ops()
     g = torch.Generator(device="cpu").manual_seed(m * 7 + n)
     a = torch.randn(m, k, generator=g).bfloat16().to(dev)
@@ -62,7 +61,6 @@ def test_gemm_f32_bf16(m, n, k, backend, monkeypatch):
 def test_gemm_stream_k(monkeypatch, grid, m, n, k):
     """Stream-K split (forced grid sizes, incl. an odd one where a tile spans 3+ blocks, and the 256x256-tile
     variant over 256 blocks) vs fp64, every epilogue (engine backend)."""
-    monkeypatch.setenv("RF_GEMM_BACKEND", "hip")
     ops = _ops()
     if grid in ("sk256", "skph"):
         if n % 256 or (grid == "skph" and k % 64):
@@ -94,15 +92,19 @@ def test_gemm_stream_k(monkeypatch, grid, m, n, k):
     assert relerr(outs.float(), refs) < 5e-3
 
 
-@pytest.mark.parametrize("tile", ["256ph", "128x256ph", "256ring"])
+TILES = {"256ph": "256", "128x256ph": "1282", "96x256ph": "963", "64x256ph": "643", "256ring": "256",
+         "96x256ring": "962", "64x256ring": "642", "64x256ring4w": "644", "128ring": "128"}
+
+
+@pytest.mark.parametrize("tile", list(TILES))
 @pytest.mark.parametrize("m,n,k", [(1, 256, 64), (300, 512, 128), (777, 256, 192), (5649, 3072, 1024),
-                                   (4096, 1024, 4096), (2000, 768, 320)])
+                                   (4096, 1024, 4096), (2000, 768, 320), (5649, 1024, 1024)])
 def test_gemm_256_tiles(monkeypatch, tile, m, n, k):
-    """The 256-wide tiles: the phased BK=64 loop at 256x256 and 128x256 and the ring engine's 256x256, forced on
-    every shape (ragged M, one to three K-tiles, long K), every epilogue, against fp64 (engine backend)."""
-    monkeypatch.setenv("RF_GEMM_BACKEND", "hip")
+    """Every tile shape of the engine (phased BK=64 loop at 256/128/96/64 x 256 — the short ones stage A from
+    only some waves —, the ring engine's 256x256, 96x256, 64x256 and 128x128), forced on every shape (ragged M,
+    one to three K-tiles, long K), every epilogue (the residual one starting from the C tile), vs fp64."""
     ops = _ops()
-    monkeypatch.setenv("RF_GEMM_TILE", "1282" if tile == "128x256ph" else "256")
+    monkeypatch.setenv("RF_GEMM_TILE", TILES[tile])
     monkeypatch.setenv("RF_GEMM_PHASED", "0" if tile == "256ring" else "1")
     g = torch.Generator(device="cpu").manual_seed(m + 3 * n + k)
     a = torch.randn(m, k, generator=g).bfloat16().to(dev)

@@ -121,18 +121,16 @@ def gemm():
             c = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
         else:
             c = torch.zeros(m, n, device=dev)
-        variants = [("blaslt", None, None, None), ("dp128", "128", None, "0"), ("dp128s4", "1284", None, "0"), ("dp128s5", "1285", None, "0"),
+        variants = [("dp128", "128", None, "0"), ("dp128s4", "1284", None, "0"), ("dp128s5", "1285", None, "0"),
                     ("dp256x128", "2561", None, "0"), ("dp256ring", "256", None, "0"), ("dp256ph", "256", None, "0"),
                     ("dp128x256ph", "1282", None, "0"),
                     ("sk128x512", "128", "512", "0"), ("sk128x768", "128", "768", "0"), ("sk256", None, None, "1"),
                     ("skph", None, None, "0"), ("auto", None, None, None),
-                    ("dp96x256", "962", None, "0"), ("dp64x256", "642", None, "0"), ("dp64x256w4", "644", None, "0")]
+                    ("dp96x256", "962", None, "0"), ("dp64x256", "642", None, "0"), ("dp64x256w4", "644", None, "0"),
+                    ("ph96x256", "963", None, "0"), ("ph64x256", "643", None, "0")]
         if os.environ.get("KB_VARIANTS"):
             variants = [v for v in variants if v[0] in os.environ["KB_VARIANTS"].split(",")]
         for label, tile, sk, gm in variants:
-            os.environ["RF_GEMM_BACKEND"] = "auto" if label == "blaslt" else "hip"
-            if label == "blaslt" and epi == ops.EPI_SWIGLU:
-                continue
             for key, val in (("RF_GEMM_TILE", tile), ("RF_GEMM_SK", sk), ("RF_GEMM_SK256", gm)):
                 if val is None:
                     os.environ.pop(key, None)
@@ -153,33 +151,11 @@ def gemm():
                   flush=True)
         wt = w.t()
         ms = timeit(lambda: torch.matmul(a, wt), reps=10 if k > 8000 else 20)
-        print(f"gemm {name:8s} {m}x{n}x{k} hipBLASLt(torch.matmul, bf16 out): {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF")
+        print(f"gemm {name:8s} {m}x{n}x{k} torch.matmul reference (vendor library, bf16 out): {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF")
     a = torch.randn(8192, 8192, device=dev).bfloat16()
     b = torch.randn(8192, 8192, device=dev).bfloat16()
     ms = timeit(lambda: a @ b, reps=10)
-    print(f"torch/hipBLASLt 8192^3 reference: {2*8192**3/ms/1e9:7.1f} TF")
-
-
-def blaslt():
-    """hipBLASLt heuristic candidates 0..15 (RF_BLASLT_ALGO) on the frame's plain projection shapes."""
-    shapes = [("s1 qkv", S, 3 * D, D, ops.EPI_BF16), ("s1 out", S, D, D, ops.EPI_ADD_F32),
-              ("s1 w2", S, D, F, ops.EPI_ADD_F32), ("s2 q", R, D, D, ops.EPI_BF16), ("s2 kv", S, 2 * D, D, ops.EPI_BF16),
-              ("s2 qkv", R, 3 * D, D, ops.EPI_BF16), ("s2 out", R, D, D, ops.EPI_ADD_F32),
-              ("s2 w2", R, D, F, ops.EPI_ADD_F32)]
-    os.environ["RF_GEMM_BACKEND"] = "auto"
-    for name, m, n, k, epi in shapes:
-        a = torch.randn(m, k, device=dev).bfloat16()
-        w = (torch.randn(n, k, device=dev) / math.sqrt(k)).bfloat16()
-        c = (torch.empty(m, n, device=dev, dtype=torch.bfloat16) if epi == ops.EPI_BF16 else torch.zeros(m, n, device=dev))
-        res = []
-        for i in range(int(os.environ.get("KB_ALGOS", "16"))):
-            os.environ["RF_BLASLT_ALGO"] = str(i)
-            ms = timeit(lambda: ops.gemm(a, w, c, None, epi), reps=20)
-            res.append(ms)
-        os.environ.pop("RF_BLASLT_ALGO", None)
-        best = min(range(len(res)), key=lambda i: res[i])
-        print(f"blaslt {name:7s} {m}x{n}x{k}: algo0 {res[0]*1e3:6.1f} us, best algo{best} {res[best]*1e3:6.1f} us "
-              f"({2*m*n*k/res[best]/1e9:6.1f} TF)  all: " + " ".join(f"{r*1e3:.1f}" for r in res), flush=True)
+    print(f"torch.matmul 8192^3 reference: {2*8192**3/ms/1e9:7.1f} TF")
 
 
 def norms():
@@ -232,7 +208,7 @@ def conv():
 
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
-    for name, fn in (("attn", attn), ("gemm", gemm), ("conv", conv), ("blaslt", blaslt), ("norms", norms)):
+    for name, fn in (("attn", attn), ("gemm", gemm), ("conv", conv), ("norms", norms)):
         if what in (name, "all"):
             fn()
 
