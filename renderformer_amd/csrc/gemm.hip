@@ -38,10 +38,11 @@ typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 
 enum Epi { E_BF16 = RF_EPI_BF16, E_F32 = RF_EPI_F32, E_ADD = RF_EPI_ADD_F32, E_SWIGLU = RF_EPI_SWIGLU, E_CONV = 16 };
 
-// Tile configuration: BM x BN block tile, WGM x WGN waves (each (BM/WGM) x (BN/WGN)), S-deep LDS ring.
-template <int BM_, int BN_, int WGM_, int WGN_, int STAGES_>
+// Tile configuration: BM x BN block tile, WGM x WGN waves (each (BM/WGM) x (BN/WGN)), S-deep LDS ring of
+// K-steps of KH x 32 (KH = 2: a 64-deep step staged as two 32-deep planes, half the barriers per K).
+template <int BM_, int BN_, int WGM_, int WGN_, int STAGES_, int KH_ = 1>
 struct Tile {
-    static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_, STAGES = STAGES_;
+    static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_, STAGES = STAGES_, KH = KH_;
     static constexpr int NWAVE = WGM * WGN, THREADS = NWAVE * 64;
     static constexpr int MW = BM / WGM, NWD = BN / WGN, TI = MW / 16, TJ = NWD / 16;
     // 1-KiB LDS-DMA pieces per wave per plane; with fewer A pieces than waves (BM < 16 x waves: the short
@@ -151,7 +152,7 @@ RF_DEV void wait_vm() {
 
 template <class C, int NTERM>
 constexpr int stage_bytes() {
-    return (NTERM == 3 ? 2 : 1) * (C::A_BYTES + C::B_BYTES);
+    return C::KH * (NTERM == 3 ? 2 : 1) * (C::A_BYTES + C::B_BYTES);
 }
 
 // Residual epilogue (x += A W^T): the accumulators START from the fp32 C tile instead of zero, loaded before
@@ -181,11 +182,13 @@ RF_DEV void load_c_acc(const EngineArgs& p, int rbase, int cbase, f32x4 (&acc)[T
 template <class C, int NTERM, bool GATHER, bool INITC = false>
 RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int kbeg, int kend,
                             f32x4 (&acc)[C::TI][C::TJ]) {
-    constexpr int S = C::STAGES, TI = C::TI, TJ = C::TJ, PA = C::PA, PB = C::PB;
+    constexpr int S = C::STAGES, TI = C::TI, TJ = C::TJ, PA = C::PA, PB = C::PB, KH = C::KH;
     constexpr int PLANE_A = C::A_BYTES, PLANE_B = C::B_BYTES;
     constexpr int STAGE_BYTES = stage_bytes<C, NTERM>();
-    constexpr int GPS = (NTERM == 3 ? 2 : 1) * (PA + PB);  // LDS-DMA instructions per thread per stage
-    constexpr int GPS_B = (NTERM == 3 ? 2 : 1) * PB;       // ... for a wave that stages no A piece (ASHARE)
+    constexpr int HALF_BYTES = STAGE_BYTES / KH;                // one 32-deep plane pair of a stage
+    constexpr int GPS = KH * (NTERM == 3 ? 2 : 1) * (PA + PB);  // LDS-DMA instructions per thread per stage
+    constexpr int GPS_B = KH * (NTERM == 3 ? 2 : 1) * PB;       // ... for a wave that stages no A piece (ASHARE)
+    static_assert(KH == 1 || (!GATHER && NTERM != 3), "64-deep steps: plain single-plane operands only");
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -224,8 +227,10 @@ RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
     }
 
     auto issue = [&](int kt, int buf) {
-        char* st = smem + buf * STAGE_BYTES;
-        const int k0 = kt * BK;
+#pragma unroll
+      for (int h = 0; h < KH; ++h) {
+        char* st = smem + buf * STAGE_BYTES + h * HALF_BYTES;
+        const int k0 = (kt * KH + h) * BK;
         int cb = k0, ky = 0, kx = 0;
         if constexpr (GATHER) {
             const int tap = udiv_m(k0, p.cin_m);
@@ -265,6 +270,7 @@ RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
                 __builtin_amdgcn_global_load_lds(GLB_PTR(void, p.w_lo + woff),
                                                  LDS_PTR(void, st + 2 * PLANE_A + PLANE_B + piece * 1024), 16, 0, 0);
         }
+      }
     };
 
     if (INITC && kbeg == 0) {
@@ -280,17 +286,21 @@ RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
     const int frag_row = lane & 15, frag_ch = lane >> 4;
     constexpr int TL = NTERM == 3 ? 1 : 0;  // lo-plane fragments present
     struct Frags {
-        bf16x8 a[TI], w[TJ], al[TL ? TI : 1], wl[TL ? TJ : 1];
+        bf16x8 a[KH][TI], w[KH][TJ], al[TL ? TI : 1], wl[TL ? TJ : 1];
     };
     auto load_frags = [&](int kt, Frags& f) {
-        const char* st = smem + (kt % S) * STAGE_BYTES;
+#pragma unroll
+      for (int h = 0; h < KH; ++h) {
+        const char* st = smem + (kt % S) * STAGE_BYTES + h * HALF_BYTES;
 #pragma unroll
         for (int i = 0; i < TI; ++i)
-            f.a[i] = *reinterpret_cast<const bf16x8*>(st + lds_off(wm * C::MW + i * 16 + frag_row, frag_ch));
+            f.a[h][i] = *reinterpret_cast<const bf16x8*>(st + lds_off(wm * C::MW + i * 16 + frag_row, frag_ch));
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
-            f.w[j] = *reinterpret_cast<const bf16x8*>(st + PLANE_A + lds_off(wn * C::NWD + j * 16 + frag_row, frag_ch));
+            f.w[h][j] = *reinterpret_cast<const bf16x8*>(st + PLANE_A + lds_off(wn * C::NWD + j * 16 + frag_row, frag_ch));
+      }
         if constexpr (TL) {
+        const char* st = smem + (kt % S) * STAGE_BYTES;
 #pragma unroll
             for (int i = 0; i < TI; ++i)
                 f.al[i] = *reinterpret_cast<const bf16x8*>(st + PLANE_A + PLANE_B +
@@ -303,29 +313,37 @@ RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
     };
     auto mma = [&](const Frags& f) {
 #pragma unroll
+      for (int h = 0; h < KH; ++h)
+#pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
             for (int j = 0; j < TJ; ++j) {
                 if constexpr (TL) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.wl[j], f.a[i], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[j], f.al[i], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.wl[j], f.a[0][i], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[0][j], f.al[i], acc[i][j], 0, 0, 0);
                 }
                 if constexpr (NTERM == P_F16)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, f.w[j]),
-                                                                       __builtin_bit_cast(f16x8, f.a[i]), acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, f.w[h][j]),
+                                                                       __builtin_bit_cast(f16x8, f.a[h][i]), acc[i][j], 0, 0, 0);
                 else
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[j], f.a[i], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[h][j], f.a[h][i], acc[i][j], 0, 0, 0);
             }
     };
-    // wait until this wave's DMA of tile t landed, given that tiles up to `last` were issued
+    // wait until this wave's DMA of step t landed, with `younger` later steps issued (and left in flight)
     auto wait_tile = [&](int younger) {
+        constexpr int G = GPS;
+        constexpr int GB = GPS_B;
         if (stage_a) {
-            if (younger >= 2) wait_vm<GPS * 2>();
-            else if (younger == 1) wait_vm<GPS>();
+            if (younger >= 4 && 4 * G <= 24) wait_vm<(4 * G <= 24 ? 4 * G : 0)>();
+            else if (younger >= 3 && 3 * G <= 24) wait_vm<(3 * G <= 24 ? 3 * G : 0)>();
+            else if (younger >= 2 && 2 * G <= 24) wait_vm<(2 * G <= 24 ? 2 * G : 0)>();
+            else if (younger >= 1) wait_vm<G>();
             else wait_vm<0>();
         } else {
-            if (younger >= 2) wait_vm<GPS_B * 2>();
-            else if (younger == 1) wait_vm<GPS_B>();
+            if (younger >= 4 && 4 * GB <= 24) wait_vm<(4 * GB <= 24 ? 4 * GB : 0)>();
+            else if (younger >= 3 && 3 * GB <= 24) wait_vm<(3 * GB <= 24 ? 3 * GB : 0)>();
+            else if (younger >= 2 && 2 * GB <= 24) wait_vm<(2 * GB <= 24 ? 2 * GB : 0)>();
+            else if (younger >= 1) wait_vm<GB>();
             else wait_vm<0>();
         }
     };
@@ -811,6 +829,164 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
     if (!late) __builtin_amdgcn_s_barrier();  // re-align the groups' barrier counts
 }
 
+// ---------------------------------------------------------------------------------------------
+// Three-buffer phased loop for the short tiles (BM = 64 / 96 / 128, BN = 256; regions RA, RB0, RB1 as in
+// the two-buffer loop).  Measured on the N = 1,024 projections with cold operands (the frame's case: each
+// layer's weights are read once per frame), the two-buffer loop stalls on its DMA: RB1 of tile t+1 is
+// issued only half a K-tile before it is read.  Here all of tile t+2 goes into the third buffer in phase 0
+// of tile t (that buffer held tile t-1, whose last reads - the lagging waves' phase 1 - are done by then)
+// and is waited for in phase 1 of tile t+1: every DMA has 1.5 K-tiles of MFMA work to land under.
+// Same stagger (waves 4-7 one section behind), same one counted vmcnt per K-tile.
+template <int BM, int NTERM, bool INITC>
+RF_DEV void phased3_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int kbeg, int kend,
+                             f32x4 (&acc)[BM / 32][4]) {
+    using namespace ph;
+    using G = Cfg<BM>;
+    static_assert(BM <= 128, "three-buffer loop: short tiles");
+    constexpr int NREG = 3, FA = G::FA;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int nk = kend - kbeg;
+    const bool has_a = BM >= 128 || __builtin_amdgcn_readfirstlane(wave) < BM / 16;
+    const int jrow = 16 * wave + (lane >> 2);
+    int trow[NREG], grow[NREG];
+    const bf16_t* src[NREG];
+#pragma unroll
+    for (int r = 0; r < NREG; ++r) {
+        trow[r] = region_row<BM>(r, jrow);
+        grow[r] = region_row<BM>(r, 16 * wave);
+    }
+    {
+        const int m = m0 + trow[0];
+        src[0] = p.a + (int64_t)(m < p.m ? m : p.m - 1) * p.lda;
+    }
+#pragma unroll
+    for (int r = 1; r < NREG; ++r) src[r] = p.w + (int64_t)(n0 + trow[r]) * p.ldw;
+    const int lch = lane & 3;
+    auto issue_tile = [&](int kt) {  // all three regions of K-tile kt into buffer kt % 3
+        char* buf = smem + (kt % 3) * G::TILE;
+#pragma unroll
+        for (int r = 0; r < NREG; ++r) {
+            const bool is_a = r == 0;
+            if (is_a && !has_a) continue;
+            char* base = buf + (is_a ? 0 : G::A_IMG);
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh) {
+                const int row = trow[r];
+                const int ch = lch ^ ((row >> 1) & 3);
+                const int k0 = (kbeg + kt) * BK2 + kh * 32;
+                char* dst = base + kh * (is_a ? BM * 64 : 256 * 64) + grow[r] * 64;
+                __builtin_amdgcn_global_load_lds(GLB_PTR(void, src[r] + k0 + ch * 8), LDS_PTR(void, dst), 16, 0, 0);
+            }
+        }
+    };
+    if (INITC && kbeg == 0) {
+        load_c_acc<BM / 32, 4>(p, m0 + wr * (BM / 2), n0 + wc * 64, acc);
+    } else {
+#pragma unroll
+        for (int i = 0; i < BM / 32; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int frow = lane & 15, fch = lane >> 4;
+    bf16x8 fa[FA][2], fb0[2][2], fb1[2][2];
+    auto read_a = [&](const char* buf) {
+#pragma unroll
+        for (int i = 0; i < FA; ++i)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+                fa[i][s] = *reinterpret_cast<const bf16x8*>(buf + img<BM>(wr * (BM / 2) + i * 16 + frow, s, fch));
+    };
+    auto read_b = [&](const char* buf, int ni, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+                fb[j][s] = *reinterpret_cast<const bf16x8*>(buf + G::A_IMG + img<256>(wc * 64 + ni * 32 + j * 16 + frow, s, fch));
+    };
+    auto mma = [&](int ni, const bf16x8 (&fb)[2][2]) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int i = 0; i < FA; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    f32x4& c = acc[i][ni * 2 + j];
+                    if constexpr (NTERM == P_F16)
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[j][s]),
+                                                                   __builtin_bit_cast(f16x8, fa[i][s]), c, 0, 0, 0);
+                    else
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], c, 0, 0, 0);
+                }
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto sync_in = [&]() {
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto sync_out = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // prologue: tiles 0 and 1 in flight, wait for tile 0 (this wave's 6 LDS-DMA per tile, 4 without RA)
+    issue_tile(0);
+    if (nk > 1) {
+        issue_tile(1);
+        if (has_a) wait_vm<6>();
+        else wait_vm<4>();
+    } else {
+        wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;
+    if (late) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    for (int t = 0; t < nk; ++t) {
+        const char* buf = smem + (t % 3) * G::TILE;
+        // phase 0: A + B(n0); tile t+2 into the buffer tile t-1 used
+        read_b(buf, 0, fb0);
+        read_a(buf);
+        if (t + 2 < nk) issue_tile(t + 2);
+        sync_in();
+        mma(0, fb0);
+        sync_out();
+        // phase 1: B(n1); publish tile t+1 (tile t+2 stays in flight)
+        read_b(buf, 1, fb1);
+        if (t + 2 < nk) {
+            if (has_a) wait_vm<6>();
+            else wait_vm<4>();
+        } else {
+            wait_vm<0>();
+        }
+        sync_in();
+        mma(1, fb1);
+        sync_out();
+    }
+    if (!late) __builtin_amdgcn_s_barrier();
+}
+
+template <int BM, int EPI>
+__global__ __launch_bounds__(512, 1) void phased3_kernel(EngineArgs p) {
+    __shared__ __attribute__((aligned(16))) char smem[3 * ph::Cfg<BM>::TILE];
+    if (gated_off(p)) return;
+    const int tiles_m = (p.m + BM - 1) / BM;
+    const int nwg = gridDim.x;
+    const int hw = blockIdx.x;
+    const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
+    int tm, tn;
+    tile_coords(wg, tiles_m, p.n / ph::BN, p.group_m, tm, tn);
+    f32x4 acc[BM / 32][4];
+    phased3_mainloop<BM, 1, EPI == E_ADD>(p, smem, tm * BM, tn * ph::BN, 0, p.k / ph::BK2, acc);
+    engine_epilogue<Tile<BM, 256, 2, 4, 4>, EPI>(p, tm * BM, tn * ph::BN, acc);
+}
+
 template <int BM, int EPI, int NTERM, bool GATHER>
 __global__ __launch_bounds__(512, 1) void phased_kernel(EngineArgs p) {
     __shared__ __attribute__((aligned(16))) char smem[ph::Cfg<BM>::LDS];
@@ -933,10 +1109,10 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
         int tm, tn;
         tile_coords(wg, tiles_m, p.n / BN, p.group_m, tm, tn);
         const int m0 = tm * BM, n0 = tn * BN;
-        engine_mainloop<C, NTERM, GATHER, EPI == E_ADD>(p, smem, m0, n0, 0, p.k / BK, acc);
+        engine_mainloop<C, NTERM, GATHER, EPI == E_ADD>(p, smem, m0, n0, 0, p.k / (BK * C::KH), acc);
         engine_epilogue<C, EPI>(p, m0, n0, acc);
     } else {
-        const int iters = p.k / BK;
+        const int iters = p.k / (BK * C::KH);
         const int64_t total = (int64_t)tiles_m * (p.n / BN) * iters;
         int64_t it = total * wg / nwg;
         const int64_t it_end = total * (wg + 1) / nwg;
@@ -1175,6 +1351,19 @@ using T256x64 = Tile<256, 64, 4, 1, 4>;  // fp16 convolutions with <= 64 output 
 using T96x256 = Tile<96, 256, 2, 4, 3>;
 using T64x256 = Tile<64, 256, 2, 4, 3>;
 using T64x256w4 = Tile<64, 256, 1, 4, 3>;
+// deeper rings (cold weights / activations come from HBM or the MALL: more K-steps in flight per block)
+using T96x256s5 = Tile<96, 256, 2, 4, 5>;
+using T96x256s6 = Tile<96, 256, 2, 4, 6>;
+using T64x256s6 = Tile<64, 256, 2, 4, 6>;
+using T128s6 = Tile<128, 128, 2, 2, 6>;
+using T128w8s6 = Tile<128, 128, 2, 4, 6>;
+// 64-deep K-steps (two 32-deep planes per stage: half the barriers)
+using T128k2s3 = Tile<128, 128, 2, 2, 3, 2>;
+using T128k2s4 = Tile<128, 128, 2, 2, 4, 2>;
+using T128w8k2s4 = Tile<128, 128, 2, 4, 4, 2>;
+using T96x256k2 = Tile<96, 256, 2, 4, 3, 2>;
+using T64x256k2 = Tile<64, 256, 2, 4, 3, 2>;
+using T64x256w4k2 = Tile<64, 256, 1, 4, 3, 2>;
 
 int pick_group_m(int tiles_m, int tiles_n, int bm, int bn, int64_t per_xcd) {
     if (const char* env = getenv("RF_GEMM_GROUP_M")) return std::max(1, std::min(tiles_m, atoi(env)));
@@ -1277,40 +1466,44 @@ int sk_grid(int m, int n, int k) {
     return grid;
 }
 
-// Tile choice by a measured cost model (tools/kbench.py gemm, profiles/r2_*): a launch of T tiles on 256 CUs
-// (x slots blocks per CU) takes ceil(T / (256 slots)) rounds, each `fixed + per_k * K / 1024` us.  Per config:
-//   256  phased 256x256          6.7 + 24.3   (best per FLOP; needs >= ~1 round of tiles)
-//   1282 phased 128x256          5.6 + 14.6
-//   963  phased  96x256          8.0 + 11.1   (M = 5,649, N = 1,024: 236 tiles = one round)
-//   643  phased  64x256          8.0 + 10.6   (M = 4,096, N = 1,024: 256 tiles = one round)
-//   962  ring    96x256          7.5 + 14.0
-//   128  ring   128x128          5.0 + 12.2 at <= 256 tiles (one block per CU), 9.0 + 14.5 per 512 (two)
-// The residual epilogue (C += ...) reads its C tile up front (load_c_acc); all configs pay it alike.
-int pick_cfg(int m, int n, int k) {
+// Tile choice by a measured cost model (tools/kbench.py coldgemm: operands rotated over > 512 MB so every call
+// reads them from HBM, as in the frame where each layer's weights are read once; profiles/r2_gemm_cold.log).
+// A launch of T tiles takes ceil(T / (256 x slots)) rounds of `fixed + per_k * K/1024 (+ add)` us each, where
+// `add` is the residual epilogue's cost (C tile read up front + fp32 store):
+//   256   phased 256x256, 2 buffers     11.0 + 20.4   add 5
+//   1282  phased 128x256, 2 buffers      2.3 + 18.4   add 5
+//   964   phased  96x256, 3 buffers      6.0 + 14.4   add 5    (M = 5,649, N = 1,024: 236 tiles = one round)
+//   645   phased  64x256, 3 buffers      6.5 + 11.8   add 5    (M = 4,096, N = 1,024: 256 tiles)
+//   962   ring    96x256, 32-deep steps  2.2 + 16.5   add 13
+//   12884 ring   128x128, 8 waves, 64-deep steps, 4 stages   6.8 + 10.9   add 5
+//   128   ring   128x128, 4 waves: 5.5 + 13.1 at <= 256 tiles, else two blocks per CU 11 + 14 per 512
+int pick_cfg(int m, int n, int k, int epilogue = RF_EPI_BF16) {
     if (const char* env = getenv("RF_GEMM_TILE")) return atoi(env);
     const char* ph = getenv("RF_GEMM_PHASED");
     const bool phased = n % 256 == 0 && k % 64 == 0 && (!ph || atoi(ph) != 0);
     const double kk = k / 1024.0;
-    auto cost = [&](int bm, int bn, int slots, double fixed, double per_k) {
+    const bool add = epilogue == RF_EPI_ADD_F32;
+    auto cost = [&](int bm, int bn, int slots, double fixed, double per_k, double add_cost) {
         const int64_t tiles = (int64_t)((m + bm - 1) / bm) * (n / bn);
         const int64_t rounds = (tiles + 256 * slots - 1) / (256 * slots);
-        return rounds * (fixed + per_k * kk);
+        return rounds * (fixed + per_k * kk + (add ? add_cost : 0.0));
     };
     int best = 128;
     const int64_t t128 = (int64_t)((m + 127) / 128) * (n / 128);
-    double best_c = t128 <= 256 ? cost(128, 128, 1, 5.0, 12.2) : cost(128, 128, 2, 9.0, 14.5);
+    double best_c = t128 <= 256 ? cost(128, 128, 1, 5.5, 13.1, 5.0) : cost(128, 128, 2, 11.0, 14.0, 5.0);
     auto consider = [&](int cfg, double c) {
         if (c < best_c) {
             best_c = c;
             best = cfg;
         }
     };
-    if (n % 256 == 0) consider(962, cost(96, 256, 1, 7.5, 14.0));
+    if (k % 64 == 0) consider(12884, cost(128, 128, 1, 6.8, 10.9, 5.0));
+    if (n % 256 == 0) consider(962, cost(96, 256, 1, 2.2, 16.5, 13.0));
     if (phased) {
-        consider(256, cost(256, 256, 1, 6.7, 24.3));
-        consider(1282, cost(128, 256, 1, 5.6, 14.6));
-        consider(963, cost(96, 256, 1, 8.0, 11.1));
-        consider(643, cost(64, 256, 1, 8.0, 10.6));
+        consider(256, cost(256, 256, 1, 11.0, 20.4, 5.0));
+        consider(1282, cost(128, 256, 1, 2.3, 18.4, 5.0));
+        consider(964, cost(96, 256, 1, 6.0, 14.4, 5.0));
+        consider(645, cost(64, 256, 1, 6.5, 11.8, 5.0));
     }
     return best;
 }
@@ -1326,6 +1519,25 @@ int launch_phased(EngineArgs a, void* stream, const char* what) {
     a.group_m = pick_group_m(tiles_m, tiles_n, BM, 256, (nwg + 7) / 8);
     hipLaunchKernelGGL((phased_kernel<BM, EPI, NTERM, GATHER>), dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
     return rf::check_launch(what);
+}
+
+template <int EPI, int BM>
+int launch_phased3(EngineArgs a, void* stream, const char* what) {
+    const int tiles_m = (a.m + BM - 1) / BM, tiles_n = a.n / 256;
+    const int nwg = tiles_n * tiles_m;
+    a.group_m = pick_group_m(tiles_m, tiles_n, BM, 256, (nwg + 7) / 8);
+    hipLaunchKernelGGL((phased3_kernel<BM, EPI>), dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    return rf::check_launch(what);
+}
+
+template <int BM>
+int run_phased3(const EngineArgs& p, int epilogue, void* stream) {
+    switch (epilogue) {
+        case RF_EPI_BF16: return launch_phased3<E_BF16, BM>(p, stream, "rf_gemm_bf16");
+        case RF_EPI_F32: return launch_phased3<E_F32, BM>(p, stream, "rf_gemm_bf16");
+        case RF_EPI_ADD_F32: return launch_phased3<E_ADD, BM>(p, stream, "rf_gemm_bf16");
+        default: return launch_phased3<E_SWIGLU, BM>(p, stream, "rf_gemm_bf16");
+    }
 }
 
 template <int EPI>
@@ -1377,6 +1589,11 @@ int run_dp(int cfg, const EngineArgs& p, int epilogue, void* stream) {
     if (cfg == 2561) return run_dp_cfg<T256x128>(p, epilogue, stream);
     if (cfg == 962 && p.n % 256 == 0) return run_dp_cfg<T96x256>(p, epilogue, stream);
     if (cfg == 642 && p.n % 256 == 0) return run_dp_cfg<T64x256>(p, epilogue, stream);
+    if (use_phased(p.n, p.k)) {  // three-buffer phased short tiles
+        if (cfg == 1283) return run_phased3<128>(p, epilogue, stream);
+        if (cfg == 964) return run_phased3<96>(p, epilogue, stream);
+        if (cfg == 645) return run_phased3<64>(p, epilogue, stream);
+    }
     if (cfg == 963 && use_phased(p.n, p.k)) {  // phased 96x256
         switch (epilogue) {
             case RF_EPI_BF16: return launch_phased<E_BF16, 1, false, 96>(p, stream, "rf_gemm_bf16");
@@ -1394,6 +1611,19 @@ int run_dp(int cfg, const EngineArgs& p, int epilogue, void* stream) {
         }
     }
     if (cfg == 644 && p.n % 256 == 0) return run_dp_cfg<T64x256w4>(p, epilogue, stream);
+    if (cfg == 965 && p.n % 256 == 0) return run_dp_cfg<T96x256s5>(p, epilogue, stream);
+    if (cfg == 966 && p.n % 256 == 0) return run_dp_cfg<T96x256s6>(p, epilogue, stream);
+    if (cfg == 646 && p.n % 256 == 0) return run_dp_cfg<T64x256s6>(p, epilogue, stream);
+    if (cfg == 1286) return run_dp_cfg<T128s6>(p, epilogue, stream);
+    if (cfg == 1288) return run_dp_cfg<T128w8s6>(p, epilogue, stream);
+    if (p.k % 64 == 0) {
+        if (cfg == 12823) return run_dp_cfg<T128k2s3>(p, epilogue, stream);
+        if (cfg == 12824) return run_dp_cfg<T128k2s4>(p, epilogue, stream);
+        if (cfg == 12884) return run_dp_cfg<T128w8k2s4>(p, epilogue, stream);
+        if (cfg == 9623 && p.n % 256 == 0) return run_dp_cfg<T96x256k2>(p, epilogue, stream);
+        if (cfg == 6423 && p.n % 256 == 0) return run_dp_cfg<T64x256k2>(p, epilogue, stream);
+        if (cfg == 6443 && p.n % 256 == 0) return run_dp_cfg<T64x256w4k2>(p, epilogue, stream);
+    }
     return run_dp_cfg<T128>(p, epilogue, stream);
 }
 
@@ -1449,7 +1679,8 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
             default: return launch_phased_sk<E_SWIGLU>(p, 256, stream, "rf_gemm_bf16");
         }
     }
-    const bool big = pick_cfg(m, n, k) != 128;
+    const int cfg = pick_cfg(m, n, k, epilogue);
+    const bool big = cfg != 128;
     const int grid = (!big && workspace && ws_bytes >= SK_WS_BYTES) ? sk_grid(m, n, k) : 0;
     if (grid) {
         sk_setup(p, workspace);
@@ -1471,7 +1702,7 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
             default: return launch_sk<T256, E_SWIGLU>(p, 256, stream, "rf_gemm_bf16");
         }
     }
-    return run_dp(pick_cfg(m, n, k), p, epilogue, stream);
+    return run_dp(cfg, p, epilogue, stream);
 }
 
 extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,

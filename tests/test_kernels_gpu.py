@@ -93,7 +93,9 @@ def test_gemm_stream_k(monkeypatch, grid, m, n, k):
 
 
 TILES = {"256ph": "256", "128x256ph": "1282", "96x256ph": "963", "64x256ph": "643", "256ring": "256",
-         "96x256ring": "962", "64x256ring": "642", "64x256ring4w": "644", "128ring": "128"}
+         "96x256ring": "962", "64x256ring": "642", "64x256ring4w": "644", "128ring": "128",
+         "128x256ph3": "1283", "96x256ph3": "964", "64x256ph3": "645", "128ring8wk64": "12884", "128ringk64": "12823",
+         "96x256ringk64": "9623", "96x256ring6": "966"}
 
 
 @pytest.mark.parametrize("tile", list(TILES))

@@ -243,3 +243,49 @@ def skstamps():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "skstamps":
     skstamps()
+
+
+def coldgemm():
+    """The frame's projection GEMMs under frame-like cache state: operands rotate over enough copies
+    (> 512 MB) that every call reads A and W from HBM (in the frame each layer's weights are read once per
+    frame and A was written by the previous kernel).  KB_TILES: comma list of RF_GEMM_TILE codes (auto = the
+    cost model's pick)."""
+    shapes = [("s1 qkv", S, 3 * D, D, ops.EPI_BF16), ("s1 out", S, D, D, ops.EPI_ADD_F32),
+              ("s1 w2", S, D, F, ops.EPI_ADD_F32), ("s2 q", R, D, D, ops.EPI_BF16),
+              ("s2 qkv", R, 3 * D, D, ops.EPI_BF16), ("s2 out", R, D, D, ops.EPI_ADD_F32),
+              ("s2 w2", R, D, F, ops.EPI_ADD_F32), ("kvall", S, 20 * D, D, ops.EPI_BF16)]
+    if os.environ.get("KB_SHAPES"):
+        shapes = [x for x in shapes if x[0] in os.environ["KB_SHAPES"].split(",")]
+    tiles = os.environ.get("KB_TILES", "auto").split(",")
+    for name, m, n, k, epi in shapes:
+        per = m * k * 2 + n * k * 2 + m * n * 4
+        nrot = max(2, int((768 << 20) // per) + 1)
+        sets = []
+        for _ in range(nrot):
+            a = torch.randn(m, k, device=dev).bfloat16()
+            w = (torch.randn(n, k, device=dev) / math.sqrt(k)).bfloat16()
+            c = (torch.empty(m, n, device=dev, dtype=torch.bfloat16) if epi == ops.EPI_BF16
+                 else torch.zeros(m, n, device=dev))
+            sets.append((a, w, c))
+        for t in tiles:
+            if t == "auto":
+                os.environ.pop("RF_GEMM_TILE", None)
+            else:
+                os.environ["RF_GEMM_TILE"] = t
+            i = [0]
+
+            def run():
+                a, w, c = sets[i[0] % nrot]
+                i[0] += 1
+                ops.gemm(a, w, c, None, epi)
+            ms = timeit(run, reps=3 * nrot)
+            err = check(sets[0][0], sets[0][1], epi)
+            print(f"cold gemm {name:7s} {m}x{n}x{k} tile={t:5s}: {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF  "
+                  f"relerr {err:.1e}  ({nrot} rotating operand sets)", flush=True)
+        os.environ.pop("RF_GEMM_TILE", None)
+        del sets
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "coldgemm":
+    coldgemm()
