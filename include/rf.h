@@ -96,6 +96,19 @@ int rf_gemm_bf16_if(const int* flag, const void* a, int64_t lda, const void* w, 
                     const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
                     void* stream);
 
+/* MX fp8 GEMM: C[M,N] (epilogue) A[M,K] * W[N,K]^T with OCP e4m3 operands (bytes, row strides lda/ldw in
+ * bytes) and one E8M0 scale byte per 32 K-elements of every row (sa [M][ld_sa], sw [N][ld_sw]; value =
+ * e4m3 * 2^(scale - 127)), fp32 accumulation on v_mfma_scale_f32_16x16x128_f8f6f4.  K % 128 == 0, N % 256 == 0.
+ * Same epilogues as rf_gemm_bf16 (RF_EPI_ADD_F32 accumulates into C).  The stage-2 fp8 mode of the model
+ * (RenderFormer(fp8=True)) runs its projections through this. */
+int rf_gemm_mx8(const void* a, int64_t lda, const void* sa, int64_t ld_sa, const void* w, int64_t ldw, const void* sw,
+                int64_t ld_sw, void* c, int64_t ldc, const float* bias, int m, int n, int k, int epilogue,
+                void* stream);
+/* bf16 rows x[rows][cols] -> e4m3 q[rows][ldq] + E8M0 scales[rows][ld_s] per 32-element block: scale
+ * 2^ceil(log2(amax / 448)) (no saturation), round to nearest even. */
+int rf_quant_mx8(const void* x, int64_t ldx, int rows, int cols, void* q, int64_t ldq, void* scales, int64_t ld_s,
+                 void* stream);
+
 /* out(bf16)[r, :] = x[r, :] * rsqrt(mean(x^2) + eps) * weight ; x f32. */
 int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, float eps, void* out, int64_t ldo,
                int rows, int dim, void* stream);

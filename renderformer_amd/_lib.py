@@ -49,6 +49,8 @@ SIGNATURES = {
     "rf_deconv2d_f16": [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P, _I, _P, _L, _P],
     "rf_split_planes": [_P, _L, _I, _L, _P, _P, _I, _I, _P],
     "rf_upsample_bilinear": [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _I, _P],
+    "rf_gemm_mx8": [_P, _L, _P, _L, _P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _P],
+    "rf_quant_mx8": [_P, _L, _I, _I, _P, _L, _P, _L, _P],
     "rf_device_error": [],
     "rf_clear_device_error": [],
     "rf_debug_raise_device_error": [_I, _P],

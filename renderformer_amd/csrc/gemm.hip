@@ -92,6 +92,10 @@ struct EngineArgs {
     int* err;         // device error word (rf::device_error_word): stream-K hand-off timeouts
     int spin;         // stream-K hand-off spin bound (polls)
     uint64_t* stamps; // diagnostics (RF_GEMM_STAMPS=1): per-block s_memtime stamps, [grid][16]; normally null
+    // MX fp8 operands (rf_gemm_mx8): per-row E8M0 scales of every 32-element K block, [rows][ld_s] bytes
+    const uint8_t* sa;
+    const uint8_t* sw;
+    int ld_sa, ld_sw;
 };
 
 // uniform early exit of a gated launch (every block reads the same flag, so a stream-K grid exits whole)
@@ -1510,6 +1514,192 @@ int pick_cfg(int m, int n, int k, int epilogue = RF_EPI_BF16) {
 
 __device__ __attribute__((aligned(16))) bf16_t g_zero_row[64];  // stays zero: source of padded conv taps
 
+// ---------------------------------------------------------------------------------------------
+// MX fp8 GEMM (OCP e4m3 operands, one E8M0 scale per 32 K-elements of every row, fp32 accumulate) on the
+// block-scaled v_mfma_scale_f32_16x16x128_f8f6f4: twice the bf16 MFMA rate.  C[M,N] (epilogue) A[M,K] W[N,K]^T
+// with A = a * 2^(sa - 127), W = w * 2^(sw - 127) blockwise.  Tile 256x256, 8 waves of 128x64 (8 x 4 MFMAs of
+// 16x16x128 per 128-deep K-step), 2-stage LDS ring filled by LDS-DMA: operand rows of 128 B with the 16-B
+// chunk index XOR (row & 7) (pre-swizzled source address, the same XOR on the read), and the step's scale
+// dwords (4 blocks per row) staged beside them.  Fragment map (ck_tile WarpGemmAttributeMfmaImpl_f32_16x16x128):
+// lane l holds row l & 15, K bytes 32 (l >> 4) .. +31, and the scale of that row's K block (l >> 4); the W
+// fragment is the instruction's first operand, so each lane's accumulator holds 4 consecutive output columns
+// of one row, as in the bf16 engine (engine_epilogue applies unchanged).
+namespace mx {
+constexpr int BM = 256, BN = 256, KS = 128;  // KS: K bytes (= elements) per step
+constexpr int A_DATA = BM * KS, B_DATA = BN * KS;
+constexpr int STAGE = A_DATA + B_DATA + (BM + BN) * 4;
+constexpr int TI = 8, TJ = 4;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+RF_DEV int off(int row, int ch) { return row * KS + ((ch ^ (row & 7)) << 4); }
+}  // namespace mx
+
+template <bool INITC>
+RF_DEV void mx8_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int kbeg, int kend,
+                         f32x4 (&acc)[mx::TI][mx::TJ]) {
+    using namespace mx;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int nk = kend - kbeg;
+    const uint8_t* A = reinterpret_cast<const uint8_t*>(p.a);
+    const uint8_t* W = reinterpret_cast<const uint8_t*>(p.w);
+    // data pieces: 8 rows x 128 B per wave-instruction; pieces 0..31 = A, 32..63 = W; 8 per wave
+    auto issue = [&](int kt, int buf) {
+        char* st = smem + buf * STAGE;
+        const int64_t k0 = (int64_t)(kbeg + kt) * KS;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int piece = wave * 8 + i;
+            const bool is_a = piece < BM / 8;
+            const int row = (is_a ? piece : piece - BM / 8) * 8 + (lane >> 3);
+            const int ch = (lane & 7) ^ (row & 7);  // logical chunk landing at physical chunk lane & 7
+            const uint8_t* src;
+            if (is_a) {
+                const int m = m0 + row;
+                src = A + (int64_t)(m < p.m ? m : p.m - 1) * p.lda + k0 + ch * 16;
+            } else {
+                src = W + (int64_t)(n0 + row) * p.ldw + k0 + ch * 16;
+            }
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, src), LDS_PTR(void, st + (is_a ? 0 : A_DATA) + piece % (BM / 8) * 1024),
+                                             16, 0, 0);
+        }
+        // scales: wave w < 4 stages A rows 64 w + lane, waves 4..7 W rows 64 (w - 4) + lane (one dword each)
+        {
+            const bool is_a = wave < BM / 64;
+            const int row = (is_a ? wave : wave - BM / 64) * 64 + lane;
+            const uint8_t* src;
+            if (is_a) {
+                const int m = m0 + row;
+                src = p.sa + (int64_t)(m < p.m ? m : p.m - 1) * p.ld_sa + (kbeg + kt) * 4;
+            } else {
+                src = p.sw + (int64_t)(n0 + row) * p.ld_sw + (kbeg + kt) * 4;
+            }
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, src),
+                                             LDS_PTR(void, st + A_DATA + B_DATA + (is_a ? 0 : BM * 4) + (row & ~63) * 4),
+                                             4, 0, 0);
+        }
+    };
+    if (INITC && kbeg == 0) {
+        load_c_acc<TI, TJ>(p, m0 + wm * 128, n0 + wn * 64, acc);
+    } else {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int frow = lane & 15, g = lane >> 4;
+    issue(0, 0);
+    if (nk > 1) {
+        issue(1, 1);
+        wait_vm<9>();
+    } else {
+        wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt < nk; ++kt) {
+        const char* st = smem + (kt & 1) * STAGE;
+        const int* sca = reinterpret_cast<const int*>(st + A_DATA + B_DATA);
+        const int* scw = sca + BM;
+        i32x8 fa[TI], fw[TJ];
+        int sa[TI], sw[TJ];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+            const int row = wm * 128 + i * 16 + frow;
+            const u32x4 lo = *reinterpret_cast<const u32x4*>(st + off(row, 2 * g));
+            const u32x4 hi = *reinterpret_cast<const u32x4*>(st + off(row, 2 * g + 1));
+            fa[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+            sa[i] = (sca[row] >> (8 * g)) & 0xff;
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+            const int row = wn * 64 + j * 16 + frow;
+            const u32x4 lo = *reinterpret_cast<const u32x4*>(st + A_DATA + off(row, 2 * g));
+            const u32x4 hi = *reinterpret_cast<const u32x4*>(st + A_DATA + off(row, 2 * g + 1));
+            fw[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+            sw[j] = (scw[row] >> (8 * g)) & 0xff;
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fw[j], fa[i], acc[i][j], 0, 0, 0, sw[j], 0,
+                                                                             sa[i]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // (every read of stage kt & 1 retired)
+        __builtin_amdgcn_s_barrier();
+        if (kt + 2 < nk) {
+            issue(kt + 2, kt & 1);
+            wait_vm<9>();
+        } else {
+            wait_vm<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+    }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void mx8_kernel(EngineArgs p) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * mx::STAGE];
+    const int tiles_m = (p.m + mx::BM - 1) / mx::BM;
+    const int nwg = gridDim.x;
+    const int hw = blockIdx.x;
+    const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
+    int tm, tn;
+    tile_coords(wg, tiles_m, p.n / mx::BN, p.group_m, tm, tn);
+    f32x4 acc[mx::TI][mx::TJ];
+    mx8_mainloop<EPI == E_ADD>(p, smem, tm * mx::BM, tn * mx::BN, 0, p.k / mx::KS, acc);
+    engine_epilogue<Tile<256, 256, 2, 4, 4>, EPI>(p, tm * mx::BM, tn * mx::BN, acc);
+}
+
+// MX quantisation of bf16 rows: every 32-element block gets the E8M0 scale 2^e with e = ceil(log2(amax / 448))
+// (the block's largest |value| lands in (224, 448], never saturating e4m3), values x / 2^e rounded to nearest
+// even e4m3 (hardware v_cvt_pk_fp8_f32).  One thread per block: 64 B in, 32 B + 1 scale byte out.
+__global__ __launch_bounds__(256) void quant_mx8_kernel(const bf16_t* __restrict__ x, int64_t ldx, int rows, int cols,
+                                                        uint8_t* __restrict__ q, int64_t ldq, uint8_t* __restrict__ sc,
+                                                        int64_t lds) {
+    const int nb = cols / 32;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)rows * nb) return;
+    const int row = (int)(t / nb), b = (int)(t % nb);
+    const uint4* src = reinterpret_cast<const uint4*>(x + (int64_t)row * ldx + b * 32);
+    float v[32];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint4 u = src[i];
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            v[i * 8 + 2 * e] = __uint_as_float(w[e] << 16);
+            v[i * 8 + 2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+        }
+    }
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) amax = fmaxf(amax, fabsf(v[i]));
+    int e = -127;
+    if (amax > 0.f) {
+        // smallest e with amax / 2^e <= 448: frexp gives amax = f 2^x (f in [0.5, 1)); 448 = 0.875 2^9
+        int ex;
+        const float f = frexpf(amax, &ex);
+        e = ex - 9 + (f > 0.875f ? 1 : 0);
+        e = e < -127 ? -127 : (e > 127 ? 127 : e);
+    }
+    const float inv = ldexpf(1.0f, -e);
+    uint32_t out[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        int pk = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * i] * inv, v[4 * i + 1] * inv, 0, false);
+        pk = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * i + 2] * inv, v[4 * i + 3] * inv, pk, true);
+        out[i] = (uint32_t)pk;
+    }
+    uint4* dst = reinterpret_cast<uint4*>(q + (int64_t)row * ldq + b * 32);
+    dst[0] = make_uint4(out[0], out[1], out[2], out[3]);
+    dst[1] = make_uint4(out[4], out[5], out[6], out[7]);
+    sc[(int64_t)row * lds + b] = (uint8_t)(e + 127);
+}
+
 }  // namespace
 
 template <int EPI, int NTERM, bool GATHER, int BM = 256>
@@ -1716,6 +1906,60 @@ extern "C" int rf_gemm_bf16_if(const int* flag, const void* a, int64_t lda, cons
                                int64_t ws_bytes, void* stream) {
     RF_REQUIRE(flag, "rf_gemm_bf16_if: null flag");
     return gemm_bf16(a, lda, w, ldw, c, ldc, bias, m, n, k, epilogue, workspace, ws_bytes, stream, flag);
+}
+
+extern "C" int rf_gemm_mx8(const void* a, int64_t lda, const void* sa, int64_t ld_sa, const void* w, int64_t ldw,
+                           const void* sw, int64_t ld_sw, void* c, int64_t ldc, const float* bias, int m, int n, int k,
+                           int epilogue, void* stream) {
+    RF_REQUIRE(a && w && sa && sw && c, "rf_gemm_mx8: null pointer");
+    RF_REQUIRE(m > 0 && n > 0 && k > 0, "rf_gemm_mx8: empty problem");
+    RF_REQUIRE(k % 128 == 0 && n % 256 == 0, "rf_gemm_mx8: K=%d must be a multiple of 128 and N=%d of 256", k, n);
+    RF_REQUIRE(lda % 16 == 0 && ldw % 16 == 0 && lda >= k && ldw >= k, "rf_gemm_mx8: lda/ldw (bytes) >= K, 16-B aligned");
+    RF_REQUIRE(ld_sa % 4 == 0 && ld_sw % 4 == 0 && ld_sa >= k / 32 && ld_sw >= k / 32,
+               "rf_gemm_mx8: scale rows must hold K/32 bytes, 4-B aligned");
+    RF_REQUIRE(((uintptr_t)a & 15) == 0 && ((uintptr_t)w & 15) == 0 && ((uintptr_t)sa & 3) == 0 && ((uintptr_t)sw & 3) == 0,
+               "rf_gemm_mx8: operands 16-B / scales 4-B aligned");
+    RF_REQUIRE(epilogue >= RF_EPI_BF16 && epilogue <= RF_EPI_SWIGLU, "rf_gemm_mx8: bad epilogue %d", epilogue);
+    RF_REQUIRE(ldc >= (epilogue == RF_EPI_SWIGLU ? n / 2 : n) && ldc % 4 == 0, "rf_gemm_mx8: ldc too small/unaligned");
+    EngineArgs p{};
+    p.a = (const bf16_t*)a;
+    p.lda = lda;
+    p.w = (const bf16_t*)w;
+    p.ldw = ldw;
+    p.sa = (const uint8_t*)sa;
+    p.sw = (const uint8_t*)sw;
+    p.ld_sa = (int)ld_sa;
+    p.ld_sw = (int)ld_sw;
+    p.m = m;
+    p.n = n;
+    p.k = k;
+    p.c = c;
+    p.ldc = ldc;
+    p.bias = bias;
+    const int tiles_m = (m + 255) / 256, tiles_n = n / 256;
+    const int nwg = tiles_m * tiles_n;
+    p.group_m = pick_group_m(tiles_m, tiles_n, 256, 256, (nwg + 7) / 8);
+    const dim3 g(nwg), b(512);
+    hipStream_t st = (hipStream_t)stream;
+    switch (epilogue) {
+        case RF_EPI_BF16: hipLaunchKernelGGL((mx8_kernel<E_BF16>), g, b, 0, st, p); break;
+        case RF_EPI_F32: hipLaunchKernelGGL((mx8_kernel<E_F32>), g, b, 0, st, p); break;
+        case RF_EPI_ADD_F32: hipLaunchKernelGGL((mx8_kernel<E_ADD>), g, b, 0, st, p); break;
+        default: hipLaunchKernelGGL((mx8_kernel<E_SWIGLU>), g, b, 0, st, p); break;
+    }
+    return rf::check_launch("rf_gemm_mx8");
+}
+
+extern "C" int rf_quant_mx8(const void* x, int64_t ldx, int rows, int cols, void* q, int64_t ldq, void* scales,
+                            int64_t ld_s, void* stream) {
+    RF_REQUIRE(x && q && scales, "rf_quant_mx8: null pointer");
+    RF_REQUIRE(cols % 32 == 0 && ldx % 8 == 0 && ldq % 16 == 0 && ldq >= cols && ld_s >= cols / 32,
+               "rf_quant_mx8: cols %% 32, 16-B rows");
+    if (rows <= 0) return RF_OK;
+    const int64_t n = (int64_t)rows * (cols / 32);
+    hipLaunchKernelGGL(quant_mx8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, ldx, rows, cols, (uint8_t*)q, ldq, (uint8_t*)scales, ld_s);
+    return rf::check_launch("rf_quant_mx8");
 }
 
 // fp16 convolutions (one MFMA per product): the 256x256 tile when the filter bank is a multiple of 256

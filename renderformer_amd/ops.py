@@ -105,6 +105,75 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias: Optional[tor
     return out
 
 
+class MX8:
+    """An MX fp8 operand: e4m3 bytes q [rows, K] (uint8) + E8M0 block scales s [rows, K/32] (uint8)."""
+    __slots__ = ("q", "s")
+
+    def __init__(self, q: torch.Tensor, s: torch.Tensor):
+        self.q, self.s = q, s
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+    @classmethod
+    def empty(cls, rows: int, cols: int, device) -> "MX8":
+        return cls(torch.empty(rows, cols, dtype=torch.uint8, device=device),
+                   torch.empty(rows, cols // 32, dtype=torch.uint8, device=device))
+
+
+def quant_mx8(x: torch.Tensor, out: Optional[MX8] = None) -> MX8:
+    """bf16 rows -> MX fp8 (rf_quant_mx8: per-32 E8M0 scale 2^ceil(log2(amax/448)), RNE e4m3)."""
+    _dev(x, torch.bfloat16, "x")
+    rows, cols = x.shape
+    out = out or MX8.empty(rows, cols, x.device)
+    _check(out.q.shape == (rows, cols) and out.s.shape[0] == rows, "quant_mx8: output shape")
+    call("rf_quant_mx8", ptr(x), x.stride(0), rows, cols, ptr(out.q), out.q.stride(0), ptr(out.s), out.s.stride(0),
+         stream())
+    return out
+
+
+def gemm_mx8(a: MX8, w: MX8, out: torch.Tensor, bias: Optional[torch.Tensor] = None, epilogue: int = EPI_BF16,
+             tag: Optional[str] = None) -> torch.Tensor:
+    """out (epilogue)= dequant(a) @ dequant(w).T on the block-scaled fp8 MFMA (rf_gemm_mx8)."""
+    for t, n in ((a.q, "a"), (w.q, "w"), (a.s, "a scales"), (w.s, "w scales")):
+        _dev(t, torch.uint8, n)
+    m, k = a.q.shape
+    n, k2 = w.q.shape
+    _check(k == k2, f"gemm_mx8: K mismatch {k} vs {k2}")
+    want = torch.bfloat16 if epilogue in (EPI_BF16, EPI_SWIGLU) else torch.float32
+    _dev(out, want, "out")
+    ncols = n // 2 if epilogue == EPI_SWIGLU else n
+    _check(out.shape[0] == m and out.shape[1] == ncols, f"gemm_mx8: out shape {tuple(out.shape)} != ({m}, {ncols})")
+    if bias is not None:
+        _dev(bias, torch.float32, "bias")
+    ev = _t0(tag)
+    call("rf_gemm_mx8", ptr(a.q), a.q.stride(0), ptr(a.s), a.s.stride(0), ptr(w.q), w.q.stride(0), ptr(w.s),
+         w.s.stride(0), ptr(out), out.stride(0), ptr(bias), m, n, k, epilogue, stream())
+    _t1(ev)
+    return out
+
+
+def mx8_dequant_ref(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    """fp32 value of an MX fp8 tensor (any device; for tests and weight checks)."""
+    v = q.view(torch.float8_e4m3fn).float()
+    scale = torch.pow(2.0, s.float() - 127.0)
+    return (v.view(v.shape[0], -1, 32) * scale[:, :, None]).view(v.shape)
+
+
+def mx8_quant_ref(x: torch.Tensor):
+    """Reference MX quantisation on any device (torch float8_e4m3fn casts, RNE): the same rule as rf_quant_mx8.
+    Used for the weights at load time and as the tests' oracle for the device quantiser."""
+    rows, cols = x.shape
+    xb = x.float().view(rows, cols // 32, 32)
+    amax = xb.abs().amax(-1)
+    m, ex = torch.frexp(amax)
+    e = ex - 9 + (m > 0.875).to(ex.dtype)
+    e = torch.where(amax > 0, e, torch.full_like(e, -127)).clamp(-127, 127)
+    q = (xb * torch.pow(2.0, -e.float())[:, :, None]).to(torch.float8_e4m3fn).view(rows, cols)
+    return q.view(torch.uint8), (e + 127).to(torch.uint8)
+
+
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor) -> torch.Tensor:
     _dev(x, torch.float32, "x")
     _dev(out, torch.bfloat16, "out")
