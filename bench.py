@@ -44,6 +44,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "rendered frames/sec at 512×512, renderformer-v1.1-swin-large, 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_FP8_TFLOPS = 5000.0   # MI355X dense fp8 MFMA (same table)
 DOMINANT = "attn_stage1"   # largest single kernel family by time in the rocprof summary (profiles/)
 FIXTURE = ("large", 5633, 512, 1, 1, 1)  # tests/golden/large_cbox_r512.npz: config, N, res, views, scenes, seed
 
@@ -65,6 +66,8 @@ def parse(argv=None):
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo: CPU-side tests)")
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (1-GPU rehearsal)")
     ap.add_argument("--dump", default=None, help="rank 0 saves the gathered frames of the last step (.npy)")
+    ap.add_argument("--fp8", action="store_true", help="stage-2 projections + FFN as MX fp8 GEMMs (config 5's fp8 "
+                                                        "path); roofline then reports the stage-2 W13 fp8 GEMM")
     a = ap.parse_args(argv)
     if a.res is None:
         a.res = 1024 if a.workload == "c5" else 512
@@ -176,7 +179,7 @@ def main():
 
     cfg = named_config(args.config)
     sd = synthetic_state_dict(cfg, seed=0)
-    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd)).to(dev)
+    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd, fp8=args.fp8)).to(dev)
 
     # ---- the units of one step: (batch tensors on the device, global frame ids)
     if args.workload == "cbox":
@@ -242,7 +245,7 @@ def main():
         dist.barrier()
     # HIP events bracket the dominant kernel's launches in the LAST timed step only: each event pair adds
     # ~11 us of queue time around its launch (profiles/r1: 14 x 11.4 us per frame when every step was timed)
-    timer = ops.KernelTimer(DOMINANT)
+    timer = ops.KernelTimer("gemm_w13_stage2" if args.fp8 else DOMINANT)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -279,6 +282,9 @@ def main():
     if args.workload == "c4":  # launches differ in S: use the mean algorithmic FLOP of this rank's scenes
         ss = [int(b["mask"].sum()) + cfg.num_register_tokens for b in batches]
         kern_flops = 4 * cfg.latent_dim * statistics.mean(s * s for s in ss) if ss else 0
+    if args.fp8:  # the fp8 roofline object: stage-2 SwiGLU W13 GEMM, 2 M N K per launch, vs the fp8 peak
+        rows = sum(int(b["c2w"].shape[0] * b["c2w"].shape[1]) for b in batches) * (args.res // cfg.patch_size) ** 2
+        kern_flops = 2 * rows * 2 * cfg.view_transformer_ffn_hidden_dim * cfg.view_transformer_latent_dim
     achieved = kern_flops / (kern_ms * 1e-3) / 1e12 if durs else float("nan")
     traffic = None
     tpath = os.path.join(REPO, "profiles", "attn_stage1_traffic.json")
@@ -302,7 +308,7 @@ def main():
         rec = {
             "metric": METRIC, "value": round(fps, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": scaling, "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "scaling": scaling, "vs_baseline": None, "dtype": "bf16+fp8" if args.fp8 else "bf16", "data": "synthetic",
             "config": {
                 "workload": f"{'large-proxy' if args.config == 'large' else args.config} {wl}",
                 "model": "renderformer-v1.1-swin-large" if args.config == "large" else args.config,
@@ -314,7 +320,8 @@ def main():
                 "gather": "RCCL all_gather of the HDR frames" if world > 1 and args.backend == "nccl" else
                           (f"{args.backend} all_gather" if world > 1 else "none (1 rank)"),
                 "weights": "synthetic seed 0 (no checkpoint offline)",
-                "precision": "bf16 MFMA operands, fp32 accumulate/softmax/residual; DPT fp16 operands, fp32 accumulate",
+                "precision": ("stage-2 projections/FFN MX fp8 (e4m3, E8M0 per 32), " if args.fp8 else "") +
+                             "bf16 MFMA operands, fp32 accumulate/softmax/residual; DPT fp16 operands, fp32 accumulate",
             },
             "frame": {
                 "gflop_per_step": round(fl_step / 1e9, 1),
@@ -322,9 +329,12 @@ def main():
                 "mfma_frac_bf16_peak": round(fl_step * args.steps / elapsed / world / 1e12 / PEAK_BF16_TFLOPS, 4),
             },
             "roofline": {
-                "kernel": "rf_attn_fwd — stage-1 triangle self-attention (attn_sk_kernel: stream-K, in-kernel merge)",
-                "bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                "kernel": ("rf_gemm_mx8 — stage-2 SwiGLU W13 projection, MX fp8 (e4m3 + E8M0 per 32)" if args.fp8 else
+                           "rf_attn_fwd — stage-1 triangle self-attention (attn_sk_kernel: stream-K, in-kernel merge)"),
+                "bound": "mfma", "achieved": round(achieved, 1),
+                "peak": PEAK_FP8_TFLOPS if args.fp8 else PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / (PEAK_FP8_TFLOPS if args.fp8 else PEAK_BF16_TFLOPS), 4),
+                "traffic": None if args.fp8 else traffic,
                 "traffic_source": "profiles/attn_stage1_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE pass)"
                 if traffic is not None else None,
                 "avg_launch_ms": round(kern_ms, 4), "launches_per_step": per_step_launches,

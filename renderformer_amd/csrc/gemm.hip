@@ -1520,10 +1520,12 @@ __device__ __attribute__((aligned(16))) bf16_t g_zero_row[64];  // stays zero: s
 // with A = a * 2^(sa - 127), W = w * 2^(sw - 127) blockwise.  Tile 256x256, 8 waves of 128x64 (8 x 4 MFMAs of
 // 16x16x128 per 128-deep K-step), 2-stage LDS ring filled by LDS-DMA: operand rows of 128 B with the 16-B
 // chunk index XOR (row & 7) (pre-swizzled source address, the same XOR on the read), and the step's scale
-// dwords (4 blocks per row) staged beside them.  Fragment map (ck_tile WarpGemmAttributeMfmaImpl_f32_16x16x128):
-// lane l holds row l & 15, K bytes 32 (l >> 4) .. +31, and the scale of that row's K block (l >> 4); the W
+// dwords (4 blocks per row) staged beside them.  Lane l holds row l & 15 (see below for its K bytes); the W
 // fragment is the instruction's first operand, so each lane's accumulator holds 4 consecutive output columns
-// of one row, as in the bf16 engine (engine_epilogue applies unchanged).
+// of one row, as in the bf16 engine (engine_epilogue applies unchanged).  Measured K map (tools/fp8_probe.py,
+// structured data): the 16-B halves h = 0, 1 of lane group g = lane >> 4 are K elements 64 h + 16 g .. +15,
+// and the scale operand of lane group b scales K block b (elements 32 b .. 32 b + 31) — so a lane reads its
+// row's 16-B chunks g and g + 4 and passes the scale byte of block g.
 namespace mx {
 constexpr int BM = 256, BN = 256, KS = 128;  // KS: K bytes (= elements) per step
 constexpr int A_DATA = BM * KS, B_DATA = BN * KS;
@@ -1605,16 +1607,16 @@ RF_DEV void mx8_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int kb
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
             const int row = wm * 128 + i * 16 + frow;
-            const u32x4 lo = *reinterpret_cast<const u32x4*>(st + off(row, 2 * g));
-            const u32x4 hi = *reinterpret_cast<const u32x4*>(st + off(row, 2 * g + 1));
+            const u32x4 lo = *reinterpret_cast<const u32x4*>(st + off(row, g));
+            const u32x4 hi = *reinterpret_cast<const u32x4*>(st + off(row, g + 4));
             fa[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
             sa[i] = (sca[row] >> (8 * g)) & 0xff;
         }
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
             const int row = wn * 64 + j * 16 + frow;
-            const u32x4 lo = *reinterpret_cast<const u32x4*>(st + A_DATA + off(row, 2 * g));
-            const u32x4 hi = *reinterpret_cast<const u32x4*>(st + A_DATA + off(row, 2 * g + 1));
+            const u32x4 lo = *reinterpret_cast<const u32x4*>(st + A_DATA + off(row, g));
+            const u32x4 hi = *reinterpret_cast<const u32x4*>(st + A_DATA + off(row, g + 4));
             fw[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
             sw[j] = (scw[row] >> (8 * g)) & 0xff;
         }

@@ -224,3 +224,23 @@ def test_model_on_non_current_device():
         outs.append(pipe(d["triangles"], d["texture"], d["mask"], d["vn"], d["c2w"], d["fov"], resolution=res).cpu())
     assert torch.cuda.current_device() == 0
     assert rel_l2(outs[1], outs[0]) < 1e-6 and rel_l2(outs[1], z["hdr"]) < HDR_TOL
+
+
+@pytest.mark.parametrize("name", ["large_cbox_r512", "large_cbox_r1024_v4"])
+def test_fp8_stage2_parity_report(name):
+    """The fp8 mode (stage-2 projections and FFN as MX fp8 GEMMs, BASELINE config 5's 'fp8 MFMA path') against
+    the same reference fixtures.  e4m3 keeps 3 mantissa bits (bf16: 7), so this mode is NOT inside the 1e-3
+    north-star bar that the default bf16 path meets; the measured error is printed and recorded in DESIGN.md,
+    and the test bounds it so that a broken kernel (not the format) fails."""
+    from renderformer_amd import RenderFormer, RenderFormerRenderingPipeline
+    cfg, sd, inp, res, z = load_case(name)
+    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd, fp8=True)).to("cuda")
+    d = {k: v.cuda() for k, v in inp.items()}
+    out = pipe(d["triangles"], d["texture"], d["mask"], d["vn"], d["c2w"], d["fov"], resolution=res)
+    ref, st = reference_hdr(z)
+    got = out[:, :, ::st, ::st].cpu()
+    err, ac = rel_l2(got, ref), rel_l2_ac(got, ref)
+    print(f"fp8 stage 2, {name}: rel L2 {err:.3e} (deviation from the mean: {ac:.3e}); bf16 bar 1e-3")
+    assert err < 3e-2
+    del pipe, out, d
+    torch.cuda.empty_cache()
