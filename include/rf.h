@@ -55,7 +55,7 @@ extern "C" {
 #define RF_ERR_UNSUPPORTED 3
 #define RF_ERR_DEVICE 4       /* an earlier launch reported a device-side error (see rf_device_error) */
 
-#define RF_ABI_VERSION 6
+#define RF_ABI_VERSION 7
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -198,9 +198,12 @@ int rf_patchify_rays(const float* rays_d, int n_views, int res, int patch, void*
 /* Triangle positions for RoPE.  tris f32 [*, 9]; valid_idx int32 [sum n_b] (rows into tris, grouped by
  * scene, offsets scene_off[B+1]).  For each set s (s = b when c2w == NULL, else s = b*n_views + v with the
  * camera transform p -> R^T (p - t)), writes n_reg centre rows then the n_b triangle rows to
- * pos_out[set_off[s] ...]. */
+ * pos_out[set_off[s] ...].  max_tris >= every n_b; partials: rf_scene_pos_partials(sets, max_tris) floats of
+ * caller workspace (per-256-triangle sums, reduced in a fixed order: deterministic). */
 int rf_scene_pos(const float* tris, const int32_t* valid_idx, const int32_t* scene_off, const float* c2w,
-                 int n_scenes, int n_views, int n_reg, float* pos_out, const int32_t* set_off, void* stream);
+                 int n_scenes, int n_views, int n_reg, float* pos_out, const int32_t* set_off, int max_tris,
+                 float* partials, int64_t partial_floats, void* stream);
+int64_t rf_scene_pos_partials(int sets, int max_tris);
 
 /* out[out_rows[r]] = base[r % base_rows] + sum_t rmsnorm(in_t[r]) * w_t   (f32; in_t / w_t may be NULL). */
 int rf_embed(float* out, int64_t ldo, const int32_t* out_rows, int rows, int dim, const float* base,

@@ -38,7 +38,7 @@ SIGNATURES = {
     "rf_vn_encode": [_P, _L, _P, _I, _P, _L, _P],
     "rf_ray_tokens": [_P, _P, _I, _I, _I, _P, _P, _P],
     "rf_patchify_rays": [_P, _I, _I, _I, _P, _P],
-    "rf_scene_pos": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P],
+    "rf_scene_pos": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _I, _P, _L, _P],
     "rf_embed": [_P, _L, _P, _I, _I, _P, _I, _P, _L, _P, _F, _P, _L, _P, _F, _P],
     "rf_hdr_output": [_P, _P, _I, _I, _I, _I, _F, _I, _I, _P],
     "rf_conv2d_bf16x3": [_P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I,
@@ -89,6 +89,8 @@ def load(require_device: bool = True):
             lib.rf_attn_workspace_bytes.restype = ctypes.c_int64
             lib.rf_gemm_workspace_bytes.restype = ctypes.c_int64
             lib.rf_gemm_workspace_bytes.argtypes = []
+            lib.rf_scene_pos_partials.restype = ctypes.c_int64
+            lib.rf_scene_pos_partials.argtypes = [_I, _I]
             lib.rf_attn_workspace_bytes.argtypes = [_L, _I, _I]
             _lib = lib
     if require_device and not torch.cuda.is_available():

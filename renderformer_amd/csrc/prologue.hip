@@ -205,31 +205,35 @@ __global__ __launch_bounds__(256) void patchify_rays_kernel(const float* __restr
 // ----------------------------------------------------------------------------- RoPE positions
 // trans_to_cam_coord (transform.py:24-27: p -> R^T p - R^T t) and process_tri_vpos_list
 // (renderformer.py:111-122: register rows = masked mean position, averaged over the 3 vertices).
-__global__ __launch_bounds__(1024) void scene_pos_kernel(const float* __restrict__ tris,
-                                                        const int32_t* __restrict__ valid_idx,
-                                                        const int32_t* __restrict__ scene_off,
-                                                        const float* __restrict__ c2w, int n_views, int n_reg,
-                                                        float* __restrict__ pos_out,
-                                                        const int32_t* __restrict__ set_off) {
-    __shared__ float red[1024 / 64][9];
-    const int set = blockIdx.x;
+// Triangle positions + register-token centres in two launches (deterministic, no atomics):
+//   1. scene_pos_tri_kernel, grid (ceil(max_n / 256), sets): one thread per triangle writes its (camera-frame)
+//      9 coordinates and each block writes the 9 sums of its triangles to partial[set][block];
+//   2. scene_pos_center_kernel, one wave per set: sums the block partials in block order and writes the
+//      n_reg centre rows (renderformer.py:113-116: mean over valid triangles / (n + 1e-5), vertex-averaged).
+// (one 1,024-thread block per set took ~19 us: each thread walked ~6 triangles through dependent loads)
+__global__ __launch_bounds__(256) void scene_pos_tri_kernel(const float* __restrict__ tris,
+                                                            const int32_t* __restrict__ valid_idx,
+                                                            const int32_t* __restrict__ scene_off,
+                                                            const float* __restrict__ c2w, int n_views, int n_reg,
+                                                            float* __restrict__ pos_out,
+                                                            const int32_t* __restrict__ set_off,
+                                                            float* __restrict__ partial) {
+    __shared__ float red[4][9];
+    const int set = blockIdx.y;
     const int scene = c2w ? set / n_views : set;
     const int t0 = scene_off[scene], n = scene_off[scene + 1] - t0;
-    float rt[9], tinv[3];
-    if (c2w) {
-        const float* m = c2w + set * 16;
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) rt[i * 3 + j] = m[j * 4 + i];
-        for (int i = 0; i < 3; ++i) tinv[i] = -(rt[i * 3 + 0] * m[3] + rt[i * 3 + 1] * m[7] + rt[i * 3 + 2] * m[11]);
-    }
-    float acc[9];
-    for (int c = 0; c < 9; ++c) acc[c] = 0.f;
-    float* dst = pos_out + (int64_t)(set_off[set] + n_reg) * 9;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    float v[9];
+    for (int c = 0; c < 9; ++c) v[c] = 0.f;
+    if (i < n) {
         const float* src = tris + (int64_t)valid_idx[t0 + i] * 9;
-        float v[9];
         for (int c = 0; c < 9; ++c) v[c] = src[c];
         if (c2w) {
+            const float* m = c2w + set * 16;
+            float rt[9], tinv[3];
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) rt[a * 3 + b] = m[b * 4 + a];
+            for (int a = 0; a < 3; ++a) tinv[a] = -(rt[a * 3 + 0] * m[3] + rt[a * 3 + 1] * m[7] + rt[a * 3 + 2] * m[11]);
             float w[9];
             for (int vert = 0; vert < 3; ++vert)
                 for (int a = 0; a < 3; ++a)
@@ -237,29 +241,38 @@ __global__ __launch_bounds__(1024) void scene_pos_kernel(const float* __restrict
                                       rt[a * 3 + 2] * v[vert * 3 + 2] + tinv[a];
             for (int c = 0; c < 9; ++c) v[c] = w[c];
         }
-        for (int c = 0; c < 9; ++c) {
-            dst[(int64_t)i * 9 + c] = v[c];
-            acc[c] += v[c];
-        }
+        float* dst = pos_out + (int64_t)(set_off[set] + n_reg + i) * 9;
+        for (int c = 0; c < 9; ++c) dst[c] = v[c];
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int c = 0; c < 9; ++c) {
-        const float s = wave_sum(acc[c]);
-        if (lane == 0) red[wave][c] = s;
+        const float sm = wave_sum(v[c]);
+        if (lane == 0) red[wave][c] = sm;
     }
     __syncthreads();
-    if (threadIdx.x < n_reg * 9) {
-        const float wgt = 1.0f / ((float)n + 1e-5f);
-        float tot[9];
-        for (int c = 0; c < 9; ++c) {
-            float sum = 0.f;
-#pragma unroll
-            for (int w = 0; w < 1024 / 64; ++w) sum += red[w][c];
-            tot[c] = sum * wgt;
-        }
-        const int k = threadIdx.x % 3;
-        const float ctr = (tot[k] + tot[3 + k] + tot[6 + k]) / 3.0f;
-        pos_out[(int64_t)set_off[set] * 9 + threadIdx.x] = ctr;
+    if (threadIdx.x < 9)
+        partial[((int64_t)set * gridDim.x + blockIdx.x) * 9 + threadIdx.x] =
+            (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+__global__ __launch_bounds__(64) void scene_pos_center_kernel(const int32_t* __restrict__ scene_off, int n_views,
+                                                              int has_c2w, int n_reg, int n_blocks,
+                                                              const float* __restrict__ partial,
+                                                              float* __restrict__ pos_out,
+                                                              const int32_t* __restrict__ set_off) {
+    const int set = blockIdx.x;
+    const int scene = has_c2w ? set / n_views : set;
+    const int n = scene_off[scene + 1] - scene_off[scene];
+    const int nb = (n + 255) / 256;  // blocks that held triangles of this set (the rest wrote zeros)
+    float tot[9];
+    for (int c = 0; c < 9; ++c) {
+        float sm = 0.f;
+        for (int b = 0; b < nb; ++b) sm += partial[((int64_t)set * n_blocks + b) * 9 + c];
+        tot[c] = sm / ((float)n + 1e-5f);
+    }
+    for (int t = threadIdx.x; t < n_reg * 9; t += 64) {
+        const int k = t % 3;
+        pos_out[(int64_t)set_off[set] * 9 + t] = (tot[k] + tot[3 + k] + tot[6 + k]) / 3.0f;
     }
 }
 
@@ -368,14 +381,24 @@ extern "C" int rf_patchify_rays(const float* rays_d, int n_views, int res, int p
 }
 
 extern "C" int rf_scene_pos(const float* tris, const int32_t* valid_idx, const int32_t* scene_off, const float* c2w,
-                            int n_scenes, int n_views, int n_reg, float* pos_out, const int32_t* set_off, void* stream) {
-    RF_REQUIRE(tris && valid_idx && scene_off && pos_out && set_off, "rf_scene_pos: null pointer");
-    RF_REQUIRE(n_reg * 9 <= 256, "rf_scene_pos: too many register tokens");
+                            int n_scenes, int n_views, int n_reg, float* pos_out, const int32_t* set_off, int max_tris,
+                            float* partials, int64_t partial_floats, void* stream) {
+    RF_REQUIRE(tris && valid_idx && scene_off && pos_out && set_off && partials, "rf_scene_pos: null pointer");
+    RF_REQUIRE(n_reg >= 0 && max_tris >= 0, "rf_scene_pos: negative sizes");
     const int sets = c2w ? n_scenes * n_views : n_scenes;
     if (sets <= 0) return RF_OK;
-    hipLaunchKernelGGL(scene_pos_kernel, dim3(sets), dim3(1024), 0, (hipStream_t)stream, tris, valid_idx, scene_off,
-                       c2w, n_views, n_reg, pos_out, set_off);
+    const int nb = max_tris > 0 ? (max_tris + 255) / 256 : 1;
+    RF_REQUIRE(partial_floats >= (int64_t)sets * nb * 9, "rf_scene_pos: partials need sets x ceil(max_tris/256) x 9 "
+               "floats (rf_scene_pos_partials)");
+    hipLaunchKernelGGL(scene_pos_tri_kernel, dim3(nb, sets), dim3(256), 0, (hipStream_t)stream, tris, valid_idx,
+                       scene_off, c2w, n_views, n_reg, pos_out, set_off, partials);
+    hipLaunchKernelGGL(scene_pos_center_kernel, dim3(sets), dim3(64), 0, (hipStream_t)stream, scene_off, n_views,
+                       c2w ? 1 : 0, n_reg, nb, partials, pos_out, set_off);
     return rf::check_launch("rf_scene_pos");
+}
+
+extern "C" int64_t rf_scene_pos_partials(int sets, int max_tris) {
+    return (int64_t)(sets > 0 ? sets : 0) * (max_tris > 0 ? (max_tris + 255) / 256 : 1) * 9;
 }
 
 extern "C" int rf_hdr_output(const float* logits, float* out, int n, int c, int h, int w, float elu_alpha,

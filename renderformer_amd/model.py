@@ -531,7 +531,8 @@ class RenderFormer:
         tris = triangles.reshape(B, -1, 9).float().contiguous()
         x1 = self._embed_triangles(plan, texture, vn.reshape(B, -1, 9).float().contiguous(), log_encode)
         pos1 = torch.empty(plan.T1, 9, dtype=torch.float32, device=dev)
-        ops.scene_pos(tris, plan.valid_flat, plan.scene_off, None, B, 1, cfg.num_register_tokens, pos1, plan.cu1)
+        ops.scene_pos(tris, plan.valid_flat, plan.scene_off, None, B, 1, cfg.num_register_tokens, pos1, plan.cu1,
+                      max(plan.counts))
         x1 = self._stage1(plan, x1, pos1)
         P = B * V
         c2w_v = c2w.reshape(P, 4, 4).float().contiguous()
@@ -543,7 +544,7 @@ class RenderFormer:
         x2 = self._ray_embed(plan, ray_in)
         pos2 = torch.empty(plan.T_kv, 9, dtype=torch.float32, device=dev)
         ops.scene_pos(tris, plan.valid_flat, plan.scene_off, pos_c2w, B, V, cfg.num_register_tokens, pos2,
-                      plan.kv_off)
+                      plan.kv_off, max(plan.counts))
         taps = self._stage2(plan, x2, x1, pos2, ray_pos)
         out = self._decode(plan, taps, log_decode=not cfg.use_ldr, channels_last=True)
         return out.view(B, V, resolution, resolution, -1)
@@ -565,7 +566,8 @@ class RenderFormer:
         x1 = self._embed_triangles(plan, texture_patch_list.float().contiguous(),
                                    vns.reshape(B, -1, 9).float().contiguous(), log_encode=False)
         pos1 = torch.empty(plan.T1, 9, dtype=torch.float32, device=dev)
-        ops.scene_pos(tris, plan.valid_flat, plan.scene_off, None, B, 1, cfg.num_register_tokens, pos1, plan.cu1)
+        ops.scene_pos(tris, plan.valid_flat, plan.scene_off, None, B, 1, cfg.num_register_tokens, pos1, plan.cu1,
+                      max(plan.counts))
         x1 = self._stage1(plan, x1, pos1)
         P = B * V
         ray_in = torch.empty(P * plan.R, 3 * cfg.patch_size ** 2, dtype=torch.bfloat16, device=dev)
@@ -579,7 +581,7 @@ class RenderFormer:
         view_off = torch.tensor([0] + [c for c in plan.counts for _ in range(V)], device=dev).cumsum(0).to(torch.int32)
         pos2 = torch.empty(plan.T_kv, 9, dtype=torch.float32, device=dev)
         ops.scene_pos(tri_vpos_view_tf.reshape(P * N, 9).float().contiguous(), view_valid, view_off, None, P, 1,
-                      cfg.num_register_tokens, pos2, plan.kv_off)
+                      cfg.num_register_tokens, pos2, plan.kv_off, max(plan.counts))
         taps = self._stage2(plan, x2, x1, pos2, ray_pos)
         out = self._decode(plan, taps, log_decode=False, channels_last=False)
         return out.view(B, V, *out.shape[1:])

@@ -380,11 +380,15 @@ def patchify_rays(rays_d: torch.Tensor, patch: int, out: torch.Tensor):
 
 
 def scene_pos(tris: torch.Tensor, valid_idx, scene_off, c2w: Optional[torch.Tensor], n_scenes: int, n_views: int,
-              n_reg: int, pos_out: torch.Tensor, set_off: torch.Tensor):
+              n_reg: int, pos_out: torch.Tensor, set_off: torch.Tensor, max_tris: int):
+    """Triangle RoPE positions + register-token centres (rf_scene_pos; max_tris >= every scene's valid count)."""
     _dev(tris, torch.float32, "tris")
     _check(tris.is_contiguous(), "tris must be contiguous")
+    sets = n_scenes * n_views if c2w is not None else n_scenes
+    nparts = int(load().rf_scene_pos_partials(sets, max_tris))
+    parts = torch.empty(max(nparts, 1), dtype=torch.float32, device=pos_out.device)
     call("rf_scene_pos", ptr(tris), ptr(valid_idx), ptr(scene_off), ptr(c2w), n_scenes, n_views, n_reg, ptr(pos_out),
-         ptr(set_off), stream())
+         ptr(set_off), max_tris, ptr(parts), parts.numel(), stream())
     return pos_out
 
 

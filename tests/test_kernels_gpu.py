@@ -476,13 +476,39 @@ def test_prologue_kernels_match_oracle():
     set_off = torch.tensor([0, S[0], 2 * S[0], 2 * S[0] + S[1], 2 * S[0] + 2 * S[1]], dtype=torch.int32)
     pos = torch.empty(int(set_off[-1]), 9, device=dev)
     ops.scene_pos(bt["triangles"].reshape(B * N, 9).contiguous().to(dev), valid.to(dev), scene_off.to(dev),
-                  c2w.to(dev), B, 2, 16, pos, set_off.to(dev))
+                  c2w.to(dev), B, 2, 16, pos, set_off.to(dev), max(counts))
     tcam = rf_ref.cam_transform(c2w, torch.repeat_interleave(bt["triangles"], 2, 0)).reshape(P, N, 9)
     refp, _ = rf_ref.center_pos(tcam, torch.repeat_interleave(mask, 2, 0), 16)
     for p in range(P):
         n = counts[p // 2]
         got = pos[int(set_off[p]):int(set_off[p + 1])].cpu()
         assert torch.allclose(got, refp[p, :16 + n], atol=2e-6), p
+
+
+def test_scene_pos_large_and_deterministic():
+    """Two-launch positions / centres on cbox-lucy-sized scenes (47 blocks of 256 triangles, ragged): vs the
+    oracle, and bit-identical run to run (block partials reduced in a fixed order, no atomics)."""
+    from oracle import rf_ref
+    from renderformer_amd.scenes import batch_scenes, synthetic_scene
+    ops = _ops()
+    counts = [11803, 5000]
+    bt = batch_scenes([synthetic_scene(n, 1, seed=40 + i) for i, n in enumerate(counts)], expand=False)
+    B, N = bt["mask"].shape
+    valid = torch.nonzero(bt["mask"].reshape(-1)).squeeze(1).to(torch.int32)
+    scene_off = torch.tensor([0, counts[0], sum(counts)], dtype=torch.int32)
+    S = [16 + c for c in counts]
+    set_off = torch.tensor([0, S[0], S[0] + S[1]], dtype=torch.int32)
+    tris = bt["triangles"].reshape(B * N, 9).contiguous()
+    outs = []
+    for _ in range(2):
+        pos = torch.empty(sum(S), 9, device=dev)
+        ops.scene_pos(tris.to(dev), valid.to(dev), scene_off.to(dev), None, B, 1, 16, pos, set_off.to(dev), max(counts))
+        outs.append(pos.cpu())
+    assert torch.equal(outs[0], outs[1])
+    refp, _ = rf_ref.center_pos(bt["triangles"].reshape(B, N, 9), bt["mask"], 16)
+    for b in range(B):
+        got = outs[0][int(set_off[b]):int(set_off[b + 1])]
+        assert torch.allclose(got, refp[b, :S[b]], atol=2e-6), b
 
 
 def test_hdr_output():
