@@ -1655,6 +1655,152 @@ __global__ __launch_bounds__(512, 1) void mx8_kernel(EngineArgs p) {
     engine_epilogue<Tile<256, 256, 2, 4, 4>, EPI>(p, tm * mx::BM, tn * mx::BN, acc);
 }
 
+// Staggered three-buffer MX fp8 loop (the default): tile 128 x 256, 8 waves of 64 x 64 (4 x 4 MFMAs of
+// 16x16x128 per 128-deep K-step), one load section {ds_read this step's fragments and scales; issue step t+2's
+// LDS-DMA into the buffer step t-1 used; counted vmcnt for step t+1} and one MFMA section per step, waves 4-7
+// one section behind (on every SIMD one wave's reads overlap its partner's MFMAs), three 49.5-KiB buffers so
+// every DMA has a whole step of both groups' MFMA work to land under (the plain loop above reads, then
+// computes: the MFMA pipe idles during every read burst).
+namespace mx3 {
+constexpr int BM = 128, BN = 256, KS = 128;
+constexpr int A_DATA = BM * KS, B_DATA = BN * KS;
+constexpr int STAGE = A_DATA + B_DATA + (BM + BN) * 4;
+constexpr int TI = 4, TJ = 4;
+}  // namespace mx3
+
+template <bool INITC>
+RF_DEV void mx8_p3_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int kbeg, int kend,
+                            f32x4 (&acc)[mx3::TI][mx3::TJ]) {
+    using namespace mx3;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int nk = kend - kbeg;
+    const uint8_t* A = reinterpret_cast<const uint8_t*>(p.a);
+    const uint8_t* W = reinterpret_cast<const uint8_t*>(p.w);
+    const bool has_sc = __builtin_amdgcn_readfirstlane(wave) < (BM + BN) / 64;  // waves 0-5 stage a scale piece
+    auto issue = [&](int kt) {
+        char* st = smem + (kt % 3) * STAGE;
+        const int64_t k0 = (int64_t)(kbeg + kt) * KS;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {  // 48 data pieces of 8 rows x 128 B: 0..15 A, 16..47 W
+            const int piece = wave * 6 + i;
+            const bool is_a = piece < BM / 8;
+            const int row = (is_a ? piece : piece - BM / 8) * 8 + (lane >> 3);
+            const int ch = (lane & 7) ^ (row & 7);
+            const uint8_t* src;
+            if (is_a) {
+                const int m = m0 + row;
+                src = A + (int64_t)(m < p.m ? m : p.m - 1) * p.lda + k0 + ch * 16;
+            } else {
+                src = W + (int64_t)(n0 + row) * p.ldw + k0 + ch * 16;
+            }
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, src),
+                                             LDS_PTR(void, st + (is_a ? piece * 1024 : A_DATA + (piece - BM / 8) * 1024)),
+                                             16, 0, 0);
+        }
+        if (has_sc) {  // scale dwords: waves 0-1 A rows 64 w + lane, waves 2-5 W rows 64 (w - 2) + lane
+            const bool is_a = wave < BM / 64;
+            const int row = (is_a ? wave : wave - BM / 64) * 64 + lane;
+            const uint8_t* src;
+            if (is_a) {
+                const int m = m0 + row;
+                src = p.sa + (int64_t)(m < p.m ? m : p.m - 1) * p.ld_sa + (kbeg + kt) * 4;
+            } else {
+                src = p.sw + (int64_t)(n0 + row) * p.ld_sw + (kbeg + kt) * 4;
+            }
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, src),
+                                             LDS_PTR(void, st + A_DATA + B_DATA + (is_a ? 0 : BM * 4) + (row & ~63) * 4),
+                                             4, 0, 0);
+        }
+    };
+    if (INITC && kbeg == 0) {
+        load_c_acc<TI, TJ>(p, m0 + wm * 64, n0 + wn * 64, acc);
+    } else {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int frow = lane & 15, g = lane >> 4;
+    issue(0);
+    if (nk > 1) {
+        issue(1);
+        if (has_sc) wait_vm<7>();
+        else wait_vm<6>();
+    } else {
+        wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;
+    if (late) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    mx::i32x8 fa[TI], fw[TJ];
+    int sa[TI], sw[TJ];
+    for (int kt = 0; kt < nk; ++kt) {
+        const char* st = smem + (kt % 3) * STAGE;
+        const int* sca = reinterpret_cast<const int*>(st + A_DATA + B_DATA);
+        const int* scw = sca + BM;
+        // ---- load section
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+            const int row = wm * 64 + i * 16 + frow;
+            const u32x4 lo = *reinterpret_cast<const u32x4*>(st + mx::off(row, g));
+            const u32x4 hi = *reinterpret_cast<const u32x4*>(st + mx::off(row, g + 4));
+            fa[i] = mx::i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+            sa[i] = (sca[row] >> (8 * g)) & 0xff;
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+            const int row = wn * 64 + j * 16 + frow;
+            const u32x4 lo = *reinterpret_cast<const u32x4*>(st + A_DATA + mx::off(row, g));
+            const u32x4 hi = *reinterpret_cast<const u32x4*>(st + A_DATA + mx::off(row, g + 4));
+            fw[j] = mx::i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+            sw[j] = (scw[row] >> (8 * g)) & 0xff;
+        }
+        if (kt + 2 < nk) {
+            issue(kt + 2);
+            if (has_sc) wait_vm<7>();  // step kt+1 landed (this wave's part), step kt+2 in flight
+            else wait_vm<6>();
+        } else {
+            wait_vm<0>();
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- MFMA section
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fw[j], fa[i], acc[i][j], 0, 0, 0, sw[j], 0,
+                                                                             sa[i]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (!late) __builtin_amdgcn_s_barrier();
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void mx8_p3_kernel(EngineArgs p) {
+    __shared__ __attribute__((aligned(16))) char smem[3 * mx3::STAGE];
+    const int tiles_m = (p.m + mx3::BM - 1) / mx3::BM;
+    const int nwg = gridDim.x;
+    const int hw = blockIdx.x;
+    const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
+    int tm, tn;
+    tile_coords(wg, tiles_m, p.n / mx3::BN, p.group_m, tm, tn);
+    f32x4 acc[mx3::TI][mx3::TJ];
+    mx8_p3_mainloop<EPI == E_ADD>(p, smem, tm * mx3::BM, tn * mx3::BN, 0, p.k / mx3::KS, acc);
+    engine_epilogue<Tile<128, 256, 2, 4, 4>, EPI>(p, tm * mx3::BM, tn * mx3::BN, acc);
+}
+
 // MX quantisation of bf16 rows: every 32-element block gets the E8M0 scale 2^e with e = ceil(log2(amax / 448))
 // (the block's largest |value| lands in (224, 448], never saturating e4m3), values x / 2^e rounded to nearest
 // even e4m3 (hardware v_cvt_pk_fp8_f32).  One thread per block: 64 B in, 32 B + 1 scale byte out.
@@ -1938,11 +2084,25 @@ extern "C" int rf_gemm_mx8(const void* a, int64_t lda, const void* sa, int64_t l
     p.c = c;
     p.ldc = ldc;
     p.bias = bias;
+    hipStream_t st = (hipStream_t)stream;
+    const bool plain = getenv("RF_MX8_PLAIN") && atoi(getenv("RF_MX8_PLAIN")) != 0;  // A/B: the unstaggered loop
+    if (!plain) {
+        const int tiles_m = (m + 127) / 128, tiles_n = n / 256;
+        const int nwg = tiles_m * tiles_n;
+        p.group_m = pick_group_m(tiles_m, tiles_n, 128, 256, (nwg + 7) / 8);
+        const dim3 g(nwg), b(512);
+        switch (epilogue) {
+            case RF_EPI_BF16: hipLaunchKernelGGL((mx8_p3_kernel<E_BF16>), g, b, 0, st, p); break;
+            case RF_EPI_F32: hipLaunchKernelGGL((mx8_p3_kernel<E_F32>), g, b, 0, st, p); break;
+            case RF_EPI_ADD_F32: hipLaunchKernelGGL((mx8_p3_kernel<E_ADD>), g, b, 0, st, p); break;
+            default: hipLaunchKernelGGL((mx8_p3_kernel<E_SWIGLU>), g, b, 0, st, p); break;
+        }
+        return rf::check_launch("rf_gemm_mx8");
+    }
     const int tiles_m = (m + 255) / 256, tiles_n = n / 256;
     const int nwg = tiles_m * tiles_n;
     p.group_m = pick_group_m(tiles_m, tiles_n, 256, 256, (nwg + 7) / 8);
     const dim3 g(nwg), b(512);
-    hipStream_t st = (hipStream_t)stream;
     switch (epilogue) {
         case RF_EPI_BF16: hipLaunchKernelGGL((mx8_kernel<E_BF16>), g, b, 0, st, p); break;
         case RF_EPI_F32: hipLaunchKernelGGL((mx8_kernel<E_F32>), g, b, 0, st, p); break;
