@@ -19,10 +19,10 @@ Multi-GPU: one process per GPU.  Under ``torch.distributed.run`` the env (RANK/W
 ``--gpus`` must equal WORLD_SIZE; run directly with ``--gpus N > 1`` this script starts
 ``torch.distributed.run --nproc-per-node N`` itself (before any GPU call) and exits with its status.
 
-The JSON line carries a roofline object for the dominant kernel (stage-1 attention), timed with HIP events
-around each of its launches in the last timed step, the parity of the last GPU frame against the reference
-(the committed reference-generated fixture when the workload is that fixture's, and the oracle frame of the
-CPU baseline), and the CPU baseline itself: the oracle restatement of the reference (oracle/rf_ref.py,
+The JSON line carries a roofline object for the dominant kernel (stage-1 attention), each of its launches in
+the last timed step timed by HIP events that its own dispatch packet timestamps (hipExtLaunchKernel), the
+parity of the last GPU frame against the reference (the committed reference-generated fixture when the
+workload is that fixture's, and the oracle frame of the CPU baseline), and the CPU baseline itself: the oracle restatement of the reference (oracle/rf_ref.py,
 PyTorch CPU fp32) on a bounded sample of the same workload, rank 0 at N = 1 only.
 """
 from __future__ import annotations
@@ -243,8 +243,10 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    # HIP events bracket the dominant kernel's launches in the LAST timed step only: each event pair adds
-    # ~11 us of queue time around its launch (profiles/r1: 14 x 11.4 us per frame when every step was timed)
+    # the dominant kernel's launches in the LAST timed step are dispatched with a start/stop HIP event pair
+    # that the dispatch packet itself timestamps (librfhip's kernel timer, hipExtLaunchKernel): the kernel's
+    # own duration, as rocprofv3 reports it (round 1 bracketed the launch with two marker events instead,
+    # which added ~11-20 us of queue time per launch to the measured duration)
     timer = ops.KernelTimer("gemm_w13_stage2" if args.fp8 else DOMINANT)
     torch.cuda.synchronize()
     if world > 1:
@@ -338,6 +340,7 @@ def main():
                 "traffic_source": "profiles/attn_stage1_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE pass)"
                 if traffic is not None else None,
                 "avg_launch_ms": round(kern_ms, 4), "launches_per_step": per_step_launches,
+                "timing": "hipExtLaunchKernel start/stop events on the launch stream (dispatch-packet timestamps)",
                 "algorithmic_flop_per_launch": kern_flops,
                 # Q, K, V read once + O written once (bf16); traffic above this = K/V re-reads + split partials
                 "algorithmic_bytes_per_launch": 4 * s_len * cfg.latent_dim * 2 * scenes_per_launch,

@@ -55,7 +55,7 @@ extern "C" {
 #define RF_ERR_UNSUPPORTED 3
 #define RF_ERR_DEVICE 4       /* an earlier launch reported a device-side error (see rf_device_error) */
 
-#define RF_ABI_VERSION 7
+#define RF_ABI_VERSION 8
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -75,6 +75,15 @@ int rf_abi_version(void);
 int rf_device_error(void);
 int rf_clear_device_error(void);
 int rf_debug_raise_device_error(int code, void* stream);
+
+/* Kernel timer (measurement only; bench.py's roofline).  rf_ktimer_arm() creates a start/stop event pair on the
+ * current device and arms it for the calling thread: the NEXT kernel the library launches (the first kernel
+ * of the next entry-point call) is dispatched with hipExtLaunchKernel, whose dispatch packet timestamps the
+ * pair — the kernel's own duration, as a rocprofv3 kernel trace reports it, with no marker packets around it.
+ * rf_ktimer_read() waits for every taken pair, writes up to max_n durations (ms, launch order), releases the
+ * pairs and returns how many were taken. */
+int rf_ktimer_arm(void);
+int rf_ktimer_read(float* ms, int max_n);
 
 /* workspace / ws_bytes of the GEMM and convolution entry points: optional (NULL = one block per
  * output tile), rf_gemm_workspace_bytes() bytes, zero-filled once when allocated, used by one stream at a

@@ -54,6 +54,8 @@ SIGNATURES = {
     "rf_device_error": [],
     "rf_clear_device_error": [],
     "rf_debug_raise_device_error": [_I, _P],
+    "rf_ktimer_arm": [],
+    "rf_ktimer_read": [_P, _I],
 }
 RF_ERR_DEVICE = 4
 

@@ -1259,28 +1259,28 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
     const dim3 g(grid), b(NW5 * 64);
     hipStream_t st = (hipStream_t)stream;
     switch (unit ? dbg : 0) {  // diagnostic variants (garbage results): ablation timing only
-        case 1: hipLaunchKernelGGL((attn_sk_kernel<true, 1>), g, b, 0, st, a); break;
-        case 2: hipLaunchKernelGGL((attn_sk_kernel<true, 2>), g, b, 0, st, a); break;
-        case 3: hipLaunchKernelGGL((attn_sk_kernel<true, 3>), g, b, 0, st, a); break;
-        case 4: hipLaunchKernelGGL((attn_sk_kernel<true, 4>), g, b, 0, st, a); break;
-        case 8: hipLaunchKernelGGL((attn_sk_kernel<true, 8>), g, b, 0, st, a); break;
-        case 16: hipLaunchKernelGGL((attn_sk_kernel<true, 16>), g, b, 0, st, a); break;
-        case 20: hipLaunchKernelGGL((attn_sk_kernel<true, 20>), g, b, 0, st, a); break;
-        case 11: hipLaunchKernelGGL((attn_sk_kernel<true, 11>), g, b, 0, st, a); break;
-        case 32: hipLaunchKernelGGL((attn_sk_kernel<true, 32>), g, b, 0, st, a); break;
-        case 64: hipLaunchKernelGGL((attn_sk_kernel<true, 64>), g, b, 0, st, a); break;
-        case 96: hipLaunchKernelGGL((attn_sk_kernel<true, 96>), g, b, 0, st, a); break;
-        case 128: hipLaunchKernelGGL((attn_sk_kernel<true, 128>), g, b, 0, st, a); break;
-        case 160: hipLaunchKernelGGL((attn_sk_kernel<true, 160>), g, b, 0, st, a); break;
-        case 256: hipLaunchKernelGGL((attn_sk_kernel<true, 256>), g, b, 0, st, a); break;
-        case 288: hipLaunchKernelGGL((attn_sk_kernel<true, 288>), g, b, 0, st, a); break;
-        case 384: hipLaunchKernelGGL((attn_sk_kernel<true, 384>), g, b, 0, st, a); break;
-        case 512: hipLaunchKernelGGL((attn_sk_kernel<true, 512>), g, b, 0, st, a); break;
+        case 1: RF_LAUNCH((attn_sk_kernel<true, 1>), g, b, 0, st, a); break;
+        case 2: RF_LAUNCH((attn_sk_kernel<true, 2>), g, b, 0, st, a); break;
+        case 3: RF_LAUNCH((attn_sk_kernel<true, 3>), g, b, 0, st, a); break;
+        case 4: RF_LAUNCH((attn_sk_kernel<true, 4>), g, b, 0, st, a); break;
+        case 8: RF_LAUNCH((attn_sk_kernel<true, 8>), g, b, 0, st, a); break;
+        case 16: RF_LAUNCH((attn_sk_kernel<true, 16>), g, b, 0, st, a); break;
+        case 20: RF_LAUNCH((attn_sk_kernel<true, 20>), g, b, 0, st, a); break;
+        case 11: RF_LAUNCH((attn_sk_kernel<true, 11>), g, b, 0, st, a); break;
+        case 32: RF_LAUNCH((attn_sk_kernel<true, 32>), g, b, 0, st, a); break;
+        case 64: RF_LAUNCH((attn_sk_kernel<true, 64>), g, b, 0, st, a); break;
+        case 96: RF_LAUNCH((attn_sk_kernel<true, 96>), g, b, 0, st, a); break;
+        case 128: RF_LAUNCH((attn_sk_kernel<true, 128>), g, b, 0, st, a); break;
+        case 160: RF_LAUNCH((attn_sk_kernel<true, 160>), g, b, 0, st, a); break;
+        case 256: RF_LAUNCH((attn_sk_kernel<true, 256>), g, b, 0, st, a); break;
+        case 288: RF_LAUNCH((attn_sk_kernel<true, 288>), g, b, 0, st, a); break;
+        case 384: RF_LAUNCH((attn_sk_kernel<true, 384>), g, b, 0, st, a); break;
+        case 512: RF_LAUNCH((attn_sk_kernel<true, 512>), g, b, 0, st, a); break;
         default:
             if (unit)
-                hipLaunchKernelGGL((attn_sk_kernel<true, 0>), g, b, 0, st, a);
+                RF_LAUNCH((attn_sk_kernel<true, 0>), g, b, 0, st, a);
             else
-                hipLaunchKernelGGL((attn_sk_kernel<false, 0>), g, b, 0, st, a);
+                RF_LAUNCH((attn_sk_kernel<false, 0>), g, b, 0, st, a);
     }
     return rf::check_launch("rf_attn_fwd");
 }
@@ -1325,11 +1325,11 @@ extern "C" int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ld
         a.part_ml = a.part_o + (int64_t)n_split * ws_rows * n_heads * HD;
     }
     if (kv == 3)
-        hipLaunchKernelGGL(attn_v3_kernel, dim3((unsigned)total), dim3(NW3 * 64), 0, (hipStream_t)stream, a);
+        RF_LAUNCH(attn_v3_kernel, dim3((unsigned)total), dim3(NW3 * 64), 0, (hipStream_t)stream, a);
     else if (kv == 28)
-        hipLaunchKernelGGL((attn_fwd_kernel<false, 8>), dim3((unsigned)total), dim3(512), 0, (hipStream_t)stream, a);
+        RF_LAUNCH((attn_fwd_kernel<false, 8>), dim3((unsigned)total), dim3(512), 0, (hipStream_t)stream, a);
     else
-        hipLaunchKernelGGL((attn_fwd_kernel<false, 4>), dim3((unsigned)total), dim3(256), 0, (hipStream_t)stream, a);
+        RF_LAUNCH((attn_fwd_kernel<false, 4>), dim3((unsigned)total), dim3(256), 0, (hipStream_t)stream, a);
     return rf::check_launch("rf_attn_fwd");
 }
 
@@ -1345,7 +1345,7 @@ extern "C" int rf_attn_combine(const void* workspace, int64_t ws_rows, int n_spl
     const float* po = (const float*)workspace;
     const float* pml = po + (int64_t)n_split * ws_rows * n_heads * HD;
     const int64_t items = (int64_t)n_rows * n_heads;
-    hipLaunchKernelGGL(attn_combine_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, (hipStream_t)stream, po,
+    RF_LAUNCH(attn_combine_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, (hipStream_t)stream, po,
                        pml, ws_rows, n_split, n_heads, rows, n_rows, (bf16_t*)o, ldo);
     return rf::check_launch("rf_attn_combine");
 }
@@ -1377,6 +1377,6 @@ extern "C" int rf_swin_attn_fwd(const void* q, int64_t ldq, const void* k, int64
     a.window = window;
     a.n_split = 1;
     dim3 grid((grid_h / window) * (grid_w / window), n_heads, n_images);
-    hipLaunchKernelGGL((attn_fwd_kernel<true, 2>), grid, dim3(128), 0, (hipStream_t)stream, a);
+    RF_LAUNCH((attn_fwd_kernel<true, 2>), grid, dim3(128), 0, (hipStream_t)stream, a);
     return rf::check_launch("rf_swin_attn_fwd");
 }

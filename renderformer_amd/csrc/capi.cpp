@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <vector>
 
 #include "common.h"
 
@@ -64,6 +65,21 @@ int check_launch(const char* what) {
     return RF_OK;
 }
 
+// kernel timer: event pairs created by rf_ktimer_arm on the caller's current device, taken by the next launch
+struct KTimer {
+    std::vector<hipEvent_t> start, stop;  // one pair per armed launch, in launch order
+    bool armed = false;
+};
+static thread_local KTimer g_kt;
+
+bool ktimer_take(hipEvent_t* s, hipEvent_t* e) {
+    if (!g_kt.armed) return false;
+    g_kt.armed = false;
+    *s = g_kt.start.back();
+    *e = g_kt.stop.back();
+    return true;
+}
+
 __global__ void raise_error_kernel(int* err, int code) {
     if (threadIdx.x == 0) report_device_error(err, code);
 }
@@ -83,13 +99,50 @@ extern "C" int rf_clear_device_error(void) {
 extern "C" int rf_debug_raise_device_error(int code, void* stream) {
     int* w = rf::device_error_word();
     RF_REQUIRE(w, "rf_debug_raise_device_error: no mapped error word");
-    hipLaunchKernelGGL(rf::raise_error_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, w, code);
+    RF_LAUNCH(rf::raise_error_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, w, code);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         rf::set_error("rf_debug_raise_device_error: launch failed: %s", hipGetErrorString(e));
         return RF_ERR_LAUNCH;
     }
     return RF_OK;
+}
+
+extern "C" int rf_ktimer_arm(void) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+        rf::set_error("rf_ktimer_arm: hipEventCreate failed");
+        return RF_ERR_LAUNCH;
+    }
+    if (rf::g_kt.armed) {  // the previous arm was never taken by a launch: drop its pair
+        (void)hipEventDestroy(rf::g_kt.start.back());
+        (void)hipEventDestroy(rf::g_kt.stop.back());
+        rf::g_kt.start.pop_back();
+        rf::g_kt.stop.pop_back();
+    }
+    rf::g_kt.start.push_back(a);
+    rf::g_kt.stop.push_back(b);
+    rf::g_kt.armed = true;
+    return RF_OK;
+}
+
+extern "C" int rf_ktimer_read(float* ms, int max_n) {
+    rf::KTimer& t = rf::g_kt;
+    const int n = (int)t.start.size() - (t.armed ? 1 : 0);
+    RF_REQUIRE(ms || max_n == 0, "rf_ktimer_read: null output");
+    int rc = n;
+    for (int i = 0; i < n; ++i) {
+        float v = -1.f;
+        if (hipEventSynchronize(t.stop[i]) != hipSuccess || hipEventElapsedTime(&v, t.start[i], t.stop[i]) != hipSuccess)
+            v = -1.f;
+        if (i < max_n) ms[i] = v;
+        (void)hipEventDestroy(t.start[i]);
+        (void)hipEventDestroy(t.stop[i]);
+    }
+    t.start.clear();
+    t.stop.clear();
+    t.armed = false;
+    return rc;
 }
 
 extern "C" const char* rf_last_error(void) { return rf::g_err; }

@@ -1,6 +1,7 @@
 // Shared device/host helpers for librfhip (gfx950 / CDNA4 only).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include "../../include/rf.h"
@@ -10,6 +11,7 @@
 typedef uint16_t bf16_t;  // raw bf16 bits in memory
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;  // MFMA A/B fragment (4 VGPRs)
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
@@ -78,6 +80,10 @@ void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 int* device_error_word();  // device pointer of the mapped error word (nullptr if it could not be allocated)
 int spin_limit();          // stream-K hand-off spin bound (RF_SPIN_LIMIT, default 2^24 polls)
+// Kernel timer (rf_ktimer_arm / rf_ktimer_read): when armed, the next library launch takes a start/stop event
+// pair that the dispatch packet itself timestamps (hipExtLaunchKernel), so the measured duration is the
+// kernel's own, as in a rocprofv3 kernel trace, with no extra packets in the queue.
+bool ktimer_take(hipEvent_t* start, hipEvent_t* stop);
 }  // namespace rf
 
 #define RF_REQUIRE(cond, ...)                          \
@@ -86,4 +92,14 @@ int spin_limit();          // stream-K hand-off spin bound (RF_SPIN_LIMIT, defau
             rf::set_error(__VA_ARGS__);                \
             return RF_ERR_INVALID;                     \
         }                                              \
+    } while (0)
+
+// Every library launch goes through RF_LAUNCH: a plain launch unless the kernel timer is armed.
+#define RF_LAUNCH(kernel, grid, block, shmem, stream, ...)                                                  \
+    do {                                                                                                 \
+        hipEvent_t rf_ev0_, rf_ev1_;                                                                     \
+        if (rf::ktimer_take(&rf_ev0_, &rf_ev1_))                                                         \
+            hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, rf_ev0_, rf_ev1_, 0, __VA_ARGS__); \
+        else                                                                                             \
+            hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);                         \
     } while (0)

@@ -145,7 +145,7 @@ extern "C" int rf_split_planes(const float* x, int64_t rows, int c, int64_t ldx,
     const int64_t n = rows * (c / 4);
     if (n <= 0) return RF_OK;
     RF_REQUIRE(n < (1ll << 31) - 256, "rf_split_planes: too many elements");
-    hipLaunchKernelGGL(split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, (int)rows, c,
+    RF_LAUNCH(split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, (int)rows, c,
                        ldx, (bf16_t*)p_hi, (bf16_t*)p_lo, p_ld, silu_act);
     return rf::check_launch("rf_split_planes");
 }
@@ -164,11 +164,11 @@ extern "C" int rf_upsample_bilinear(const float* in, int n_img, int hi, int wi, 
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (c % 8 == 0 && (!p_hi || p_ld % 8 == 0) && al16(in) && al16(out) && al16(p_hi) && al16(p_lo)) {
         const dim3 grid((unsigned)((wo * (c / 8) + 255) / 256), (unsigned)(n_img * ho));
-        hipLaunchKernelGGL(upsample8_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, out, (bf16_t*)p_hi,
+        RF_LAUNCH(upsample8_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, out, (bf16_t*)p_hi,
                            (bf16_t*)p_lo, p_ld, hi, wi, c, ho, wo, sh, sw);
     } else {
         const dim3 grid((unsigned)((wo * (c / 4) + 255) / 256), (unsigned)(n_img * ho));
-        hipLaunchKernelGGL(upsample_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, out, (bf16_t*)p_hi,
+        RF_LAUNCH(upsample_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, out, (bf16_t*)p_hi,
                            (bf16_t*)p_lo, p_ld, hi, wi, c, ho, wo, sh, sw);
     }
     return rf::check_launch("rf_upsample_bilinear");

@@ -96,6 +96,7 @@ struct EngineArgs {
     const uint8_t* sa;
     const uint8_t* sw;
     int ld_sa, ld_sw;
+    int persist;  // phased_sk_kernel: whole tiles strided over the grid, next tile's first K-tiles prefetched
 };
 
 // uniform early exit of a gated launch (every block reads the same flag, so a stream-K grid exits whole)
@@ -635,7 +636,7 @@ RF_DEV int img(int row, int kh, int ch) { return kh * (ROWS * 64) + row * 64 + (
 
 template <int BM, int NTERM, bool GATHER, bool INITC = false>
 RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int kbeg, int kend,
-                            f32x4 (&acc)[BM / 32][4]) {
+                            f32x4 (&acc)[BM / 32][4], bool pre = false) {
     using namespace ph;
     using G = Cfg<BM>;
     constexpr int NREG = G::NREG, NA = G::NA, MI = G::MI;
@@ -756,11 +757,16 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
 
     // prologue: tile 0 and (BM = 256) all of tile 1 / (BM = 128) tile 1 minus RB1 in flight; wait for tile 0
     constexpr int AHEAD = BM == 256 ? 8 : 4;  // LDS-DMA of tile 1 issued here (and of tile t+2 at a tile's wait)
+    // (pre: the caller already issued K-tiles 0 and 1 of this call, in this order - phased_issue01)
+    if (!pre) {
 #pragma unroll
-    for (int r = 0; r < NREG; ++r) issue(0, r);
+        for (int r = 0; r < NREG; ++r) issue(0, r);
+    }
     if (nk > 1) {
+        if (!pre) {
 #pragma unroll
-        for (int r = 0; r < (BM == 256 ? NREG : 2); ++r) issue(1, r);
+            for (int r = 0; r < (BM == 256 ? NREG : 2); ++r) issue(1, r);
+        }
         if (has_a) wait_vm<AHEAD>();
         else wait_vm<AHEAD - 2>();  // (BM < 128, no RA: RB0 of tile 1 only)
     } else {
@@ -1007,6 +1013,40 @@ __global__ __launch_bounds__(512, 1) void phased_kernel(EngineArgs p) {
     engine_epilogue<Tile<BM, 256, 2, 4, 4>, EPI>(p, tm * BM, tn * ph::BN, acc);
 }
 
+// K-tiles 0 and 1 of a 256x256 phased tile, issued exactly as phased_mainloop's prologue issues them (same
+// regions, rows, swizzle and order), so that a persistent block can start the next tile's operand stream
+// before it runs the current tile's epilogue; the next phased_mainloop call then runs with pre = true.
+RF_DEV void phased_issue01(const EngineArgs& p, char* smem, int m0, int n0, int nk) {
+    using namespace ph;
+    using G = Cfg<256>;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int jrow = 16 * wave + (lane >> 2), lch = lane & 3;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+        if (kt == 1 && nk < 2) break;
+#pragma unroll
+        for (int r = 0; r < G::NREG; ++r) {
+            const bool is_a = r < G::NA;
+            const int trow = region_row<256>(r, jrow), grow = region_row<256>(r, 16 * wave);
+            const bf16_t* src;
+            if (is_a) {
+                const int m = m0 + trow;
+                src = p.a + (int64_t)(m < p.m ? m : p.m - 1) * p.lda;
+            } else {
+                src = p.w + (int64_t)(n0 + trow) * p.ldw;
+            }
+            char* base = smem + (kt & 1) * G::TILE + (is_a ? 0 : G::A_IMG);
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh) {
+                const int ch = lch ^ ((trow >> 1) & 3);
+                const bf16_t* g = src + kt * BK2 + kh * 32 + ch * 8;
+                char* dst = base + kh * (256 * 64) + grow * 64;
+                __builtin_amdgcn_global_load_lds(GLB_PTR(void, g), LDS_PTR(void, dst), 16, 0, 0);
+            }
+        }
+    }
+}
+
 // Stream-K over the phased loop: the grid's blocks (<= one per CU, all co-resident) split the
 // tiles x K-tiles iteration space evenly; partial tiles go to the workspace in accumulator order
 // (sc1 stores), the block holding a tile's first K-tile folds them in and runs the epilogue.
@@ -1026,6 +1066,26 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
     const int64_t it_end = total * (wg + 1) / nwg;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     f32x4 acc[TI][TJ];
+    if (p.persist) {
+        // whole tiles wg, wg + nwg, ...: before each epilogue the next tile's first two K-tiles go into the
+        // (now free) LDS buffers, so its operand stream lands while this tile's results are stored
+        const int ntiles = tiles_m * tiles_n;
+        bool pre = false;
+        for (int tile = wg; tile < ntiles; tile += nwg) {
+            int tm, tn;
+            tile_coords(tile, tiles_m, tiles_n, p.group_m, tm, tn);
+            phased_mainloop<BM, NTERM, false, EPI == E_ADD>(p, smem, tm * BM, tn * ph::BN, 0, iters, acc, pre);
+            pre = tile + nwg < ntiles;
+            if (pre) {
+                int tm2, tn2;
+                tile_coords(tile + nwg, tiles_m, tiles_n, p.group_m, tm2, tn2);
+                __syncthreads();  // every wave's last LDS reads of this tile are done (lgkmcnt drained per phase)
+                phased_issue01(p, smem, tm2 * BM, tn2 * ph::BN, iters);
+            }
+            engine_epilogue<Tile<256, 256, 2, 4, 4>, EPI>(p, tm * BM, tn * ph::BN, acc);
+        }
+        return;
+    }
     uint64_t st[16];
     int ns = 0;
     const bool stamp = p.stamps != nullptr;
@@ -1383,7 +1443,7 @@ int launch(EngineArgs a, void* stream, const char* what) {
     const int tiles_m = (a.m + C::BM - 1) / C::BM, tiles_n = a.n / C::BN;
     const int nwg = tiles_n * tiles_m;
     a.group_m = pick_group_m(tiles_m, tiles_n, C::BM, C::BN, (nwg + 7) / 8);
-    hipLaunchKernelGGL((engine_kernel<C, EPI, NTERM, GATHER, false>), dim3(nwg), dim3(C::THREADS), 0, (hipStream_t)stream,
+    RF_LAUNCH((engine_kernel<C, EPI, NTERM, GATHER, false>), dim3(nwg), dim3(C::THREADS), 0, (hipStream_t)stream,
                        a);
     return rf::check_launch(what);
 }
@@ -1406,7 +1466,7 @@ int launch_halo(EngineArgs a, void* stream, const char* what) {
     const int tiles_m = a.m / C::BM, tiles_n = a.n / C::BN;
     const int nwg = tiles_n * tiles_m;
     a.group_m = pick_group_m(tiles_m, tiles_n, C::BM, C::BN, (nwg + 7) / 8);
-    hipLaunchKernelGGL((halo_kernel<C, EPI>), dim3(nwg), dim3(C::THREADS), 0, (hipStream_t)stream, a);
+    RF_LAUNCH((halo_kernel<C, EPI>), dim3(nwg), dim3(C::THREADS), 0, (hipStream_t)stream, a);
     return rf::check_launch(what);
 }
 
@@ -1433,7 +1493,7 @@ template <class C, int EPI, int NTERM = 1, bool GATHER = false>
 int launch_sk(EngineArgs a, int grid, void* stream, const char* what) {
     const int tiles_m = (a.m + C::BM - 1) / C::BM, tiles_n = a.n / C::BN;
     a.group_m = pick_group_m(tiles_m, tiles_n, C::BM, C::BN, ((int64_t)tiles_m * tiles_n + 7) / 8);
-    hipLaunchKernelGGL((engine_kernel<C, EPI, NTERM, GATHER, true>), dim3(grid), dim3(C::THREADS), 0,
+    RF_LAUNCH((engine_kernel<C, EPI, NTERM, GATHER, true>), dim3(grid), dim3(C::THREADS), 0,
                        (hipStream_t)stream, a);
     return rf::check_launch(what);
 }
@@ -1850,12 +1910,27 @@ __global__ __launch_bounds__(256) void quant_mx8_kernel(const bf16_t* __restrict
 
 }  // namespace
 
+// Persistent 256x256 phased launches (RF_GEMM_PERSIST=0 turns them off): more than one round of tiles runs as
+// one block per CU looping over whole tiles, each block prefetching its next tile's first K-tiles before the
+// current tile's epilogue (phased_sk_kernel, p.persist) instead of one block per tile.
+bool persist_on() {
+    static const bool on = !getenv("RF_GEMM_PERSIST") || atoi(getenv("RF_GEMM_PERSIST")) != 0;
+    return on;
+}
+
 template <int EPI, int NTERM, bool GATHER, int BM = 256>
 int launch_phased(EngineArgs a, void* stream, const char* what) {
     const int tiles_m = (a.m + BM - 1) / BM, tiles_n = a.n / 256;
     const int nwg = tiles_n * tiles_m;
     a.group_m = pick_group_m(tiles_m, tiles_n, BM, 256, (nwg + 7) / 8);
-    hipLaunchKernelGGL((phased_kernel<BM, EPI, NTERM, GATHER>), dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    if constexpr (BM == 256 && NTERM == 1 && !GATHER) {
+        if (nwg > 256 && persist_on()) {
+            a.persist = 1;
+            RF_LAUNCH((phased_sk_kernel<EPI, 1>), dim3(256), dim3(512), 0, (hipStream_t)stream, a);
+            return rf::check_launch(what);
+        }
+    }
+    RF_LAUNCH((phased_kernel<BM, EPI, NTERM, GATHER>), dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
     return rf::check_launch(what);
 }
 
@@ -1864,7 +1939,7 @@ int launch_phased3(EngineArgs a, void* stream, const char* what) {
     const int tiles_m = (a.m + BM - 1) / BM, tiles_n = a.n / 256;
     const int nwg = tiles_n * tiles_m;
     a.group_m = pick_group_m(tiles_m, tiles_n, BM, 256, (nwg + 7) / 8);
-    hipLaunchKernelGGL((phased3_kernel<BM, EPI>), dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    RF_LAUNCH((phased3_kernel<BM, EPI>), dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
     return rf::check_launch(what);
 }
 
@@ -1882,7 +1957,7 @@ template <int EPI>
 int launch_phased_sk(EngineArgs a, int grid, void* stream, const char* what) {
     const int tiles_m = (a.m + 255) / 256, tiles_n = a.n / 256;
     a.group_m = pick_group_m(tiles_m, tiles_n, 256, 256, ((int64_t)tiles_m * tiles_n + 7) / 8);
-    hipLaunchKernelGGL((phased_sk_kernel<EPI, 1>), dim3(grid), dim3(512), 0, (hipStream_t)stream, a);
+    RF_LAUNCH((phased_sk_kernel<EPI, 1>), dim3(grid), dim3(512), 0, (hipStream_t)stream, a);
     return rf::check_launch(what);
 }
 
@@ -2010,6 +2085,8 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
     p.gate = gate;
     if (workspace && ws_bytes >= SK_WS_BYTES && skph(m, n, k)) {
         sk_setup(p, workspace);
+        const int64_t tiles = (int64_t)((m + 255) / 256) * (n / 256);
+        p.persist = tiles % 256 == 0 && persist_on();  // whole tiles per block either way: prefetching form
         switch (epilogue) {
             case RF_EPI_BF16: return launch_phased_sk<E_BF16>(p, 256, stream, "rf_gemm_bf16");
             case RF_EPI_F32: return launch_phased_sk<E_F32>(p, 256, stream, "rf_gemm_bf16");
@@ -2085,17 +2162,17 @@ extern "C" int rf_gemm_mx8(const void* a, int64_t lda, const void* sa, int64_t l
     p.ldc = ldc;
     p.bias = bias;
     hipStream_t st = (hipStream_t)stream;
-    const bool plain = getenv("RF_MX8_PLAIN") && atoi(getenv("RF_MX8_PLAIN")) != 0;  // A/B: the unstaggered loop
+    static const bool plain = getenv("RF_MX8_PLAIN") && atoi(getenv("RF_MX8_PLAIN")) != 0;  // A/B: the unstaggered loop
     if (!plain) {
         const int tiles_m = (m + 127) / 128, tiles_n = n / 256;
         const int nwg = tiles_m * tiles_n;
         p.group_m = pick_group_m(tiles_m, tiles_n, 128, 256, (nwg + 7) / 8);
         const dim3 g(nwg), b(512);
         switch (epilogue) {
-            case RF_EPI_BF16: hipLaunchKernelGGL((mx8_p3_kernel<E_BF16>), g, b, 0, st, p); break;
-            case RF_EPI_F32: hipLaunchKernelGGL((mx8_p3_kernel<E_F32>), g, b, 0, st, p); break;
-            case RF_EPI_ADD_F32: hipLaunchKernelGGL((mx8_p3_kernel<E_ADD>), g, b, 0, st, p); break;
-            default: hipLaunchKernelGGL((mx8_p3_kernel<E_SWIGLU>), g, b, 0, st, p); break;
+            case RF_EPI_BF16: RF_LAUNCH((mx8_p3_kernel<E_BF16>), g, b, 0, st, p); break;
+            case RF_EPI_F32: RF_LAUNCH((mx8_p3_kernel<E_F32>), g, b, 0, st, p); break;
+            case RF_EPI_ADD_F32: RF_LAUNCH((mx8_p3_kernel<E_ADD>), g, b, 0, st, p); break;
+            default: RF_LAUNCH((mx8_p3_kernel<E_SWIGLU>), g, b, 0, st, p); break;
         }
         return rf::check_launch("rf_gemm_mx8");
     }
@@ -2104,10 +2181,10 @@ extern "C" int rf_gemm_mx8(const void* a, int64_t lda, const void* sa, int64_t l
     p.group_m = pick_group_m(tiles_m, tiles_n, 256, 256, (nwg + 7) / 8);
     const dim3 g(nwg), b(512);
     switch (epilogue) {
-        case RF_EPI_BF16: hipLaunchKernelGGL((mx8_kernel<E_BF16>), g, b, 0, st, p); break;
-        case RF_EPI_F32: hipLaunchKernelGGL((mx8_kernel<E_F32>), g, b, 0, st, p); break;
-        case RF_EPI_ADD_F32: hipLaunchKernelGGL((mx8_kernel<E_ADD>), g, b, 0, st, p); break;
-        default: hipLaunchKernelGGL((mx8_kernel<E_SWIGLU>), g, b, 0, st, p); break;
+        case RF_EPI_BF16: RF_LAUNCH((mx8_kernel<E_BF16>), g, b, 0, st, p); break;
+        case RF_EPI_F32: RF_LAUNCH((mx8_kernel<E_F32>), g, b, 0, st, p); break;
+        case RF_EPI_ADD_F32: RF_LAUNCH((mx8_kernel<E_ADD>), g, b, 0, st, p); break;
+        default: RF_LAUNCH((mx8_kernel<E_SWIGLU>), g, b, 0, st, p); break;
     }
     return rf::check_launch("rf_gemm_mx8");
 }
@@ -2119,7 +2196,7 @@ extern "C" int rf_quant_mx8(const void* x, int64_t ldx, int rows, int cols, void
                "rf_quant_mx8: cols %% 32, 16-B rows");
     if (rows <= 0) return RF_OK;
     const int64_t n = (int64_t)rows * (cols / 32);
-    hipLaunchKernelGGL(quant_mx8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+    RF_LAUNCH(quant_mx8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)x, ldx, rows, cols, (uint8_t*)q, ldq, (uint8_t*)scales, ld_s);
     return rf::check_launch("rf_quant_mx8");
 }

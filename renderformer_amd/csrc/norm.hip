@@ -426,13 +426,13 @@ extern "C" int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, floa
     const bool al = ((uintptr_t)x & 15) == 0 && ((uintptr_t)weight & 15) == 0 && ((uintptr_t)out & 7) == 0;
     static const bool generic = getenv("RF_RMSNORM_GENERIC") && atoi(getenv("RF_RMSNORM_GENERIC"));  // A/B only
     switch (al && !generic && dim % 256 == 0 ? dim / 256 : 0) {
-        case 2: hipLaunchKernelGGL(rmsnorm_v_kernel<2>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
-        case 3: hipLaunchKernelGGL(rmsnorm_v_kernel<3>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
-        case 4: hipLaunchKernelGGL(rmsnorm_v_kernel<4>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
-        case 6: hipLaunchKernelGGL(rmsnorm_v_kernel<6>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
-        case 8: hipLaunchKernelGGL(rmsnorm_v_kernel<8>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
+        case 2: RF_LAUNCH(rmsnorm_v_kernel<2>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
+        case 3: RF_LAUNCH(rmsnorm_v_kernel<3>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
+        case 4: RF_LAUNCH(rmsnorm_v_kernel<4>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
+        case 6: RF_LAUNCH(rmsnorm_v_kernel<6>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
+        case 8: RF_LAUNCH(rmsnorm_v_kernel<8>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
         default:
-            hipLaunchKernelGGL(rmsnorm_kernel, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows, dim);
+            RF_LAUNCH(rmsnorm_kernel, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows, dim);
     }
     return rf::check_launch("rf_rmsnorm");
 }
@@ -464,7 +464,7 @@ extern "C" int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t s
             bf16_t* d = (bf16_t*)dst + g * dst_gstride;
             const float* w = norm_w ? norm_w + g * w_gstride : nullptr;
 #define RF_QKL(U)                                                                                                 \
-    hipLaunchKernelGGL(qk_norm_rope_kernel<U>, grid, dim3(256), 0, st, s, ld_src, d, ld_dst, src_rows, rows,      \
+    RF_LAUNCH(qk_norm_rope_kernel<U>, grid, dim3(256), 0, st, s, ld_src, d, ld_dst, src_rows, rows,      \
                        n_heads, n_seg, w, eps, seg0_scale, pos, ld_pos, pos_div, freqs, n_freqs)
             if (units <= 64) RF_QKL(1);
             else if (units <= 128) RF_QKL(2);
@@ -475,7 +475,7 @@ extern "C" int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t s
     }
     const dim3 grid(blocks, n_groups);
 #define RF_QKN(U)                                                                                                 \
-    hipLaunchKernelGGL(qk_norm_rope_row_kernel<U>, grid, dim3(256), 0, st, (const bf16_t*)src, ld_src, (bf16_t*)dst, \
+    RF_LAUNCH(qk_norm_rope_row_kernel<U>, grid, dim3(256), 0, st, (const bf16_t*)src, ld_src, (bf16_t*)dst, \
                        ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, seg0_scale, pos, ld_pos, pos_div, freqs, \
                        n_freqs, src_gstride, dst_gstride, (int)w_gstride)
     if (units <= 64) RF_QKN(1);
@@ -506,7 +506,7 @@ extern "C" int rf_embed(float* out, int64_t ldo, const int32_t* out_rows, int ro
     const bool vec = dim % 256 == 0 && ldo % 4 == 0 && ld0 % 4 == 0 && ld1 % 4 == 0 && al(out) && al(base) &&
                      al(in0) && al(w0) && al(in1) && al(w1);
 #define RF_EMB(NV)                                                                                                \
-    hipLaunchKernelGGL(embed_v_kernel<NV>, grid, dim3(256), 0, st, out, ldo, out_rows, rows, base, base_rows, in0, \
+    RF_LAUNCH(embed_v_kernel<NV>, grid, dim3(256), 0, st, out, ldo, out_rows, rows, base, base_rows, in0, \
                        ld0, w0, eps0, in1, ld1, w1, eps1)
     switch (vec ? dim / 256 : 0) {
         case 3: RF_EMB(3); break;
@@ -514,7 +514,7 @@ extern "C" int rf_embed(float* out, int64_t ldo, const int32_t* out_rows, int ro
         case 6: RF_EMB(6); break;
         case 8: RF_EMB(8); break;
         default:
-            hipLaunchKernelGGL(embed_kernel, grid, dim3(256), 0, st, out, ldo, out_rows, rows, dim, base, base_rows,
+            RF_LAUNCH(embed_kernel, grid, dim3(256), 0, st, out, ldo, out_rows, rows, dim, base, base_rows,
                                in0, ld0, w0, eps0, in1, ld1, w1, eps1);
     }
 #undef RF_EMB

@@ -301,7 +301,7 @@ extern "C" int rf_texture_pack(float* texture, int64_t n_rows, int channels, int
     RF_REQUIRE(ldo >= (int64_t)channels * patch_elems && ldo % 4 == 0, "rf_texture_pack: bad ldo");
     RF_REQUIRE(n_rows < (1ll << 31), "rf_texture_pack: too many rows");
     if (n_rows <= 0) return RF_OK;
-    hipLaunchKernelGGL(texture_pack_kernel, dim3((unsigned)n_rows), dim3(256), 0, (hipStream_t)stream, texture,
+    RF_LAUNCH(texture_pack_kernel, dim3((unsigned)n_rows), dim3(256), 0, (hipStream_t)stream, texture,
                        channels, patch_elems, channels - log_channels, dst_row, (bf16_t*)out, ldo, nullptr);
     return rf::check_launch("rf_texture_pack");
 }
@@ -313,7 +313,7 @@ extern "C" int rf_texture_pack_if(const int* flag, float* texture, int64_t n_row
     RF_REQUIRE(ldo >= (int64_t)channels * patch_elems && ldo % 4 == 0, "rf_texture_pack_if: bad ldo");
     RF_REQUIRE(n_rows < (1ll << 31), "rf_texture_pack_if: too many rows");
     if (n_rows <= 0) return RF_OK;
-    hipLaunchKernelGGL(texture_pack_kernel, dim3((unsigned)n_rows), dim3(256), 0, (hipStream_t)stream, texture,
+    RF_LAUNCH(texture_pack_kernel, dim3((unsigned)n_rows), dim3(256), 0, (hipStream_t)stream, texture,
                        channels, patch_elems, channels - log_channels, dst_row, (bf16_t*)out, ldo, flag);
     return rf::check_launch("rf_texture_pack_if");
 }
@@ -331,7 +331,7 @@ extern "C" int rf_texture_scan(float* texture, int64_t n_rows, int channels, int
         return RF_ERR_LAUNCH;
     }
     if (n_rows <= 0) return RF_OK;
-    hipLaunchKernelGGL(texture_scan_kernel, dim3((unsigned)n_rows), dim3(256), 0, (hipStream_t)stream, texture,
+    RF_LAUNCH(texture_scan_kernel, dim3((unsigned)n_rows), dim3(256), 0, (hipStream_t)stream, texture,
                        channels, channels - log_channels, dst_row, coef, ldc, flag);
     return rf::check_launch("rf_texture_scan");
 }
@@ -344,7 +344,7 @@ extern "C" int rf_texture_linear(const float* coef, int64_t ldc, int rows, int c
     RF_REQUIRE(((uintptr_t)out & 15) == 0 && ((uintptr_t)wsum & 15) == 0 && (!bias || ((uintptr_t)bias & 15) == 0),
                "rf_texture_linear: out/wsum/bias must be 16-B aligned");
     if (rows <= 0) return RF_OK;
-    hipLaunchKernelGGL(texture_linear_kernel, dim3((unsigned)((rows + TL_ROWS - 1) / TL_ROWS)), dim3(256), 0,
+    RF_LAUNCH(texture_linear_kernel, dim3((unsigned)((rows + TL_ROWS - 1) / TL_ROWS)), dim3(256), 0,
                        (hipStream_t)stream,
                        coef, ldc, rows, channels, wsum, bias, out, ldo, n, flag);
     return rf::check_launch("rf_texture_linear");
@@ -355,7 +355,7 @@ extern "C" int rf_vn_encode(const float* vn, int64_t n_rows, const int32_t* dst_
     RF_REQUIRE(vn && out, "rf_vn_encode: null pointer");
     RF_REQUIRE(ldo >= 9 * (2 * n_freqs + 1), "rf_vn_encode: ldo too small");
     if (n_rows <= 0) return RF_OK;
-    hipLaunchKernelGGL(vn_encode_kernel, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, vn,
+    RF_LAUNCH(vn_encode_kernel, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, vn,
                        n_rows, dst_row, n_freqs, (bf16_t*)out, ldo);
     return rf::check_launch("rf_vn_encode");
 }
@@ -366,7 +366,7 @@ extern "C" int rf_ray_tokens(const float* c2w, const float* fov_deg, int n_views
     RF_REQUIRE(res % patch == 0, "rf_ray_tokens: resolution %d not divisible by patch %d", res, patch);
     if (n_views <= 0) return RF_OK;
     dim3 grid((res * res + 255) / 256, n_views);
-    hipLaunchKernelGGL(ray_tokens_kernel, grid, dim3(256), 0, (hipStream_t)stream, c2w, fov_deg, res, patch,
+    RF_LAUNCH(ray_tokens_kernel, grid, dim3(256), 0, (hipStream_t)stream, c2w, fov_deg, res, patch,
                        (bf16_t*)out, ray_pos);
     return rf::check_launch("rf_ray_tokens");
 }
@@ -376,7 +376,7 @@ extern "C" int rf_patchify_rays(const float* rays_d, int n_views, int res, int p
     RF_REQUIRE(res % patch == 0, "rf_patchify_rays: resolution %d not divisible by patch %d", res, patch);
     if (n_views <= 0) return RF_OK;
     dim3 grid((res * res + 255) / 256, n_views);
-    hipLaunchKernelGGL(patchify_rays_kernel, grid, dim3(256), 0, (hipStream_t)stream, rays_d, res, patch, (bf16_t*)out);
+    RF_LAUNCH(patchify_rays_kernel, grid, dim3(256), 0, (hipStream_t)stream, rays_d, res, patch, (bf16_t*)out);
     return rf::check_launch("rf_patchify_rays");
 }
 
@@ -390,9 +390,9 @@ extern "C" int rf_scene_pos(const float* tris, const int32_t* valid_idx, const i
     const int nb = max_tris > 0 ? (max_tris + 255) / 256 : 1;
     RF_REQUIRE(partial_floats >= (int64_t)sets * nb * 9, "rf_scene_pos: partials need sets x ceil(max_tris/256) x 9 "
                "floats (rf_scene_pos_partials)");
-    hipLaunchKernelGGL(scene_pos_tri_kernel, dim3(nb, sets), dim3(256), 0, (hipStream_t)stream, tris, valid_idx,
+    RF_LAUNCH(scene_pos_tri_kernel, dim3(nb, sets), dim3(256), 0, (hipStream_t)stream, tris, valid_idx,
                        scene_off, c2w, n_views, n_reg, pos_out, set_off, partials);
-    hipLaunchKernelGGL(scene_pos_center_kernel, dim3(sets), dim3(64), 0, (hipStream_t)stream, scene_off, n_views,
+    RF_LAUNCH(scene_pos_center_kernel, dim3(sets), dim3(64), 0, (hipStream_t)stream, scene_off, n_views,
                        c2w ? 1 : 0, n_reg, nb, partials, pos_out, set_off);
     return rf::check_launch("rf_scene_pos");
 }
@@ -406,7 +406,7 @@ extern "C" int rf_hdr_output(const float* logits, float* out, int n, int c, int 
     RF_REQUIRE(logits && out, "rf_hdr_output: null pointer");
     const int64_t n_pix = (int64_t)n * h * w;
     if (n_pix <= 0) return RF_OK;
-    hipLaunchKernelGGL(hdr_output_kernel, dim3((unsigned)((n_pix + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+    RF_LAUNCH(hdr_output_kernel, dim3((unsigned)((n_pix + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        logits, out, n_pix, c, h * w, elu_alpha, log_decode, channels_last);
     return rf::check_launch("rf_hdr_output");
 }

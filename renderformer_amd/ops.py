@@ -21,23 +21,28 @@ CUS = 256  # MI355X compute units
 
 
 class KernelTimer:
-    """Brackets every launch of one tagged op with HIP events on the launch stream (bench.py roofline)."""
+    """Times every launch of one tagged op (bench.py roofline): before the launch the library's kernel timer is
+    armed (rf_ktimer_arm), so the kernel is dispatched with a start/stop event pair that its own dispatch packet
+    timestamps (hipExtLaunchKernel) on the launch stream — the kernel's duration as rocprofv3's kernel trace
+    reports it, with no marker packets around the launch."""
 
     def __init__(self, tag: str):
         self.tag = tag
-        self.pairs = []
+        self.n = 0
 
     def start(self, tag):
         if tag != self.tag:
             return None
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        self.pairs.append((e0, e1))
-        return e1
+        call("rf_ktimer_arm")
+        self.n += 1
+        return None
 
     def durations_ms(self):
-        torch.cuda.synchronize()
-        return [a.elapsed_time(b) for a, b in self.pairs]
+        import ctypes
+        buf = (ctypes.c_float * max(self.n, 1))()
+        n = int(load().rf_ktimer_read(buf, self.n))
+        self.n = 0
+        return [float(buf[i]) for i in range(min(n, len(buf)))]
 
 
 TIMER: Optional[KernelTimer] = None
@@ -45,11 +50,6 @@ TIMER: Optional[KernelTimer] = None
 
 def _t0(tag):
     return TIMER.start(tag) if TIMER is not None and tag is not None else None
-
-
-def _t1(ev):
-    if ev is not None:
-        ev.record()
 
 
 def _check(cond, msg):
@@ -93,7 +93,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias: Optional[tor
     if bias is not None:
         _dev(bias, torch.float32, "bias")
     ws = _gemm_workspace(a.device)
-    ev = _t0(tag)
+    _t0(tag)
     if flag is None:
         call("rf_gemm_bf16", ptr(a), a.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), ptr(bias), m, n, k,
              epilogue, ptr(ws), ws.numel(), stream())
@@ -101,7 +101,6 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias: Optional[tor
         _dev(flag, torch.int32, "flag")
         call("rf_gemm_bf16_if", ptr(flag), ptr(a), a.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0),
              ptr(bias), m, n, k, epilogue, ptr(ws), ws.numel(), stream())
-    _t1(ev)
     return out
 
 
@@ -147,10 +146,9 @@ def gemm_mx8(a: MX8, w: MX8, out: torch.Tensor, bias: Optional[torch.Tensor] = N
     _check(out.shape[0] == m and out.shape[1] == ncols, f"gemm_mx8: out shape {tuple(out.shape)} != ({m}, {ncols})")
     if bias is not None:
         _dev(bias, torch.float32, "bias")
-    ev = _t0(tag)
+    _t0(tag)
     call("rf_gemm_mx8", ptr(a.q), a.q.stride(0), ptr(a.s), a.s.stride(0), ptr(w.q), w.q.stride(0), ptr(w.s),
          w.s.stride(0), ptr(out), out.stride(0), ptr(bias), m, n, k, epilogue, stream())
-    _t1(ev)
     return out
 
 
@@ -282,12 +280,11 @@ def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int
     elif n_split > 1:
         nbytes = load().rf_attn_workspace_bytes(rows, n_heads, n_split)
         ws = torch.empty(nbytes // 4, dtype=torch.float32, device=out.device)
-    ev = _t0(tag)
+    _t0(tag)
     call("rf_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out), out.stride(0),
          ptr(problems), problems.shape[0], max_q_len, n_heads, hd, scale, n_split, ptr(ws), rows, stream())
     if n_split > 1:
         call("rf_attn_combine", ptr(ws), rows, n_split, n_heads, None, rows, ptr(out), out.stride(0), stream())
-    _t1(ev)
     return out
 
 

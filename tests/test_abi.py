@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load(require_device=False)
     for fn in header_functions():
         assert hasattr(lib, fn), fn
-    assert lib.rf_abi_version() == 7
+    assert lib.rf_abi_version() == 8
     # every int-returning entry point has a ctypes signature in the binding
     assert set(_lib.SIGNATURES) == set(header_functions()) - {"rf_last_error", "rf_abi_version",
                                                                "rf_attn_workspace_bytes", "rf_gemm_workspace_bytes",
@@ -65,3 +65,31 @@ def test_device_error_word_surfaces_on_next_call():
         ops.rmsnorm(x, torch.ones(256, device="cuda"), 1e-6, out)
     lib.rf_clear_device_error()
     ops.rmsnorm(x, torch.ones(256, device="cuda"), 1e-6, out)  # clean again
+
+
+@pytest.mark.gpu
+def test_kernel_timer_times_the_tagged_launch():
+    """rf_ktimer_arm + a tagged op: exactly the tagged launch is timed (dispatch-packet events), its duration is
+    positive and no longer than a marker-event bracket around the same launch."""
+    import torch
+    from renderformer_amd import ops
+    a = torch.randn(4096, 1024, device="cuda").bfloat16()
+    w = torch.randn(8192, 1024, device="cuda").bfloat16()
+    out = torch.empty(4096, 8192, device="cuda", dtype=torch.bfloat16)
+    ops.gemm(a, w, out)  # warm
+    t = ops.KernelTimer("timed")
+    ops.TIMER = t
+    try:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ops.gemm(a, w, out, tag="timed")
+        e1.record()
+        ops.gemm(a, w, out, tag="other")  # not timed
+        ops.gemm(a, w, out, tag="timed")
+    finally:
+        ops.TIMER = None
+    d = t.durations_ms()
+    torch.cuda.synchronize()
+    assert len(d) == 2 and all(x > 0 for x in d), d
+    assert d[0] <= e0.elapsed_time(e1) + 1e-3
+    assert t.durations_ms() == []  # pairs released
