@@ -288,14 +288,23 @@ def main():
         rows = sum(int(b["c2w"].shape[0] * b["c2w"].shape[1]) for b in batches) * (args.res // cfg.patch_size) ** 2
         kern_flops = 2 * rows * 2 * cfg.view_transformer_ffn_hidden_dim * cfg.view_transformer_latent_dim
     achieved = kern_flops / (kern_ms * 1e-3) / 1e12 if durs else float("nan")
-    traffic = None
+    # roofline.traffic: the stage-1 attention's HBM bytes per launch from the rocprofv3 FETCH_SIZE / WRITE_SIZE
+    # passes (tools/gpu.sh round -> tools/pmc_traffic.py), reported only when that record was taken on the
+    # attention sources of this tree (digest match); otherwise null with the reason
+    traffic, traffic_src = None, None
     tpath = os.path.join(REPO, "profiles", "attn_stage1_traffic.json")
     if os.path.exists(tpath) and args.workload == "cbox" and args.scenes == 1:
+        from renderformer_amd._lib import ATTN_SOURCES, source_digest
         try:
-            traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
-            traffic = None if traffic is None else int(traffic)
-        except Exception:
-            traffic = None
+            trec = json.load(open(tpath))
+            if trec.get("source_digest") == source_digest(*ATTN_SOURCES):
+                traffic = int(trec["hbm_bytes_per_launch"])
+                traffic_src = (f"profiles/attn_stage1_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes on "
+                               f"attention sources {trec['source_digest']}, this tree's)")
+            else:
+                traffic_src = "stale: profiles/attn_stage1_traffic.json was measured on other attention sources"
+        except Exception as e:
+            traffic_src = f"unreadable: {e}"
 
     if args.dump and rank == 0:
         import numpy as np
@@ -337,8 +346,7 @@ def main():
                 "peak": PEAK_FP8_TFLOPS if args.fp8 else PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / (PEAK_FP8_TFLOPS if args.fp8 else PEAK_BF16_TFLOPS), 4),
                 "traffic": None if args.fp8 else traffic,
-                "traffic_source": "profiles/attn_stage1_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE pass)"
-                if traffic is not None else None,
+                "traffic_source": None if args.fp8 else traffic_src,
                 "avg_launch_ms": round(kern_ms, 4), "launches_per_step": per_step_launches,
                 "timing": "hipExtLaunchKernel start/stop events on the launch stream (dispatch-packet timestamps)",
                 "algorithmic_flop_per_launch": kern_flops,

@@ -15,6 +15,20 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RF_LIB", os.path.join(_HERE, "lib", "librfhip.so"))
 
+
+def source_digest(*names: str) -> str:
+    """sha256 (first 16 hex digits) over csrc/<names>: ties a measured counter record (profiles/) to the
+    kernel source it was taken on, so a stale record is detected instead of reported."""
+    import hashlib
+    h = hashlib.sha256()
+    for n in names:
+        with open(os.path.join(_HERE, "csrc", n), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+ATTN_SOURCES = ("attention.hip", "common.h")
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _L = ctypes.c_int64

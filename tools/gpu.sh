@@ -1,0 +1,78 @@
+# One runner for every GPU-box job (run through gpurun from the repo root):
+#   bash tools/gpu.sh <task> <tag> [args...]      outputs under gpurun_out/<tag>/
+# tasks
+#   check            GPU test suite + default bench (20 steps)
+#   round            round evidence: tests, bench (+ CPU baseline), smoke, kernel-trace stats, HBM traffic
+#                    (FETCH_SIZE / WRITE_SIZE, one --pmc pass each), attention MFMA counters and in-kernel clock
+#   prof [bench args]  rocprofv3 kernel-trace stats of a short bench run
+#   trace            kernel + HIP API + memory-copy trace of a 2-frame bench run (no counters)
+#   attn             attention GPU tests, ablation timings, per-segment stamps
+#   ab "<envA>" "<envB>"   the bench twice under each of two env settings, interleaved
+#   kb <mode>...     tools/kbench.py micro-benchmarks (KB_* env passed through)
+#   configs          the other SURVEY 8d configurations (bunny, 1024^2, 4 views, 4 scenes, v1-base 256^2)
+#   c5               config 5 (24 views at 1024^2), bf16 and MX fp8
+#   pmc <script args...>   SQ counter passes (one rocprofv3 run each) over one python command
+# Every GPU step runs under its own timeout and the steps are chained with && (set -e): the first failure
+# (fault, abort, time limit) ends the job.
+set -e
+TASK=$1
+TAG=${2:-$1}
+shift 2 || shift $#
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
+prof_run() {  # rocprofv3 needs a cwd and TMPDIR it can write
+    (cd /tmp && TMPDIR=/tmp "$@")
+}
+case $TASK in
+check)
+    timeout -k 10 900 $T tests -m gpu > $O/tests.log 2>&1
+    timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err ;;
+round)
+    timeout -k 10 900 $T tests -m gpu > $O/tests.log 2>&1
+    timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+    prof_run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --profile --steps 5 --warmup 2 > $O/prof.log 2>&1
+    prof_run timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --profile --steps 2 --warmup 1 > $O/pmc_fetch.log 2>&1
+    prof_run timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 $R/bench.py --profile --steps 2 --warmup 1 > $O/pmc_write.log 2>&1
+    RF_TRAFFIC_OUT=$O/attn_stage1_traffic.json python tools/pmc_traffic.py $(find $O/pmc_fetch -name '*counter_collection.csv' -print -quit) $(find $O/pmc_write -name '*counter_collection.csv' -print -quit) $O/pmc_traffic.json > $O/pmc_traffic.txt 2>&1
+    timeout -k 10 300 python tools/attn_ablate.py stamps > $O/attn_clock.log 2>&1
+    prof_run timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_mfma -o run -- python3 $R/tools/attn_ablate.py pmc 5 > $O/pmc_mfma.log 2>&1 ;;
+prof)
+    prof_run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --profile --steps 5 --warmup 2 "$@" > $O/prof.log 2>&1 ;;
+trace)
+    prof_run timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --memory-copy-trace -d $O/trace -o run -- python3 $R/bench.py --profile --steps 2 --warmup 1 > $O/trace.log 2>&1 ;;
+attn)
+    timeout -k 10 300 $T tests/test_kernels_gpu.py -k "attention or swin or attn" > $O/t_attn.log 2>&1
+    timeout -k 10 300 python tools/attn_ablate.py > $O/ablate.log 2>&1
+    timeout -k 10 120 python tools/attn_ablate.py stamps 32 > $O/stamps.log 2>&1 ;;
+ab)
+    for i in 1 2; do
+        env $1 timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_a$i.json 2>> $O/bench.err
+        env $2 timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_b$i.json 2>> $O/bench.err
+    done ;;
+kb)
+    for W in "$@"; do timeout -k 10 400 python -u tools/kbench.py $W > $O/kb_$W.log 2>&1; done ;;
+configs)
+    timeout -k 10 200 python bench.py --no-cpu-baseline --tris 6209 > $O/bunny.json 2> $O/configs.err
+    timeout -k 10 300 python bench.py --no-cpu-baseline --res 1024 --steps 5 --warmup 2 > $O/r1024.json 2>> $O/configs.err
+    timeout -k 10 300 python bench.py --no-cpu-baseline --views 4 --steps 5 --warmup 2 > $O/v4.json 2>> $O/configs.err
+    timeout -k 10 300 python bench.py --no-cpu-baseline --scenes 4 --steps 5 --warmup 2 > $O/s4.json 2>> $O/configs.err
+    timeout -k 10 200 python bench.py --no-cpu-baseline --config base --res 256 > $O/base256.json 2>> $O/configs.err ;;
+c5)
+    timeout -k 10 400 python bench.py --workload c5 --steps 3 --warmup 1 > $O/c5bf16.json 2> $O/c5.err
+    timeout -k 10 400 python bench.py --workload c5 --fp8 --steps 3 --warmup 1 > $O/c5fp8.json 2>> $O/c5.err ;;
+pmc)
+    i=0
+    for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
+             "SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS" \
+             "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM"; do
+        i=$((i+1))
+        prof_run timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $O/p$i -o run -- python3 "$@" > $O/p$i.log 2>&1
+    done ;;
+*)
+    echo "unknown task $TASK" >&2; exit 2 ;;
+esac
+echo done

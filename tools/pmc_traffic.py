@@ -6,11 +6,17 @@ Corrections follow MI355X_MICROARCH.md §HBM: both counters are in KiB; on gfx95
 tallies exactly half of the bytes of wide (16 B/lane) coalesced reads, so it is doubled; WRITE_SIZE
 is exact for 16-B stores.  Rows are grouped by (kernel, grid size) so that e.g. the stage-1 and the
 cross-attention launches of one kernel stay apart.  The stage-1 attention entry (grid of the
-bench workload) is written to profiles/attn_stage1_traffic.json for bench.py's roofline.traffic."""
+bench workload) is written to profiles/attn_stage1_traffic.json (or $RF_TRAFFIC_OUT) for bench.py's
+roofline.traffic, with the digest of the attention sources it was measured on: bench.py reports the figure
+only while the sources still match (run this on the GPU box right after the passes, tools/gpu.sh round)."""
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from renderformer_amd._lib import ATTN_SOURCES, source_digest  # noqa: E402
 
 
 ATTN_CYCLE = (14, 10)  # bench frame: 14 stage-1 then 10 cross-attention launches of attn_sk_kernel
@@ -53,8 +59,9 @@ def main():
         json.dump({"kernel": st1[0]["kernel"], "hbm_bytes_per_launch": st1[0]["hbm_bytes_per_launch"],
                    "read_bytes_per_launch": st1[0]["read_bytes_per_launch"],
                    "write_bytes_per_launch": st1[0]["write_bytes_per_launch"], "launches": st1[0]["launches"],
-                   "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --profile (separate runs)"},
-                  open("profiles/attn_stage1_traffic.json", "w"), indent=1)
+                   "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --profile (separate runs)",
+                   "source_digest": source_digest(*ATTN_SOURCES)},
+                  open(os.environ.get("RF_TRAFFIC_OUT", "profiles/attn_stage1_traffic.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":
