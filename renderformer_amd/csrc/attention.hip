@@ -1187,6 +1187,488 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// One-wave-per-SIMD stream-K kernel (attn_p4_kernel): the unit decomposition, partial format and owner merge
+// of attn_sk_kernel, but 4 waves per workgroup, each owning 64 query rows (two 32-row sub-blocks qs = 0, 1)
+// with the whole register file (O and Q in AGPRs, scores and P in VGPRs): every K / V fragment read from LDS
+// feeds two MFMAs (half the LDS reads of the 8-wave kernel), and the softmax is spread at one exp per MFMA gap
+// over both phases of a tile:
+//   Q(t): S(t+1) = K(t+1) Q^T (32 MFMAs)  ||  exps of tile t, keys 32-63 (b = 1)
+//   P(t): O^T += V(t)^T P(t)^T (32 MFMAs) ||  exps of tile t+1, keys 0-31 (b = 0)
+// K(t+3) / V(t+1) arrive by LDS-DMA issued one piece every 8 MFMAs of P(t) / Q(t) into 2-deep rings (three
+// phases of flight), waited for with counted vmcnt at the phase tops.  Every wave issues every piece (tiles past
+// the piece's end re-read row k_len - 1 into a free slot), so the counts are fixed; the QK^T of the tile after
+// the piece's last is computed and dropped (one half-tile per piece).
+// Running max: exact on the piece's first tile and then FIXED — no O rescale in the loop.  Scores later in the
+// piece may exceed it (P > 1): harmless up to the half-row sum threshold 2^60 (fp32 O / l and bf16 P keep
+// their relative precision).  Past it (a key far above everything before it) the wave raises a workgroup flag
+// with a higher floor for its rows' max, and the workgroup replays the piece from its first tile (rare; each
+// replay raises the floor by >= 1 octave, so replays end).
+constexpr int NW4 = 4;
+constexpr float P4_SUM_THR_LOG2 = 60.0f;
+
+// MFMAs with pinned register files: S chains in VGPRs (read by the softmax VALU), Q and O in AGPRs (only MFMAs
+// touch them).  hipcc would otherwise put every accumulator of a 512-register kernel in AGPRs (each score then
+// costs a v_accvgpr_read) and spill.  Hazards the compiler no longer sees: VALU reads of S / O after the chains
+// are separated by s_nop pads (mfma_drain).
+RF_DEV void mfma_qk0(f32x16& d, const bf16x8& k, const bf16x8& q, const f32x16& c) {
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(d) : "v"(k), "a"(q), "v"(c));
+}
+RF_DEV void mfma_qk(f32x16& d, const bf16x8& k, const bf16x8& q) {
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(k), "a"(q));
+}
+RF_DEV void mfma_pv(f32x16& o, const bf16x8& v, const bf16x8& p) {
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o) : "v"(v), "v"(p));
+}
+RF_DEV void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
+
+template <bool UNIT>
+__global__ __launch_bounds__(NW4 * 64, 1) void attn_p4_kernel(AttnArgs p) {
+    __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // K ring 2 x 16 KiB, V ring 2 x 16 KiB
+    __shared__ int s_bad;  // replay request of the current piece
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int half = lane >> 5;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
+    if (tid == 0) s_bad = 0;  // ordered before its first read by the first piece's barrier
+
+    const int nwg = gridDim.x, hw = blockIdx.x;
+    const int xcd = hw & 7, qd = nwg >> 3, rm = nwg & 7;
+    const int wg = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + (hw >> 3);
+
+    int64_t total = 0;
+    for (int i = 0; i < p.n_problems; ++i) {
+        const int32_t* d = p.problems + 5 * i;
+        total += (int64_t)p.n_heads * ((d[1] + QB5 - 1) / QB5) * ((d[3] + KT - 1) / KT);
+    }
+    int64_t it = total * wg / nwg;
+    const int64_t it_end = total * (wg + 1) / nwg;
+
+    const float c = UNIT ? 1.f : p.c;
+    const float inv_c = UNIT ? 1.f : 1.f / p.c;
+    const float sum_thr = exp2f(p.thr);
+    const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+    // K/V LDS image as attn_sk_kernel (8-row x 32-column subtiles); wave w DMA-fills row groups w and w + 4
+    const int d_row = 8 * wave + ((lane >> 2) & 7);
+    const int d_ch = 4 * (lane >> 5) + ((lane & 3) ^ ((d_row >> 2) & 3));
+    const int kr = lane & 31;
+    const int kb_even = 2048 * (kr >> 3) + 64 * (kr & 7) + 16 * (half ^ ((kr >> 2) & 3));
+    const int kb_odd = 2048 * (kr >> 3) + 64 * (kr & 7) + 16 * ((2 + half) ^ ((kr >> 2) & 3));
+    const int vb_lo = 64 * (4 * (g >> 1) + qq) + 16 * ((2 * (g & 1) + (pp >> 1)) ^ ((g >> 1) & 3)) + 8 * (pp & 1);
+    const int vb_hi = 64 * (4 * (g >> 1) + qq) + 16 * ((2 * (g & 1) + (pp >> 1)) ^ ((2 + (g >> 1)) & 3)) + 8 * (pp & 1);
+
+    int pi = -1;
+    int64_t base = 0, usz = 0;
+    int q_start = 0, q_len = 0, k_start = 0, k_len = 0, v_start = 0, nqb = 1, nt = 1;
+    while (it < it_end) {
+        while (it >= base + usz) {
+            base += usz;
+            ++pi;
+            const int32_t* d = p.problems + 5 * pi;
+            q_start = d[0];
+            q_len = d[1];
+            k_start = d[2];
+            k_len = d[3];
+            v_start = d[4];
+            nqb = (q_len + QB5 - 1) / QB5;
+            nt = (k_len + KT - 1) / KT;
+            usz = (int64_t)p.n_heads * nqb * nt;
+        }
+        const int64_t rel = it - base;
+        const int unit = (int)(rel / nt);
+        const int kt0 = (int)(rel - (int64_t)unit * nt);
+        const int kt1 = (int)min((int64_t)nt, kt0 + (it_end - it));
+        const int n = kt1 - kt0;
+        const int64_t unit_end = base + (int64_t)(unit + 1) * nt;
+        it += n;
+        const int h = unit / nqb, qb = unit - (unit / nqb) * nqb;
+        const int q0 = (int)((int64_t)qb * q_len / nqb), q1 = (int)((int64_t)(qb + 1) * q_len / nqb);
+        const int hoff = h * HD;
+        const int r0 = q0 + wave * 64;  // first row of sub-block 0 of this wave
+        const bool act0 = r0 < q1, act1 = r0 + 32 < q1;
+        // rows past k_len (the tail tile, and tiles past the piece's end: loaded into a free slot, never read)
+        // re-read row k_len - 1
+        const bf16_t* kb0 = p.k + (int64_t)k_start * p.ldk + hoff + 8 * d_ch;
+        const bf16_t* vb0 = p.v + (int64_t)v_start * p.ldv + hoff + 8 * d_ch;
+        auto piece = [&](const bf16_t* src, int64_t ld, int t, uint32_t dst, int e) {
+            const int rg = e >> 1;
+            const uint32_t d0 = __builtin_amdgcn_readfirstlane(dst + (wave + 4 * rg) * 2048 + 1024 * (e & 1));
+            const int row = min(t * KT + 32 * rg + d_row, k_len - 1);
+            dma_piece(src + (int64_t)row * ld + 64 * (e & 1), d0);
+        };
+        // the 4 piece sources of tile t, computed at a phase top (off the MFMA gaps: 3 dependent VALU each)
+        auto piece_src = [&](const bf16_t* src, int64_t ld, int t, const bf16_t* (&a)[4]) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                a[e] = src + (int64_t)min(t * KT + 32 * (e >> 1) + d_row, k_len - 1) * ld + 64 * (e & 1);
+        };
+        auto piece_go = [&](const bf16_t* a, uint32_t dst, int e) {
+            dma_piece(a, __builtin_amdgcn_readfirstlane(dst + (wave + 4 * (e >> 1)) * 2048 + 1024 * (e & 1)));
+        };
+        auto issue_all = [&](const bf16_t* src, int64_t ld, int t, uint32_t dst) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) piece(src, ld, t, dst, e);
+        };
+        auto kread = [&](int koff, int j) {  // K fragment j: key block b = j & 1, k-slice st = j >> 1
+            const int b = j & 1, st = j >> 1;
+            return *reinterpret_cast<const bf16x8*>(smem + koff + (st & 1 ? kb_odd : kb_even) + 8192 * b +
+                                                    512 * (st >> 1));
+        };
+        auto vread = [&](int voff, int j) {  // V^T fragment j: chain dt = j & 3, key block (b, sp) = j >> 2
+            const int dt = j & 3, b = (j >> 2) >> 1, sp = (j >> 2) & 1;
+            const int imm = voff + 2048 * (4 * b + 2 * sp) + 512 * dt;
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, smem + imm + vb_lo));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, smem + imm + 2048 + vb_hi));
+            return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        };
+        auto mask_tail = [&](f32x16 (&sv)[2][2], int t) {  // keys >= k_len of tile t -> -inf
+            if ((t + 1) * KT > k_len) {
+#pragma unroll
+                for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int key = b * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                            sv[qs][b][r] = t * KT + key >= k_len ? NEG : sv[qs][b][r];
+                        }
+            }
+        };
+        auto row_max = [&](const f32x16& s0, const f32x16* s1) {  // max over both lane halves (the whole row)
+            float mt = vmax3(s0[0], s0[1], s0[2]);
+#pragma unroll
+            for (int r = 3; r < 15; r += 2) mt = vmax3(mt, s0[r], s0[r + 1]);
+            mt = __builtin_fmaxf(mt, s0[15]);
+            if (s1) {
+#pragma unroll
+                for (int r = 0; r < 16; r += 2) mt = vmax3(mt, (*s1)[r], (*s1)[r + 1]);
+            }
+            return __builtin_fmaxf(mt, __shfl_xor(mt, 32, 64));
+        };
+        // exp2 of scores r, r+1 of one 16-score chain into the bf16 P fragment and the row sums
+        // software-pipelined form for the MFMA gaps: value v = 0..31 of a half (sub-block v & 1, score v >> 1
+        // of its 16-score chain); gap v takes exp(v), the row-sum add of v - 1 and the bf16 pack of the pair
+        // (v - 3, v - 1) when v - 3 is the even score of a pair: every dependent VALU is >= 1 MFMA after its input
+        auto gap_soft = [&](const f32x16 (&sv)[2][2], int b, bf16x8 (&pq)[2][2][2], float (&ls)[2][4], float (&e)[32],
+                            int v) {
+            e[v] = fast_exp2(UNIT ? sv[v & 1][b][v >> 1] : sv[v & 1][b][v >> 1] * c);
+            if (v >= 1) {
+                const int u = v - 1, qs = u & 1, r = u >> 1;
+                ls[qs][r & 3] = r < 4 ? e[u] : ls[qs][r & 3] + e[u];
+                asm volatile("" : "+v"(ls[qs][r & 3]));
+            }
+            if (v >= 3 && (((v - 3) >> 1) & 1) == 0) {
+                const int u = v - 3, qs = u & 1, r = u >> 1;
+                set_pk(pq[qs][b][r >> 3], (r & 7) >> 1, cvt_pk_bf16(e[u], e[u + 2]));
+            }
+        };
+        auto gap_soft_tail = [&](int b, bf16x8 (&pq)[2][2][2], float (&ls)[2][4], float (&e)[32]) {  // after gap 31
+            ls[1][3] += e[31];
+            asm volatile("" : "+v"(ls[1][3]));
+            set_pk(pq[1][b][1], 3, cvt_pk_bf16(e[29], e[31]));
+        };
+        auto soft = [&](const f32x16& sv, bf16x8 (&pq)[2], float (&ls)[4], int r, int first) {
+            float e[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const float v = sv[r + u];
+                e[u] = fast_exp2(UNIT ? v : v * c);
+                ls[(r + u) & 3] = first ? e[u] : ls[(r + u) & 3] + e[u];
+                asm volatile("" : "+v"(ls[(r + u) & 3]));
+            }
+            set_pk(pq[r >> 3], (r & 7) >> 1, cvt_pk_bf16(e[0], e[1]));
+        };
+
+        float m_floor[2] = {-3.0e38f, -3.0e38f};  // log2 units; raised by a replay request
+        f32x16 o[2][4];
+        float m_run[2], l_run[2];
+        for (;;) {  // one attempt at the piece (a replay is rare)
+            attn_wait_vm<0>();
+            __syncthreads();  // the previous piece's / attempt's LDS readers and stores are done
+
+            bf16x8 qf[2][8];
+#pragma unroll
+            for (int qs = 0; qs < 2; ++qs) {
+                const int qrow = q_start + min(r0 + 32 * qs + kr, q1 - 1);
+                const bf16_t* src = p.q + (int64_t)qrow * p.ldq + hoff + 8 * half;
+#pragma unroll
+                for (int st = 0; st < 8; ++st) qf[qs][st] = *reinterpret_cast<const bf16x8*>(src + 16 * st);
+            }
+#pragma unroll
+            for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) o[qs][dt][r] = 0.f;
+            f32x16 minit[2];
+#pragma unroll
+            for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) minit[qs][r] = 0.f;
+
+            // ---- prologue: Q, K(t0), K(t0+1), V(t0) in flight; S(t0) raw; the running max; P(t0) keys 0-31
+            issue_all(kb0, p.ldk, kt0, lds0 + K5);
+            issue_all(kb0, p.ldk, kt0 + 1, lds0 + K5 + TILE_BYTES);
+            issue_all(vb0, p.ldv, kt0, lds0 + V5);
+            attn_wait_vm<8>();
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+
+            f32x16 sA[2][2], sB[2][2];
+            bf16x8 pA[2][2][2], pB[2][2][2];
+            float lsA[2][4], lsB[2][4];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const bf16x8 kf = kread(K5, j);
+                const int b = j & 1, st = j >> 1;
+#pragma unroll
+                for (int qs = 0; qs < 2; ++qs) {
+                    if (st == 0)
+                        mfma_qk0(sA[qs][b], kf, qf[qs][st], minit[qs]);
+                    else
+                        mfma_qk(sA[qs][b], kf, qf[qs][st]);
+                }
+            }
+            mfma_drain();
+            mask_tail(sA, kt0);
+#pragma unroll
+            for (int qs = 0; qs < 2; ++qs) {
+                const float mrow = __builtin_fmaxf(row_max(sA[qs][0], &sA[qs][1]) * c, m_floor[qs]);
+                m_run[qs] = mrow;
+                const float ds = mrow * inv_c;
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) sA[qs][b][r] -= ds;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) minit[qs][r] = -ds;
+#pragma unroll
+                for (int r = 0; r < 16; r += 2) soft(sA[qs][0], pA[qs][0], lsA[qs], r, r < 4);
+                l_run[qs] = (lsA[qs][0] + lsA[qs][1]) + (lsA[qs][2] + lsA[qs][3]);
+            }
+            __builtin_amdgcn_s_barrier();  // every wave is done reading K(t0): its slot takes K(t0+2)
+            issue_all(kb0, p.ldk, kt0 + 2, lds0 + K5);
+            __builtin_amdgcn_sched_barrier(0);
+
+            // a replay request: rows whose max grew get a new floor (rounded up to whole octaves, so replays end);
+            // returns whether any row of the lane grew (a sum over the threshold with no growth needs no replay)
+            auto request_replay = [&](int qs, float mt) {
+                const float up = mt * c;
+                if (up > 0.f) m_floor[qs] = __builtin_fmaxf(m_floor[qs], m_run[qs] + __builtin_ceilf(up));
+                return up > 0.f;
+            };
+            auto raise_flag = [&]() {
+                if (lane == 0) s_bad = 1;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // visible before this wave's next barrier
+            };
+
+            // ---- one tile: Q(t) then P(t).  s / pc / lsc: tile t (keys 0-31 already in pc[.][0]); sn / pn / lsn:
+            // t+1.  Returns true when the workgroup must replay the piece (flag read one phase after it is set).
+            int pend = 0;
+            auto body = [&](const int i, auto par_c, f32x16 (&s)[2][2], f32x16 (&sn)[2][2], bf16x8 (&pc)[2][2][2],
+                            bf16x8 (&pn)[2][2][2], float (&lsc)[2][4], float (&lsn)[2][4]) -> bool {
+                constexpr int PAR = decltype(par_c)::value;
+                const int t = kt0 + i;
+                const bool has1 = t + 1 < kt1;
+                const int koff = K5 + (PAR ^ 1) * TILE_BYTES;  // K(t+1)
+                const int voff = V5 + PAR * TILE_BYTES;        // V(t)
+                const uint32_t vdst = lds0 + V5 + (PAR ^ 1) * TILE_BYTES;
+                const uint32_t kdst = lds0 + K5 + (PAR ^ 1) * TILE_BYTES;
+                __builtin_amdgcn_sched_barrier(0);
+                // ---- top of Q(t): K(t+1) landed (younger: V(t), K(t+2))
+                attn_wait_vm<8>();
+                __builtin_amdgcn_s_barrier();  // all waves done with P(t-1): V slot PAR^1 is free
+                if (pend) return true;         // (uniform: every wave read the flag after the same barrier)
+                __builtin_amdgcn_sched_barrier(0);
+                {
+                    bf16x8 kf[3];
+                    const bf16_t* va[4];
+                    piece_src(vb0, p.ldv, t + 1, va);
+                    kf[0] = kread(koff, 0);
+                    kf[1] = kread(koff, 1);
+                    float e[32];
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int m = 0; m < 32; ++m) {
+                        const int j = m >> 1, qs = m & 1, b = j & 1, st = j >> 1;
+                        if (st == 0)
+                            mfma_qk0(sn[qs][b], kf[j % 3], qf[qs][st], minit[qs]);
+                        else
+                            mfma_qk(sn[qs][b], kf[j % 3], qf[qs][st]);
+                        __builtin_amdgcn_sched_barrier(0);  // the gap's fillers stay behind its MFMA
+                        if (qs == 0 && j + 2 < 16) kf[(j + 2) % 3] = kread(koff, j + 2);
+                        gap_soft(s, 1, pc, lsc, e, m);  // exps of tile t, keys 32-63
+                        if ((m & 7) == 5) piece_go(va[m >> 3], vdst, m >> 3);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    gap_soft_tail(1, pc, lsc, e);
+                    mfma_drain();
+                }
+                // ---- keys 32-63 of tile t: within the threshold, or a replay request
+                float lh[2];
+#pragma unroll
+                for (int qs = 0; qs < 2; ++qs) lh[qs] = (lsc[qs][0] + lsc[qs][1]) + (lsc[qs][2] + lsc[qs][3]);
+                if (__any(lh[0] > sum_thr || lh[1] > sum_thr)) {
+                    bool grew = false;
+#pragma unroll
+                    for (int qs = 0; qs < 2; ++qs) grew |= request_replay(qs, row_max(s[qs][1], nullptr));
+                    if (__any(grew)) raise_flag();
+                }
+                l_run[0] += lh[0];
+                l_run[1] += lh[1];
+                __builtin_amdgcn_sched_barrier(0);
+
+                // ---- top of P(t): V(t) landed (younger: K(t+2), V(t+1))
+                attn_wait_vm<8>();
+                __builtin_amdgcn_s_barrier();  // all waves done with Q(t): K slot PAR^1 is free
+                pend = __builtin_amdgcn_readfirstlane(s_bad);  // consumed at the next phase top
+                __builtin_amdgcn_sched_barrier(0);
+                mask_tail(sn, t + 1);
+                {
+                    bf16x8 vf[3];
+                    const bf16_t* ka[4];
+                    piece_src(kb0, p.ldk, t + 3, ka);
+                    vf[0] = vread(voff, 0);
+                    vf[1] = vread(voff, 1);
+                    float e[32];
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int m = 0; m < 32; ++m) {
+                        const int j = m >> 1, qs = m & 1, dt = j & 3, b = (j >> 2) >> 1, sp = (j >> 2) & 1;
+                        mfma_pv(o[qs][dt], vf[j % 3], pc[qs][b][sp]);
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (qs == 0 && j + 2 < 16) vf[(j + 2) % 3] = vread(voff, j + 2);
+                        gap_soft(sn, 0, pn, lsn, e, m);  // exps of tile t+1, keys 0-31
+                        if ((m & 7) == 5) piece_go(ka[m >> 3], kdst, m >> 3);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    gap_soft_tail(0, pn, lsn, e);
+                    mfma_drain();
+                }
+                if (has1) {
+                    // ---- keys 0-31 of tile t+1
+#pragma unroll
+                    for (int qs = 0; qs < 2; ++qs) lh[qs] = (lsn[qs][0] + lsn[qs][1]) + (lsn[qs][2] + lsn[qs][3]);
+                    if (__any(lh[0] > sum_thr || lh[1] > sum_thr)) {
+                        bool grew = false;
+#pragma unroll
+                        for (int qs = 0; qs < 2; ++qs) grew |= request_replay(qs, row_max(sn[qs][0], &sn[qs][1]));
+                        if (__any(grew)) raise_flag();
+                    }
+                    l_run[0] += lh[0];
+                    l_run[1] += lh[1];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                return false;
+            };
+            bool replay = false;
+            int i = 0;
+            for (; i + 1 < n; i += 2) {
+                if (body(i, std::integral_constant<int, 0>{}, sA, sB, pA, pB, lsA, lsB) ||
+                    body(i + 1, std::integral_constant<int, 1>{}, sB, sA, pB, pA, lsB, lsA)) {
+                    replay = true;
+                    break;
+                }
+            }
+            if (!replay && i < n) replay = body(i, std::integral_constant<int, 0>{}, sA, sB, pA, pB, lsA, lsB);
+            if (!replay) {  // a flag raised in the last tile's checks
+                __syncthreads();
+                replay = pend || __builtin_amdgcn_readfirstlane(s_bad);
+            }
+            if (!replay) break;
+            attn_wait_vm<0>();
+            __syncthreads();  // every wave has read the flag
+            if (tid == 0) s_bad = 0;  // (ordered before the next reads by the attempt's first barrier)
+        }
+
+        // ---- piece epilogue.  Register order: lane owns query (lane & 31) of sub-block qs, d = dt*32 + 8 gq + 4 half
+        float* pc_ = p.part_o + (int64_t)wg * PIECE_FLOATS;
+        if (kt0 > 0) {
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pc_, 0, PIECE_FLOATS * 4, 0x00020000);
+#pragma unroll
+            for (int qs = 0; qs < 2; ++qs) {
+                if (!(qs ? act1 : act0)) continue;
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int gq = 0; gq < 4; ++gq) {
+                        const f32x4 v4 = {o[qs][dt][4 * gq], o[qs][dt][4 * gq + 1], o[qs][dt][4 * gq + 2], o[qs][dt][4 * gq + 3]};
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v4), rs,
+                                                               ((((wave * 2 + qs) * 16 + dt * 4 + gq) * 64) + lane) * 16, 0, 16);
+                    }
+                const f32x2 ml = {m_run[qs], l_run[qs]};
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ml), rs,
+                                                      PIECE_O * 4 + ((wave * 2 + qs) * 64 + lane) * 8, 0, 16);
+            }
+            attn_wait_vm<0>();
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(p.flag + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+        }
+        if (kt1 < nt) {
+            for (int cw = wg + 1; cw < nwg; ++cw) {
+                const int64_t cs = total * cw / nwg, ce = total * (cw + 1) / nwg;
+                if (cs >= unit_end) break;
+                if (ce == cs) continue;
+                if (tid == 0) {
+                    int spins = 0;
+                    while (__hip_atomic_load(p.flag + cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1 &&
+                           ++spins < p.spin)
+                        __builtin_amdgcn_s_sleep(1);
+                    if (spins >= p.spin) report_device_error(p.err, RF_DEVERR_SK_ATTN);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(p.flag + cw, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                __syncthreads();
+                const float* src = p.part_o + (int64_t)cw * PIECE_FLOATS;
+#pragma unroll
+                for (int qs = 0; qs < 2; ++qs) {
+                    if (!(qs ? act1 : act0)) continue;
+                    const f32x2 ml = *reinterpret_cast<const f32x2*>(src + PIECE_O + ((wave * 2 + qs) * 64 + lane) * 2);
+                    const float mx = __builtin_fmaxf(m_run[qs], ml[0]);
+                    const float wa = fast_exp2(m_run[qs] - mx), wb = fast_exp2(ml[0] - mx);
+                    l_run[qs] = l_run[qs] * wa + ml[1] * wb;
+                    m_run[qs] = mx;
+#pragma unroll
+                    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                        for (int gq = 0; gq < 4; ++gq) {
+                            const f32x4 v4 = *reinterpret_cast<const f32x4*>(
+                                src + ((((wave * 2 + qs) * 16 + dt * 4 + gq) * 64) + lane) * 4);
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) o[qs][dt][4 * gq + e] = o[qs][dt][4 * gq + e] * wa + v4[e] * wb;
+                        }
+                }
+            }
+        }
+#pragma unroll
+        for (int qs = 0; qs < 2; ++qs) {
+            if (!(qs ? act1 : act0)) continue;
+            const float l_tot = l_run[qs] + __shfl_xor(l_run[qs], 32, 64);
+            const int qrow_o = r0 + 32 * qs + kr;
+            if (qrow_o < q1) {
+                const float inv = l_tot > 0.f ? 1.0f / l_tot : 0.f;
+                bf16_t* dst = p.o + (int64_t)(q_start + qrow_o) * p.ldo + hoff;
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int gq = 0; gq < 4; gq += 2) {
+                        uint32_t a0 = pack_bf16x2(o[qs][dt][4 * gq + 0] * inv, o[qs][dt][4 * gq + 1] * inv);
+                        uint32_t a1 = pack_bf16x2(o[qs][dt][4 * gq + 2] * inv, o[qs][dt][4 * gq + 3] * inv);
+                        uint32_t b0 = pack_bf16x2(o[qs][dt][4 * gq + 4] * inv, o[qs][dt][4 * gq + 5] * inv);
+                        uint32_t b1 = pack_bf16x2(o[qs][dt][4 * gq + 6] * inv, o[qs][dt][4 * gq + 7] * inv);
+                        const auto w0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+                        const auto w1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+                        *reinterpret_cast<uint4*>(dst + dt * 32 + 8 * gq + 8 * half) = make_uint4(w0[0], w1[0], w0[1], w1[1]);
+                    }
+            }
+        }
+    }
+}
+
 // merge split partials: out = sum_s 2^(m_s - M) O_s / sum_s 2^(m_s - M) l_s   (one wave per (row, head))
 __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restrict__ part_o,
                                                            const float* __restrict__ part_ml, int64_t part_rows,
@@ -1258,6 +1740,14 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
     const int dbg = getenv("RF_ATTN_DBG") ? atoi(getenv("RF_ATTN_DBG")) : 0;
     const dim3 g(grid), b(NW5 * 64);
     hipStream_t st = (hipStream_t)stream;
+    if (getenv("RF_ATTN_P4") && atoi(getenv("RF_ATTN_P4")) == 1) {  // one-wave-per-SIMD kernel
+        a.thr = getenv("RF_ATTN_THR") ? (float)atof(getenv("RF_ATTN_THR")) : P4_SUM_THR_LOG2;
+        if (unit)
+            RF_LAUNCH((attn_p4_kernel<true>), g, dim3(NW4 * 64), 0, st, a);
+        else
+            RF_LAUNCH((attn_p4_kernel<false>), g, dim3(NW4 * 64), 0, st, a);
+        return rf::check_launch("rf_attn_fwd");
+    }
     switch (unit ? dbg : 0) {  // diagnostic variants (garbage results): ablation timing only
         case 1: RF_LAUNCH((attn_sk_kernel<true, 1>), g, b, 0, st, a); break;
         case 2: RF_LAUNCH((attn_sk_kernel<true, 2>), g, b, 0, st, a); break;

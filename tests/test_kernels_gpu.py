@@ -248,14 +248,23 @@ def _ref_attn(q, k, v, H):
     return (torch.softmax(s, -1) @ vh).transpose(0, 1).reshape(lq, H * 128)
 
 
-@pytest.fixture(params=["sk", "sk_grid7", "sk_grid61", "legacy"])
+@pytest.fixture(params=["sk", "sk_grid7", "sk_grid61", "p4", "p4_grid7", "p4_grid61", "legacy"])
 def attn_mode(request, monkeypatch):
     """Varlen attention modes: the stream-K kernel on the full grid, on small grids that cut most units
-    into 2-3 pieces merged by their owner (RF_ATTN_GRID), and the legacy per-unit kernel (n_split=1).
-    Returns the n_split to pass."""
-    if request.param.startswith("sk_grid"):
-        monkeypatch.setenv("RF_ATTN_GRID", request.param[len("sk_grid"):])
+    into 2-3 pieces merged by their owner (RF_ATTN_GRID), the same for the one-wave-per-SIMD stream-K kernel
+    (RF_ATTN_P4=1), and the legacy per-unit kernel (n_split=1).  Returns the n_split to pass."""
+    if request.param.startswith("p4"):
+        monkeypatch.setenv("RF_ATTN_P4", "1")
+    if "_grid" in request.param:
+        monkeypatch.setenv("RF_ATTN_GRID", request.param.split("_grid")[1])
     return 1 if request.param == "legacy" else None
+
+
+@pytest.fixture(params=["sk", "p4"])
+def sk_kernel(request, monkeypatch):
+    """The two stream-K kernels: 8 waves x 32 rows (default) and 4 waves x 64 rows (RF_ATTN_P4=1)."""
+    monkeypatch.setenv("RF_ATTN_P4", "1" if request.param == "p4" else "0")
+    return request.param
 
 
 @pytest.mark.parametrize("lens", [[1], [63], [64, 65], [77, 200, 1], [5649]])
@@ -343,11 +352,12 @@ def test_attention_cross_shared_v(attn_mode):
 
 @pytest.mark.parametrize("thr", ["8", "0"])
 @pytest.mark.parametrize("grid", [None, "5", "23"])
-def test_attention_stream_k_prescaled_rescale(thr, grid, monkeypatch):
+def test_attention_stream_k_prescaled_rescale(thr, grid, sk_kernel, monkeypatch):
     """The model's form: q pre-scaled by scale*log2(e) (scores are exp2 exponents, no per-score multiply),
     ragged problems with tail tiles, key spikes that force the deferred-rescale branch at chosen tiles
     (incl. right after a piece boundary), repeated launches on the re-armed workspace.  THR=0 (rescale on
-    every growth) and the shipped THR=8 must both match the fp64 reference (guide rule 26)."""
+    every growth) and the shipped THR=8 must both match the fp64 reference (guide rule 26).  For the p4 kernel
+    the same spikes force piece replays (its running max is fixed per piece; THR=0: a replay on every growth)."""
     monkeypatch.setenv("RF_ATTN_THR", thr)
     if grid:
         monkeypatch.setenv("RF_ATTN_GRID", grid)
