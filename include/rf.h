@@ -55,7 +55,7 @@ extern "C" {
 #define RF_ERR_UNSUPPORTED 3
 #define RF_ERR_DEVICE 4       /* an earlier launch reported a device-side error (see rf_device_error) */
 
-#define RF_ABI_VERSION 8
+#define RF_ABI_VERSION 9
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -161,6 +161,20 @@ int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const vo
                 void* o, int64_t ldo, const int32_t* problems, int n_problems, int max_q_len, int n_heads,
                 int head_dim, float scale, int n_split, void* workspace, int64_t ws_rows, void* stream);
 int64_t rf_attn_workspace_bytes(int64_t rows, int n_heads, int n_split);
+/* Cost-balanced stream-K ranges for the n_split == 0 kernel (host function, no device work): from the
+ * HOST copy of `problems`, bounds[0..grid] (int64) = the first tile of each workgroup's range over the
+ * flattened (problem, head, 256-row block, 64-key tile) space, chosen so every workgroup's prologues,
+ * tiles, partial publishes and merges end together (equal tile counts leave the owners of units cut
+ * three ways last).  grid = rf_attn_grid() (the device's CU count) for rf_attn_fwd_sched.
+ * Replaces nothing in the reference (flash_attn schedules internally); a plan-time companion of
+ * rf_attn_fwd, computed once per mask pattern like the problems table itself. */
+int rf_attn_grid(void);
+int rf_attn_schedule(const int32_t* problems_host, int n_problems, int n_heads, int grid, int64_t* bounds);
+/* rf_attn_fwd (n_split == 0) with the workgroup ranges taken from `bounds` (device copy of the
+ * rf_attn_schedule result; the grid is `grid` workgroups).  Same results up to the fp32 merge order. */
+int rf_attn_fwd_sched(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                      void* o, int64_t ldo, const int32_t* problems, int n_problems, int n_heads, int head_dim,
+                      float scale, void* workspace, const int64_t* bounds, int grid, void* stream);
 int rf_attn_combine(const void* workspace, int64_t ws_rows, int n_split, int n_heads, const int32_t* rows,
                     int n_rows, void* o, int64_t ldo, void* stream);
 

@@ -42,6 +42,8 @@ SIGNATURES = {
     "rf_qk_norm_rope_groups": [_P, _L, _L, _P, _L, _L, _P, _I, _I, _I, _I, _I, _P, _L, _F, _F, _P, _L, _I, _P, _I,
                                _P],
     "rf_attn_fwd": [_P, _L, _P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _F, _I, _P, _L, _P],
+    "rf_attn_fwd_sched": [_P, _L, _P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _F, _P, _P, _I, _P],
+    "rf_attn_schedule": [_P, _I, _I, _I, _P],
     "rf_attn_combine": [_P, _L, _I, _I, _P, _I, _P, _L, _P],
     "rf_swin_attn_fwd": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _I, _I, _F, _P],
     "rf_texture_pack": [_P, _L, _I, _I, _I, _P, _P, _L, _P],
@@ -108,6 +110,7 @@ def load(require_device: bool = True):
             lib.rf_scene_pos_partials.restype = ctypes.c_int64
             lib.rf_scene_pos_partials.argtypes = [_I, _I]
             lib.rf_attn_workspace_bytes.argtypes = [_L, _I, _I]
+            lib.rf_attn_grid.argtypes = []
             _lib = lib
     if require_device and not torch.cuda.is_available():
         raise HipLibraryError("renderformer_amd needs a HIP device (MI355X); none is visible")

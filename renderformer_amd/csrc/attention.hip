@@ -37,6 +37,9 @@
 // (problem, head, split, q-block): the q-blocks sharing one K/V stream sit on one
 // XCD and read it from that XCD's L2.
 #include <math.h>
+#include <stdio.h>
+#include <algorithm>
+#include <vector>
 
 #include <type_traits>
 
@@ -73,7 +76,14 @@ struct AttnArgs {
     float thr;  // deferred-rescale threshold (log2 units; RF_ATTN_THR, default 8)
     int* err;   // device error word (rf::device_error_word): stream-K hand-off timeouts
     int spin;   // stream-K hand-off spin bound (polls)
+    // stream-K range boundaries [grid + 1] (rf_attn_schedule: cost-balanced); null = equal tile counts
+    const int64_t* bounds;
 };
+
+// first tile of workgroup w's stream-K range (w == nwg: the total)
+RF_DEV int64_t sk_bound(const AttnArgs& p, int64_t total, int w, int nwg) {
+    return p.bounds ? p.bounds[w] : total * w / nwg;
+}
 
 RF_DEV int swz_off(int row, int ch) { return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4); }
 
@@ -716,8 +726,8 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         const int32_t* d = p.problems + 5 * i;
         total += (int64_t)p.n_heads * ((d[1] + QB5 - 1) / QB5) * ((d[3] + KT - 1) / KT);
     }
-    int64_t it = total * wg / nwg;
-    const int64_t it_end = total * (wg + 1) / nwg;
+    int64_t it = sk_bound(p, total, wg, nwg);
+    const int64_t it_end = sk_bound(p, total, wg + 1, nwg);
 
     const float c = UNIT ? 1.f : p.c;
     const float inv_c = UNIT ? 1.f : 1.f / p.c;
@@ -755,6 +765,10 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             t_prev = now;
         }
     };
+    // publish pending: this workgroup's partial stores were issued at the end of its previous piece and are
+    // covered by the next piece's prologue wait; the flag goes up after that piece's first barrier (all
+    // waves' stores complete), so the store latency hides under the next piece's Q / K / V loads
+    bool pend = false;
     while (it < it_end) {
         uint64_t t_piece = 0;  // DBG & 32: piece prologue cycles -> stamp[6]
         if constexpr (DBG & 32) t_piece = __builtin_amdgcn_s_memtime();
@@ -783,8 +797,8 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         const int hoff = h * HD;
         const bool active = q0 + wave * 32 < q1;  // wave-uniform: this wave owns at least one row
 
-        attn_wait_vm<0>();
-        __syncthreads();  // the previous piece's LDS readers and stores are done
+        if (!pend) attn_wait_vm<0>();
+        __syncthreads();  // the previous piece's LDS readers are done
 
         bf16x8 qf[8];
         {
@@ -891,6 +905,10 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         }
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
+        if (pend) {  // every wave's older partial stores completed before its counted wait above
+            if (tid == 0) __hip_atomic_store(p.flag + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pend = false;
+        }
         f32x16 sA[2], sB[2];
         qk(K5, sA);  // raw scores of the piece's first tile (base 0)
         mask_tail(sA, kt0);
@@ -1099,68 +1117,76 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ml), rs,
                                                       PIECE_O * 4 + (wave * 64 + lane) * 8, 0, 16);
             }
-            attn_wait_vm<0>();
-            __syncthreads();
-            if (tid == 0) __hip_atomic_store(p.flag + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pend = true;  // flag raised in the next piece's prologue, or after the loop
             continue;
         }
         if (kt1 < nt) {
-            // owner of a cut unit: fold in the partials of the later workgroups that hold its other tiles
-            for (int cw = wg + 1; cw < nwg; ++cw) {
-                const int64_t cs = total * cw / nwg, ce = total * (cw + 1) / nwg;
-                if (cs >= unit_end) break;
-                if (ce == cs) continue;
-                if (tid == 0) {
-                    int spins = 0;
-                    while (__hip_atomic_load(p.flag + cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1 &&
-                           ++spins < p.spin)
-                        __builtin_amdgcn_s_sleep(1);
-                    if (spins >= p.spin) report_device_error(p.err, RF_DEVERR_SK_ATTN);  // never silent
+            // owner of a cut unit: fold in the partials of the later workgroups that hold its other tiles.  One
+            // flag wait + acquire + barrier per batch of up to 32 of them (normally all), then the merges back to
+            // back (the owners of units cut three ways end the launch: a second wait / acquire / barrier round
+            // cost them ~10k cycles).  The batch is found in uniform (scalar) code.
+            int cw0 = wg + 1;
+            while (cw0 < nwg) {
+                uint32_t mask = 0;
+                int cw = cw0;
+                bool done = false;
+                for (; cw < nwg && cw - cw0 < 32; ++cw) {
+                    const int64_t cs = sk_bound(p, total, cw, nwg), ce = sk_bound(p, total, cw + 1, nwg);
+                    if (cs >= unit_end) {
+                        done = true;
+                        break;
+                    }
+                    if (ce > cs) mask |= 1u << (cw - cw0);
+                }
+                if (tid == 0 && mask) {
+                    for (uint32_t m = mask; m; m &= m - 1) {
+                        const int f = cw0 + __builtin_ctz(m);
+                        int spins = 0;
+                        while (__hip_atomic_load(p.flag + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1 &&
+                               ++spins < p.spin)
+                            __builtin_amdgcn_s_sleep(1);
+                        if (spins >= p.spin) report_device_error(p.err, RF_DEVERR_SK_ATTN);  // never silent
+                    }
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __hip_atomic_store(p.flag + cw, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+                    for (uint32_t m = mask; m; m &= m - 1)  // re-arm
+                        __hip_atomic_store(p.flag + cw0 + __builtin_ctz(m), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 __syncthreads();
-                if (active) {
-                    const float* src = p.part_o + (int64_t)cw * PIECE_FLOATS;
-                    const f32x2 ml = *reinterpret_cast<const f32x2*>(src + PIECE_O + (wave * 64 + lane) * 2);
-                    const float mx = __builtin_fmaxf(m_run, ml[0]);
-                    const float wa = fast_exp2(m_run - mx), wb = fast_exp2(ml[0] - mx);
-                    l_run = l_run * wa + ml[1] * wb;
-                    m_run = mx;
+                for (uint32_t m = mask; m; m &= m - 1) {
+                    if (active) {
+                        const float* src = p.part_o + (int64_t)(cw0 + __builtin_ctz(m)) * PIECE_FLOATS;
+                        const f32x2 ml = *reinterpret_cast<const f32x2*>(src + PIECE_O + (wave * 64 + lane) * 2);
+                        const float mx = __builtin_fmaxf(m_run, ml[0]);
+                        const float wa = fast_exp2(m_run - mx), wb = fast_exp2(ml[0] - mx);
+                        l_run = l_run * wa + ml[1] * wb;
+                        m_run = mx;
 #pragma unroll
-                    for (int dt = 0; dt < 4; ++dt)
+                        for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-                        for (int gq = 0; gq < 4; ++gq) {
-                            const f32x4 v4 = *reinterpret_cast<const f32x4*>(
-                                src + (((wave * 16 + dt * 4 + gq) * 64) + lane) * 4);
+                            for (int gq = 0; gq < 4; ++gq) {
+                                const f32x4 v4 = *reinterpret_cast<const f32x4*>(
+                                    src + (((wave * 16 + dt * 4 + gq) * 64) + lane) * 4);
 #pragma unroll
-                            for (int e = 0; e < 4; ++e) o[dt][4 * gq + e] = o[dt][4 * gq + e] * wa + v4[e] * wb;
-                        }
+                                for (int e = 0; e < 4; ++e) o[dt][4 * gq + e] = o[dt][4 * gq + e] * wa + v4[e] * wb;
+                            }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
                 }
+                if (done) break;
+                cw0 = cw;
             }
         }
         if (!active) continue;
         const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+        const float inv = l_tot > 0.f ? 1.0f / l_tot : 0.f;
+        // row-per-lane store widened to 16 B (guide T21): column group k = 4 dt + gq is split across the halves
+        // (lane l: columns 8k..8k+3, lane l+32: 8k+4..8k+7); one v_permlane32_swap per dword of the pair (k, k+1)
+        // gives the lower half columns 8k..8k+7 and the upper half 8k+8..8k+15.  (Staging the tile through LDS for
+        // whole-line stores measured slower: 137 vs 129 us per stage-1 launch, the extra registers spill.)
         const int qrow_o = q0 + qi;
         if (qrow_o < q1) {  // (lanes l and l + 32 hold the same query row: both store or neither)
-            const float inv = l_tot > 0.f ? 1.0f / l_tot : 0.f;
             bf16_t* dst = p.o + (int64_t)(q_start + qrow_o) * p.ldo + hoff;
-            // row-per-lane store widened to 16 B (guide T21): column group k = 4 dt + gq is split across the
-            // halves (lane l: columns 8k..8k+3, lane l+32: 8k+4..8k+7); one v_permlane32_swap per dword of
-            // the pair (k, k+1) gives the lower half columns 8k..8k+7 and the upper half 8k+8..8k+15
-            if constexpr (DBG & 512) {  // A/B: the unwidened 8-B stores
-#pragma unroll
-                for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-                    for (int gq = 0; gq < 4; ++gq) {
-                        uint2 pk;
-                        pk.x = pack_bf16x2(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
-                        pk.y = pack_bf16x2(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
-                        *reinterpret_cast<uint2*>(dst + dt * 32 + 8 * gq + 4 * half) = pk;
-                    }
-                continue;
-            }
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
@@ -1174,6 +1200,11 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                     *reinterpret_cast<uint4*>(dst + dt * 32 + 8 * gq + 8 * half) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
                 }
         }
+    }
+    if (pend) {  // the range ended with a published piece
+        attn_wait_vm<0>();
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(p.flag + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if constexpr (DBG & 32) {  // diagnostic: [wg][wave][8] u64 in the last piece slot of the workspace;
         // slots 4 / 5 hold the wave's shader-clock and 100-MHz reference-clock spans (in-kernel clock)
@@ -1243,8 +1274,8 @@ __global__ __launch_bounds__(NW4 * 64, 1) void attn_p4_kernel(AttnArgs p) {
         const int32_t* d = p.problems + 5 * i;
         total += (int64_t)p.n_heads * ((d[1] + QB5 - 1) / QB5) * ((d[3] + KT - 1) / KT);
     }
-    int64_t it = total * wg / nwg;
-    const int64_t it_end = total * (wg + 1) / nwg;
+    int64_t it = sk_bound(p, total, wg, nwg);
+    const int64_t it_end = sk_bound(p, total, wg + 1, nwg);
 
     const float c = UNIT ? 1.f : p.c;
     const float inv_c = UNIT ? 1.f : 1.f / p.c;
@@ -1609,7 +1640,7 @@ __global__ __launch_bounds__(NW4 * 64, 1) void attn_p4_kernel(AttnArgs p) {
         }
         if (kt1 < nt) {
             for (int cw = wg + 1; cw < nwg; ++cw) {
-                const int64_t cs = total * cw / nwg, ce = total * (cw + 1) / nwg;
+                const int64_t cs = sk_bound(p, total, cw, nwg), ce = sk_bound(p, total, cw + 1, nwg);
                 if (cs >= unit_end) break;
                 if (ce == cs) continue;
                 if (tid == 0) {
@@ -1712,12 +1743,15 @@ int cu_count() {  // per-device, queried once
 
 int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv, void* o,
                    int64_t ldo, const int32_t* problems, int n_problems, int n_heads, float scale, void* workspace,
-                   void* stream) {
+                   void* stream, const int64_t* bounds = nullptr, int grid = 0) {
     RF_REQUIRE(workspace, "rf_attn_fwd: stream-K mode needs the workspace (rf_attn_workspace_bytes(0, H, 0))");
-    int grid = cu_count();
-    if (const char* env = getenv("RF_ATTN_GRID")) grid = atoi(env);  // tests: force many cut units
+    if (!bounds) {
+        grid = cu_count();
+        if (const char* env = getenv("RF_ATTN_GRID")) grid = atoi(env);  // tests: force many cut units
+    }
     RF_REQUIRE(grid >= 1 && grid <= SK5_MAX_GRID, "rf_attn_fwd: grid %d out of range", grid);
     AttnArgs a{};
+    a.bounds = bounds;
     a.q = (const bf16_t*)q;
     a.k = (const bf16_t*)k;
     a.v = (const bf16_t*)v;
@@ -1821,6 +1855,147 @@ extern "C" int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ld
     else
         RF_LAUNCH((attn_fwd_kernel<false, 4>), dim3((unsigned)total), dim3(256), 0, (hipStream_t)stream, a);
     return rf::check_launch("rf_attn_fwd");
+}
+
+// ---------------------------------------------------------------------------------------------
+// Cost-balanced stream-K ranges (rf_attn_schedule).  With equal tile counts per workgroup the launch
+// ends with the owners of units cut three ways: a workgroup whose range lies inside one unit ("mid")
+// has one piece (one prologue, one publish) and finishes ~14 % early, while the owner of that unit
+// has two pieces and merges two partials (bench shape, per-role lifetimes from the s_memtime stamps of
+// tools/attn_ablate.py stamps: mid 222k, owners of 3-way units 257k, others 246k cycles).  Here every
+// piece costs a prologue, its tiles, and a publish (non-first piece of its unit) or a finish (first
+// piece: one merge per later piece, each after that piece's publish, then the O store), and the
+// ranges are chosen backwards from the last workgroup (whose successors' publish times are then known)
+// so that every workgroup finishes by a common time T, the smallest T that covers all tiles.
+namespace {
+struct SkCost {
+    double tile = 3170, pro = 8700, pub = 8500, merge = 9800, store = 6000;  // shader cycles
+};
+
+struct SkUnits {
+    std::vector<int64_t> base;  // first tile of problem i
+    std::vector<int64_t> nt;    // tiles per unit of problem i (0: problem holds no tiles)
+    int64_t total = 0;
+    void unit_of(int64_t x, int64_t& us, int64_t& ue) const {  // [start, end) of the unit holding tile x
+        int64_t i = (int64_t)(std::upper_bound(base.begin(), base.end(), x) - base.begin()) - 1;
+        while (nt[i] == 0) --i;
+        const int64_t u = (x - base[i]) / nt[i];
+        us = base[i] + u * nt[i];
+        ue = us + nt[i];
+    }
+};
+
+// finish time of workgroup w with range [a, b), given the later workgroups' bounds and publish times;
+// *pub = the publish time of its first piece when that piece is a unit's later piece
+double sk_simulate(const SkUnits& U, const SkCost& c, int w, int64_t a, int64_t b, const std::vector<int64_t>& bnd,
+                   const std::vector<double>& pubt, int grid, double* pub) {
+    double t = 0;
+    *pub = 0;
+    for (int64_t x = a; x < b;) {
+        int64_t us, ue;
+        U.unit_of(x, us, ue);
+        const int64_t e = std::min(b, ue);
+        t += c.pro + (double)(e - x) * c.tile;
+        if (x > us) {
+            t += c.pub;
+            *pub = t;
+        } else {
+            if (e < ue)
+                for (int cw = w + 1; cw < grid && bnd[cw] < ue; ++cw)
+                    if (bnd[cw + 1] > bnd[cw]) t = std::max(t, pubt[cw]) + c.merge;
+            t += c.store;
+        }
+        x = e;
+    }
+    return t;
+}
+
+// backward fill with finish time T; returns bnd[0] (0 = every tile placed).  A range is feasible when the
+// workgroup finishes by T and its published piece (if any) lands early enough for the owner to merge it
+// and store by T; the largest feasible range is found by bisection on its start (the finish time grows
+// with the range except at unit boundaries, where a piece changes role).
+int64_t sk_fill(const SkUnits& U, const SkCost& c, int grid, double T, std::vector<int64_t>& bnd,
+                std::vector<double>& pubt) {
+    bnd.assign(grid + 1, 0);
+    pubt.assign(grid + 1, 0);
+    bnd[grid] = U.total;
+    const double pub_by = T - 2 * c.merge - c.store;  // room for the owner's merges (normally <= 2) and store
+    auto ok = [&](int w, int64_t a, int64_t b, double* pub) {
+        return sk_simulate(U, c, w, a, b, bnd, pubt, grid, pub) <= T && *pub <= pub_by;
+    };
+    for (int w = grid - 1; w >= 0; --w) {
+        const int64_t b = bnd[w + 1];
+        double pub = 0;
+        int64_t lo = b, hi = 0;  // lo: feasible start (empty range), search [hi, lo)
+        if (b > 0 && ok(w, 0, b, &pub)) {
+            lo = 0;
+        } else if (b > 0) {
+            hi = 1;
+            while (hi < lo) {  // smallest feasible a in [hi, lo]
+                const int64_t mid = (hi + lo) / 2;
+                if (ok(w, mid, b, &pub)) lo = mid;
+                else hi = mid + 1;
+            }
+        }
+        bnd[w] = lo;
+        ok(w, lo, b, &pub);
+        pubt[w] = lo < b ? pub : 0;
+    }
+    return bnd[0];
+}
+}  // namespace
+
+extern "C" int rf_attn_grid(void) { return cu_count(); }
+
+extern "C" int rf_attn_schedule(const int32_t* problems, int n_problems, int n_heads, int grid, int64_t* bounds) {
+    RF_REQUIRE(problems && bounds && n_problems > 0 && n_heads > 0, "rf_attn_schedule: bad arguments");
+    RF_REQUIRE(grid >= 1 && grid <= SK5_MAX_GRID, "rf_attn_schedule: grid %d out of range", grid);
+    SkUnits U;
+    for (int i = 0; i < n_problems; ++i) {
+        const int32_t* d = problems + 5 * i;
+        RF_REQUIRE(d[1] >= 0 && d[3] >= 0, "rf_attn_schedule: negative length in problem %d", i);
+        const int64_t nt = (d[3] + KT - 1) / KT;
+        const int64_t tiles = (int64_t)n_heads * ((d[1] + QB5 - 1) / QB5) * nt;
+        U.base.push_back(U.total);
+        U.nt.push_back(tiles > 0 ? nt : 0);
+        U.total += tiles;
+    }
+    if (U.total == 0) {
+        for (int w = 0; w <= grid; ++w) bounds[w] = 0;
+        return RF_OK;
+    }
+    SkCost c;
+    if (const char* env = getenv("RF_ATTN_COST"))  // tile,pro,pub,merge,store (tuning)
+        sscanf(env, "%lf,%lf,%lf,%lf,%lf", &c.tile, &c.pro, &c.pub, &c.merge, &c.store);
+    std::vector<int64_t> bnd;
+    std::vector<double> pubt;
+    // lo is infeasible (less than the average tile work); hi doubled until feasible
+    double lo = (double)U.total * c.tile / grid;
+    double hi = 2 * lo + 4 * (c.pro + c.pub + c.merge + c.store);
+    while (sk_fill(U, c, grid, hi, bnd, pubt) != 0) {
+        lo = hi;
+        hi *= 2;
+    }
+    for (int iter = 0; iter < 60 && hi - lo > 0.1 * c.tile; ++iter) {
+        const double mid = 0.5 * (lo + hi);
+        (sk_fill(U, c, grid, mid, bnd, pubt) == 0 ? hi : lo) = mid;
+    }
+    RF_REQUIRE(sk_fill(U, c, grid, hi, bnd, pubt) == 0, "rf_attn_schedule: internal error (tiles left)");
+    for (int w = 0; w <= grid; ++w) bounds[w] = bnd[w];
+    return RF_OK;
+}
+
+extern "C" int rf_attn_fwd_sched(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                                 void* o, int64_t ldo, const int32_t* problems, int n_problems, int n_heads,
+                                 int head_dim, float scale, void* workspace, const int64_t* bounds, int grid,
+                                 void* stream) {
+    RF_REQUIRE(q && k && v && o && problems && bounds, "rf_attn_fwd_sched: null pointer");
+    RF_REQUIRE(head_dim == HD, "rf_attn_fwd_sched: head_dim must be 128 (got %d)", head_dim);
+    RF_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0,
+               "rf_attn_fwd_sched: strides must be 16-B aligned");
+    if (n_problems <= 0) return RF_OK;
+    return attn_sk_launch(q, ldq, k, ldk, v, ldv, o, ldo, problems, n_problems, n_heads, scale, workspace, stream,
+                          bounds, grid);
 }
 
 extern "C" int64_t rf_attn_workspace_bytes(int64_t rows, int n_heads, int n_split) {

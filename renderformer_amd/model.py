@@ -174,11 +174,13 @@ class _Plan:
     prob1: torch.Tensor        # int32 [B, 5]
     prob2: torch.Tensor        # int32 [P, 5]
     prob_self: torch.Tensor    # int32 [P, 5]
+    sched1: Optional[torch.Tensor] = None      # int64 [grid + 1] stream-K ranges of prob1 (ops.attn_schedule)
+    sched2: Optional[torch.Tensor] = None      # ... of prob2
     view_valid: Optional[torch.Tensor] = None  # for forward(): valid rows into [P*N]
     view_off: Optional[torch.Tensor] = None
 
 
-def _build_plan(mask: torch.Tensor, V: int, res: int, patch: int, n_reg: int, device) -> _Plan:
+def _build_plan(mask: torch.Tensor, V: int, res: int, patch: int, n_reg: int, device, n_heads: int = 0) -> _Plan:
     B, N = mask.shape
     counts = [int(c) for c in mask.sum(dim=1).tolist()]  # host sync (like flash_attn unpad_input)
     flat = mask.reshape(-1)
@@ -215,7 +217,9 @@ def _build_plan(mask: torch.Tensor, V: int, res: int, patch: int, n_reg: int, de
     return _Plan(B=B, V=V, res=res, counts=counts, T_tri=T_tri, T1=cu1[-1], T_kv=kv_off[-1], R=R, hp=hp, wp=wp,
                  max_s=max(S), valid_flat=valid_flat, dst_row=dst_row, tri_rows=dev(tri_rows), reg_rows=dev(reg_rows),
                  scene_off=dev(scene_off), cu1=dev(cu1), kv_off=dev(kv_off), kv_src_rows=dev(kv_src),
-                 prob1=dev(prob1).view(-1, 5), prob2=dev(prob2).view(-1, 5), prob_self=dev(prob_self).view(-1, 5))
+                 prob1=dev(prob1).view(-1, 5), prob2=dev(prob2).view(-1, 5), prob_self=dev(prob_self).view(-1, 5),
+                 sched1=ops.attn_schedule(prob1, n_heads, device) if n_heads else None,
+                 sched2=ops.attn_schedule(prob2, n_heads, device) if n_heads else None)
 
 
 def _hf_cache_snapshot(model_id: str) -> Optional[str]:
@@ -339,7 +343,8 @@ class RenderFormer:
         if plan is None:
             if len(self._plans) > 16:
                 self._plans.clear()
-            plan = _build_plan(mask, V, res, self.config.patch_size, self.config.num_register_tokens, self._device)
+            plan = _build_plan(mask, V, res, self.config.patch_size, self.config.num_register_tokens, self._device,
+                               self.config.num_heads)
             self._plans[key] = plan
         self._last_plan = (mask, (mask._version, V, res), plan)
         return plan
@@ -395,7 +400,7 @@ class RenderFormer:
             ops.qk_norm_rope(qk_pair, qk_pair, H, L.qk_norm if cfg.view_indep_qk_norm else None, EPS, pos1, W.enc_freqs,
                              n_seg=2, q_scale=ops.Q_LOG2_SCALE)
             ops.attention(q, k, v, att, plan.prob1, plan.max_s, H, tag="attn_stage1", max_k_len=plan.max_s,
-                          q_prescaled=True)
+                          q_prescaled=True, schedule=plan.sched1)
             ops.gemm(att, L.w_out, x, None, ops.EPI_ADD_F32)
             ops.rmsnorm(x, L.ffn_norm, EPS, h)
             ops.gemm(h, L.w13, g, None, ops.EPI_SWIGLU, tag="gemm_w13_stage1")
@@ -465,7 +470,7 @@ class RenderFormer:
                 ops.qk_norm_rope(kv[:, :D], kview, H, L.k_norm if qk else None, EPS, pos2, W.dec_freqs,
                                  src_rows=plan.kv_src_rows)
             ops.attention(q2, kview, kv[:, D:], att, plan.prob2, R, H, tag="attn_cross", max_k_len=plan.max_s,
-                          q_prescaled=True)
+                          q_prescaled=True, schedule=plan.sched2)
             proj(att, L.wo, getattr(L, "wo8", None), x, ops.EPI_ADD_F32)
             # (ii) self-attention between ray tokens
             if qkv is not None:

@@ -254,12 +254,43 @@ def _attn_workspace(device) -> torch.Tensor:
     return ws
 
 
+def attn_grid(device=None) -> int:
+    """Workgroups of the stream-K attention grid: RF_ATTN_GRID (tests) or the device's CU count."""
+    env = os.environ.get("RF_ATTN_GRID")
+    if env:
+        return int(env)
+    with torch.cuda.device(device):
+        return int(load().rf_attn_grid())
+
+
+def attn_schedule_host(problems, n_heads: int, grid: int):
+    """rf_attn_schedule (host only, no device): cost-balanced stream-K range bounds, int64 numpy [grid + 1]."""
+    import numpy as np
+    arr = np.ascontiguousarray(np.asarray(problems, dtype=np.int32).reshape(-1, 5))
+    out = np.zeros(grid + 1, dtype=np.int64)
+    lib = load(require_device=False)
+    rc = lib.rf_attn_schedule(arr.ctypes.data, arr.shape[0], n_heads, grid, out.ctypes.data)
+    if rc != 0:
+        raise ValueError(lib.rf_last_error().decode(errors="replace"))
+    return out
+
+
+def attn_schedule(problems, n_heads: int, device) -> Optional[torch.Tensor]:
+    """Device copy of the cost-balanced ranges for `problems` (host [P, 5] list/array), built once per plan;
+    None when RF_ATTN_SCHED=0 (equal tile counts per workgroup, for A/B)."""
+    if os.environ.get("RF_ATTN_SCHED", "1") == "0":
+        return None
+    return torch.from_numpy(attn_schedule_host(problems, n_heads, attn_grid(device))).to(device)
+
+
 def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int,
               scale: Optional[float] = None, tag: Optional[str] = None, max_k_len: Optional[int] = None,
-              n_split: Optional[int] = None, q_prescaled: bool = False) -> torch.Tensor:
+              n_split: Optional[int] = None, q_prescaled: bool = False,
+              schedule: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Varlen attention; problems int32 [P, 5] = (q_start, q_len, k_start, k_len, v_start).
 
-    n_split None/0: the stream-K kernel (balanced over the CUs, cut units merged in-kernel);
+    n_split None/0: the stream-K kernel (balanced over the CUs, cut units merged in-kernel), with the
+    workgroup ranges of `schedule` (attn_schedule of the same problems and heads) when given;
     n_split >= 1: the legacy per-unit kernel with flash-decoding splits + rf_attn_combine.
     q_prescaled: q already carries scale*log2(e) (qk_norm_rope q_scale=Q_LOG2_SCALE)."""
     for t, nme in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
@@ -281,6 +312,12 @@ def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int
         nbytes = load().rf_attn_workspace_bytes(rows, n_heads, n_split)
         ws = torch.empty(nbytes // 4, dtype=torch.float32, device=out.device)
     _t0(tag)
+    if n_split == 0 and schedule is not None:
+        _dev(schedule, torch.int64, "schedule")
+        call("rf_attn_fwd_sched", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+             out.stride(0), ptr(problems), problems.shape[0], n_heads, hd, scale, ptr(ws), ptr(schedule),
+             schedule.numel() - 1, stream())
+        return out
     call("rf_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out), out.stride(0),
          ptr(problems), problems.shape[0], max_q_len, n_heads, hd, scale, n_split, ptr(ws), rows, stream())
     if n_split > 1:

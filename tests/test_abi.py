@@ -25,11 +25,11 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load(require_device=False)
     for fn in header_functions():
         assert hasattr(lib, fn), fn
-    assert lib.rf_abi_version() == 8
+    assert lib.rf_abi_version() == 9
     # every int-returning entry point has a ctypes signature in the binding
     assert set(_lib.SIGNATURES) == set(header_functions()) - {"rf_last_error", "rf_abi_version",
                                                                "rf_attn_workspace_bytes", "rf_gemm_workspace_bytes",
-                                                               "rf_scene_pos_partials"}
+                                                               "rf_scene_pos_partials", "rf_attn_grid"}
 
 
 def test_invalid_arguments_raise_value_error_without_device():
@@ -93,3 +93,73 @@ def test_kernel_timer_times_the_tagged_launch():
     assert len(d) == 2 and all(x > 0 for x in d), d
     assert d[0] <= e0.elapsed_time(e1) + 1e-3
     assert t.durations_ms() == []  # pairs released
+
+
+def _sk_pieces(bounds, units):
+    """(workgroup, first tile, end tile, unit start, unit end) of every piece of a stream-K range table"""
+    out = []
+    for w in range(len(bounds) - 1):
+        x = int(bounds[w])
+        while x < bounds[w + 1]:
+            us, ue = next((a, b) for a, b in units if a <= x < b)
+            e = min(int(bounds[w + 1]), ue)
+            out.append((w, x, e, us, ue))
+            x = e
+    return out
+
+
+@pytest.mark.parametrize("probs,grid", [
+    ([[0, 5649, 0, 5649, 0]], 256),                                   # stage 1 at the bench shape
+    ([[0, 4096, 0, 5649, 0]], 256),                                   # cross-attention, one view
+    ([[0, 5649, 0, 5649, 0], [5649, 3000, 5649, 3000, 5649]], 256),   # two scenes, ragged
+    ([[0, 0, 0, 0, 0], [0, 300, 0, 70, 0], [300, 40, 70, 1, 70]], 64),  # empty problem, tiny ones
+    ([[0, 100, 0, 100, 0]], 512),                                      # fewer tiles than workgroups
+])
+def test_attn_schedule_covers_every_tile_once(probs, grid):
+    """rf_attn_schedule (host only): monotone bounds from 0 to the total tile count, so every tile of the
+    flattened (problem, head, 256-row block, 64-key tile) space belongs to exactly one workgroup, and each unit's
+    pieces are consecutive workgroups (the kernel's owner walks workgroups wg+1.. until the unit ends)."""
+    import numpy as np
+    import torch  # noqa: F401
+    from renderformer_amd import _lib, ops
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("librfhip.so not built")
+    H = 8
+    b = ops.attn_schedule_host(probs, H, grid)
+    units, tot = [], 0
+    for q0, ql, k0, kl, v0 in probs:
+        nt = (kl + 63) // 64
+        n_units = H * ((ql + 255) // 256) if ql > 0 else 0
+        for _ in range(n_units if nt else 0):
+            units.append((tot, tot + nt))
+            tot += nt
+    assert b.shape == (grid + 1,) and b[0] == 0 and b[-1] == tot
+    assert np.all(np.diff(b) >= 0)
+    pieces = _sk_pieces(b, units)
+    assert sum(e - x for _, x, e, _, _ in pieces) == tot
+    by_unit = {}
+    for w, x, e, us, ue in pieces:
+        by_unit.setdefault(us, []).append(w)
+    for ws in by_unit.values():
+        assert ws == list(range(ws[0], ws[0] + len(ws)))
+
+
+def test_attn_schedule_balances_the_bench_shape():
+    """At the stage-1 bench shape the balanced table gives the workgroups that hold a single piece ("mid": one
+    prologue, one publish) more tiles than those with two pieces, and no workgroup is left empty."""
+    import numpy as np
+    import torch  # noqa: F401
+    from renderformer_amd import _lib, ops
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("librfhip.so not built")
+    b = ops.attn_schedule_host([[0, 5649, 0, 5649, 0]], 8, 256)
+    d = np.diff(b)
+    assert d.min() > 0
+    units = [(89 * u, 89 * u + 89) for u in range(184)]
+    pieces = _sk_pieces(b, units)
+    per_wg = {}
+    for w, *_ in pieces:
+        per_wg[w] = per_wg.get(w, 0) + 1
+    single = [d[w] for w in range(256) if per_wg[w] == 1]
+    double = [d[w] for w in range(256) if per_wg[w] == 2]
+    assert single and double and np.mean(single) > np.mean(double)

@@ -20,8 +20,12 @@ out = torch.empty(S, D, device="cuda", dtype=torch.bfloat16)
 prob = torch.tensor([[0, S, 0, S, 0]], dtype=torch.int32, device="cuda")
 
 
-def run():
-    ops.attention(qs, qkv[:, D:2 * D], qkv[:, 2 * D:], out, prob, S, H, q_prescaled=True)
+# cost-balanced stream-K ranges as the model uses them (RF_ATTN_SCHED=0: equal tile counts)
+sched = ops.attn_schedule([[0, S, 0, S, 0]], H, out.device)
+
+
+def run(schedule=sched):
+    ops.attention(qs, qkv[:, D:2 * D], qkv[:, 2 * D:], out, prob, S, H, q_prescaled=True, schedule=schedule)
 
 
 if len(sys.argv) > 1 and sys.argv[1] == "stamps":
@@ -45,6 +49,31 @@ if len(sys.argv) > 1 and sys.argv[1] == "stamps":
         per = (st[:, sl, :4] / tiles[:, sl, None]).mean(dim=(0, 1))
         print(grp, "cycles/tile:", ", ".join(f"{n} {v:.0f}" for n, v in zip(names, per.tolist())),
               f"| total {per.sum():.0f}", flush=True)
+    # workgroup lifetimes by role in the contiguous stream-K schedule (all workgroups start together, so the
+    # spread of lifetimes is the kernel's tail): "mid" = range strictly inside one unit (publishes at its end),
+    # "own3" = holds the head of a unit that has a mid piece (merges that late partial), "other"
+    nt = (S + 63) // 64
+    total = H * ((S + 255) // 256) * nt
+    life = st[..., 4].max(dim=1).values  # per workgroup: its slowest wave
+    bnd = sched.tolist() if sched is not None else [total * w // 256 for w in range(257)]
+    print("schedule:", "cost-balanced" if sched is not None else "equal tiles",
+          "tiles per workgroup min/max", min(b - a for a, b in zip(bnd, bnd[1:])), max(b - a for a, b in zip(bnd, bnd[1:])))
+    roles = []
+    for w in range(256):
+        a, b = bnd[w], bnd[w + 1]
+        roles.append("empty" if a == b else "mid" if a % nt and a // nt == (b - 1) // nt else "other")
+    for w in range(255):
+        if roles[w + 1] == "mid" and roles[w] == "other":
+            roles[w] = "own3"
+    q = torch.tensor([0.5, 0.9, 1.0], dtype=torch.float64)
+    print(f"workgroup lifetime (cycles): all p50/p90/max {torch.quantile(life, q).tolist()}")
+    for r in ("mid", "own3", "other"):
+        sel = torch.tensor([x == r for x in roles])
+        if sel.any():
+            ep = (st[sel, :, 4] - st[sel, :, :4].sum(-1) - st[sel, :, 6]).mean()
+            print(f"  {r:5s} n={int(sel.sum()):3d} lifetime p50/p90/max "
+                  f"{[round(v) for v in torch.quantile(life[sel], q).tolist()]}  epilogue/merge mean {ep:.0f}"
+                  f"  prologue mean {st[sel, :, 6].mean():.0f}  tiles {st[sel, :, 7].mean():.1f}", flush=True)
     sys.exit(0)
 if len(sys.argv) > 1 and sys.argv[1] == "pmc":
     for _ in range(int(sys.argv[2]) if len(sys.argv) > 2 else 5):
@@ -52,17 +81,19 @@ if len(sys.argv) > 1 and sys.argv[1] == "pmc":
     torch.cuda.synchronize()
     sys.exit(0)
 fl = 4 * S * S * D
-VARIANTS = os.environ.get("ABL", "0,64,1,2,4,8,16,20").split(",")
+VARIANTS = os.environ.get("ABL", "0,u,64,1,2,4,8,16,20").split(",")
 
 
 def timed(dbg, reps=20):
-    os.environ["RF_ATTN_DBG"] = dbg
-    run()
+    """dbg = an RF_ATTN_DBG value, or "u": the shipped kernel on equal tile counts (no schedule)"""
+    os.environ["RF_ATTN_DBG"] = "0" if dbg == "u" else dbg
+    sch = None if dbg == "u" else sched
+    run(sch)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        run()
+        run(sch)
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps
