@@ -350,9 +350,10 @@ def test_attention_cross_shared_v(attn_mode):
         assert relerr(out[qs:qs + ql], ref) < 6e-3
 
 
+@pytest.mark.parametrize("sched", [False, True])
 @pytest.mark.parametrize("thr", ["8", "0"])
 @pytest.mark.parametrize("grid", [None, "5", "23"])
-def test_attention_stream_k_prescaled_rescale(thr, grid, sk_kernel, monkeypatch):
+def test_attention_stream_k_prescaled_rescale(thr, grid, sched, sk_kernel, monkeypatch):
     """The model's form: q pre-scaled by scale*log2(e) (scores are exp2 exponents, no per-score multiply),
     ragged problems with tail tiles, key spikes that force the deferred-rescale branch at chosen tiles
     (incl. right after a piece boundary), repeated launches on the re-armed workspace.  THR=0 (rescale on
@@ -377,9 +378,11 @@ def test_attention_stream_k_prescaled_rescale(thr, grid, sk_kernel, monkeypatch)
     d = qkv.to(dev)
     qs = (d[:, :D].float() * ops.Q_LOG2_SCALE).bfloat16()
     pt = torch.tensor(probs, dtype=torch.int32, device=dev)
+    # sched: the cost-balanced ranges of rf_attn_schedule (over RF_ATTN_GRID workgroups when it is set)
+    sch = ops.attn_schedule(probs, H, dev) if sched else None
     for _ in range(3):
         out = torch.zeros(T, D, device=dev, dtype=torch.bfloat16)
-        ops.attention(qs, d[:, D:2 * D], d[:, 2 * D:], out, pt, max(lens), H, q_prescaled=True)
+        ops.attention(qs, d[:, D:2 * D], d[:, 2 * D:], out, pt, max(lens), H, q_prescaled=True, schedule=sch)
         o = out.float().cpu()
         off = 0
         for n in lens:
@@ -390,9 +393,11 @@ def test_attention_stream_k_prescaled_rescale(thr, grid, sk_kernel, monkeypatch)
             off += n
 
 
-def test_attention_stream_k_many_problems():
+@pytest.mark.parametrize("sched", [False, True])
+def test_attention_stream_k_many_problems(sched):
     """A batch of scenes of very different lengths (batch_infer form): 24 problems, 8 heads, the
-    flattened space crossing problem boundaries inside workgroup ranges."""
+    flattened space crossing problem boundaries inside workgroup ranges (equal tile counts, or the
+    cost-balanced ranges of rf_attn_schedule)."""
     ops = _ops()
     H = 8
     D = H * 128
@@ -407,7 +412,7 @@ def test_attention_stream_k_many_problems():
     d = qkv.to(dev)
     out = torch.zeros(T, D, device=dev, dtype=torch.bfloat16)
     ops.attention(d[:, :D], d[:, D:2 * D], d[:, 2 * D:], out, torch.tensor(probs, dtype=torch.int32, device=dev),
-                  max(lens), H)
+                  max(lens), H, schedule=ops.attn_schedule(probs, H, dev) if sched else None)
     o = out.float().cpu()
     off = 0
     for n in lens:
@@ -817,3 +822,28 @@ def test_texture_embedding_fast_vs_general(monkeypatch):
         outs[fast] = m._embed_triangles(plan, inp["texture"].clone().cuda(), vns, True).cpu()
     assert int(m._w.tex_flag.item()) == 0
     assert relerr(outs["1"], outs["0"]) < 2e-3
+
+
+def test_attention_schedule_matches_equal_ranges_at_bench_shape():
+    """Stage 1 at the bench shape (S = 5,649, 8 heads) on the cost-balanced ranges vs equal tile counts: the
+    decompositions differ only in where units are cut — each piece's P = exp2(S - m) is rounded to bf16 on its own
+    running-max base — so the outputs agree to bf16-level rounding, and the balanced one is as close to the fp64
+    reference as the equal-range one."""
+    ops = _ops()
+    S, H = 5649, 8
+    D = H * 128
+    g = torch.Generator(device="cpu").manual_seed(5)
+    qkv = torch.randn(S, 3 * D, generator=g).bfloat16().to(dev)
+    qs = (qkv[:, :D].float() * ops.Q_LOG2_SCALE).bfloat16()
+    probs = [[0, S, 0, S, 0]]
+    pt = torch.tensor(probs, dtype=torch.int32, device=dev)
+    outs = []
+    for sch in (None, ops.attn_schedule(probs, H, dev)):
+        out = torch.empty(S, D, device=dev, dtype=torch.bfloat16)
+        ops.attention(qs, qkv[:, D:2 * D], qkv[:, 2 * D:], out, pt, S, H, q_prescaled=True, schedule=sch)
+        outs.append(out.float())
+    assert relerr(outs[1], outs[0]) < 6e-3
+    rows = torch.arange(0, S, 97)
+    ref = _ref_attn(qs[rows].float().cpu() / ops.Q_LOG2_SCALE, qkv[:, D:2 * D].float().cpu(), qkv[:, 2 * D:].float().cpu(), H)
+    e_sched, e_equal = relerr(outs[1][rows].cpu(), ref), relerr(outs[0][rows].cpu(), ref)
+    assert e_sched < 6e-3 and e_sched < 1.25 * e_equal, (e_sched, e_equal)
