@@ -199,6 +199,11 @@ int rf_texture_pack_if(const int* flag, float* texture, int64_t n_rows, int chan
  * (row-major i, j) and 0 outside it (exact compares; NaN fails). */
 int rf_texture_scan(float* texture, int64_t n_rows, int channels, int patch_elems, int log_channels,
                     const int32_t* dst_row, float* coef, int64_t ldc, int* flag, void* stream);
+/* rf_texture_scan with no reset launch: *flag must be 0 on entry and the kernel zeroes *flag_clear (a second
+ * flag): alternating two flags by frame parity, frame i raises flags[i % 2] and clears flags[(i + 1) % 2]
+ * (the reset otherwise costs a hipMemsetAsync blit kernel per frame).  n_rows >= 1. */
+int rf_texture_scan2(float* texture, int64_t n_rows, int channels, int patch_elems, int log_channels,
+                     const int32_t* dst_row, float* coef, int64_t ldc, int* flag, int* flag_clear, void* stream);
 /* When *flag == 0: out f32 [rows, n] = bias + coef[rows, channels] * wsum[channels, n], with
  * wsum[c, o] = sum over the patch mask of W[o, c*1024 + e] (the texture Linear on scanned rows);
  * no-op otherwise.  channels <= 16, n % 4 == 0, 16-B aligned out/wsum/bias (bias may be NULL). */

@@ -49,6 +49,7 @@ SIGNATURES = {
     "rf_texture_pack": [_P, _L, _I, _I, _I, _P, _P, _L, _P],
     "rf_texture_pack_if": [_P, _P, _L, _I, _I, _I, _P, _P, _L, _P],
     "rf_texture_scan": [_P, _L, _I, _I, _I, _P, _P, _L, _P, _P],
+    "rf_texture_scan2": [_P, _L, _I, _I, _I, _P, _P, _L, _P, _P, _P],
     "rf_texture_linear": [_P, _L, _I, _I, _P, _P, _P, _L, _I, _P, _P],
     "rf_gemm_bf16_if": [_P, _P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _L, _P],
     "rf_vn_encode": [_P, _L, _P, _I, _P, _L, _P],

@@ -54,9 +54,11 @@ RF_DEV bool tex_in_mask(int e) { return (e >> 5) + (e & 31) <= TEX_SIDE; }
 // owns texels 4t..4t+3 of every channel (patch row t >> 3)
 __global__ __launch_bounds__(256) void texture_scan_kernel(float* __restrict__ tex, int channels, int log_from,
                                                            const int32_t* __restrict__ dst_row,
-                                                           float* __restrict__ coef, int64_t ldc, int* flag) {
+                                                           float* __restrict__ coef, int64_t ldc, int* flag,
+                                                           int* flag_clear) {
     const int64_t r = blockIdx.x;
     const int t = threadIdx.x;
+    if (r == 0 && t == 0 && flag_clear) *flag_clear = 0;  // the other frame-parity flag (rf_texture_scan2)
     float* base = tex + r * (int64_t)channels * (TEX_SIDE * TEX_SIDE);
     __shared__ float c_raw[32];
     if (t < channels) c_raw[t] = base[t * TEX_SIDE * TEX_SIDE];  // texel (0, 0): inside the mask
@@ -332,8 +334,25 @@ extern "C" int rf_texture_scan(float* texture, int64_t n_rows, int channels, int
     }
     if (n_rows <= 0) return RF_OK;
     RF_LAUNCH(texture_scan_kernel, dim3((unsigned)n_rows), dim3(256), 0, (hipStream_t)stream, texture,
-                       channels, channels - log_channels, dst_row, coef, ldc, flag);
+                       channels, channels - log_channels, dst_row, coef, ldc, flag, (int*)nullptr);
     return rf::check_launch("rf_texture_scan");
+}
+
+// rf_texture_scan without the flag reset in the queue (the hipMemsetAsync above is a ~5 us blit kernel in
+// every frame): *flag must be 0 on entry, and the kernel zeroes *flag_clear — the caller alternates two
+// flags by frame parity, so each frame clears the flag the next frame raises into.
+extern "C" int rf_texture_scan2(float* texture, int64_t n_rows, int channels, int patch_elems, int log_channels,
+                                const int32_t* dst_row, float* coef, int64_t ldc, int* flag, int* flag_clear,
+                                void* stream) {
+    RF_REQUIRE(texture && coef && flag && flag_clear && flag != flag_clear, "rf_texture_scan2: null or aliased pointer");
+    RF_REQUIRE(patch_elems == TEX_SIDE * TEX_SIDE, "rf_texture_scan2: patch_elems must be %d", TEX_SIDE * TEX_SIDE);
+    RF_REQUIRE(channels >= 1 && channels <= 32 && ldc >= channels, "rf_texture_scan2: bad channels/ldc");
+    RF_REQUIRE(log_channels >= 0 && log_channels <= channels, "rf_texture_scan2: bad log_channels");
+    RF_REQUIRE(((uintptr_t)texture & 15) == 0, "rf_texture_scan2: texture must be 16-B aligned");
+    RF_REQUIRE(n_rows > 0 && n_rows < (1ll << 31), "rf_texture_scan2: need 1 .. 2^31 rows");
+    RF_LAUNCH(texture_scan_kernel, dim3((unsigned)n_rows), dim3(256), 0, (hipStream_t)stream, texture,
+                       channels, channels - log_channels, dst_row, coef, ldc, flag, flag_clear);
+    return rf::check_launch("rf_texture_scan2");
 }
 
 extern "C" int rf_texture_linear(const float* coef, int64_t ldc, int rows, int channels, const float* wsum,

@@ -74,7 +74,10 @@ class _DeviceWeights:
             mask = (i + j <= 32).double().reshape(1, 1, 1024)
             ws = (tw.detach().double().reshape(d, cfg.texture_channels, 1024) * mask).sum(-1)
             self.tex_wsum = _f32(ws.t(), device)
-        self.tex_flag = torch.zeros(1, dtype=torch.int32, device=device)
+        # texture fast-path flags by frame parity: frame i raises tex_flags[i % 2] and its scan clears the other
+        # one for frame i + 1 (no reset launch in the frame; rf_texture_scan2)
+        self.tex_flags = torch.zeros(2, dtype=torch.int32, device=device)
+        self.tex_parity = 0
         self.tex_norm = _f32(sd["texture_encoder_norm.weight"], device)
         self.enc_freqs = _f32(sd["transformer.rope_emb.freqs"], device)
         self.enc = []
@@ -135,6 +138,11 @@ class _DeviceWeights:
         self.ctx_unit = torch.ones(self.wkv_all.shape[1], dtype=torch.float32, device=device)
         self.dpt = DPTHead(sd, vt + "out_dpt", device, precision=dpt_precision)
         self.fp8_ready = False
+
+    @property
+    def tex_flag(self) -> torch.Tensor:
+        """The texture fast-path flag of the most recent frame (1: the scan rejected the fast path)."""
+        return self.tex_flags[1 - self.tex_parity:2 - self.tex_parity]
 
     def make_fp8(self):
         """MX fp8 copies (e4m3 + E8M0 per 32 K-elements, ops.mx8_quant_ref) of the stage-2 projection weights:
@@ -364,10 +372,12 @@ class RenderFormer:
             # the C-wide product replaces the K=13,312 GEMM; the general path below it runs only when the
             # scan's device flag says some row is not of that form
             coef = torch.empty(plan.T_tri, 16, dtype=torch.float32, device=dev)
-            ops.texture_scan(texture, log_ch, plan.dst_row, coef, W.tex_flag)
-            ops.texture_linear(coef, W.tex_wsum, W.tex_b, tex_lin, W.tex_flag)
-            ops.texture_pack_if(W.tex_flag, texture, 0, plan.dst_row, tex_in)
-            ops.gemm(tex_in, W.tex_w, tex_lin, W.tex_b, ops.EPI_F32, flag=W.tex_flag)
+            flag = W.tex_flags[W.tex_parity:W.tex_parity + 1]
+            ops.texture_scan(texture, log_ch, plan.dst_row, coef, flag, W.tex_flags[1 - W.tex_parity:2 - W.tex_parity])
+            W.tex_parity ^= 1
+            ops.texture_linear(coef, W.tex_wsum, W.tex_b, tex_lin, flag)
+            ops.texture_pack_if(flag, texture, 0, plan.dst_row, tex_in)
+            ops.gemm(tex_in, W.tex_w, tex_lin, W.tex_b, ops.EPI_F32, flag=flag)
         else:
             ops.texture_pack(texture, log_ch, plan.dst_row, tex_in)
             if plan.T_tri:

@@ -358,15 +358,21 @@ def texture_pack_if(flag: torch.Tensor, texture: torch.Tensor, log_channels: int
 
 
 def texture_scan(texture: torch.Tensor, log_channels: int, dst_row: torch.Tensor, coef: torch.Tensor,
-                 flag: torch.Tensor):
+                 flag: torch.Tensor, flag_clear: Optional[torch.Tensor] = None):
     """In-place log encode + per-row channel constants of to_h5-format textures; flag = 1 if any valid row is
-    not of that form (rf_texture_scan)."""
+    not of that form.  Without flag_clear (rf_texture_scan) the flag is reset first by a memset; with it
+    (rf_texture_scan2) flag must already be 0 and the kernel zeroes flag_clear instead (frame-parity flags)."""
     _dev(texture, torch.float32, "texture")
     _dev(coef, torch.float32, "coef")
     _dev(flag, torch.int32, "flag")
     _check(texture.is_contiguous() and texture.dim() == 5 and tuple(texture.shape[3:]) == (32, 32),
            "texture_scan: texture must be contiguous [B, N, C, 32, 32]")
     b, n, c = texture.shape[:3]
+    if flag_clear is not None:
+        _dev(flag_clear, torch.int32, "flag_clear")
+        call("rf_texture_scan2", ptr(texture), b * n, c, 32 * 32, log_channels, ptr(dst_row), ptr(coef),
+             coef.stride(0), ptr(flag), ptr(flag_clear), stream())
+        return coef
     call("rf_texture_scan", ptr(texture), b * n, c, 32 * 32, log_channels, ptr(dst_row), ptr(coef), coef.stride(0),
          ptr(flag), stream())
     return coef

@@ -135,6 +135,27 @@ def test_texture_paths_match_reference(mode, monkeypatch):
         assert int(pipe.model._w.tex_flag.item()) == 1  # the scan rejected the fast path
 
 
+def test_texture_flag_parity_across_frames():
+    """The fast-path flag alternates between two device scalars by frame parity (rf_texture_scan2: each frame's
+    scan clears the flag the next frame raises into, no reset launch): good / perturbed / good / perturbed /
+    good textures in a row must each take the right path and match the oracle."""
+    cfg, sd, inp, res, z = load_case("tiny_swin")
+    pipe = _pipeline(cfg, sd)
+    d = {k: v.cuda() for k, v in inp.items()}
+    bad = inp["texture"].clone()
+    bad[0, 3, 2, 5, 7] += 0.25
+    refs = {}
+    for i, kind in enumerate(["good", "bad", "good", "bad", "good"]):
+        tex = inp["texture"] if kind == "good" else bad
+        if kind not in refs:
+            refs[kind] = rf_ref.render(sd, cfg, inp["triangles"], tex.clone(), inp["mask"], inp["vn"], inp["c2w"],
+                                       inp["fov"], resolution=res)
+        out = pipe(d["triangles"], tex.clone().cuda(), d["mask"], d["vn"], d["c2w"], d["fov"], resolution=res,
+                   torch_dtype=torch.bfloat16)
+        assert int(pipe.model._w.tex_flag.item()) == (kind == "bad"), (i, kind)
+        assert rel_l2(out.cpu(), refs[kind]) < HDR_TOL, (i, kind)
+
+
 def test_plan_cache_follows_in_place_mask_edits():
     """The per-call plan is reused only for the same, unmodified mask tensor: an in-place edit of the mask
     must produce the same image as a fresh tensor with the edited content."""
