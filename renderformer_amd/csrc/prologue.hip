@@ -266,12 +266,32 @@ __global__ __launch_bounds__(64) void scene_pos_center_kernel(const int32_t* __r
     const int scene = has_c2w ? set / n_views : set;
     const int n = scene_off[scene + 1] - scene_off[scene];
     const int nb = (n + 255) / 256;  // blocks that held triangles of this set (the rest wrote zeros)
-    float tot[9];
-    for (int c = 0; c < 9; ++c) {
-        float sm = 0.f;
-        for (int b = 0; b < nb; ++b) sm += partial[((int64_t)set * n_blocks + b) * 9 + c];
-        tot[c] = sm / ((float)n + 1e-5f);
+    // the partials of 64 blocks at a time come in with one load round trip (lane b loads block b's 9 sums into
+    // LDS), then lane c < 9 adds them in block order: the same sums in the same order as a serial loop (whose
+    // ~200 dependent loads took 11 us), so the result is bit-identical to it
+    __shared__ float part_lds[64][9];
+    const int lane = threadIdx.x;
+    float acc = 0.f;  // lane c < 9: channel c
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+        const int b = b0 + lane;
+        if (b < nb) {
+            const float* src = partial + ((int64_t)set * n_blocks + b) * 9;
+#pragma unroll
+            for (int c = 0; c < 9; ++c) part_lds[lane][c] = src[c];
+        }
+        __syncthreads();
+        if (lane < 9) {
+            const int m = min(64, nb - b0);
+            for (int j = 0; j < m; ++j) acc += part_lds[j][lane];
+        }
+        __syncthreads();
     }
+    __shared__ float tot_lds[9];
+    if (lane < 9) tot_lds[lane] = acc / ((float)n + 1e-5f);
+    __syncthreads();
+    float tot[9];
+#pragma unroll
+    for (int c = 0; c < 9; ++c) tot[c] = tot_lds[c];
     for (int t = threadIdx.x; t < n_reg * 9; t += 64) {
         const int k = t % 3;
         pos_out[(int64_t)set_off[set] * 9 + t] = (tot[k] + tot[3 + k] + tot[6 + k]) / 3.0f;
