@@ -1818,7 +1818,8 @@ extern "C" int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ld
     RF_REQUIRE(head_dim == HD, "rf_attn_fwd: head_dim must be 128 (got %d)", head_dim);
     RF_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0, "rf_attn_fwd: strides must be 16-B aligned");
     RF_REQUIRE(n_split >= 0 && n_split <= 16, "rf_attn_fwd: n_split must be 0..16");
-    RF_REQUIRE(n_split == 1 || (workspace && ws_rows > 0), "rf_attn_fwd: split needs a workspace");
+    // (n_split == 0: the stream-K workspace only, ws_rows ignored as rf.h says; n_split > 1: the split partials)
+    RF_REQUIRE(n_split <= 1 || (workspace && ws_rows > 0), "rf_attn_fwd: split needs a workspace");
     if (n_problems <= 0 || max_q_len <= 0) return RF_OK;
     if (n_split == 0) return attn_sk_launch(q, ldq, k, ldk, v, ldv, o, ldo, problems, n_problems, n_heads, scale,
                                             workspace, stream);

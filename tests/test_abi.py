@@ -163,3 +163,50 @@ def test_attn_schedule_balances_the_bench_shape():
     single = [d[w] for w in range(256) if per_wg[w] == 1]
     double = [d[w] for w in range(256) if per_wg[w] == 2]
     assert single and double and np.mean(single) > np.mean(double)
+
+
+def _integration_binding_source():
+    """The reference-side ctypes binding sketched in INTEGRATION.md (the first ```python block of section 2)."""
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    sec = text[text.index("## 2. C ABI"):]
+    m = re.search(r"```python\n(.*?)```", sec, flags=re.S)
+    assert m, "INTEGRATION.md section 2 lost its binding example"
+    return m.group(1)
+
+
+def test_integration_binding_parses():
+    """The documented binding is valid Python that binds only symbols the header declares."""
+    import ast
+    src = _integration_binding_source()
+    ast.parse(src)
+    used = set(re.findall(r"_rf\.(rf_\w+)", src))
+    assert used and used <= set(header_functions()) | {"rf_last_error"}, used - set(header_functions())
+
+
+@pytest.mark.gpu
+def test_integration_binding_runs_against_reference_attention():
+    """Execute INTEGRATION.md's reference-side binding verbatim (only the library path filled in) the way the
+    reference's attention switch would call it — flash_attn's qkv-packed varlen layout [T, 3, H, 128] with
+    cu_seqlens — and compare with the fp64 softmax attention of every sequence."""
+    import math
+    import torch
+    from renderformer_amd import _lib
+    src = _integration_binding_source().replace('ctypes.CDLL("librfhip.so")', f'ctypes.CDLL({_lib.LIB_PATH!r})')
+    ns = {}
+    exec(compile(src, "INTEGRATION.md", "exec"), ns)
+    H, hd = 4, 128
+    lens = [300, 77, 1000]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device="cuda")
+    T = sum(lens)
+    g = torch.Generator(device="cpu").manual_seed(2)
+    qkv = torch.randn(T, 3, H, hd, generator=g).bfloat16().cuda()
+    out = ns["rfhip_varlen_qkvpacked"](qkv, cu, max(lens))
+    torch.cuda.synchronize()
+    assert out.shape == (T, H, hd)
+    o = out.float().cpu()
+    q, k, v = (qkv[:, i].double().cpu() for i in range(3))
+    for a, b in zip(cu.tolist(), cu.tolist()[1:]):
+        s = torch.einsum("qhd,khd->hqk", q[a:b], k[a:b]) / math.sqrt(hd)
+        ref = torch.einsum("hqk,khd->qhd", torch.softmax(s, -1), v[a:b])
+        err = ((o[a:b].double() - ref).norm() / ref.norm()).item()
+        assert err < 6e-3, (a, b, err)
