@@ -1121,10 +1121,11 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             continue;
         }
         if (kt1 < nt) {
-            // owner of a cut unit: fold in the partials of the later workgroups that hold its other tiles.  One
-            // flag wait + acquire + barrier per batch of up to 32 of them (normally all), then the merges back to
-            // back (the owners of units cut three ways end the launch: a second wait / acquire / barrier round
-            // cost them ~10k cycles).  The batch is found in uniform (scalar) code.
+            // owner of a cut unit: fold in the partials of the later workgroups that hold its other tiles, the
+            // LAST one first: the middle piece of a unit cut three ways (a workgroup whose whole range lies inside
+            // the unit) publishes at the end of its range, the tail piece at the start of its range, so merging
+            // the tail first leaves the middle piece one more merge of slack (rf_attn_schedule prices it so).
+            // The batch (up to 32 later workgroups, normally 1-2) is found in uniform (scalar) code.
             int cw0 = wg + 1;
             while (cw0 < nwg) {
                 uint32_t mask = 0;
@@ -1138,24 +1139,23 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                     }
                     if (ce > cs) mask |= 1u << (cw - cw0);
                 }
-                if (tid == 0 && mask) {
-                    for (uint32_t m = mask; m; m &= m - 1) {
-                        const int f = cw0 + __builtin_ctz(m);
+                for (uint32_t m = mask; m;) {
+                    const int bit = 31 - __builtin_clz(m);
+                    m &= ~(1u << bit);
+                    const int f = cw0 + bit;
+                    if (tid == 0) {
                         int spins = 0;
                         while (__hip_atomic_load(p.flag + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1 &&
                                ++spins < p.spin)
                             __builtin_amdgcn_s_sleep(1);
                         if (spins >= p.spin) report_device_error(p.err, RF_DEVERR_SK_ATTN);  // never silent
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        __hip_atomic_store(p.flag + f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
                     }
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    for (uint32_t m = mask; m; m &= m - 1)  // re-arm
-                        __hip_atomic_store(p.flag + cw0 + __builtin_ctz(m), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                __syncthreads();
-                for (uint32_t m = mask; m; m &= m - 1) {
+                    __syncthreads();
                     if (active) {
-                        const float* src = p.part_o + (int64_t)(cw0 + __builtin_ctz(m)) * PIECE_FLOATS;
+                        const float* src = p.part_o + (int64_t)f * PIECE_FLOATS;
                         const f32x2 ml = *reinterpret_cast<const f32x2*>(src + PIECE_O + (wave * 64 + lane) * 2);
                         const float mx = __builtin_fmaxf(m_run, ml[0]);
                         const float wa = fast_exp2(m_run - mx), wb = fast_exp2(ml[0] - mx);
@@ -1901,9 +1901,12 @@ double sk_simulate(const SkUnits& U, const SkCost& c, int w, int64_t a, int64_t 
             t += c.pub;
             *pub = t;
         } else {
-            if (e < ue)
-                for (int cw = w + 1; cw < grid && bnd[cw] < ue; ++cw)
+            if (e < ue) {  // merges in the kernel's order: the last later workgroup first
+                int last = w + 1;
+                while (last < grid && bnd[last] < ue) ++last;
+                for (int cw = last - 1; cw > w; --cw)
                     if (bnd[cw + 1] > bnd[cw]) t = std::max(t, pubt[cw]) + c.merge;
+            }
             t += c.store;
         }
         x = e;
@@ -1920,9 +1923,15 @@ int64_t sk_fill(const SkUnits& U, const SkCost& c, int grid, double T, std::vect
     bnd.assign(grid + 1, 0);
     pubt.assign(grid + 1, 0);
     bnd[grid] = U.total;
-    const double pub_by = T - 2 * c.merge - c.store;  // room for the owner's merges (normally <= 2) and store
+    // a published piece must land in time for the owner's merges after it and its store: a unit's middle piece
+    // (the range lies strictly inside one unit) is merged last, after one merge; a tail piece first, with up to
+    // two more merges (three-way cuts) behind it
     auto ok = [&](int w, int64_t a, int64_t b, double* pub) {
-        return sk_simulate(U, c, w, a, b, bnd, pubt, grid, pub) <= T && *pub <= pub_by;
+        if (sk_simulate(U, c, w, a, b, bnd, pubt, grid, pub) > T) return false;
+        int64_t us, ue;
+        U.unit_of(a, us, ue);
+        const bool mid = a > us && b < ue;
+        return *pub <= T - (mid ? 1 : 2) * c.merge - c.store;
     };
     for (int w = grid - 1; w >= 0; --w) {
         const int64_t b = bnd[w + 1];
