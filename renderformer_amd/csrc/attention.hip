@@ -1923,15 +1923,18 @@ int64_t sk_fill(const SkUnits& U, const SkCost& c, int grid, double T, std::vect
     bnd.assign(grid + 1, 0);
     pubt.assign(grid + 1, 0);
     bnd[grid] = U.total;
-    // a published piece must land in time for the owner's merges after it and its store: a unit's middle piece
-    // (the range lies strictly inside one unit) is merged last, after one merge; a tail piece first, with up to
-    // two more merges (three-way cuts) behind it
+    // a published piece must land in time for the owner's merges from it on and its store: a unit's middle piece
+    // (the range lies strictly inside one unit) is merged last, so one merge follows; a tail piece is merged
+    // first, so one merge follows when the rest of its unit fits one earlier range (a two-way cut, e.g. every
+    // cross-attention unit) and two when it needs two (a three-way cut)
+    const double avg = (double)U.total / grid;
     auto ok = [&](int w, int64_t a, int64_t b, double* pub) {
         if (sk_simulate(U, c, w, a, b, bnd, pubt, grid, pub) > T) return false;
         int64_t us, ue;
         U.unit_of(a, us, ue);
         const bool mid = a > us && b < ue;
-        return *pub <= T - (mid ? 1 : 2) * c.merge - c.store;
+        const int after = (mid || (double)(a - us) <= 1.3 * avg) ? 1 : 2;
+        return *pub <= T - after * c.merge - c.store;
     };
     for (int w = grid - 1; w >= 0; --w) {
         const int64_t b = bnd[w + 1];
@@ -1946,12 +1949,31 @@ int64_t sk_fill(const SkUnits& U, const SkCost& c, int grid, double T, std::vect
                 if (ok(w, mid, b, &pub)) lo = mid;
                 else hi = mid + 1;
             }
+            // feasibility is not monotone where the first piece changes role: a start just inside a unit makes a
+            // published piece, the unit's first tile an owned one; prefer the owned start when it also fits
+            if (lo < b) {
+                int64_t us, ue;
+                U.unit_of(lo, us, ue);
+                if (us < lo && ok(w, us, b, &pub)) lo = us;
+            }
         }
         bnd[w] = lo;
         ok(w, lo, b, &pub);
         pubt[w] = lo < b ? pub : 0;
     }
     return bnd[0];
+}
+// the model's finish time of a given table (every workgroup, successors first so publish times are known)
+double sk_span(const SkUnits& U, const SkCost& c, int grid, const std::vector<int64_t>& bnd) {
+    std::vector<double> pubt(grid + 1, 0.0);
+    double span = 0;
+    for (int w = grid - 1; w >= 0; --w) {
+        double pub = 0;
+        const double t = bnd[w + 1] > bnd[w] ? sk_simulate(U, c, w, bnd[w], bnd[w + 1], bnd, pubt, grid, &pub) : 0.0;
+        pubt[w] = pub;
+        span = std::max(span, t);
+    }
+    return span;
 }
 }  // namespace
 
@@ -1974,6 +1996,17 @@ extern "C" int rf_attn_schedule(const int32_t* problems, int n_problems, int n_h
         for (int w = 0; w <= grid; ++w) bounds[w] = 0;
         return RF_OK;
     }
+    if (U.total <= grid) {
+        // fewer tiles than workgroups (small launches): one whole unit per workgroup, nothing cut, so a unit's
+        // result does not depend on the rest of the launch (a view rendered alone equals the same view in a batch)
+        int w = 0;
+        for (size_t i = 0; i < U.base.size(); ++i)
+            if (U.nt[i])
+                for (int64_t x = U.base[i]; x < (i + 1 < U.base.size() ? U.base[i + 1] : U.total); x += U.nt[i])
+                    bounds[w++] = x;
+        for (; w <= grid; ++w) bounds[w] = U.total;
+        return RF_OK;
+    }
     SkCost c;
     if (const char* env = getenv("RF_ATTN_COST"))  // tile,pro,pub,merge,store (tuning)
         sscanf(env, "%lf,%lf,%lf,%lf,%lf", &c.tile, &c.pro, &c.pub, &c.merge, &c.store);
@@ -1991,7 +2024,11 @@ extern "C" int rf_attn_schedule(const int32_t* problems, int n_problems, int n_h
         (sk_fill(U, c, grid, mid, bnd, pubt) == 0 ? hi : lo) = mid;
     }
     RF_REQUIRE(sk_fill(U, c, grid, hi, bnd, pubt) == 0, "rf_attn_schedule: internal error (tiles left)");
-    for (int w = 0; w <= grid; ++w) bounds[w] = bnd[w];
+    // the backward fill is greedy; keep equal tile counts when the model prices them no worse
+    std::vector<int64_t> eq(grid + 1);
+    for (int w = 0; w <= grid; ++w) eq[w] = U.total * w / grid;
+    const std::vector<int64_t>& best = sk_span(U, c, grid, eq) <= sk_span(U, c, grid, bnd) ? eq : bnd;
+    for (int w = 0; w <= grid; ++w) bounds[w] = best[w];
     return RF_OK;
 }
 
