@@ -1939,11 +1939,13 @@ int64_t sk_fill(const SkUnits& U, const SkCost& c, int grid, double T, std::vect
     for (int w = grid - 1; w >= 0; --w) {
         const int64_t b = bnd[w + 1];
         double pub = 0;
+        // no range holds more than T / tile tiles: search starts in [b - that - 1, b) only
+        const int64_t reach = (int64_t)(T / c.tile) + 1;
         int64_t lo = b, hi = 0;  // lo: feasible start (empty range), search [hi, lo)
-        if (b > 0 && ok(w, 0, b, &pub)) {
+        if (b > 0 && b <= reach && ok(w, 0, b, &pub)) {
             lo = 0;
         } else if (b > 0) {
-            hi = 1;
+            hi = std::max<int64_t>(1, b - reach);
             while (hi < lo) {  // smallest feasible a in [hi, lo]
                 const int64_t mid = (hi + lo) / 2;
                 if (ok(w, mid, b, &pub)) lo = mid;
@@ -2019,7 +2021,7 @@ extern "C" int rf_attn_schedule(const int32_t* problems, int n_problems, int n_h
         lo = hi;
         hi *= 2;
     }
-    for (int iter = 0; iter < 60 && hi - lo > 0.1 * c.tile; ++iter) {
+    for (int iter = 0; iter < 60 && hi - lo > 0.25 * c.tile; ++iter) {
         const double mid = 0.5 * (lo + hi);
         (sk_fill(U, c, grid, mid, bnd, pubt) == 0 ? hi : lo) = mid;
     }
