@@ -8,9 +8,10 @@ Workloads (all synthetic, seeded, inputs resident in HBM before the t
   scenes (N = 5,633 triangles) x ``--views`` views at 512x512 through the drop-in pipeline (texture/vn
   encoders, stage 1 (14 layers), ray tokens, stage 2 (10 layers, Swin), DPT, HDR decode); with N > 1 ranks
   the finished HDR frames are all-gathered to every rank over RCCL (xGMI) inside the timed region.
-* ``c4`` (BASELINE config 4; strong scaling): one step = 64 scenes, triangle counts cycling through the 16
-  example scenes (examples/*.json), assigned to ranks by longest-processing-time on the FLOP model
-  (parallel.assign_units), frames all-gathered.
+* ``c4`` (BASELINE config 4; strong scaling): one step = 64 scenes cycling through the reference's 16 example
+  scenes (examples/*.json converted to HDF5 by renderformer_amd.examples before the timed region, read back
+  with the HDF5 reader), assigned to ranks by longest-processing-time on the FLOP model (parallel.assign_units),
+  frames all-gathered.
 * ``c5`` (BASELINE config 5's shape; strong scaling): one step = ONE scene with ``--views`` views (default 24)
   at ``--res`` (default 1024), the views split across ranks (parallel.shard_views; stage 1 recomputed on each
   rank), frames all-gathered.
@@ -66,6 +67,9 @@ def parse(argv=None):
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo: CPU-side tests)")
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (1-GPU rehearsal)")
     ap.add_argument("--dump", default=None, help="rank 0 saves the gathered frames of the last step (.npy)")
+    ap.add_argument("--view-chunk", type=int, default=None,
+                    help="stage 2 + DPT over at most this many views per pass (default: 1 for c5, so a view's image "
+                         "does not depend on the rank split; all views otherwise)")
     ap.add_argument("--fp8", action="store_true", help="stage-2 projections + FFN as MX fp8 GEMMs (config 5's fp8 "
                                                         "path); roofline then reports the stage-2 W13 fp8 GEMM")
     a = ap.parse_args(argv)
@@ -75,6 +79,8 @@ def parse(argv=None):
         a.views = 24 if a.workload == "c5" else 1
     if a.workload == "c4" and a.scenes == 1:
         a.scenes = 64
+    if a.view_chunk is None and a.workload == "c5":
+        a.view_chunk = 1
     return a
 
 
@@ -174,12 +180,12 @@ def main():
     from renderformer_amd.config import named_config
     from renderformer_amd.flops import frame_flops
     from renderformer_amd.parallel import assign_units, gather_frames, max_over_ranks, scene_cost, shard_views
-    from renderformer_amd.scenes import EXAMPLE_SCENE_TRIS, batch_scenes, synthetic_scene
+    from renderformer_amd.scenes import batch_scenes, synthetic_scene
     from renderformer_amd.weights import synthetic_state_dict
 
     cfg = named_config(args.config)
     sd = synthetic_state_dict(cfg, seed=0)
-    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd, fp8=args.fp8)).to(dev)
+    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd, fp8=args.fp8, view_chunk=args.view_chunk)).to(dev)
 
     # ---- the units of one step: (batch tensors on the device, global frame ids)
     if args.workload == "cbox":
@@ -190,10 +196,24 @@ def main():
         n_frames_step = n_per_rank * world
         scaling = "weak"
     elif args.workload == "c4":
-        counts = [EXAMPLE_SCENE_TRIS[i % len(EXAMPLE_SCENE_TRIS)] for i in range(args.scenes)]
+        # the reference's 16 example scenes (examples/*.json), converted to HDF5 by the package's converter
+        # (cached; before the timed region) and read back with the HDF5 reader, cycled to --scenes
+        from renderformer_amd.examples import convert_all, example_names
+        from renderformer_amd.h5io import load_single_h5_data
+        names = example_names()
+        files = convert_all(names, workers=8)
+        step_names = [names[i % len(names)] for i in range(args.scenes)]
+        scene_data = {n: load_single_h5_data(files[n]) for n in set(step_names)}
+        counts = [int(scene_data[n]["triangles"].shape[0]) for n in step_names]
         costs = [scene_cost(cfg, n, args.views, args.res) for n in counts]
         mine = assign_units(costs, world)[rank]
-        hosts = [batch_scenes([synthetic_scene(counts[i], args.views, seed=100 + i)]) for i in mine]
+        hosts = []
+        for i in mine:
+            d = scene_data[step_names[i]]
+            nv = int(d["c2w"].shape[0])
+            vsel = [v % nv for v in range(args.views)]  # --views views of the scene's cameras (cycled)
+            hosts.append({"triangles": d["triangles"][None], "texture": d["texture"][None], "mask": d["mask"][None],
+                          "vn": d["vn"][None], "c2w": d["c2w"][vsel][None], "fov": d["fov"][vsel].reshape(1, -1, 1)})
         ids = [[i * args.views + v for v in range(args.views)] for i in mine]
         n_frames_step = args.scenes * args.views
         scaling = "strong"
@@ -271,14 +291,13 @@ def main():
         fl_frame = frame_flops(cfg, args.tris, args.res, args.views)["total"] / args.views
         fl_step = fl_frame * n_frames_step
     elif args.workload == "c4":
-        fl_step = sum(frame_flops(cfg, EXAMPLE_SCENE_TRIS[i % len(EXAMPLE_SCENE_TRIS)], args.res, args.views)["total"]
-                      for i in range(args.scenes))
+        fl_step = sum(frame_flops(cfg, n, args.res, args.views)["total"] for n in counts)
     else:
         fl_step = frame_flops(cfg, args.tris, args.res, args.views)["total"] * world  # stage 1 on every rank
     durs = timer.durations_ms()
     per_step_launches = len(durs)  # one timed step
     kern_ms = statistics.mean(durs) if durs else float("nan")
-    s_len = (args.tris if args.workload != "c4" else EXAMPLE_SCENE_TRIS[0]) + cfg.num_register_tokens
+    s_len = (args.tris if args.workload != "c4" else max(counts)) + cfg.num_register_tokens
     scenes_per_launch = args.scenes if args.workload == "cbox" else 1
     kern_flops = 4 * s_len * s_len * cfg.latent_dim * scenes_per_launch  # QK^T + PV per launch
     if args.workload == "c4":  # launches differ in S: use the mean algorithmic FLOP of this rank's scenes
@@ -310,16 +329,22 @@ def main():
         import numpy as np
         np.save(args.dump, out.cpu().numpy())
     if rank == 0:
-        wl = {"cbox": f"cbox-sized scene N={args.tris}, {args.res}x{args.res}, {args.views} view(s) x {args.scenes} "
-                      f"scene(s) per rank per step",
-              "c4": f"{args.scenes} scenes per step (N cycling through the 16 example scenes' counts), {args.res}x"
-                    f"{args.res}, {args.views} view(s) each, LPT-sharded over ranks",
-              "c5": f"one scene N={args.tris}, {args.views} views at {args.res}x{args.res} per step, views split "
-                    f"over ranks (stage 1 on every rank)"}[args.workload]
+        if args.workload == "cbox":
+            wl = (f"cbox-sized scene N={args.tris}, {args.res}x{args.res}, {args.views} view(s) x {args.scenes} "
+                  f"scene(s) per rank per step")
+        elif args.workload == "c4":
+            wl = (f"{args.scenes} scenes per step cycling through the reference's 16 example scenes "
+                  f"(examples/*.json -> HDF5, N {min(counts)}..{max(counts)}), {args.res}x{args.res}, "
+                  f"{args.views} view(s) each, LPT-sharded over ranks")
+        else:
+            wl = (f"one scene N={args.tris}, {args.views} views at {args.res}x{args.res} per step, views split over "
+                  f"ranks (stage 1 on every rank; stage 2 + DPT {args.view_chunk} view(s) per pass)")
         rec = {
             "metric": METRIC, "value": round(fps, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": scaling, "vs_baseline": None, "dtype": "bf16+fp8" if args.fp8 else "bf16", "data": "synthetic",
+            "scaling": scaling, "vs_baseline": None, "dtype": "bf16+fp8" if args.fp8 else "bf16",
+            "data": ("the reference's example scenes (examples/*.json -> HDF5), synthetic weights" if args.workload == "c4"
+                     else "synthetic"),
             "config": {
                 "workload": f"{'large-proxy' if args.config == 'large' else args.config} {wl}",
                 "model": "renderformer-v1.1-swin-large" if args.config == "large" else args.config,

@@ -85,8 +85,9 @@ class HipLibraryError(RuntimeError):
 
 
 class DeviceError(RuntimeError):
-    """A kernel reported a device-side failure (a stream-K hand-off that timed out): the outputs of that launch
-    are invalid; rf_clear_device_error() + fresh workspaces recover."""
+    """A kernel reported a device-side failure (a stream-K hand-off that timed out, or a range table that does not
+    fit its launch): the outputs of that launch are invalid.  ``renderformer_amd.ops.clear_device_error()``
+    recovers (it drains the device, clears the error word and drops the stream-K workspaces)."""
 
 
 def load(require_device: bool = True):
@@ -126,7 +127,7 @@ def call(name: str, *args) -> None:
         if rc == 1:
             raise ValueError(msg)
         if rc == RF_ERR_DEVICE:
-            raise DeviceError(f"{name}: {msg}")
+            raise DeviceError(f"{name}: {msg} -- recover with renderformer_amd.ops.clear_device_error()")
         raise RuntimeError(f"{name} failed ({rc}): {msg}")
 
 

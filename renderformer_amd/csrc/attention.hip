@@ -39,6 +39,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 #include <type_traits>
@@ -51,6 +52,7 @@ constexpr int HD = 128;
 constexpr int KT = 64;                   // keys per tile
 constexpr int TILE_BYTES = KT * HD * 2;  // 16 KiB
 constexpr float NEG = -1.0e30f;
+constexpr int QB5_ = 256;  // query rows per stream-K unit (= QB5 of attn_sk_kernel / 4 x 64 of attn_p4_kernel)
 constexpr float RESCALE_LOG2 = 8.0f;  // legacy kernels: row-max growth (log2 units) that forces a rescale
 constexpr float SUM_THR_LOG2 = 12.0f;  // stream-K kernel: half-row tile sum (log2) that forces a rescale
 
@@ -76,13 +78,62 @@ struct AttnArgs {
     float thr;  // deferred-rescale threshold (log2 units; RF_ATTN_THR, default 8)
     int* err;   // device error word (rf::device_error_word): stream-K hand-off timeouts
     int spin;   // stream-K hand-off spin bound (polls)
-    // stream-K range boundaries [grid + 1] (rf_attn_schedule: cost-balanced); null = equal tile counts
+    // stream-K range boundaries [grid + 1] by LOGICAL block index (common.h SkLayout; rf_attn_schedule:
+    // cost-balanced, group-aligned); null = equal tile counts per group
     const int64_t* bounds;
+    int epoch;  // hand-off flag value of this launch (> 0, new every launch: no re-arm, stale flags never match)
 };
 
-// first tile of workgroup w's stream-K range (w == nwg: the total)
-RF_DEV int64_t sk_bound(const AttnArgs& p, int64_t total, int w, int nwg) {
-    return p.bounds ? p.bounds[w] : total * w / nwg;
+// Stream-K ranges in the forward-progress layout (common.h SkLayout): the launch's units (head x q-block of
+// every problem that has keys) in G contiguous chunks, one per XCD group, each chunk's tiles over the group's
+// blocks in descending blockIdx order.  The stream-K kernels read their ranges from a table by LOGICAL block
+// index, bounds[L] = first tile of logical block L (bounds[grid] = total): the cost-balanced host table
+// (rf_attn_schedule), or the equal split written on the device by attn_equal_bounds_kernel.  The kernels check
+// the table against the launch instead of trusting it.
+RF_DEV void sk_attn_count(const AttnArgs& p, int64_t& total, int64_t& units) {
+    total = 0;
+    units = 0;
+    for (int i = 0; i < p.n_problems; ++i) {
+        const int32_t* d = p.problems + 5 * i;
+        const int64_t nt = (d[3] + KT - 1) / KT, nu = nt > 0 ? (int64_t)p.n_heads * ((d[1] + QB5_ - 1) / QB5_) : 0;
+        total += nu * nt;
+        units += nu;
+    }
+}
+RF_DEV int64_t sk_unit_tile(const AttnArgs& p, int64_t u, int64_t total) {  // first tile of unit u (u = units: total)
+    int64_t t = 0;
+    for (int i = 0; i < p.n_problems; ++i) {
+        const int32_t* d = p.problems + 5 * i;
+        const int64_t nt = (d[3] + KT - 1) / KT, nu = nt > 0 ? (int64_t)p.n_heads * ((d[1] + QB5_ - 1) / QB5_) : 0;
+        if (u < nu) return t + u * nt;
+        u -= nu;
+        t += nu * nt;
+    }
+    return total;
+}
+// equal tile counts per block inside each group (no host schedule): one workgroup writes the table
+__global__ __launch_bounds__(64) void attn_equal_bounds_kernel(AttnArgs p, int nwg, int64_t* out) {
+    int64_t total, units;
+    sk_attn_count(p, total, units);
+    const SkLayout lay(nwg, units);
+    for (int g = 0; g < lay.G; ++g) {
+        const int64_t t0 = sk_unit_tile(p, units * g / lay.G, total), t1 = sk_unit_tile(p, units * (g + 1) / lay.G, total);
+        const int nb = lay.size(g), b0 = lay.base(g);
+        for (int li = threadIdx.x; li < nb; li += 64) out[b0 + li] = t0 + (t1 - t0) * li / nb;
+    }
+    if (threadIdx.x == 0) out[nwg] = total;
+}
+// this block's logical index and its group's end (partners of an owner lie in (L, gend)); -1 = bad table
+RF_DEV int sk_attn_block(const AttnArgs& p, int hw, int nwg, int& gend) {
+    int64_t total, units;
+    sk_attn_count(p, total, units);
+    const SkLayout lay(nwg, units);
+    int g = 0;
+    const int L = lay.logical(hw, &g);
+    gend = lay.base(g) + lay.size(g);
+    const int64_t b = p.bounds[L], e = p.bounds[L + 1];
+    const bool bad = b < 0 || e < b || e > total || (L == 0 && b != 0) || (L == nwg - 1 && e != total);
+    return bad ? -1 : L;
 }
 
 RF_DEV int swz_off(int row, int ch) { return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4); }
@@ -718,16 +769,14 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         if (late) __builtin_amdgcn_s_setprio(1);
 
     const int nwg = gridDim.x, hw = blockIdx.x;
-    const int xcd = hw & 7, qd = nwg >> 3, rm = nwg & 7;
-    const int wg = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + (hw >> 3);
-
-    int64_t total = 0;
-    for (int i = 0; i < p.n_problems; ++i) {
-        const int32_t* d = p.problems + 5 * i;
-        total += (int64_t)p.n_heads * ((d[1] + QB5 - 1) / QB5) * ((d[3] + KT - 1) / KT);
+    int gend = 0;
+    const int wg = sk_attn_block(p, hw, nwg, gend);  // logical index: ranges, partial slots and flags
+    if (wg < 0) {  // a range table that does not fit this launch: refuse it (never read past the problems)
+        if (tid == 0) report_device_error(p.err, RF_DEVERR_SK_SCHED);
+        return;
     }
-    int64_t it = sk_bound(p, total, wg, nwg);
-    const int64_t it_end = sk_bound(p, total, wg + 1, nwg);
+    int64_t it = p.bounds[wg];
+    const int64_t it_end = p.bounds[wg + 1];
 
     const float c = UNIT ? 1.f : p.c;
     const float inv_c = UNIT ? 1.f : 1.f / p.c;
@@ -906,7 +955,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         if (pend) {  // every wave's older partial stores completed before its counted wait above
-            if (tid == 0) __hip_atomic_store(p.flag + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0) __hip_atomic_store(p.flag + wg, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             pend = false;
         }
         f32x16 sA[2], sB[2];
@@ -1121,18 +1170,19 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             continue;
         }
         if (kt1 < nt) {
-            // owner of a cut unit: fold in the partials of the later workgroups that hold its other tiles, the
-            // LAST one first: the middle piece of a unit cut three ways (a workgroup whose whole range lies inside
-            // the unit) publishes at the end of its range, the tail piece at the start of its range, so merging
-            // the tail first leaves the middle piece one more merge of slack (rf_attn_schedule prices it so).
-            // The batch (up to 32 later workgroups, normally 1-2) is found in uniform (scalar) code.
+            // owner of a cut unit: fold in the partials of the logically later workgroups that hold its other
+            // tiles (lower blockIdx: SkLayout), the LAST one first: the middle piece of a unit cut three ways (a
+            // workgroup whose whole range lies inside the unit) publishes at the end of its range, the tail piece
+            // at the start of its range, so merging the tail first leaves the middle piece one more merge of slack
+            // (rf_attn_schedule prices it so).  The batch (up to 32 later workgroups, normally 1-2) is found in
+            // uniform (scalar) code; a unit running past the group's end is a bad table (device error).
             int cw0 = wg + 1;
-            while (cw0 < nwg) {
+            bool done = false;
+            while (cw0 < gend) {
                 uint32_t mask = 0;
                 int cw = cw0;
-                bool done = false;
-                for (; cw < nwg && cw - cw0 < 32; ++cw) {
-                    const int64_t cs = sk_bound(p, total, cw, nwg), ce = sk_bound(p, total, cw + 1, nwg);
+                for (; cw < gend && cw - cw0 < 32; ++cw) {
+                    const int64_t cs = p.bounds[cw], ce = p.bounds[cw + 1];
                     if (cs >= unit_end) {
                         done = true;
                         break;
@@ -1145,13 +1195,12 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                     const int f = cw0 + bit;
                     if (tid == 0) {
                         int spins = 0;
-                        while (__hip_atomic_load(p.flag + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1 &&
+                        while (__hip_atomic_load(p.flag + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.epoch &&
                                ++spins < p.spin)
                             __builtin_amdgcn_s_sleep(1);
                         if (spins >= p.spin) report_device_error(p.err, RF_DEVERR_SK_ATTN);  // never silent
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        __hip_atomic_store(p.flag + f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
                     }
                     __syncthreads();
                     if (active) {
@@ -1176,6 +1225,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 if (done) break;
                 cw0 = cw;
             }
+            if (!done && p.bounds[gend] < unit_end && tid == 0) report_device_error(p.err, RF_DEVERR_SK_SCHED);
         }
         if (!active) continue;
         const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
@@ -1204,7 +1254,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     if (pend) {  // the range ended with a published piece
         attn_wait_vm<0>();
         __syncthreads();
-        if (tid == 0) __hip_atomic_store(p.flag + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) __hip_atomic_store(p.flag + wg, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if constexpr (DBG & 32) {  // diagnostic: [wg][wave][8] u64 in the last piece slot of the workspace;
         // slots 4 / 5 hold the wave's shader-clock and 100-MHz reference-clock spans (in-kernel clock)
@@ -1266,16 +1316,14 @@ __global__ __launch_bounds__(NW4 * 64, 1) void attn_p4_kernel(AttnArgs p) {
     if (tid == 0) s_bad = 0;  // ordered before its first read by the first piece's barrier
 
     const int nwg = gridDim.x, hw = blockIdx.x;
-    const int xcd = hw & 7, qd = nwg >> 3, rm = nwg & 7;
-    const int wg = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + (hw >> 3);
-
-    int64_t total = 0;
-    for (int i = 0; i < p.n_problems; ++i) {
-        const int32_t* d = p.problems + 5 * i;
-        total += (int64_t)p.n_heads * ((d[1] + QB5 - 1) / QB5) * ((d[3] + KT - 1) / KT);
+    int gend = 0;
+    const int wg = sk_attn_block(p, hw, nwg, gend);
+    if (wg < 0) {
+        if (tid == 0) report_device_error(p.err, RF_DEVERR_SK_SCHED);
+        return;
     }
-    int64_t it = sk_bound(p, total, wg, nwg);
-    const int64_t it_end = sk_bound(p, total, wg + 1, nwg);
+    int64_t it = p.bounds[wg];
+    const int64_t it_end = p.bounds[wg + 1];
 
     const float c = UNIT ? 1.f : p.c;
     const float inv_c = UNIT ? 1.f : 1.f / p.c;
@@ -1635,23 +1683,23 @@ __global__ __launch_bounds__(NW4 * 64, 1) void attn_p4_kernel(AttnArgs p) {
             }
             attn_wait_vm<0>();
             __syncthreads();
-            if (tid == 0) __hip_atomic_store(p.flag + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0) __hip_atomic_store(p.flag + wg, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             continue;
         }
         if (kt1 < nt) {
-            for (int cw = wg + 1; cw < nwg; ++cw) {
-                const int64_t cs = sk_bound(p, total, cw, nwg), ce = sk_bound(p, total, cw + 1, nwg);
+            int cw = wg + 1;
+            for (; cw < gend; ++cw) {  // later pieces: lower blockIdx (SkLayout)
+                const int64_t cs = p.bounds[cw], ce = p.bounds[cw + 1];
                 if (cs >= unit_end) break;
                 if (ce == cs) continue;
                 if (tid == 0) {
                     int spins = 0;
-                    while (__hip_atomic_load(p.flag + cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1 &&
+                    while (__hip_atomic_load(p.flag + cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.epoch &&
                            ++spins < p.spin)
                         __builtin_amdgcn_s_sleep(1);
                     if (spins >= p.spin) report_device_error(p.err, RF_DEVERR_SK_ATTN);
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __hip_atomic_store(p.flag + cw, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 __syncthreads();
                 const float* src = p.part_o + (int64_t)cw * PIECE_FLOATS;
@@ -1674,6 +1722,7 @@ __global__ __launch_bounds__(NW4 * 64, 1) void attn_p4_kernel(AttnArgs p) {
                         }
                 }
             }
+            if (cw == gend && p.bounds[gend] < unit_end && tid == 0) report_device_error(p.err, RF_DEVERR_SK_SCHED);
         }
 #pragma unroll
         for (int qs = 0; qs < 2; ++qs) {
@@ -1751,7 +1800,6 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
     }
     RF_REQUIRE(grid >= 1 && grid <= SK5_MAX_GRID, "rf_attn_fwd: grid %d out of range", grid);
     AttnArgs a{};
-    a.bounds = bounds;
     a.q = (const bf16_t*)q;
     a.k = (const bf16_t*)k;
     a.v = (const bf16_t*)v;
@@ -1766,9 +1814,20 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
     a.c = scale * LOG2E;
     a.part_o = (float*)workspace;
     a.flag = (int*)(a.part_o + (int64_t)SK5_MAX_GRID * PIECE_FLOATS);
+    a.bounds = bounds;
+    if (!bounds) {  // equal split per XCD group, written on the device ahead of the launch (stream-ordered)
+        int64_t* eq = (int64_t*)(a.flag + SK5_MAX_GRID);
+        RF_LAUNCH(attn_equal_bounds_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a, grid, eq);
+        a.bounds = eq;
+    }
     a.thr = getenv("RF_ATTN_THR") ? (float)atof(getenv("RF_ATTN_THR")) : SUM_THR_LOG2;
     a.err = rf::device_error_word();
     a.spin = rf::spin_limit();
+    // a fresh flag value per launch: a publisher's flag from an earlier launch (even one that timed out and left
+    // a late flag behind) never equals this launch's, so flags need no re-arm and no memset
+    static std::atomic<int> epoch{0};
+    a.epoch = 1 + (epoch.fetch_add(1) & 0x3fffffff);
+    // (the grid may exceed the CUs: the SkLayout waits only go to earlier-dispatched blocks)
     // q pre-scaled by scale*log2(e) upstream (scale = ln 2): scores are already exp2 exponents
     const bool unit = fabsf(a.c - 1.0f) < 1e-6f;
     const int dbg = getenv("RF_ATTN_DBG") ? atoi(getenv("RF_ATTN_DBG")) : 0;
@@ -1981,37 +2040,21 @@ double sk_span(const SkUnits& U, const SkCost& c, int grid, const std::vector<in
 
 extern "C" int rf_attn_grid(void) { return cu_count(); }
 
-extern "C" int rf_attn_schedule(const int32_t* problems, int n_problems, int n_heads, int grid, int64_t* bounds) {
-    RF_REQUIRE(problems && bounds && n_problems > 0 && n_heads > 0, "rf_attn_schedule: bad arguments");
-    RF_REQUIRE(grid >= 1 && grid <= SK5_MAX_GRID, "rf_attn_schedule: grid %d out of range", grid);
-    SkUnits U;
-    for (int i = 0; i < n_problems; ++i) {
-        const int32_t* d = problems + 5 * i;
-        RF_REQUIRE(d[1] >= 0 && d[3] >= 0, "rf_attn_schedule: negative length in problem %d", i);
-        const int64_t nt = (d[3] + KT - 1) / KT;
-        const int64_t tiles = (int64_t)n_heads * ((d[1] + QB5 - 1) / QB5) * nt;
-        U.base.push_back(U.total);
-        U.nt.push_back(tiles > 0 ? nt : 0);
-        U.total += tiles;
-    }
-    if (U.total == 0) {
-        for (int w = 0; w <= grid; ++w) bounds[w] = 0;
-        return RF_OK;
-    }
+namespace {
+// One XCD group's ranges (sk_fill + bisection on the common finish time; equal tile counts kept when the model
+// prices them no worse), bounds relative to the group's first tile: out[0..grid].
+void sk_schedule_group(const SkUnits& U, const SkCost& c, int grid, int64_t* out) {
     if (U.total <= grid) {
-        // fewer tiles than workgroups (small launches): one whole unit per workgroup, nothing cut, so a unit's
-        // result does not depend on the rest of the launch (a view rendered alone equals the same view in a batch)
+        // fewer tiles than workgroups: one whole unit per workgroup, nothing cut, so a unit's result does not
+        // depend on the rest of the launch (a view rendered alone equals the same view in a batch)
         int w = 0;
         for (size_t i = 0; i < U.base.size(); ++i)
             if (U.nt[i])
                 for (int64_t x = U.base[i]; x < (i + 1 < U.base.size() ? U.base[i + 1] : U.total); x += U.nt[i])
-                    bounds[w++] = x;
-        for (; w <= grid; ++w) bounds[w] = U.total;
-        return RF_OK;
+                    out[w++] = x;
+        for (; w <= grid; ++w) out[w] = U.total;
+        return;
     }
-    SkCost c;
-    if (const char* env = getenv("RF_ATTN_COST"))  // tile,pro,pub,merge,store (tuning)
-        sscanf(env, "%lf,%lf,%lf,%lf,%lf", &c.tile, &c.pro, &c.pub, &c.merge, &c.store);
     std::vector<int64_t> bnd;
     std::vector<double> pubt;
     // lo is infeasible (less than the average tile work); hi doubled until feasible
@@ -2025,12 +2068,72 @@ extern "C" int rf_attn_schedule(const int32_t* problems, int n_problems, int n_h
         const double mid = 0.5 * (lo + hi);
         (sk_fill(U, c, grid, mid, bnd, pubt) == 0 ? hi : lo) = mid;
     }
-    RF_REQUIRE(sk_fill(U, c, grid, hi, bnd, pubt) == 0, "rf_attn_schedule: internal error (tiles left)");
-    // the backward fill is greedy; keep equal tile counts when the model prices them no worse
+    sk_fill(U, c, grid, hi, bnd, pubt);
     std::vector<int64_t> eq(grid + 1);
     for (int w = 0; w <= grid; ++w) eq[w] = U.total * w / grid;
     const std::vector<int64_t>& best = sk_span(U, c, grid, eq) <= sk_span(U, c, grid, bnd) ? eq : bnd;
-    for (int w = 0; w <= grid; ++w) bounds[w] = best[w];
+    for (int w = 0; w <= grid; ++w) out[w] = best[w];
+}
+}  // namespace
+
+// Cost-balanced stream-K ranges in the forward-progress layout (common.h SkLayout): the units (head x q-block
+// of each problem with keys, in problem order) are cut into one contiguous chunk per XCD group, balanced by
+// tiles, so a unit never spans two groups (its pieces' blocks share an XCD's L2 when there are 8 groups, and
+// an owner only waits on lower-numbered blocks); each chunk is scheduled over its group's blocks by the cost
+// model above.  bounds[L] is the first tile of LOGICAL block L (bounds[grid] = total), as the kernel reads it.
+extern "C" int rf_attn_schedule(const int32_t* problems, int n_problems, int n_heads, int grid, int64_t* bounds) {
+    RF_REQUIRE(problems && bounds && n_problems > 0 && n_heads > 0, "rf_attn_schedule: bad arguments");
+    RF_REQUIRE(grid >= 1 && grid <= SK5_MAX_GRID, "rf_attn_schedule: grid %d out of range", grid);
+    // every unit as (first tile, tiles): the problems' units in order
+    std::vector<int64_t> ustart, unt;
+    int64_t total = 0;
+    for (int i = 0; i < n_problems; ++i) {
+        const int32_t* d = problems + 5 * i;
+        RF_REQUIRE(d[1] >= 0 && d[3] >= 0, "rf_attn_schedule: negative length in problem %d", i);
+        const int64_t nt = (d[3] + KT - 1) / KT;
+        const int64_t nu = nt > 0 ? (int64_t)n_heads * ((d[1] + QB5 - 1) / QB5) : 0;
+        for (int64_t u = 0; u < nu; ++u) {
+            ustart.push_back(total);
+            unt.push_back(nt);
+            total += nt;
+        }
+    }
+    const int64_t NU = (int64_t)ustart.size();
+    if (total == 0) {
+        for (int w = 0; w <= grid; ++w) bounds[w] = 0;
+        return RF_OK;
+    }
+    SkCost c;
+    if (const char* env = getenv("RF_ATTN_COST"))  // tile,pro,pub,merge,store (tuning)
+        sscanf(env, "%lf,%lf,%lf,%lf,%lf", &c.tile, &c.pro, &c.pub, &c.merge, &c.store);
+    const SkLayout lay(grid, NU);
+    int64_t u0 = 0;
+    for (int g = 0; g < lay.G; ++g) {
+        // this group's units: up to the unit boundary nearest its share of the tiles (>= 1 unit per group)
+        int64_t u1 = NU;
+        if (g + 1 < lay.G) {
+            const int64_t target = total * lay.base(g + 1) / grid;
+            u1 = (int64_t)(std::lower_bound(ustart.begin(), ustart.end(), target) - ustart.begin());
+            if (u1 > 0 && u1 < NU && target - ustart[u1 - 1] < ustart[u1] - target) --u1;  // nearer boundary
+            u1 = std::max(u1, u0 + 1);
+            u1 = std::min(u1, NU - (lay.G - g - 1));
+        }
+        SkUnits U;  // the chunk as runs of equal-size units, relative tiles
+        const int64_t t0 = ustart[u0];
+        for (int64_t u = u0; u < u1; ++u) {
+            if (u == u0 || unt[u] != unt[u - 1] || U.nt.back() == 0) {
+                U.base.push_back(ustart[u] - t0);
+                U.nt.push_back(unt[u]);
+            }
+            U.total += unt[u];
+        }
+        const int nb = lay.size(g), b0 = lay.base(g);
+        std::vector<int64_t> rel(nb + 1);
+        sk_schedule_group(U, c, nb, rel.data());
+        for (int i = 0; i < nb; ++i) bounds[b0 + i] = t0 + rel[i];
+        u0 = u1;
+    }
+    bounds[grid] = total;
     return RF_OK;
 }
 
@@ -2048,7 +2151,8 @@ extern "C" int rf_attn_fwd_sched(const void* q, int64_t ldq, const void* k, int6
 }
 
 extern "C" int64_t rf_attn_workspace_bytes(int64_t rows, int n_heads, int n_split) {
-    if (n_split == 0) return (int64_t)SK5_MAX_GRID * PIECE_FLOATS * 4 + SK5_MAX_GRID * 4;
+    if (n_split == 0)  // partial slots, flags, the device-built equal range table
+        return (int64_t)SK5_MAX_GRID * PIECE_FLOATS * 4 + SK5_MAX_GRID * 4 + (SK5_MAX_GRID + 1) * 8;
     return n_split <= 1 ? 0 : (int64_t)n_split * rows * n_heads * (HD + 2) * (int64_t)sizeof(float);
 }
 

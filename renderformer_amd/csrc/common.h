@@ -73,6 +73,62 @@ RF_DEV void report_device_error(int* err, int code) {
 }
 #define RF_DEVERR_SK_GEMM 1
 #define RF_DEVERR_SK_ATTN 2
+#define RF_DEVERR_SK_SCHED 3  // a stream-K range table that does not cover the launch's tiles (rejected in-kernel)
+
+// ------------------------------------------------------------------------------------------------------
+// Stream-K block layout with forward progress (attention, GEMM and conv stream-K kernels).  The block that
+// holds a unit's first iteration (the owner: it reaches that piece last in its range) waits for the partials
+// of the blocks holding the unit's later iterations.  Every such wait goes to a block with a LOWER blockIdx,
+// i.e. one dispatched earlier, and the awaited piece is always the first piece of its block's range (published
+// before that block waits on anything).  So the lowest-numbered waiting block only ever waits on a block that
+// is already resident and never blocks: the launch drains whatever else occupies the chip (two renders on two
+// streams, or fewer CUs than blocks), with no co-residency assumption.
+// Layout: blocks carry XCD labels x = blockIdx % nx (blocks b and b + 8 share an XCD's L2); the labels are
+// cut into G groups and the units into G contiguous chunks, one per group, so no unit spans two groups (a
+// group's blocks share one XCD's L2 when G = 8); inside a group the LOGICAL order, in which ranges are laid
+// out, is DESCENDING blockIdx.  Logical index L = group base + rank; the host scheduler (rf_attn_schedule)
+// and the kernels share these formulas.
+#define RF_HD __host__ __device__ __forceinline__
+struct SkLayout {
+    int nwg, nx, G;
+    RF_HD SkLayout(int nwg_, int64_t units) : nwg(nwg_), nx(nwg_ < 8 ? nwg_ : 8), G(1) {
+        G = units < (int64_t)nx ? (int)(units > 0 ? units : 1) : nx;
+    }
+    RF_HD int cnt(int x) const { return (nwg - x + nx - 1) / nx; }       // blocks with label x
+    RF_HD int xlo(int g) const { return (g * nx + G - 1) / G; }          // first label of group g
+    RF_HD int group_of(int x) const { return x * G / nx; }
+    RF_HD int base(int g) const {  // first logical index of group g
+        int s = 0;
+        for (int x = 0; x < xlo(g); ++x) s += cnt(x);
+        return s;
+    }
+    RF_HD int size(int g) const {
+        int s = 0;
+        for (int x = xlo(g); x < xlo(g + 1); ++x) s += cnt(x);
+        return s;
+    }
+    // logical index of block hw: its group's base + the number of the group's blocks with a larger blockIdx
+    RF_HD int logical(int hw, int* grp = nullptr) const {
+        const int x = hw % nx, g = group_of(x);
+        int rank = 0;
+        for (int y = xlo(g); y < xlo(g + 1); ++y) {
+            const int jmin = hw - y >= 0 ? (hw - y) / nx + 1 : 0;  // blocks nx j + y > hw
+            const int c = cnt(y);
+            rank += c > jmin ? c - jmin : 0;
+        }
+        if (grp) *grp = g;
+        return base(g) + rank;
+    }
+    // equal split (no host schedule): group g takes units [U g / G, U (g+1) / G), its blocks equal shares of
+    // their iterations (units of `per` iterations each)
+    RF_HD void equal_range(int L, int g, int64_t units, int64_t per, int64_t& b, int64_t& e) const {
+        const int64_t u0 = units * g / G, u1 = units * (g + 1) / G;
+        const int64_t t0 = u0 * per, tn = (u1 - u0) * per;
+        const int nb = size(g), li = L - base(g);
+        b = t0 + tn * li / nb;
+        e = t0 + tn * (li + 1) / nb;
+    }
+};
 
 // ------------------------------------------------------------------------- host side
 namespace rf {

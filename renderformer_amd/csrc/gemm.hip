@@ -1061,9 +1061,15 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
     const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
     const int iters = p.k / ph::BK2;
-    const int64_t total = (int64_t)tiles_m * tiles_n * iters;
-    int64_t it = total * wg / nwg;
-    const int64_t it_end = total * (wg + 1) / nwg;
+    const int64_t ntiles64 = (int64_t)tiles_m * tiles_n;
+    // partial-tile stream-K: ranges in the forward-progress layout (common.h SkLayout): a tile's owner only
+    // waits on lower-numbered blocks
+    const SkLayout lay(nwg, ntiles64);
+    int grp = 0;
+    const int L = lay.logical(hw, &grp);
+    const int gend = lay.base(grp) + lay.size(grp);
+    int64_t it, it_end;
+    lay.equal_range(L, grp, ntiles64, iters, it, it_end);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     f32x4 acc[TI][TJ];
     if (p.persist) {
@@ -1102,7 +1108,7 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
         if (stamp && ns < 14) st[ns++] = __builtin_amdgcn_s_memtime();
         if (kf != 0) {
             const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(p.sk_part + (int64_t)wg * TS, 0, TS * 4, 0x00020000);
+                __builtin_amdgcn_make_buffer_rsrc(p.sk_part + (int64_t)L * TS, 0, TS * 4, 0x00020000);
 #pragma unroll
             for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -1112,12 +1118,15 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
                 }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (threadIdx.x == 0) __hip_atomic_store(p.sk_flag + wg, p.sk_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (threadIdx.x == 0) __hip_atomic_store(p.sk_flag + L, p.sk_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             if (kl < iters) {
                 const int64_t tile_end = (int64_t)(tile + 1) * iters;
-                for (int c = wg + 1; c < nwg && total * c / nwg < tile_end; ++c) {
-                    if (total * (c + 1) / nwg == total * c / nwg) continue;  // empty range: no partial
+                for (int c = L + 1; c < gend; ++c) {  // the tile's later pieces: lower blockIdx (SkLayout)
+                    int64_t cb, ce;
+                    lay.equal_range(c, grp, ntiles64, iters, cb, ce);
+                    if (cb >= tile_end) break;
+                    if (ce == cb) continue;  // empty range: no partial
                     if (threadIdx.x == 0) {
                         int spins = 0;
                         while (__hip_atomic_load(p.sk_flag + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.sk_epoch &&
@@ -1148,7 +1157,7 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
         it += kl - kf;
     }
     if (stamp && threadIdx.x == 0) {
-        for (int i = 0; i < 16; ++i) p.stamps[wg * 16 + i] = i < ns ? st[i] : 0;
+        for (int i = 0; i < 16; ++i) p.stamps[L * 16 + i] = i < ns ? st[i] : 0;
     }
 }
 
@@ -1177,9 +1186,13 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
         engine_epilogue<C, EPI>(p, m0, n0, acc);
     } else {
         const int iters = p.k / (BK * C::KH);
-        const int64_t total = (int64_t)tiles_m * (p.n / BN) * iters;
-        int64_t it = total * wg / nwg;
-        const int64_t it_end = total * (wg + 1) / nwg;
+        const int64_t ntiles64 = (int64_t)tiles_m * (p.n / BN);
+        const SkLayout lay(nwg, ntiles64);  // forward-progress layout (common.h)
+        int grp = 0;
+        const int L = lay.logical(hw, &grp);
+        const int gend = lay.base(grp) + lay.size(grp);
+        int64_t it, it_end;
+        lay.equal_range(L, grp, ntiles64, iters, it, it_end);
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
         while (it < it_end) {
             const int tile = (int)(it / iters), kf = (int)(it % iters);
@@ -1195,7 +1208,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
                 // (sc1) so no release fence is needed; every storing wave drains, then one lane flags
                 // (guide Guideline 16, R1)
                 const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                    p.sk_part + (int64_t)wg * (BM * BN), 0, BM * BN * 4, 0x00020000);
+                    p.sk_part + (int64_t)L * (BM * BN), 0, BM * BN * 4, 0x00020000);
 #pragma unroll
                 for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -1205,12 +1218,15 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
                     }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
-                if (threadIdx.x == 0) __hip_atomic_store(p.sk_flag + wg, p.sk_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (threadIdx.x == 0) __hip_atomic_store(p.sk_flag + L, p.sk_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 if (kl < iters) {
                     const int64_t tile_end = (int64_t)(tile + 1) * iters;
-                    for (int c = wg + 1; c < nwg && total * c / nwg < tile_end; ++c) {
-                        if (total * (c + 1) / nwg == total * c / nwg) continue;  // empty range: no partial
+                    for (int c = L + 1; c < gend; ++c) {  // the tile's later pieces: lower blockIdx (SkLayout)
+                        int64_t cb, ce;
+                        lay.equal_range(c, grp, ntiles64, iters, cb, ce);
+                        if (cb >= tile_end) break;
+                        if (ce == cb) continue;  // empty range: no partial
                         if (threadIdx.x == 0) {
                             int spins = 0;
                             while (__hip_atomic_load(p.sk_flag + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.sk_epoch &&

@@ -563,16 +563,18 @@ class _Writer:
 SCENE_KEYS = ("triangles", "vn", "texture", "c2w", "fov")
 
 
-def write_scene(path: str, triangles, vn, texture, c2w, fov, texture_dtype=np.float16) -> None:
+def write_scene(path: str, triangles, vn, texture, c2w, fov, texture_dtype=np.float16,
+                compression_level: Optional[int] = 9) -> None:
     """The datasets and dtypes of `scene_processor/to_h5.py:87-92` (gzip level 9); texture_dtype=np.float32
-    writes the texture as other producers may (the readers keep whatever dtype the file holds)."""
+    writes the texture as other producers may (the readers keep whatever dtype the file holds).  A lower
+    compression_level only changes the file's bytes, not its data (test/bench caches use 1)."""
     write_datasets(path, {
         "triangles": np.asarray(triangles, dtype=np.float32),
         "vn": np.asarray(vn, dtype=np.float32),
         "texture": np.asarray(texture, dtype=texture_dtype),
         "c2w": np.asarray(c2w, dtype=np.float32),
         "fov": np.asarray(fov, dtype=np.float32),
-    })
+    }, compression_level=compression_level)
 
 
 def load_single_h5_data(file_path: str):

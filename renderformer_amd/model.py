@@ -30,6 +30,7 @@ from .dpt import DPTHead
 from .weights import check_state_dict, load_snapshot, synthetic_state_dict
 
 EPS = 1e-6  # layers/attention.py:16
+FP8_PROJECTIONS = ("q", "out", "self_in", "self_out", "w13", "w2")  # stage-2 projections the fp8 mode can take
 SWIN_WINDOW, SWIN_SHIFT = 8, 4  # attention.py:604-605
 
 
@@ -254,12 +255,18 @@ class RenderFormer:
     """Drop-in for renderformer.models.renderformer.RenderFormer (inference only)."""
 
     def __init__(self, config: RenderFormerConfig, state_dict: Optional[Dict[str, torch.Tensor]] = None,
-                 seed: int = 0, dpt_precision: Optional[str] = None, fp8: Optional[bool] = None):
+                 seed: int = 0, dpt_precision: Optional[str] = None, fp8: Optional[bool] = None,
+                 view_chunk: Optional[int] = None):
         self.config = config
+        # render_views: stage 2 + DPT over at most view_chunk views per pass (stage 1 once per scene); None = all
+        # views of the batch in one pass.  A fixed chunk makes each view's image independent of the batching.
+        self.view_chunk = view_chunk if view_chunk is not None else (int(os.environ.get("RF_VIEW_CHUNK", "0")) or None)
         # fp8 mode (BASELINE config 5's "fp8 MFMA path"): the stage-2 projections and FFN run as MX fp8 GEMMs
         # (rf_gemm_mx8, 2x the bf16 MFMA rate) on activations quantised per 32-element block; off by default
         # (its HDR error is reported by tests/test_parity_gpu.py); RF_FP8=1 or fp8=True turns it on
         self.fp8 = (os.environ.get("RF_FP8", "0") != "0") if fp8 is None else bool(fp8)
+        # which stage-2 projections the fp8 mode quantises (RF_FP8_PROJ, comma list of FP8_PROJECTIONS)
+        self.fp8_projections = set(os.environ.get("RF_FP8_PROJ", ",".join(FP8_PROJECTIONS)).split(","))
         # DPT operand precision (dpt.py): "f16" (default) or "bf16x3"; RF_DPT_PRECISION overrides the default
         self.dpt_precision = dpt_precision or os.environ.get("RF_DPT_PRECISION", "f16")
         if self.dpt_precision not in DPT_PRECISIONS:
@@ -278,6 +285,7 @@ class RenderFormer:
         self._last_plan = None
         self._w: Optional[_DeviceWeights] = None
         self._plans: Dict = {}
+        self._capture: Optional[dict] = None
         self.skip_token_num = cfg.num_register_tokens
 
     # ------------------------------------------------------------------ module-like API
@@ -357,6 +365,19 @@ class RenderFormer:
         self._last_plan = (mask, (mask._version, V, res), plan)
         return plan
 
+    def capture_taps(self, enc_rows=None, dec_rows=None, dec_views=None) -> dict:
+        """Arm a one-shot capture of intermediates for the NEXT render (parity tests at production size): the
+        stage-1 output rows `enc_rows` of scene 0 (packed rows: 16 register tokens, then the valid triangles in
+        order, = the reference's sequence) and their row norms, and for every decoder layer the ray-token rows
+        `dec_rows` of views `dec_views` of scene 0.  Returns the dict the render fills (device fp32 tensors:
+        'enc_rows' [n, D], 'enc_rownorm' [S], 'dec_rows' [layers, views, n, D])."""
+        out: dict = {}
+        dev = self._device
+        as_idx = lambda x: None if x is None else torch.as_tensor(x, dtype=torch.long).to(dev)  # noqa: E731
+        self._capture = {"enc": as_idx(enc_rows), "dec": as_idx(dec_rows), "views": list(dec_views or []),
+                         "out": out}
+        return out
+
     # ------------------------------------------------------------------ stages
     def _embed_triangles(self, plan: _Plan, texture: torch.Tensor, vns: torch.Tensor, log_encode: bool):
         cfg, W, dev = self.config, self._w, self._device
@@ -415,6 +436,12 @@ class RenderFormer:
             ops.rmsnorm(x, L.ffn_norm, EPS, h)
             ops.gemm(h, L.w13, g, None, ops.EPI_SWIGLU, tag="gemm_w13_stage1")
             ops.gemm(g, L.w2, x, None, ops.EPI_ADD_F32)
+        cap = self._capture
+        if cap is not None:  # (test capture, capture_taps): scene 0's rows of the stage-1 output
+            s0 = cfg.num_register_tokens + plan.counts[0]
+            cap["out"]["enc_rownorm"] = x[:s0].norm(dim=-1)
+            if cap["enc"] is not None:
+                cap["out"]["enc_rows"] = x.index_select(0, cap["enc"]).clone()
         return x
 
     def _stage2(self, plan: _Plan, x: torch.Tensor, ctx: torch.Tensor, pos2: torch.Tensor, ray_pos: torch.Tensor):
@@ -455,8 +482,10 @@ class RenderFormer:
             xq = ops.MX8.empty(T2, D, dev)
             gq = ops.MX8.empty(T2, F, dev)
 
-        def proj(inp, w_bf16, w_fp8, out, epi=ops.EPI_BF16, tag=None):
-            if fp8:
+        fp8_set = self.fp8_projections
+
+        def proj(inp, w_bf16, w_fp8, out, epi=ops.EPI_BF16, tag=None, name=""):
+            if fp8 and name in fp8_set:
                 ops.gemm_mx8(ops.quant_mx8(inp, gq if inp.shape[1] == F and F != D else xq), w_fp8, out, None, epi,
                              tag=tag)
             else:
@@ -466,7 +495,7 @@ class RenderFormer:
         for i, L in enumerate(W.dec):
             # (i) cross-attention: K/V projections once per scene, K rotated per view
             ops.rmsnorm(x, L.query_norm, EPS, h)
-            proj(h, L.wq, getattr(L, "wq8", None), q2)
+            proj(h, L.wq, getattr(L, "wq8", None), q2, name="q")
             if kv_batch:
                 kv = kv_all[:, 2 * D * i:2 * D * (i + 1)]
             else:
@@ -481,11 +510,11 @@ class RenderFormer:
                                  src_rows=plan.kv_src_rows)
             ops.attention(q2, kview, kv[:, D:], att, plan.prob2, R, H, tag="attn_cross", max_k_len=plan.max_s,
                           q_prescaled=True, schedule=plan.sched2)
-            proj(att, L.wo, getattr(L, "wo8", None), x, ops.EPI_ADD_F32)
+            proj(att, L.wo, getattr(L, "wo8", None), x, ops.EPI_ADD_F32, name="out")
             # (ii) self-attention between ray tokens
             if qkv is not None:
                 ops.rmsnorm(x, L.self_norm, EPS, h)
-                proj(h, L.ws_in, getattr(L, "ws_in8", None), qkv)
+                proj(h, L.ws_in, getattr(L, "ws_in8", None), qkv, name="self_in")
                 qs, ks, vs = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
                 qks = qkv[:, :2 * D]
                 if swin:
@@ -496,13 +525,22 @@ class RenderFormer:
                     ops.qk_norm_rope(qks, qks, H, L.sqk_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R,
                                      n_seg=2, q_scale=ops.Q_LOG2_SCALE)
                     ops.attention(qs, ks, vs, att, plan.prob_self, R, H, max_k_len=R, q_prescaled=True)
-                proj(att, L.ws_out, getattr(L, "ws_out8", None), x, ops.EPI_ADD_F32)
+                proj(att, L.ws_out, getattr(L, "ws_out8", None), x, ops.EPI_ADD_F32, name="self_out")
             # (iii) FFN
             ops.rmsnorm(x, L.ffn_norm, EPS, h)
-            proj(h, L.w13, getattr(L, "w13_8", None), g, ops.EPI_SWIGLU, tag="gemm_w13_stage2")
-            proj(g, L.w2, getattr(L, "w2_8", None), x, ops.EPI_ADD_F32)
+            proj(h, L.w13, getattr(L, "w13_8", None), g, ops.EPI_SWIGLU, tag="gemm_w13_stage2", name="w13")
+            proj(g, L.w2, getattr(L, "w2_8", None), x, ops.EPI_ADD_F32, name="w2")
             if i in outl:  # straight into the DPT projection's operand planes (no fp32 copy of x)
                 taps.append(W.dpt.tap_planes(len(taps), x, P, plan.hp, plan.wp))
+            cap = self._capture
+            if cap is not None and cap["dec"] is not None:  # (test capture, capture_taps)
+                rows = torch.cat([v * R + cap["dec"] for v in cap["views"]])
+                cap["out"].setdefault("dec_rows", []).append(
+                    x.index_select(0, rows).view(len(cap["views"]), -1, D).clone())
+        if self._capture is not None:
+            if "dec_rows" in self._capture["out"]:
+                self._capture["out"]["dec_rows"] = torch.stack(self._capture["out"]["dec_rows"])
+            self._capture = None  # one-shot
         return taps
 
     def _ray_embed(self, plan: _Plan, ray_in: torch.Tensor):
@@ -542,13 +580,34 @@ class RenderFormer:
                 raise ValueError(f"{n} must be on {dev} (got {t.device})")
         if resolution % (cfg.patch_size * (SWIN_WINDOW if cfg.view_transformer_use_swin_attn else 1)) != 0:
             raise ValueError(f"resolution {resolution} incompatible with patch/window size")
-        plan = self._plan(mask, V, resolution)
+        # views in chunks of at most view_chunk (stage 1 once): every chunk runs the same launch sequence on the
+        # same problem tables whatever the other views are, so a view's image does not depend on how the views of
+        # a scene are batched or split over ranks (bench.py c5)
+        chunk = V if not self.view_chunk else min(V, int(self.view_chunk))
+        plan = self._plan(mask, chunk, resolution)
         tris = triangles.reshape(B, -1, 9).float().contiguous()
         x1 = self._embed_triangles(plan, texture, vn.reshape(B, -1, 9).float().contiguous(), log_encode)
         pos1 = torch.empty(plan.T1, 9, dtype=torch.float32, device=dev)
         ops.scene_pos(tris, plan.valid_flat, plan.scene_off, None, B, 1, cfg.num_register_tokens, pos1, plan.cu1,
                       max(plan.counts))
         x1 = self._stage1(plan, x1, pos1)
+        if chunk == V:
+            return self._views(plan, x1, tris, c2w, fov, resolution).view(B, V, resolution, resolution, -1)
+        out = None
+        for v0 in range(0, V, chunk):
+            v1 = min(V, v0 + chunk)
+            pc = plan if v1 - v0 == chunk else self._plan(mask, v1 - v0, resolution)
+            o = self._views(pc, x1, tris, c2w[:, v0:v1], fov[:, v0:v1], resolution)
+            o = o.view(B, v1 - v0, resolution, resolution, -1)
+            if out is None:
+                out = torch.empty(B, V, *o.shape[2:], dtype=o.dtype, device=dev)
+            out[:, v0:v1] = o
+        return out
+
+    def _views(self, plan: _Plan, x1, tris, c2w, fov, resolution):
+        """Stage 2 + DPT + decode for the plan's views of every scene (c2w [B, Vc, 4, 4], fov [B, Vc, ...])."""
+        cfg, dev = self.config, self._device
+        B, V = plan.B, plan.V
         P = B * V
         c2w_v = c2w.reshape(P, 4, 4).float().contiguous()
         eye = torch.eye(4, dtype=torch.float32, device=dev).expand(P, 4, 4).contiguous()
@@ -561,8 +620,7 @@ class RenderFormer:
         ops.scene_pos(tris, plan.valid_flat, plan.scene_off, pos_c2w, B, V, cfg.num_register_tokens, pos2,
                       plan.kv_off, max(plan.counts))
         taps = self._stage2(plan, x2, x1, pos2, ray_pos)
-        out = self._decode(plan, taps, log_decode=not cfg.use_ldr, channels_last=True)
-        return out.view(B, V, resolution, resolution, -1)
+        return self._decode(plan, taps, log_decode=not cfg.use_ldr, channels_last=True)
 
     @torch.no_grad()
     def forward(self, tri_vpos_list, texture_patch_list, valid_mask, vns, rays_o, rays_d, tri_vpos_view_tf,

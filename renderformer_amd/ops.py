@@ -77,6 +77,19 @@ def _gemm_workspace(device) -> torch.Tensor:
     return ws
 
 
+def clear_device_error() -> None:
+    """Recover from a DeviceError: wait for every queued launch, clear the library's device error word and drop
+    the stream-K workspaces of this process (fresh zero-filled ones are made on the next launch), so no partial
+    or hand-off flag of the failed launch can reach a later one."""
+    if torch.cuda.is_available():
+        for i in range(torch.cuda.device_count()):
+            with torch.cuda.device(i):
+                torch.cuda.synchronize()
+    load(require_device=False).rf_clear_device_error()
+    _GEMM_WS.clear()
+    _ATTN_WS.clear()
+
+
 def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias: Optional[torch.Tensor] = None,
          epilogue: int = EPI_BF16, tag: Optional[str] = None, flag: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out (epilogue)= a @ w.T ; a [M,K] bf16, w [N,K] bf16.  With ``flag`` (int32 device scalar) the HIP engine

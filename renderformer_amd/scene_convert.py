@@ -313,12 +313,13 @@ def scene_arrays(cfg: SceneConfig, scene_dir: str, size: int = 32):
     return {"triangles": tris, "vn": vns, "texture": tex, "c2w": c2w, "fov": fov}
 
 
-def convert_scene(config_path: str, output_h5_path: Optional[str] = None) -> str:
+def convert_scene(config_path: str, output_h5_path: Optional[str] = None, compression_level: int = 9) -> str:
     """convert_scene.py:11-45 without the intermediate mesh files: JSON -> HDF5 (returns the written path)."""
     cfg = load_scene_config(config_path)
     out = output_h5_path or os.path.splitext(config_path)[0] + ".h5"
     arr = scene_arrays(cfg, os.path.dirname(os.path.abspath(config_path)))
     if os.path.dirname(out):
         os.makedirs(os.path.dirname(out), exist_ok=True)
-    write_scene(out, arr["triangles"], arr["vn"], arr["texture"], arr["c2w"], arr["fov"])
+    write_scene(out, arr["triangles"], arr["vn"], arr["texture"], arr["c2w"], arr["fov"],
+                compression_level=compression_level)
     return out

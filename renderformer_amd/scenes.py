@@ -20,9 +20,9 @@ import numpy as np
 import torch
 
 SCENE_TRIS = {"cbox": 5633, "cbox-bunny": 6209, "cbox-lucy": 11803, "shader-ball": 11036, "init-template": 513}
-# triangle counts of all 16 example scenes (examples/*.json: 'f' lines of the OBJ files each one lists), in
-# sorted file-name order; the 64-scene batch workload (BASELINE config 4) cycles through them
-EXAMPLE_SCENE_TRIS = [6209, 11803, 9397, 5633, 6073, 4527, 3073, 1949, 1418, 5023, 513, 6386, 6847, 10588, 4400, 3231]
+# triangle counts of all 16 example scenes after conversion (examples/*.json through scene_convert: polygons
+# fanned into triangles), in natsort order of the file names (renderformer_amd.examples.example_names)
+EXAMPLE_SCENE_TRIS = [5633, 6209, 11803, 9397, 7321, 4527, 3073, 1949, 1418, 5023, 513, 6386, 7141, 11036, 4400, 4575]
 
 
 def look_at_to_c2w(position, target=(0.0, 0.0, 0.0), up=(0.0, 0.0, 1.0)) -> np.ndarray:

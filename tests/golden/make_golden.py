@@ -66,9 +66,24 @@ CASES = {
     "base_cbox_r256": (BASE, [5633], None, 1, 256, 0, 3, False),         # config 1 shape (v1-base, full depth)
     "large_cbox_r1024_v4": (LARGE, [5633], None, 4, 1024, 0, 4, False),  # config 5 shape, 4 views of 1 scene
 }
+# The reference's own example scenes (examples/*.json, converted by renderformer_amd.examples: the fixture
+# records the digest of the converted tensors instead of the tensors): config 4's scenes, incl. the longest
+# triangle sequence (cbox-lucy, N = 11,803 -> S = 11,819).  name: (example, config, res, weight seed, unused)
+REAL_CASES = {
+    "real_cbox-lucy_r512": ("cbox-lucy", LARGE, 512, 0, True),
+    "real_shader-ball_r512": ("shader-ball", LARGE, 512, 0, False),
+    "real_cbox-teapot_r512": ("cbox-teapot", LARGE, 512, 0, False),
+    "real_init-template_r512": ("init-template", LARGE, 512, 0, False),
+}
 # 1024^2 x 4 views is 50 MB of fp32 HDR: such fixtures keep every SUB-th pixel row and column (plus the
 # full-image sum and sum of squares), the GPU test compares the same sample
-HDR_SUB = {"large_cbox_r1024_v4": 4}
+HDR_SUB = {"large_cbox_r1024_v4": 4, **{n: 2 for n in REAL_CASES}}
+# production-size intermediate taps (the big cases): a fixed row sample of the stage-1 output (the 16 register
+# rows + seeded triangle rows), of every decoder layer's output (seeded ray-token rows of the first views) and
+# the pre-ELU DPT logits every DPT_SUB-th pixel
+PROD_TAPS = {"large_cbox_r512", "large_bunny_r512", "base_cbox_r256", "large_cbox_r1024_v4", "real_cbox-lucy_r512"}
+N_ENC_ROWS, N_DEC_ROWS, N_DEC_VIEWS = 128, 16, 2
+DPT_SUB = {256: 2, 512: 4, 1024: 8}
 
 
 def weight_checksums(sd):
@@ -76,7 +91,28 @@ def weight_checksums(sd):
     return names, np.array([[float(sd[n].double().sum()), float(sd[n].double().abs().sum())] for n in names])
 
 
-def run_case(name, over, ntris, pad, nv, res, wseed, sseed, taps):
+def tap_rows(name, S, R, V):
+    """The fixed row samples of a production-size case: stage-1 rows (16 register rows + seeded triangle rows),
+    decoder ray-token rows (the same rows in each recorded view), the recorded views."""
+    g = np.random.default_rng(sum(map(ord, name)))
+    enc = np.concatenate([np.arange(16), np.sort(g.choice(np.arange(16, S), N_ENC_ROWS - 16, replace=False))])
+    dec = np.sort(g.choice(R, N_DEC_ROWS, replace=False))
+    return enc.astype(np.int64), dec.astype(np.int64), np.arange(min(V, N_DEC_VIEWS), dtype=np.int64)
+
+
+def real_batch(example):
+    """One example scene (examples/<example>.json through this package's converter) as a batch of one."""
+    from renderformer_amd.examples import inputs_digest, scene_inputs
+    from renderformer_amd.scenes import expand_texture
+    a = scene_inputs(example)
+    b = {k: torch.from_numpy(v)[None] for k, v in a.items() if k != "fov"}
+    b["fov"] = torch.from_numpy(a["fov"]).reshape(1, -1, 1)
+    b["mask"] = torch.ones(1, a["triangles"].shape[0], dtype=torch.bool)
+    b["texture"] = torch.from_numpy(expand_texture(a["tex_channels"]))[None]
+    return b, inputs_digest(a)
+
+
+def run_case(name, over, ntris, pad, nv, res, wseed, sseed, taps, example=None):
     from renderformer.models.config import RenderFormerConfig as RefConfig
     from renderformer.models.renderformer import RenderFormer as RefModel
     from renderformer.pipelines.rendering_pipeline import RenderFormerRenderingPipeline as RefPipeline
@@ -88,13 +124,35 @@ def run_case(name, over, ntris, pad, nv, res, wseed, sseed, taps):
     model.eval()
     pipe = RefPipeline(model)
 
-    scenes = [synthetic_scene(n, nv, seed=sseed + i) for i, n in enumerate(ntris)]
-    batch = batch_scenes(scenes, padding_length=pad)
+    digest = None
+    if example is not None:
+        batch, digest = real_batch(example)
+        nv = int(batch["c2w"].shape[1])
+    else:
+        scenes = [synthetic_scene(n, nv, seed=sseed + i) for i, n in enumerate(ntris)]
+        batch = batch_scenes(scenes, padding_length=pad)
     tex = batch["texture"].clone()
     t0 = time.time()
 
     got = {}
     hooks = []
+    prod = name in PROD_TAPS
+    S = int(batch["mask"][0].sum()) + cfg.num_register_tokens
+    R = (res // cfg.patch_size) ** 2
+    if prod:
+        enc_idx, dec_idx, dec_views = tap_rows(name, S, R, nv)
+        got["enc_row_idx"] = torch.from_numpy(enc_idx)
+        got["dec_row_idx"] = torch.from_numpy(dec_idx)
+        got["dec_views"] = torch.from_numpy(dec_views)
+        hooks.append(model.transformer.register_forward_hook(
+            lambda m, a, o: got.__setitem__("enc_rows", o[0, enc_idx].clone())))
+        dec_rows = []
+        for i, layer in enumerate(model.view_transformer.transformer.layers):
+            hooks.append(layer.register_forward_hook(
+                lambda m, a, o: dec_rows.append(o[dec_views][:, dec_idx].clone())))
+        sub = DPT_SUB[res]
+        hooks.append(model.view_transformer.out_dpt.register_forward_hook(
+            lambda m, a, o: got.__setitem__("dpt_sub", o[:, :, ::sub, ::sub].clone())))
     if not taps:  # size-independent signature of stage 1 at production sequence length
         hooks.append(model.transformer.register_forward_hook(
             lambda m, a, o: got.__setitem__("enc_rownorm", o.norm(dim=-1).clone())))
@@ -111,15 +169,21 @@ def run_case(name, over, ntris, pad, nv, res, wseed, sseed, taps):
                           resolution=res, torch_dtype=torch.float32)
     for h in hooks:
         h.remove()
+    if prod:
+        got["dec_rows"] = torch.stack(dec_rows)  # [layers, views, rows, D]
+        got["dpt_sub_stride"] = torch.tensor(DPT_SUB[res])
 
     names, sums = weight_checksums(sd)
     rec = dict(
         cfg=json.dumps(cfg.to_dict()), weight_seed=np.int64(wseed), weight_names=np.array(names),
-        weight_sums=sums, res=np.int64(res),
-        triangles=batch["triangles"].numpy(), vn=batch["vn"].numpy(), tex_channels=batch["tex_channels"].numpy(),
-        mask=batch["mask"].numpy(), c2w=batch["c2w"].numpy(), fov=batch["fov"].numpy(),
-        texture_after_ch10=tex[:, :, 10, 0, 0].numpy(),
+        weight_sums=sums, res=np.int64(res), texture_after_ch10=tex[:, :, 10, 0, 0].numpy(),
     )
+    if example is None:
+        rec.update(triangles=batch["triangles"].numpy(), vn=batch["vn"].numpy(),
+                   tex_channels=batch["tex_channels"].numpy(), mask=batch["mask"].numpy(), c2w=batch["c2w"].numpy(),
+                   fov=batch["fov"].numpy())
+    else:  # the converted example: its tensors are regenerated by the tests and checked against this digest
+        rec.update(example=np.array(example), inputs_digest=np.array(digest))
     sub = HDR_SUB.get(name)
     if sub:
         o64 = out.double()
@@ -127,7 +191,14 @@ def run_case(name, over, ntris, pad, nv, res, wseed, sseed, taps):
                    hdr_shape=np.array(out.shape), hdr_sum=np.float64(o64.sum()), hdr_sumsq=np.float64((o64 ** 2).sum()))
     else:
         rec["hdr"] = out.numpy().astype(np.float32)
+    if nv >= 2:  # how far apart two views of the scene are (the tests' discrimination guard)
+        a, b = out[0, 1].double(), out[0, 0].double()
+        rec["view01_rel_l2"] = np.float64((a - b).norm() / b.norm())
+        rec["view01_rel_l2_ac"] = np.float64((a - b).norm() / (b - b.mean()).norm())
     for k, v in got.items():
+        if k.endswith("_idx") or k in ("dec_views", "dpt_sub_stride"):
+            rec[k] = v.numpy().astype(np.int64)
+            continue
         key = k if k == "enc_rownorm" else "tap_" + k
         rec[key] = v.numpy().astype(np.float32)
     path = os.path.join(HERE, f"{name}.npz")
@@ -174,3 +245,6 @@ if __name__ == "__main__":
     for name, args in CASES.items():
         if not only or name in only:
             run_case(name, *args)
+    for name, (example, over, res, wseed, taps) in REAL_CASES.items():
+        if not only or name in only:
+            run_case(name, over, None, None, 1, res, wseed, 0, False, example=example)

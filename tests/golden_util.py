@@ -14,6 +14,11 @@ CASES = ["tiny_swin", "tiny_swin_r128", "tiny_full", "tiny_large", "cbox_base"]
 # BASELINE.json configs at their own sizes (full depth, make_golden.py): config 2 (large-proxy, cbox, 512^2),
 # config 3 (cbox-bunny N=6,209), config 1's shape (v1-base, 256^2), config 5's shape (4 views at 1024^2)
 BIG_CASES = ["large_cbox_r512", "large_bunny_r512", "base_cbox_r256", "large_cbox_r1024_v4"]
+# the reference's own example scenes (examples/*.json through the package's converter), large-proxy at 512^2:
+# config 4's scenes, incl. the longest triangle sequence (cbox-lucy, S = 11,819)
+REAL_CASES = ["real_cbox-lucy_r512", "real_shader-ball_r512", "real_cbox-teapot_r512", "real_init-template_r512"]
+# cases whose fixture holds production-size intermediate taps (make_golden.PROD_TAPS)
+PROD_TAP_CASES = BIG_CASES + ["real_cbox-lucy_r512"]
 
 
 def reference_hdr(z):
@@ -36,10 +41,20 @@ def load_case(name):
     sums = np.array([[float(sd[n].double().sum()), float(sd[n].double().abs().sum())] for n in names])
     if not np.allclose(sums, z["weight_sums"], rtol=1e-9, atol=1e-9):
         raise AssertionError(f"{name}: synthetic weight generator drifted from the fixture")
+    if "example" in z.files:  # an example scene: regenerate its tensors with the converter and pin them
+        from renderformer_amd.examples import inputs_digest, scene_inputs
+        a = scene_inputs(str(z["example"]))
+        if inputs_digest(a) != str(z["inputs_digest"]):
+            raise AssertionError(f"{name}: the converter's output for {z['example']} drifted from the fixture")
+        arrays = dict(triangles=a["triangles"][None], vn=a["vn"][None], tex_channels=a["tex_channels"][None],
+                      mask=np.ones((1, a["triangles"].shape[0]), dtype=bool), c2w=a["c2w"][None],
+                      fov=a["fov"].reshape(1, -1, 1))
+    else:
+        arrays = {k: z[k] for k in ("triangles", "vn", "tex_channels", "mask", "c2w", "fov")}
     inputs = dict(
-        triangles=torch.from_numpy(z["triangles"]), vn=torch.from_numpy(z["vn"]),
-        texture=torch.from_numpy(expand_texture(z["tex_channels"])), mask=torch.from_numpy(z["mask"]),
-        c2w=torch.from_numpy(z["c2w"]), fov=torch.from_numpy(z["fov"]),
+        triangles=torch.from_numpy(arrays["triangles"]), vn=torch.from_numpy(arrays["vn"]),
+        texture=torch.from_numpy(expand_texture(arrays["tex_channels"])), mask=torch.from_numpy(arrays["mask"]),
+        c2w=torch.from_numpy(arrays["c2w"]), fov=torch.from_numpy(arrays["fov"]),
     )
     return cfg, sd, inputs, int(z["res"]), z
 

@@ -144,6 +144,64 @@ def test_attn_schedule_covers_every_tile_once(probs, grid):
         assert ws == list(range(ws[0], ws[0] + len(ws)))
 
 
+def _sk_logical(nwg, units):
+    """Python mirror of common.h SkLayout: logical index of every blockIdx, and the groups' logical spans."""
+    nx = min(8, nwg)
+    G = max(1, units) if units < nx else nx
+    cnt = [(nwg - x + nx - 1) // nx for x in range(nx)]
+    xlo = [(g * nx + G - 1) // G for g in range(G + 1)]
+    base = [sum(cnt[:xlo[g]]) for g in range(G + 1)]
+    logical = {}
+    for hw in range(nwg):
+        x = hw % nx
+        g = x * G // nx
+        rank = sum(1 for y in range(xlo[g], xlo[g + 1]) for j in range(cnt[y]) if nx * j + y > hw)
+        logical[hw] = base[g] + rank
+    assert sorted(logical.values()) == list(range(nwg))  # a bijection
+    return logical, [(base[g], base[g + 1]) for g in range(G)]
+
+
+@pytest.mark.parametrize("probs,grid", [
+    ([[0, 5649, 0, 5649, 0]], 256),                                   # stage 1, bench shape (23 units per group)
+    ([[0, 4096, 0, 5649, 0]], 256),                                   # cross-attention, one view (2-way cuts)
+    ([[0, 6225, 0, 6225, 0], [6225, 11819, 6225, 11819, 6225]], 256),  # bunny + lucy sized scenes in one launch
+    ([[0, 5649, 0, 5649, 0]], 100),                                   # grid not a multiple of 8
+    ([[0, 700, 0, 900, 0]], 256),                                     # fewer units than groups
+])
+def test_attn_schedule_forward_progress(probs, grid):
+    """Every owner (the block holding a unit's first tile, which merges the unit's other pieces) has a HIGHER
+    blockIdx than every block it waits on, and a unit never spans two XCD groups: the waits only go to
+    earlier-dispatched blocks, so the launch drains with no co-residency assumption (common.h SkLayout)."""
+    import numpy as np
+    import torch  # noqa: F401
+    from renderformer_amd import _lib, ops
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("librfhip.so not built")
+    H = 8
+    b = ops.attn_schedule_host(probs, H, grid)
+    units, tot = [], 0
+    for q0, ql, k0, kl, v0 in probs:
+        nt = (kl + 63) // 64
+        for _ in range(H * ((ql + 255) // 256) if nt and ql else 0):
+            units.append((tot, tot + nt))
+            tot += nt
+    assert b[0] == 0 and b[-1] == tot and np.all(np.diff(b) >= 0)
+    logical, spans = _sk_logical(grid, len(units))
+    hw_of = {L: hw for hw, L in logical.items()}
+    group_of = {L: g for g, (s, e) in enumerate(spans) for L in range(s, e)}
+    by_unit = {}
+    for w, x, e, us, ue in _sk_pieces(b, units):
+        by_unit.setdefault(us, []).append(w)
+    cut = 0
+    for ws in by_unit.values():
+        assert len({group_of[w] for w in ws}) == 1, ws        # one group per unit
+        owner = ws[0]
+        assert all(hw_of[owner] > hw_of[w] for w in ws[1:])    # owner waits only on lower blockIdx
+        cut += len(ws) > 1
+    if probs == [[0, 5649, 0, 5649, 0]] and grid == 256:
+        assert cut == 184  # every unit (89 tiles) is longer than a workgroup's share (64): all are cut
+
+
 def test_attn_schedule_balances_the_bench_shape():
     """At the stage-1 bench shape the balanced table gives the workgroups that hold a single piece ("mid": one
     prologue, one publish) more tiles than those with two pieces, and no workgroup is left empty."""

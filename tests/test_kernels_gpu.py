@@ -422,6 +422,70 @@ def test_attention_stream_k_many_problems(sched):
         off += n
 
 
+@pytest.mark.parametrize("sk_kernel_name", ["sk", "p4"])
+def test_attention_longest_example_sequence(sk_kernel_name, monkeypatch):
+    """S = 11,819 (cbox-lucy: 11,803 triangles + 16 register tokens, the longest example scene; SURVEY §5 needs
+    S ~ 12k in one pass) at the model's 8 heads, pre-scaled q, with the cost-balanced schedule: 376 units of
+    185 key tiles cut over 256 workgroups.  Checked against fp64 on 768 sampled query rows of every head."""
+    monkeypatch.setenv("RF_ATTN_P4", "1" if sk_kernel_name == "p4" else "0")
+    ops = _ops()
+    H, S = 8, 11819
+    D = H * 128
+    g = torch.Generator(device="cpu").manual_seed(11819)
+    qkv = torch.randn(S, 3 * D, generator=g).bfloat16()
+    d = qkv.to(dev)
+    qs = (d[:, :D].float() * ops.Q_LOG2_SCALE).bfloat16()
+    probs = [[0, S, 0, S, 0]]
+    out = torch.zeros(S, D, device=dev, dtype=torch.bfloat16)
+    ops.attention(qs, d[:, D:2 * D], d[:, 2 * D:], out, torch.tensor(probs, dtype=torch.int32, device=dev), S, H,
+                  q_prescaled=True, schedule=ops.attn_schedule(probs, H, dev))
+    torch.cuda.synchronize()
+    assert _lib_mod().rf_device_error() == 0
+    rows = torch.cat([torch.arange(0, 16), torch.randperm(S, generator=g)[:736].sort().values, torch.tensor([S - 1])])
+    qref = qs[rows].float().cpu() / ops.Q_LOG2_SCALE
+    ref = _ref_attn(qref, qkv[:, D:2 * D].float(), qkv[:, 2 * D:].float(), H)
+    assert relerr(out.float().cpu()[rows], ref) < 6e-3
+
+
+def _lib_mod():
+    from renderformer_amd import _lib
+    return _lib.load()
+
+
+def test_attention_bad_schedule_is_refused_and_recovers():
+    """A range table built for another launch: the kernel checks it against its own problems instead
+    of reading past them, reports a device error (DeviceError at the next call), and after
+    ops.clear_device_error() the next launches on fresh workspaces are correct again."""
+    from renderformer_amd._lib import DeviceError
+    ops = _ops()
+    H = 2
+    D = H * 128
+    g = torch.Generator(device="cpu").manual_seed(3)
+    qkv = torch.randn(900, 3 * D, generator=g).bfloat16()
+    d = qkv.to(dev)
+    small = [[0, 600, 0, 600, 0]]
+    big = [[0, 900, 0, 900, 0]]
+    wrong = ops.attn_schedule(big, H, dev)  # covers more tiles than the `small` launch has
+    out = torch.zeros(900, D, device=dev, dtype=torch.bfloat16)
+    ops.attention(d[:, :D], d[:, D:2 * D], d[:, 2 * D:], out, torch.tensor(small, dtype=torch.int32, device=dev), 600, H,
+                  schedule=wrong)
+    torch.cuda.synchronize()
+    assert _lib_mod().rf_device_error() != 0
+    with pytest.raises(DeviceError, match="clear_device_error"):
+        ops.rmsnorm(torch.ones(4, 256, device=dev), torch.ones(256, device=dev), 1e-6,
+                    torch.empty(4, 256, device=dev, dtype=torch.bfloat16))
+    ops.clear_device_error()
+    assert _lib_mod().rf_device_error() == 0
+    for sched in (None, ops.attn_schedule(big, H, dev)):
+        out.zero_()
+        ops.attention(d[:, :D], d[:, D:2 * D], d[:, 2 * D:], out, torch.tensor(big, dtype=torch.int32, device=dev),
+                      900, H, schedule=sched)
+        ref = _ref_attn(qkv[:, :D].float(), qkv[:, D:2 * D].float(), qkv[:, 2 * D:].float(), H)
+        assert relerr(out.float().cpu(), ref) < 6e-3
+    torch.cuda.synchronize()
+    assert _lib_mod().rf_device_error() == 0
+
+
 @pytest.mark.parametrize("grid,shift", [(8, 0), (8, 4), (16, 4), (16, 0)])
 def test_swin_attention_matches_oracle_layout(grid, shift):
     ops = _ops()

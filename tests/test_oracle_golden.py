@@ -6,7 +6,7 @@ import torch
 from oracle import rf_ref
 import os
 
-from golden_util import BIG_CASES, CASES, GOLDEN, hdr_shape, load_case, reference_hdr, rel_l2
+from golden_util import BIG_CASES, CASES, GOLDEN, REAL_CASES, hdr_shape, load_case, reference_hdr, rel_l2
 
 TOL = 1e-5  # restatement vs reference on identical CPU fp32 kernels
 
@@ -15,12 +15,13 @@ SLOW = os.environ.get("RF_SLOW_TESTS", "0") != "0"
 
 
 def _big(name):
-    # the 4-view 1024^2 case takes ~2 min of CPU: run with RF_SLOW_TESTS=1
-    marks = [pytest.mark.slow, pytest.mark.skipif(not SLOW, reason="RF_SLOW_TESTS=1 runs it")] if "1024" in name else []
+    # the 4-view 1024^2 case takes ~2 min of CPU, the long example scenes ~30 s each: run with RF_SLOW_TESTS=1
+    slow = "1024" in name or (name.startswith("real_") and "init-template" not in name)
+    marks = [pytest.mark.slow, pytest.mark.skipif(not SLOW, reason="RF_SLOW_TESTS=1 runs it")] if slow else []
     return pytest.param(name, marks=marks)
 
 
-@pytest.mark.parametrize("name", CASES + [_big(n) for n in BIG_CASES])
+@pytest.mark.parametrize("name", CASES + [_big(n) for n in BIG_CASES + REAL_CASES])
 def test_oracle_matches_reference(name):
     cfg, sd, inp, res, z = load_case(name)
     taps = {}
@@ -34,8 +35,15 @@ def test_oracle_matches_reference(name):
         assert rel_l2(enc.norm(dim=-1), z["enc_rownorm"]) < TOL
     # in-place log encoding of the emission channels (rendering_pipeline.py:67-68)
     np.testing.assert_allclose(tex[:, :, 10, 0, 0].numpy(), z["texture_after_ch10"], rtol=1e-6, atol=1e-7)
+    if "enc_row_idx" in z.files:  # production-size taps: row samples of stage 1 / every decoder layer, DPT logits
+        idx, didx, views = (torch.from_numpy(z[k]) for k in ("enc_row_idx", "dec_row_idx", "dec_views"))
+        assert rel_l2(taps[f"enc{cfg.num_layers - 1}"][0, idx], z["tap_enc_rows"]) < TOL
+        for i in range(z["tap_dec_rows"].shape[0]):
+            assert rel_l2(taps[f"dec{i}"][views][:, didx], z["tap_dec_rows"][i]) < TOL, i
+        s = int(z["dpt_sub_stride"])
+        assert rel_l2(taps["dpt"][:, :, ::s, ::s], z["tap_dpt_sub"]) < TOL
     for k in z.files:
-        if not k.startswith("tap_"):
+        if not k.startswith("tap_") or k in ("tap_enc_rows", "tap_dec_rows", "tap_dpt_sub"):
             continue
         key = k[4:]
         mine = {"enc_out": taps.get(f"enc{cfg.num_layers - 1}")}.get(key, taps.get(key))

@@ -4,10 +4,12 @@ Golden fixtures (tests/golden/*.npz) were produced by the reference itself on
 CPU fp32; the oracle restatement is bit-identical to them (test_oracle_golden).
 Bar (BASELINE.json north_star): <= 1e-3 relative L2 on the HDR pixels.
 """
+import numpy as np
 import pytest
 import torch
 
-from golden_util import BIG_CASES, CASES, hdr_shape, load_case, reference_hdr, rel_l2, rel_l2_ac
+from golden_util import (BIG_CASES, CASES, PROD_TAP_CASES, REAL_CASES, hdr_shape, load_case, reference_hdr, rel_l2,
+                         rel_l2_ac)
 from oracle import rf_ref
 
 pytestmark = pytest.mark.gpu
@@ -82,6 +84,43 @@ def test_concurrent_renders_on_two_streams():
     torch.cuda.synchronize()
     for o, r in zip(outs, serial):
         assert torch.equal(o.cpu(), r)
+
+
+def test_concurrent_bench_frames_on_two_streams():
+    """Two full bench-shape frames (large-proxy, 14+10 layers, 512^2: cbox N=5,633 and cbox-bunny N=6,209) enqueued
+    on two streams at once.  Here every stream-K launch cuts units (stage 1: 184 units of 89 tiles on 256
+    workgroups), and two concurrent kernels can hold every CU between them: the owners' waits only go to
+    earlier-dispatched blocks (common.h SkLayout), so both frames drain, raise no device error, and equal the
+    same frames rendered one after the other bit for bit."""
+    from renderformer_amd import _lib
+    cases = [load_case("large_cbox_r512"), load_case("large_bunny_r512")]
+    cfg, sd = cases[0][0], cases[0][1]
+    pipes = [_pipeline(cfg, sd), _pipeline(cfg, sd)]
+    batches = [{k: v.cuda() for k, v in c[2].items()} for c in cases]
+
+    def render(p, b):
+        return p(b["triangles"], b["texture"].clone(), b["mask"], b["vn"], b["c2w"], b["fov"], resolution=512)
+
+    serial = [render(p, b).cpu() for p, b in zip(pipes, batches)]
+    for p, b, c in zip(pipes, batches, cases):  # warm plans on both pipelines before the concurrent pass
+        render(p, b)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    main = torch.cuda.current_stream()
+    for _ in range(2):
+        outs = []
+        for s, p, b in zip(streams, pipes, batches):
+            s.wait_stream(main)
+            with torch.cuda.stream(s):
+                outs.append(render(p, b))
+        torch.cuda.synchronize()
+        assert _lib.load().rf_device_error() == 0
+        for o, r in zip(outs, serial):
+            assert torch.equal(o.cpu(), r)
+    for o, c in zip(serial, cases):
+        ref, st = reference_hdr(c[4])
+        assert rel_l2(o[:, :, ::st, ::st], ref) < HDR_TOL
+    del pipes, batches
+    torch.cuda.empty_cache()
 
 
 def test_model_forward_reference_signature():
@@ -198,6 +237,47 @@ def test_baseline_configs_match_reference(name):
         o64 = out.double()
         assert abs(float(o64.sum()) - float(z["hdr_sum"])) / abs(float(z["hdr_sum"])) < 1e-3
         assert abs(float((o64 ** 2).sum()) - float(z["hdr_sumsq"])) / float(z["hdr_sumsq"]) < 2e-3
+    del pipe, out, d
+    torch.cuda.empty_cache()
+
+
+TAP_TOL = 1e-3  # per-tap relative L2 bar at production size
+
+
+@pytest.mark.parametrize("name", PROD_TAP_CASES)
+def test_production_taps_match_reference(name):
+    """The HIP path's intermediates at production size vs the reference's own (make_golden.PROD_TAPS): a fixed
+    sample of stage-1 output rows (the 16 register tokens + seeded triangle rows) and every stage-1 row's norm,
+    every decoder layer's output on seeded ray-token rows of the first views, and the DPT logits (the
+    reference's pre-ELU out_dpt output through the ELU, vs log10(HDR + 1) of the GPU frame) every few pixels.
+    A wrong view, scene, layer or token order is far outside these bars (the sampled rows are different
+    triangles / rays: swapping them costs O(1) relative error)."""
+    cfg, sd, inp, res, z = load_case(name)
+    pipe = _pipeline(cfg, sd)
+    d = {k: v.cuda() for k, v in inp.items()}
+    cap = pipe.model.capture_taps(enc_rows=z["enc_row_idx"], dec_rows=z["dec_row_idx"],
+                                  dec_views=[int(v) for v in z["dec_views"]])
+    out = pipe(d["triangles"], d["texture"], d["mask"], d["vn"], d["c2w"], d["fov"], resolution=res,
+               torch_dtype=torch.bfloat16)
+    errs = {"enc_rows": rel_l2(cap["enc_rows"].cpu(), z["tap_enc_rows"])}
+    if "enc_rownorm" in z.files:
+        errs["enc_rownorm"] = rel_l2(cap["enc_rownorm"].cpu(), z["enc_rownorm"][0])
+    dec = cap["dec_rows"].cpu()
+    assert tuple(dec.shape) == z["tap_dec_rows"].shape
+    for i in range(dec.shape[0]):
+        errs[f"dec{i}"] = rel_l2(dec[i], z["tap_dec_rows"][i])
+    st = int(z["dpt_sub_stride"])
+    logits = torch.from_numpy(z["tap_dpt_sub"]).double()  # [B*V, 3, H/st, W/st], pre-ELU
+    ref_log = torch.where(logits > 0, logits, 1e-3 * torch.expm1(logits))  # ELU(alpha=1e-3), view_transformer.py:86
+    # [B, V, res, res, 3] -> [B*V, 3, res/st, res/st]
+    got_log = torch.log10(out.double().cpu()[:, :, ::st, ::st, :3].flatten(0, 1).permute(0, 3, 1, 2) + 1.0)
+    errs["dpt_logits"] = rel_l2(got_log, ref_log)
+    # discrimination: the same sample against shuffled reference rows (a token-order / view mix-up)
+    shuffled = rel_l2(cap["enc_rows"].cpu(), np.roll(z["tap_enc_rows"], 1, axis=0))
+    print(f"{name}: " + ", ".join(f"{k} {v:.2e}" for k, v in errs.items()) + f"; rows shifted by one: {shuffled:.2e}")
+    for k, v in errs.items():
+        assert v < TAP_TOL, (k, v)
+    assert shuffled > 100 * errs["enc_rows"]
     del pipe, out, d
     torch.cuda.empty_cache()
 

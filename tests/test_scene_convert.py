@@ -1,6 +1,6 @@
 """JSON -> HDF5 scene conversion (renderformer_amd.scene_convert, restating scene_processor/*.py).
 
-Fixture: the reference's own examples/cbox.json and the OBJ files it lists (tests/golden/scenes/, data
+Fixture: the reference's own examples/cbox.json and the OBJ files it lists (examples/ at the repository root, data
 copied from the reference's examples/).  Pinned: dataset names / shapes / dtypes (to_h5.py:87-92), the
 texture patch layout (constant x {i + j <= 32}, to_h5.py:41-66), the look-at camera (to_h5.py:10-34),
 the transforms (scene_mesh.py:31-55) and the uint8 diffuse round trip (:87-90).  The smooth-shading normals
@@ -19,7 +19,7 @@ from renderformer_amd import scene_convert as sc
 from renderformer_amd.scenes import texture_mask
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-CBOX = os.path.join(HERE, "golden", "scenes", "cbox.json")
+CBOX = os.path.join(os.path.dirname(HERE), "examples", "cbox.json")
 
 
 def test_cbox_converts_to_reference_format(tmp_path):
@@ -40,7 +40,7 @@ def test_cbox_converts_to_reference_format(tmp_path):
     assert np.allclose(ch[-1, 10:13], 5000.0) and np.allclose(ch[:-1, 10:13], 0.0)
     assert np.allclose(ch[0, :3], np.float16(102 / 255)) and np.allclose(ch[:, 7:10], [0.5, 0.5, 1.0])
     # light triangle: tri.obj scaled 2.5 then translated to z = 2.1 (scene_mesh.py:41-55)
-    lv, lf = sc.load_obj(os.path.join(HERE, "golden", "scenes", "templates", "lighting", "tri.obj"))
+    lv, lf = sc.load_obj(os.path.join(os.path.dirname(HERE), "examples", "templates", "lighting", "tri.obj"))
     assert np.allclose(tri[-1], (lv[lf[0]] * 2.5 + [0.0, 0.0, 2.1]).astype(np.float32), atol=1e-6)
     # normals are unit length; planar groups give the plane normal
     assert np.allclose(np.linalg.norm(vn, axis=-1), 1.0, atol=1e-5)
