@@ -68,8 +68,8 @@ def parse(argv=None):
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (1-GPU rehearsal)")
     ap.add_argument("--dump", default=None, help="rank 0 saves the gathered frames of the last step (.npy)")
     ap.add_argument("--view-chunk", type=int, default=None,
-                    help="stage 2 + DPT over at most this many views per pass (default: 1 for c5, so a view's image "
-                         "does not depend on the rank split; all views otherwise)")
+                    help="stage 2 + DPT over at most this many views per pass (c5 default: 3 when views % 24 == 0, "
+                         "else 1, so a view's image does not depend on the rank split; all views otherwise)")
     ap.add_argument("--fp8", action="store_true", help="stage-2 projections + FFN as MX fp8 GEMMs (config 5's fp8 "
                                                         "path); roofline then reports the stage-2 W13 fp8 GEMM")
     a = ap.parse_args(argv)
@@ -80,7 +80,9 @@ def parse(argv=None):
     if a.workload == "c4" and a.scenes == 1:
         a.scenes = 64
     if a.view_chunk is None and a.workload == "c5":
-        a.view_chunk = 1
+        # fixed chunks make a view's image independent of the rank split; 3 views per pass (1024^2: 49k ray
+        # tokens per GEMM) when every rank of a 1/2/4/8-GPU run holds whole chunks of the 24 views
+        a.view_chunk = 3 if a.views % 24 == 0 else 1
     return a
 
 

@@ -55,7 +55,7 @@ extern "C" {
 #define RF_ERR_UNSUPPORTED 3
 #define RF_ERR_DEVICE 4       /* an earlier launch reported a device-side error (see rf_device_error) */
 
-#define RF_ABI_VERSION 9
+#define RF_ABI_VERSION 10
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -63,6 +63,12 @@ extern "C" {
 #define RF_EPI_ADD_F32 2    /* C(f32)  += A W^T + bias   (residual stream update)         */
 #define RF_EPI_SWIGLU 3     /* C(bf16)[M, N/2] = silu(A W1^T) * (A W3^T); W rows interleaved
                                in 16-row groups [w1[16g:16g+16]; w3[16g:16g+16]]            */
+#define RF_EPI_F16 4        /* C(fp16)  = A W^T + bias                                   */
+#define RF_EPI_SWIGLU_F16 5 /* RF_EPI_SWIGLU with an fp16 C                               */
+
+/* 16-bit element types of an output (the *_dt / _sk entry points) */
+#define RF_DT_BF16 0
+#define RF_DT_F16 1
 
 const char* rf_last_error(void);
 int rf_abi_version(void);
@@ -99,6 +105,13 @@ int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c
                  const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
                  void* stream);
 int64_t rf_gemm_workspace_bytes(void);
+/* rf_gemm_bf16 with fp16 operands A, W (fp16 MFMAs, the bf16 rate; 11-bit mantissa: the model's default operand
+ * format, 6-7x less rounding error than bf16 end to end).  Every epilogue of rf_gemm_bf16 (RF_EPI_BF16 still
+ * writes bf16, e.g. q/k/v for the attention kernels); RF_EPI_F16 / RF_EPI_SWIGLU_F16 write fp16 (the operand of
+ * the next fp16 GEMM), also from rf_gemm_bf16. */
+int rf_gemm_f16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
+                const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
+                void* stream);
 /* rf_gemm_bf16 on the HIP engine that does nothing unless *flag != 0 (read on the device when the launch
  * runs); stream-ordered after whatever wrote the flag. */
 int rf_gemm_bf16_if(const int* flag, const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
@@ -121,6 +134,9 @@ int rf_quant_mx8(const void* x, int64_t ldx, int rows, int cols, void* q, int64_
 /* out(bf16)[r, :] = x[r, :] * rsqrt(mean(x^2) + eps) * weight ; x f32. */
 int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, float eps, void* out, int64_t ldo,
                int rows, int dim, void* stream);
+/* rf_rmsnorm with an fp16 out (the A operand of rf_gemm_f16). */
+int rf_rmsnorm_f16(const float* x, int64_t ldx, const float* weight, float eps, void* out, int64_t ldo,
+                   int rows, int dim, void* stream);
 
 /* dst[r] = rope(rmsnorm(src[src_rows ? src_rows[r] : r]))  (bf16 -> bf16, may alias when src_rows == NULL)
  * over n_seg consecutive segments of width dim (q and k of one qkv row), each with its own full-width
@@ -152,8 +168,10 @@ int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t src_gstride,
  * scores are then used as exp2 exponents directly.
  * n_split == 0 (default mode): stream-K kernel, one workgroup per CU over the flattened
  *   (problem, head, 256-row block, 64-key tile) space; `workspace` = rf_attn_workspace_bytes(0, H, 0)
- *   bytes, ZEROED before its first use and reused as is afterwards (the kernel re-arms its flags);
- *   one launch at a time per workspace.  ws_rows is ignored.
+ *   bytes, ZEROED before its first use and reused as is afterwards (every launch uses fresh hand-off flag
+ *   values); one launch at a time per workspace.  ws_rows is ignored.  Forward progress: a workgroup that
+ *   merges a cut unit waits only on workgroups with a lower blockIdx (dispatched earlier) whose awaited piece
+ *   is the first of their range, so launches drain with no co-residency assumption (two streams at once).
  * n_split >= 1: one workgroup per (problem, head, block, split); for n_split > 1 partials go to
  *   `workspace` (rf_attn_workspace_bytes(ws_rows, n_heads, n_split) bytes, ws_rows >= every output
  *   row + 1) and rf_attn_combine(rows = NULL, n_rows = ws_rows) writes O. */
@@ -171,12 +189,20 @@ int64_t rf_attn_workspace_bytes(int64_t rows, int n_heads, int n_split);
 int rf_attn_grid(void);
 int rf_attn_schedule(const int32_t* problems_host, int n_problems, int n_heads, int grid, int64_t* bounds);
 /* rf_attn_fwd (n_split == 0) with the workgroup ranges taken from `bounds` (device copy of the
- * rf_attn_schedule result; the grid is `grid` workgroups).  Same results up to the fp32 merge order. */
+ * rf_attn_schedule result; the grid is `grid` workgroups).  Same results up to the fp32 merge order.
+ * The kernel checks the table against its own problems (bounds[0] == 0, monotone, bounds[grid] == the
+ * launch's tile count, no unit across an XCD group) and reports RF_ERR_DEVICE (device error 3) instead of
+ * reading past the problems when a table built for another launch is passed. */
 int rf_attn_fwd_sched(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                       void* o, int64_t ldo, const int32_t* problems, int n_problems, int n_heads, int head_dim,
                       float scale, void* workspace, const int64_t* bounds, int grid, void* stream);
 int rf_attn_combine(const void* workspace, int64_t ws_rows, int n_split, int n_heads, const int32_t* rows,
                     int n_rows, void* o, int64_t ldo, void* stream);
+/* The stream-K attention (rf_attn_fwd_sched, or rf_attn_fwd n_split == 0 when bounds == NULL) with O written as
+ * o_dtype: RF_DT_F16 when O is the A operand of an fp16 out-projection (rf_gemm_f16); q/k/v stay bf16. */
+int rf_attn_fwd_sk(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                   void* o, int64_t ldo, int o_dtype, const int32_t* problems, int n_problems, int n_heads,
+                   int head_dim, float scale, void* workspace, const int64_t* bounds, int grid, void* stream);
 
 /* Shifted-window attention over n_images patch grids [grid_h, grid_w] stored row-major (token
  * r = img*gh*gw + y*gw + x); windows of window x window tokens on the grid rolled by -shift,
@@ -184,6 +210,10 @@ int rf_attn_combine(const void* workspace, int64_t ws_rows, int n_split, int n_h
 int rf_swin_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                      void* o, int64_t ldo, int n_images, int grid_h, int grid_w, int window, int shift,
                      int n_heads, int head_dim, float scale, void* stream);
+/* rf_swin_attn_fwd with O written as o_dtype (RF_DT_BF16 / RF_DT_F16). */
+int rf_swin_attn_fwd_dt(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                        void* o, int64_t ldo, int o_dtype, int n_images, int grid_h, int grid_w, int window, int shift,
+                        int n_heads, int head_dim, float scale, void* stream);
 
 /* texture: f32 [n_rows, channels, patch_elems]; channels >= channels-log_channels are log10(x+1)
  * encoded IN PLACE for every row; rows with dst_row[r] >= 0 are written as bf16 to out[dst_row[r]]. */
@@ -213,15 +243,24 @@ int rf_texture_linear(const float* coef, int64_t ldc, int rows, int channels, co
 /* NeRF encoding (include_input) of vn f32 [n_rows, 9] into bf16 out[dst_row[r], 0:ldo] (zero padded). */
 int rf_vn_encode(const float* vn, int64_t n_rows, const int32_t* dst_row, int n_freqs, void* out,
                  int64_t ldo, void* stream);
+/* rf_vn_encode with out written as out_dtype (RF_DT_BF16 / RF_DT_F16: the operand of an fp16 GEMM). */
+int rf_vn_encode_dt(const float* vn, int64_t n_rows, const int32_t* dst_row, int n_freqs, void* out,
+                    int64_t ldo, int out_dtype, void* stream);
 
 /* Pinhole rays for n_views cameras (c2w f32 [n_views,4,4], fov degrees [n_views]) at res x res,
  * normalised, patchified into bf16 tokens out[view*R + t, c*patch*patch + p1*patch + p2];
  * ray_pos[view, 9] = camera origin repeated 3x. */
 int rf_ray_tokens(const float* c2w, const float* fov_deg, int n_views, int res, int patch, void* out,
                   float* ray_pos, void* stream);
+/* rf_ray_tokens with out written as out_dtype (RF_DT_BF16 / RF_DT_F16). */
+int rf_ray_tokens_dt(const float* c2w, const float* fov_deg, int n_views, int res, int patch, void* out,
+                     float* ray_pos, int out_dtype, void* stream);
 
 /* rays_d f32 [n_views, res, res, 3] (already generated) -> the same bf16 token layout as rf_ray_tokens. */
 int rf_patchify_rays(const float* rays_d, int n_views, int res, int patch, void* out, void* stream);
+/* rf_patchify_rays with out written as out_dtype (RF_DT_BF16 / RF_DT_F16). */
+int rf_patchify_rays_dt(const float* rays_d, int n_views, int res, int patch, void* out, int out_dtype,
+                        void* stream);
 
 /* Triangle positions for RoPE.  tris f32 [*, 9]; valid_idx int32 [sum n_b] (rows into tris, grouped by
  * scene, offsets scene_off[B+1]).  For each set s (s = b when c2w == NULL, else s = b*n_views + v with the

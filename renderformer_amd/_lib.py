@@ -37,6 +37,10 @@ _F = ctypes.c_float
 # name -> argtypes (every function returns int status)
 SIGNATURES = {
     "rf_gemm_bf16": [_P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _L, _P],
+    "rf_gemm_f16": [_P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _L, _P],
+    "rf_rmsnorm_f16": [_P, _L, _P, _F, _P, _L, _I, _I, _P],
+    "rf_attn_fwd_sk": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _P, _I, _I, _I, _F, _P, _P, _I, _P],
+    "rf_swin_attn_fwd_dt": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P],
     "rf_rmsnorm": [_P, _L, _P, _F, _P, _L, _I, _I, _P],
     "rf_qk_norm_rope": [_P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _F, _F, _P, _L, _I, _P, _I, _P],
     "rf_qk_norm_rope_groups": [_P, _L, _L, _P, _L, _L, _P, _I, _I, _I, _I, _I, _P, _L, _F, _F, _P, _L, _I, _P, _I,
@@ -53,6 +57,9 @@ SIGNATURES = {
     "rf_texture_linear": [_P, _L, _I, _I, _P, _P, _P, _L, _I, _P, _P],
     "rf_gemm_bf16_if": [_P, _P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _L, _P],
     "rf_vn_encode": [_P, _L, _P, _I, _P, _L, _P],
+    "rf_vn_encode_dt": [_P, _L, _P, _I, _P, _L, _I, _P],
+    "rf_ray_tokens_dt": [_P, _P, _I, _I, _I, _P, _P, _I, _P],
+    "rf_patchify_rays_dt": [_P, _I, _I, _I, _P, _I, _P],
     "rf_ray_tokens": [_P, _P, _I, _I, _I, _P, _P, _P],
     "rf_patchify_rays": [_P, _I, _I, _I, _P, _P],
     "rf_scene_pos": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _I, _P, _L, _P],

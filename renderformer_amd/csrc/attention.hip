@@ -82,7 +82,12 @@ struct AttnArgs {
     // cost-balanced, group-aligned); null = equal tile counts per group
     const int64_t* bounds;
     int epoch;  // hand-off flag value of this launch (> 0, new every launch: no re-arm, stale flags never match)
+    int o_f16;  // output O as fp16 (the A operand of an fp16 out-projection) instead of bf16
 };
+
+// two f32 -> the 16-bit output pair: fp16 (OF16) or bf16, RNE
+template <bool OF16>
+RF_DEV uint32_t pack_o(float lo, float hi) { return OF16 ? pack_f16x2(lo, hi) : pack_bf16x2(lo, hi); }
 
 // Stream-K ranges in the forward-progress layout (common.h SkLayout): the launch's units (head x q-block of
 // every problem that has keys) in G contiguous chunks, one per XCD group, each chunk's tiles over the group's
@@ -144,7 +149,7 @@ RF_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 RF_DEV float max3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
 
-template <bool SWIN, int NW>
+template <bool SWIN, int NW, bool OF16 = false>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_fwd_kernel(AttnArgs p) {
     constexpr int T = NW * 64;
     constexpr int CPT = (KT * HD / 8) / T;  // 16-B chunks per thread per tile (per operand)
@@ -436,8 +441,8 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_fwd_kernel(Attn
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
             uint2 pk;
-            pk.x = pack_bf16x2(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
-            pk.y = pack_bf16x2(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
+            pk.x = pack_o<OF16>(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
+            pk.y = pack_o<OF16>(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
             *reinterpret_cast<uint2*>(dst + dt * 32 + 8 * gq + 4 * half) = pk;
         }
 }
@@ -679,8 +684,10 @@ __global__ __launch_bounds__(NW3 * 64, 1) void attn_v3_kernel(AttnArgs p) {
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
             uint2 pk;
-            pk.x = pack_bf16x2(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
-            pk.y = pack_bf16x2(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
+            pk.x = p.o_f16 ? pack_f16x2(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv)
+                           : pack_bf16x2(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
+            pk.y = p.o_f16 ? pack_f16x2(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv)
+                           : pack_bf16x2(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
             *reinterpret_cast<uint2*>(dst + dt * 32 + 8 * gq + 4 * half) = pk;
         }
 }
@@ -746,7 +753,7 @@ RF_DEV void dma_piece(const bf16_t* g, uint32_t lds) {
 // 2 = no top-of-tile wait + barrier, 4 = no PV MFMAs, 8 = no exp2 (P = bf16(S)), 16 = no QK MFMAs,
 // 32 = s_memtime stamps per segment (cycles summed over tiles) into the workspace's last piece slot,
 // 64 = no static priority for waves 4-7
-template <bool UNIT, int DBG = 0>
+template <bool UNIT, int DBG = 0, bool OF16 = false>
 __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     // SPLIT: half of each tile's softmax (keys 32-63) moves from phase A (QK^T, VALU-heavy) into the first
     // half of phase B (PV, VALU-light), balancing the two phases that share each SIMD; DBG & 128 = unsplit
@@ -1241,10 +1248,10 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
                 for (int gq = 0; gq < 4; gq += 2) {
-                    uint32_t a0 = pack_bf16x2(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
-                    uint32_t a1 = pack_bf16x2(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
-                    uint32_t b0 = pack_bf16x2(o[dt][4 * gq + 4] * inv, o[dt][4 * gq + 5] * inv);
-                    uint32_t b1 = pack_bf16x2(o[dt][4 * gq + 6] * inv, o[dt][4 * gq + 7] * inv);
+                    uint32_t a0 = pack_o<OF16>(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
+                    uint32_t a1 = pack_o<OF16>(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
+                    uint32_t b0 = pack_o<OF16>(o[dt][4 * gq + 4] * inv, o[dt][4 * gq + 5] * inv);
+                    uint32_t b1 = pack_o<OF16>(o[dt][4 * gq + 6] * inv, o[dt][4 * gq + 7] * inv);
                     const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
                     const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
                     *reinterpret_cast<uint4*>(dst + dt * 32 + 8 * gq + 8 * half) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
@@ -1736,10 +1743,11 @@ __global__ __launch_bounds__(NW4 * 64, 1) void attn_p4_kernel(AttnArgs p) {
                 for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
                     for (int gq = 0; gq < 4; gq += 2) {
-                        uint32_t a0 = pack_bf16x2(o[qs][dt][4 * gq + 0] * inv, o[qs][dt][4 * gq + 1] * inv);
-                        uint32_t a1 = pack_bf16x2(o[qs][dt][4 * gq + 2] * inv, o[qs][dt][4 * gq + 3] * inv);
-                        uint32_t b0 = pack_bf16x2(o[qs][dt][4 * gq + 4] * inv, o[qs][dt][4 * gq + 5] * inv);
-                        uint32_t b1 = pack_bf16x2(o[qs][dt][4 * gq + 6] * inv, o[qs][dt][4 * gq + 7] * inv);
+                        auto pk = [&](float lo, float hi) { return p.o_f16 ? pack_f16x2(lo, hi) : pack_bf16x2(lo, hi); };
+                        uint32_t a0 = pk(o[qs][dt][4 * gq + 0] * inv, o[qs][dt][4 * gq + 1] * inv);
+                        uint32_t a1 = pk(o[qs][dt][4 * gq + 2] * inv, o[qs][dt][4 * gq + 3] * inv);
+                        uint32_t b0 = pk(o[qs][dt][4 * gq + 4] * inv, o[qs][dt][4 * gq + 5] * inv);
+                        uint32_t b1 = pk(o[qs][dt][4 * gq + 6] * inv, o[qs][dt][4 * gq + 7] * inv);
                         const auto w0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
                         const auto w1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
                         *reinterpret_cast<uint4*>(dst + dt * 32 + 8 * gq + 8 * half) = make_uint4(w0[0], w1[0], w0[1], w1[1]);
@@ -1792,7 +1800,7 @@ int cu_count() {  // per-device, queried once
 
 int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv, void* o,
                    int64_t ldo, const int32_t* problems, int n_problems, int n_heads, float scale, void* workspace,
-                   void* stream, const int64_t* bounds = nullptr, int grid = 0) {
+                   void* stream, const int64_t* bounds = nullptr, int grid = 0, bool o_f16 = false) {
     RF_REQUIRE(workspace, "rf_attn_fwd: stream-K mode needs the workspace (rf_attn_workspace_bytes(0, H, 0))");
     if (!bounds) {
         grid = cu_count();
@@ -1814,6 +1822,7 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
     a.c = scale * LOG2E;
     a.part_o = (float*)workspace;
     a.flag = (int*)(a.part_o + (int64_t)SK5_MAX_GRID * PIECE_FLOATS);
+    a.o_f16 = o_f16;
     a.bounds = bounds;
     if (!bounds) {  // equal split per XCD group, written on the device ahead of the launch (stream-ordered)
         int64_t* eq = (int64_t*)(a.flag + SK5_MAX_GRID);
@@ -1860,8 +1869,12 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
         case 384: RF_LAUNCH((attn_sk_kernel<true, 384>), g, b, 0, st, a); break;
         case 512: RF_LAUNCH((attn_sk_kernel<true, 512>), g, b, 0, st, a); break;
         default:
-            if (unit)
+            if (unit && o_f16)
+                RF_LAUNCH((attn_sk_kernel<true, 0, true>), g, b, 0, st, a);
+            else if (unit)
                 RF_LAUNCH((attn_sk_kernel<true, 0>), g, b, 0, st, a);
+            else if (o_f16)
+                RF_LAUNCH((attn_sk_kernel<false, 0, true>), g, b, 0, st, a);
             else
                 RF_LAUNCH((attn_sk_kernel<false, 0>), g, b, 0, st, a);
     }
@@ -2150,6 +2163,19 @@ extern "C" int rf_attn_fwd_sched(const void* q, int64_t ldq, const void* k, int6
                           bounds, grid);
 }
 
+extern "C" int rf_attn_fwd_sk(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                              void* o, int64_t ldo, int o_dtype, const int32_t* problems, int n_problems, int n_heads,
+                              int head_dim, float scale, void* workspace, const int64_t* bounds, int grid,
+                              void* stream) {
+    RF_REQUIRE(q && k && v && o && problems && workspace, "rf_attn_fwd_sk: null pointer");
+    RF_REQUIRE(head_dim == HD, "rf_attn_fwd_sk: head_dim must be 128 (got %d)", head_dim);
+    RF_REQUIRE(o_dtype == RF_DT_BF16 || o_dtype == RF_DT_F16, "rf_attn_fwd_sk: o_dtype must be RF_DT_BF16/F16");
+    RF_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0, "rf_attn_fwd_sk: strides must be 16-B aligned");
+    if (n_problems <= 0) return RF_OK;
+    return attn_sk_launch(q, ldq, k, ldk, v, ldv, o, ldo, problems, n_problems, n_heads, scale, workspace, stream,
+                          bounds, bounds ? grid : 0, o_dtype == RF_DT_F16);
+}
+
 extern "C" int64_t rf_attn_workspace_bytes(int64_t rows, int n_heads, int n_split) {
     if (n_split == 0)  // partial slots, flags, the device-built equal range table
         return (int64_t)SK5_MAX_GRID * PIECE_FLOATS * 4 + SK5_MAX_GRID * 4 + (SK5_MAX_GRID + 1) * 8;
@@ -2168,8 +2194,8 @@ extern "C" int rf_attn_combine(const void* workspace, int64_t ws_rows, int n_spl
     return rf::check_launch("rf_attn_combine");
 }
 
-extern "C" int rf_swin_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
-                                void* o, int64_t ldo, int n_images, int grid_h, int grid_w, int window, int shift,
+extern "C" int rf_swin_attn_fwd_dt(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                                   void* o, int64_t ldo, int o_dtype, int n_images, int grid_h, int grid_w, int window, int shift,
                                 int n_heads, int head_dim, float scale, void* stream) {
     RF_REQUIRE(q && k && v && o, "rf_swin_attn_fwd: null pointer");
     RF_REQUIRE(head_dim == HD, "rf_swin_attn_fwd: head_dim must be 128");
@@ -2195,6 +2221,17 @@ extern "C" int rf_swin_attn_fwd(const void* q, int64_t ldq, const void* k, int64
     a.window = window;
     a.n_split = 1;
     dim3 grid((grid_h / window) * (grid_w / window), n_heads, n_images);
-    RF_LAUNCH((attn_fwd_kernel<true, 2>), grid, dim3(128), 0, (hipStream_t)stream, a);
+    RF_REQUIRE(o_dtype == RF_DT_BF16 || o_dtype == RF_DT_F16, "rf_swin_attn_fwd: o_dtype must be RF_DT_BF16/F16");
+    if (o_dtype == RF_DT_F16)
+        RF_LAUNCH((attn_fwd_kernel<true, 2, true>), grid, dim3(128), 0, (hipStream_t)stream, a);
+    else
+        RF_LAUNCH((attn_fwd_kernel<true, 2>), grid, dim3(128), 0, (hipStream_t)stream, a);
     return rf::check_launch("rf_swin_attn_fwd");
+}
+
+extern "C" int rf_swin_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                                void* o, int64_t ldo, int n_images, int grid_h, int grid_w, int window, int shift,
+                                int n_heads, int head_dim, float scale, void* stream) {
+    return rf_swin_attn_fwd_dt(q, ldq, k, ldk, v, ldv, o, ldo, RF_DT_BF16, n_images, grid_h, grid_w, window, shift,
+                               n_heads, head_dim, scale, stream);
 }

@@ -34,6 +34,15 @@ RF_DEV uint32_t pack_bf16x2(float lo, float hi) {
     return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
 }
 
+// f32 -> the raw bits of a 16-bit operand: fp16 when f16, else bf16 (both round to nearest even)
+RF_DEV uint16_t f32_to_16(float v, bool f16) {
+    if (f16) {
+        _Float16 h = (_Float16)v;
+        return __builtin_bit_cast(uint16_t, h);
+    }
+    return f32_to_bf16(v);
+}
+
 // round-to-nearest-even f32 -> fp16 pair (overflow -> inf, like a torch .half() cast)
 RF_DEV uint32_t pack_f16x2(float lo, float hi) {
     _Float16 a = (_Float16)lo, b = (_Float16)hi;

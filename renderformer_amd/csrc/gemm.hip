@@ -97,7 +97,13 @@ struct EngineArgs {
     const uint8_t* sw;
     int ld_sa, ld_sw;
     int persist;  // phased_sk_kernel: whole tiles strided over the grid, next tile's first K-tiles prefetched
+    int out_f16;  // E_BF16 / E_SWIGLU: 16-bit output as fp16 instead of bf16 (rf_gemm_f16's RF_EPI_*_F16)
 };
+
+// two f32 -> the kernel's 16-bit output pair (RNE): fp16 when the launch asks for it, else bf16
+RF_DEV uint32_t pack16(const EngineArgs& p, float lo, float hi) {
+    return p.out_f16 ? pack_f16x2(lo, hi) : pack_bf16x2(lo, hi);
+}
 
 // uniform early exit of a gated launch (every block reads the same flag, so a stream-K grid exits whole)
 RF_DEV bool gated_off(const EngineArgs& p) { return p.gate && *p.gate == 0; }
@@ -417,7 +423,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                         o[e] = silu(g) * u;
                     }
                     *reinterpret_cast<uint2*>(c + (int64_t)row * p.ldc + ocol) =
-                        make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+                        make_uint2(pack16(p, o[0], o[1]), pack16(p, o[2], o[3]));
                 }
             }
         }
@@ -566,7 +572,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                 const int64_t o = (int64_t)row * p.ldc + col;
                 if constexpr (EPI == E_BF16) {
                     *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.c) + o) =
-                        make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+                        make_uint2(pack16(p, v[0], v[1]), pack16(p, v[2], v[3]));
                 } else {  // E_F32, or E_ADD whose accumulators started from the C tile (load_c_acc)
                     *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + o) = make_float4(v[0], v[1], v[2], v[3]);
                 }
@@ -981,7 +987,7 @@ RF_DEV void phased3_mainloop(const EngineArgs& p, char* smem, int m0, int n0, in
     if (!late) __builtin_amdgcn_s_barrier();
 }
 
-template <int BM, int EPI>
+template <int BM, int EPI, int NTERM = 1>
 __global__ __launch_bounds__(512, 1) void phased3_kernel(EngineArgs p) {
     __shared__ __attribute__((aligned(16))) char smem[3 * ph::Cfg<BM>::TILE];
     if (gated_off(p)) return;
@@ -993,7 +999,7 @@ __global__ __launch_bounds__(512, 1) void phased3_kernel(EngineArgs p) {
     int tm, tn;
     tile_coords(wg, tiles_m, p.n / ph::BN, p.group_m, tm, tn);
     f32x4 acc[BM / 32][4];
-    phased3_mainloop<BM, 1, EPI == E_ADD>(p, smem, tm * BM, tn * ph::BN, 0, p.k / ph::BK2, acc);
+    phased3_mainloop<BM, NTERM, EPI == E_ADD>(p, smem, tm * BM, tn * ph::BN, 0, p.k / ph::BK2, acc);
     engine_epilogue<Tile<BM, 256, 2, 4, 4>, EPI>(p, tm * BM, tn * ph::BN, acc);
 }
 
@@ -1939,10 +1945,10 @@ int launch_phased(EngineArgs a, void* stream, const char* what) {
     const int tiles_m = (a.m + BM - 1) / BM, tiles_n = a.n / 256;
     const int nwg = tiles_n * tiles_m;
     a.group_m = pick_group_m(tiles_m, tiles_n, BM, 256, (nwg + 7) / 8);
-    if constexpr (BM == 256 && NTERM == 1 && !GATHER) {
+    if constexpr (BM == 256 && (NTERM == 1 || NTERM == P_F16) && !GATHER) {
         if (nwg > 256 && persist_on()) {
             a.persist = 1;
-            RF_LAUNCH((phased_sk_kernel<EPI, 1>), dim3(256), dim3(512), 0, (hipStream_t)stream, a);
+            RF_LAUNCH((phased_sk_kernel<EPI, NTERM>), dim3(256), dim3(512), 0, (hipStream_t)stream, a);
             return rf::check_launch(what);
         }
     }
@@ -1950,30 +1956,30 @@ int launch_phased(EngineArgs a, void* stream, const char* what) {
     return rf::check_launch(what);
 }
 
-template <int EPI, int BM>
+template <int EPI, int BM, int NT = 1>
 int launch_phased3(EngineArgs a, void* stream, const char* what) {
     const int tiles_m = (a.m + BM - 1) / BM, tiles_n = a.n / 256;
     const int nwg = tiles_n * tiles_m;
     a.group_m = pick_group_m(tiles_m, tiles_n, BM, 256, (nwg + 7) / 8);
-    RF_LAUNCH((phased3_kernel<BM, EPI>), dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    RF_LAUNCH((phased3_kernel<BM, EPI, NT>), dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
     return rf::check_launch(what);
 }
 
-template <int BM>
+template <int BM, int NT = 1>
 int run_phased3(const EngineArgs& p, int epilogue, void* stream) {
     switch (epilogue) {
-        case RF_EPI_BF16: return launch_phased3<E_BF16, BM>(p, stream, "rf_gemm_bf16");
-        case RF_EPI_F32: return launch_phased3<E_F32, BM>(p, stream, "rf_gemm_bf16");
-        case RF_EPI_ADD_F32: return launch_phased3<E_ADD, BM>(p, stream, "rf_gemm_bf16");
-        default: return launch_phased3<E_SWIGLU, BM>(p, stream, "rf_gemm_bf16");
+        case RF_EPI_BF16: return launch_phased3<E_BF16, BM, NT>(p, stream, "rf_gemm");
+        case RF_EPI_F32: return launch_phased3<E_F32, BM, NT>(p, stream, "rf_gemm");
+        case RF_EPI_ADD_F32: return launch_phased3<E_ADD, BM, NT>(p, stream, "rf_gemm");
+        default: return launch_phased3<E_SWIGLU, BM, NT>(p, stream, "rf_gemm");
     }
 }
 
-template <int EPI>
+template <int EPI, int NT = 1>
 int launch_phased_sk(EngineArgs a, int grid, void* stream, const char* what) {
     const int tiles_m = (a.m + 255) / 256, tiles_n = a.n / 256;
     a.group_m = pick_group_m(tiles_m, tiles_n, 256, 256, ((int64_t)tiles_m * tiles_n + 7) / 8);
-    RF_LAUNCH((phased_sk_kernel<EPI, 1>), dim3(grid), dim3(512), 0, (hipStream_t)stream, a);
+    RF_LAUNCH((phased_sk_kernel<EPI, NT>), dim3(grid), dim3(512), 0, (hipStream_t)stream, a);
     return rf::check_launch(what);
 }
 
@@ -1983,14 +1989,43 @@ bool use_phased(int n, int k) {
     return (!env || atoi(env) != 0) && n % 256 == 0 && k % 64 == 0;
 }
 
-template <class C>
+template <class C, int NT = 1>
 int run_dp_cfg(const EngineArgs& p, int epilogue, void* stream) {
     switch (epilogue) {
-        case RF_EPI_BF16: return launch<C, E_BF16, 1>(p, stream, "rf_gemm_bf16");
-        case RF_EPI_F32: return launch<C, E_F32, 1>(p, stream, "rf_gemm_bf16");
-        case RF_EPI_ADD_F32: return launch<C, E_ADD, 1>(p, stream, "rf_gemm_bf16");
-        default: return launch<C, E_SWIGLU, 1>(p, stream, "rf_gemm_bf16");
+        case RF_EPI_BF16: return launch<C, E_BF16, NT>(p, stream, "rf_gemm");
+        case RF_EPI_F32: return launch<C, E_F32, NT>(p, stream, "rf_gemm");
+        case RF_EPI_ADD_F32: return launch<C, E_ADD, NT>(p, stream, "rf_gemm");
+        default: return launch<C, E_SWIGLU, NT>(p, stream, "rf_gemm");
     }
+}
+
+// fp16 operands (rf_gemm_f16): the loops pick_cfg chooses from, each with fp16 MFMAs (same rate as bf16)
+int run_dp_f16(int cfg, const EngineArgs& p, int epilogue, void* stream) {
+    constexpr int NT = P_F16;
+    if (use_phased(p.n, p.k)) {
+        if (cfg == 256) {
+            switch (epilogue) {
+                case RF_EPI_BF16: return launch_phased<E_BF16, NT, false>(p, stream, "rf_gemm_f16");
+                case RF_EPI_F32: return launch_phased<E_F32, NT, false>(p, stream, "rf_gemm_f16");
+                case RF_EPI_ADD_F32: return launch_phased<E_ADD, NT, false>(p, stream, "rf_gemm_f16");
+                default: return launch_phased<E_SWIGLU, NT, false>(p, stream, "rf_gemm_f16");
+            }
+        }
+        if (cfg == 1282) {
+            switch (epilogue) {
+                case RF_EPI_BF16: return launch_phased<E_BF16, NT, false, 128>(p, stream, "rf_gemm_f16");
+                case RF_EPI_F32: return launch_phased<E_F32, NT, false, 128>(p, stream, "rf_gemm_f16");
+                case RF_EPI_ADD_F32: return launch_phased<E_ADD, NT, false, 128>(p, stream, "rf_gemm_f16");
+                default: return launch_phased<E_SWIGLU, NT, false, 128>(p, stream, "rf_gemm_f16");
+            }
+        }
+        if (cfg == 1283) return run_phased3<128, NT>(p, epilogue, stream);
+        if (cfg == 964) return run_phased3<96, NT>(p, epilogue, stream);
+        if (cfg == 645) return run_phased3<64, NT>(p, epilogue, stream);
+    }
+    if (cfg == 962 && p.n % 256 == 0) return run_dp_cfg<T96x256, NT>(p, epilogue, stream);
+    if (cfg == 12884 && p.k % 64 == 0) return run_dp_cfg<T128w8k2s4, NT>(p, epilogue, stream);
+    return run_dp_cfg<T128, NT>(p, epilogue, stream);
 }
 
 // cfg codes: 128 = T128, 256 = T256 (needs N % 256 == 0), 1284 / 1285 = 128x128 with a 4 / 5-stage ring,
@@ -2077,8 +2112,13 @@ extern "C" int64_t rf_gemm_workspace_bytes(void) { return SK_WS_BYTES; }
 
 static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
                      const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
-                     void* stream, const int* gate) {
+                     void* stream, const int* gate, bool f16 = false) {
     RF_REQUIRE(a && w && c, "rf_gemm_bf16: null pointer");
+    int out_f16 = 0;
+    if (epilogue == RF_EPI_F16 || epilogue == RF_EPI_SWIGLU_F16) {  // fp16 16-bit outputs
+        out_f16 = 1;
+        epilogue = epilogue == RF_EPI_F16 ? RF_EPI_BF16 : RF_EPI_SWIGLU;
+    }
     RF_REQUIRE(m > 0 && n > 0 && k > 0, "rf_gemm_bf16: empty problem m=%d n=%d k=%d", m, n, k);
     RF_REQUIRE(k % BK == 0, "rf_gemm_bf16: K=%d must be a multiple of %d", k, BK);
     RF_REQUIRE(n % 128 == 0, "rf_gemm_bf16: N=%d must be a multiple of 128", n);
@@ -2099,10 +2139,19 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
     p.ldc = ldc;
     p.bias = bias;
     p.gate = gate;
+    p.out_f16 = out_f16;
     if (workspace && ws_bytes >= SK_WS_BYTES && skph(m, n, k)) {
         sk_setup(p, workspace);
         const int64_t tiles = (int64_t)((m + 255) / 256) * (n / 256);
         p.persist = tiles % 256 == 0 && persist_on();  // whole tiles per block either way: prefetching form
+        if (f16) {
+            switch (epilogue) {
+                case RF_EPI_BF16: return launch_phased_sk<E_BF16, P_F16>(p, 256, stream, "rf_gemm_f16");
+                case RF_EPI_F32: return launch_phased_sk<E_F32, P_F16>(p, 256, stream, "rf_gemm_f16");
+                case RF_EPI_ADD_F32: return launch_phased_sk<E_ADD, P_F16>(p, 256, stream, "rf_gemm_f16");
+                default: return launch_phased_sk<E_SWIGLU, P_F16>(p, 256, stream, "rf_gemm_f16");
+            }
+        }
         switch (epilogue) {
             case RF_EPI_BF16: return launch_phased_sk<E_BF16>(p, 256, stream, "rf_gemm_bf16");
             case RF_EPI_F32: return launch_phased_sk<E_F32>(p, 256, stream, "rf_gemm_bf16");
@@ -2111,6 +2160,7 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
         }
     }
     const int cfg = pick_cfg(m, n, k, epilogue);
+    if (f16) return run_dp_f16(cfg, p, epilogue, stream);
     const bool big = cfg != 128;
     const int grid = (!big && workspace && ws_bytes >= SK_WS_BYTES) ? sk_grid(m, n, k) : 0;
     if (grid) {
@@ -2140,6 +2190,12 @@ extern "C" int rf_gemm_bf16(const void* a, int64_t lda, const void* w, int64_t l
                             const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
                             void* stream) {
     return gemm_bf16(a, lda, w, ldw, c, ldc, bias, m, n, k, epilogue, workspace, ws_bytes, stream, nullptr);
+}
+
+extern "C" int rf_gemm_f16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
+                           const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
+                           void* stream) {
+    return gemm_bf16(a, lda, w, ldw, c, ldc, bias, m, n, k, epilogue, workspace, ws_bytes, stream, nullptr, true);
 }
 
 extern "C" int rf_gemm_bf16_if(const int* flag, const void* a, int64_t lda, const void* w, int64_t ldw, void* c,

@@ -13,6 +13,11 @@ namespace {
 constexpr int ROWS_PER_BLOCK = 4;  // 4 waves, one row each
 
 // ----------------------------------------------------------------------------- RMSNorm
+// F16: the 16-bit output is fp16 (the A operand of an fp16 GEMM) instead of bf16
+template <bool F16>
+RF_DEV uint32_t pack_out(float lo, float hi) { return F16 ? pack_f16x2(lo, hi) : pack_bf16x2(lo, hi); }
+
+template <bool F16>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ x, int64_t ldx,
                                                       const float* __restrict__ w, float eps,
                                                       bf16_t* __restrict__ out, int64_t ldo, int rows, int dim) {
@@ -32,15 +37,15 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
         const float4 v = *reinterpret_cast<const float4*>(xr + c);
         const float4 g = *reinterpret_cast<const float4*>(w + c);
         uint2 pk;
-        pk.x = pack_bf16x2(v.x * inv * g.x, v.y * inv * g.y);
-        pk.y = pack_bf16x2(v.z * inv * g.z, v.w * inv * g.w);
+        pk.x = pack_out<F16>(v.x * inv * g.x, v.y * inv * g.y);
+        pk.y = pack_out<F16>(v.z * inv * g.z, v.w * inv * g.w);
         *reinterpret_cast<uint2*>(orow + c) = pk;
     }
 }
 
 // dim = 256 * NV: the whole row and its weights are loaded up front (NV float4 per lane each, all in
 // flight at once), so a row costs one memory round trip instead of one per 256 columns plus a re-read
-template <int NV>
+template <int NV, bool F16>
 __global__ __launch_bounds__(256) void rmsnorm_v_kernel(const float* __restrict__ x, int64_t ldx,
                                                         const float* __restrict__ w, float eps,
                                                         bf16_t* __restrict__ out, int64_t ldo, int rows) {
@@ -62,8 +67,8 @@ __global__ __launch_bounds__(256) void rmsnorm_v_kernel(const float* __restrict_
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
         uint2 pk;
-        pk.x = pack_bf16x2(v[i].x * inv * g[i].x, v[i].y * inv * g[i].y);
-        pk.y = pack_bf16x2(v[i].z * inv * g[i].z, v[i].w * inv * g[i].w);
+        pk.x = pack_out<F16>(v[i].x * inv * g[i].x, v[i].y * inv * g[i].y);
+        pk.y = pack_out<F16>(v[i].z * inv * g[i].z, v[i].w * inv * g[i].w);
         *reinterpret_cast<uint2*>(orow + 256 * i) = pk;
     }
 }
@@ -416,25 +421,39 @@ __global__ __launch_bounds__(256) void embed_v_kernel(float* __restrict__ out, i
 
 }  // namespace
 
-extern "C" int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, float eps, void* out, int64_t ldo,
-                          int rows, int dim, void* stream) {
-    RF_REQUIRE(x && weight && out, "rf_rmsnorm: null pointer");
-    RF_REQUIRE(dim % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0, "rf_rmsnorm: dim/ld must be multiples of 4");
+namespace {
+template <bool F16>
+int rmsnorm_launch(const float* x, int64_t ldx, const float* weight, float eps, void* out, int64_t ldo, int rows,
+                   int dim, void* stream, const char* what) {
+    RF_REQUIRE(x && weight && out, "%s: null pointer", what);
+    RF_REQUIRE(dim % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0, "%s: dim/ld must be multiples of 4", what);
     if (rows <= 0) return RF_OK;
     const dim3 grid((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK);
     hipStream_t st = (hipStream_t)stream;
     const bool al = ((uintptr_t)x & 15) == 0 && ((uintptr_t)weight & 15) == 0 && ((uintptr_t)out & 7) == 0;
     static const bool generic = getenv("RF_RMSNORM_GENERIC") && atoi(getenv("RF_RMSNORM_GENERIC"));  // A/B only
+    bf16_t* o = (bf16_t*)out;
     switch (al && !generic && dim % 256 == 0 ? dim / 256 : 0) {
-        case 2: RF_LAUNCH(rmsnorm_v_kernel<2>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
-        case 3: RF_LAUNCH(rmsnorm_v_kernel<3>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
-        case 4: RF_LAUNCH(rmsnorm_v_kernel<4>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
-        case 6: RF_LAUNCH(rmsnorm_v_kernel<6>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
-        case 8: RF_LAUNCH(rmsnorm_v_kernel<8>, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows); break;
+        case 2: RF_LAUNCH((rmsnorm_v_kernel<2, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows); break;
+        case 3: RF_LAUNCH((rmsnorm_v_kernel<3, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows); break;
+        case 4: RF_LAUNCH((rmsnorm_v_kernel<4, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows); break;
+        case 6: RF_LAUNCH((rmsnorm_v_kernel<6, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows); break;
+        case 8: RF_LAUNCH((rmsnorm_v_kernel<8, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows); break;
         default:
-            RF_LAUNCH(rmsnorm_kernel, grid, dim3(256), 0, st, x, ldx, weight, eps, (bf16_t*)out, ldo, rows, dim);
+            RF_LAUNCH(rmsnorm_kernel<F16>, grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows, dim);
     }
-    return rf::check_launch("rf_rmsnorm");
+    return rf::check_launch(what);
+}
+}  // namespace
+
+extern "C" int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, float eps, void* out, int64_t ldo,
+                          int rows, int dim, void* stream) {
+    return rmsnorm_launch<false>(x, ldx, weight, eps, out, ldo, rows, dim, stream, "rf_rmsnorm");
+}
+
+extern "C" int rf_rmsnorm_f16(const float* x, int64_t ldx, const float* weight, float eps, void* out, int64_t ldo,
+                              int rows, int dim, void* stream) {
+    return rmsnorm_launch<true>(x, ldx, weight, eps, out, ldo, rows, dim, stream, "rf_rmsnorm_f16");
 }
 
 extern "C" int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t src_gstride, void* dst, int64_t ld_dst,

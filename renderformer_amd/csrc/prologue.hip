@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256) void texture_linear_kernel(const float* __rest
 // NeRFEncoding(in_dim=9, L, include_input) (nerf_encoding.py:76-84): [x, sin(x_d 2^l), sin(x_d 2^l + pi/2)]
 __global__ __launch_bounds__(256) void vn_encode_kernel(const float* __restrict__ vn, int64_t n_rows,
                                                         const int32_t* __restrict__ dst_row, int L,
-                                                        bf16_t* __restrict__ out, int64_t ldo) {
+                                                        bf16_t* __restrict__ out, int64_t ldo, int f16) {
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n_rows) return;
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void vn_encode_kernel(const float* __restrict_
             const float s = x[j / L] * exp2f((float)(j % L));
             val = (e - 9) < n_sin ? sinf(s) : sinf(s + 1.5707963267948966f);
         }
-        out[(int64_t)d * ldo + e] = f32_to_bf16(val);
+        out[(int64_t)d * ldo + e] = f32_to_16(val, f16);
     }
 }
 
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void vn_encode_kernel(const float* __restrict_
 // RayGenerator (ray_generator.py:31-50) + rearrange 'b (h p1) (w p2) c -> b (h w) (c p1 p2)'
 __global__ __launch_bounds__(256) void ray_tokens_kernel(const float* __restrict__ c2w, const float* __restrict__ fov,
                                                          int res, int patch, bf16_t* __restrict__ out,
-                                                         float* __restrict__ ray_pos) {
+                                                         float* __restrict__ ray_pos, int f16) {
     const int view = blockIdx.y;
     const int pix = blockIdx.x * blockDim.x + threadIdx.x;
     const float* m = c2w + view * 16;
@@ -183,13 +183,13 @@ __global__ __launch_bounds__(256) void ray_tokens_kernel(const float* __restrict
     const int pp = patch * patch;
     const int feat = (y % patch) * patch + (x % patch);
     bf16_t* o = out + ((int64_t)view * pw * pw + tok) * (3 * pp);
-    o[feat] = f32_to_bf16(r0);
-    o[pp + feat] = f32_to_bf16(r1);
-    o[2 * pp + feat] = f32_to_bf16(r2);
+    o[feat] = f32_to_16(r0, f16);
+    o[pp + feat] = f32_to_16(r1, f16);
+    o[2 * pp + feat] = f32_to_16(r2, f16);
 }
 
 __global__ __launch_bounds__(256) void patchify_rays_kernel(const float* __restrict__ rays, int res, int patch,
-                                                            bf16_t* __restrict__ out) {
+                                                            bf16_t* __restrict__ out, int f16) {
     const int view = blockIdx.y;
     const int pix = blockIdx.x * blockDim.x + threadIdx.x;
     if (pix >= res * res) return;
@@ -199,9 +199,9 @@ __global__ __launch_bounds__(256) void patchify_rays_kernel(const float* __restr
     const int tok = (y / patch) * pw + (x / patch);
     const int feat = (y % patch) * patch + (x % patch);
     bf16_t* o = out + ((int64_t)view * pw * pw + tok) * (3 * pp);
-    o[feat] = f32_to_bf16(r[0]);
-    o[pp + feat] = f32_to_bf16(r[1]);
-    o[2 * pp + feat] = f32_to_bf16(r[2]);
+    o[feat] = f32_to_16(r[0], f16);
+    o[pp + feat] = f32_to_16(r[1], f16);
+    o[2 * pp + feat] = f32_to_16(r[2], f16);
 }
 
 // ----------------------------------------------------------------------------- RoPE positions
@@ -389,34 +389,53 @@ extern "C" int rf_texture_linear(const float* coef, int64_t ldc, int rows, int c
     return rf::check_launch("rf_texture_linear");
 }
 
-extern "C" int rf_vn_encode(const float* vn, int64_t n_rows, const int32_t* dst_row, int n_freqs, void* out,
-                            int64_t ldo, void* stream) {
+extern "C" int rf_vn_encode_dt(const float* vn, int64_t n_rows, const int32_t* dst_row, int n_freqs, void* out,
+                               int64_t ldo, int out_dtype, void* stream) {
     RF_REQUIRE(vn && out, "rf_vn_encode: null pointer");
     RF_REQUIRE(ldo >= 9 * (2 * n_freqs + 1), "rf_vn_encode: ldo too small");
+    RF_REQUIRE(out_dtype == RF_DT_BF16 || out_dtype == RF_DT_F16, "rf_vn_encode: bad out_dtype");
     if (n_rows <= 0) return RF_OK;
     RF_LAUNCH(vn_encode_kernel, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, vn,
-                       n_rows, dst_row, n_freqs, (bf16_t*)out, ldo);
+                       n_rows, dst_row, n_freqs, (bf16_t*)out, ldo, (int)(out_dtype == RF_DT_F16));
     return rf::check_launch("rf_vn_encode");
+}
+
+extern "C" int rf_vn_encode(const float* vn, int64_t n_rows, const int32_t* dst_row, int n_freqs, void* out,
+                            int64_t ldo, void* stream) {
+    return rf_vn_encode_dt(vn, n_rows, dst_row, n_freqs, out, ldo, RF_DT_BF16, stream);
+}
+
+extern "C" int rf_ray_tokens_dt(const float* c2w, const float* fov_deg, int n_views, int res, int patch, void* out,
+                                float* ray_pos, int out_dtype, void* stream) {
+    RF_REQUIRE(c2w && fov_deg && out, "rf_ray_tokens: null pointer");
+    RF_REQUIRE(res % patch == 0, "rf_ray_tokens: resolution %d not divisible by patch %d", res, patch);
+    RF_REQUIRE(out_dtype == RF_DT_BF16 || out_dtype == RF_DT_F16, "rf_ray_tokens: bad out_dtype");
+    if (n_views <= 0) return RF_OK;
+    dim3 grid((res * res + 255) / 256, n_views);
+    RF_LAUNCH(ray_tokens_kernel, grid, dim3(256), 0, (hipStream_t)stream, c2w, fov_deg, res, patch,
+                       (bf16_t*)out, ray_pos, (int)(out_dtype == RF_DT_F16));
+    return rf::check_launch("rf_ray_tokens");
 }
 
 extern "C" int rf_ray_tokens(const float* c2w, const float* fov_deg, int n_views, int res, int patch, void* out,
                              float* ray_pos, void* stream) {
-    RF_REQUIRE(c2w && fov_deg && out, "rf_ray_tokens: null pointer");
-    RF_REQUIRE(res % patch == 0, "rf_ray_tokens: resolution %d not divisible by patch %d", res, patch);
+    return rf_ray_tokens_dt(c2w, fov_deg, n_views, res, patch, out, ray_pos, RF_DT_BF16, stream);
+}
+
+extern "C" int rf_patchify_rays_dt(const float* rays_d, int n_views, int res, int patch, void* out, int out_dtype,
+                                   void* stream) {
+    RF_REQUIRE(rays_d && out, "rf_patchify_rays: null pointer");
+    RF_REQUIRE(res % patch == 0, "rf_patchify_rays: resolution %d not divisible by patch %d", res, patch);
+    RF_REQUIRE(out_dtype == RF_DT_BF16 || out_dtype == RF_DT_F16, "rf_patchify_rays: bad out_dtype");
     if (n_views <= 0) return RF_OK;
     dim3 grid((res * res + 255) / 256, n_views);
-    RF_LAUNCH(ray_tokens_kernel, grid, dim3(256), 0, (hipStream_t)stream, c2w, fov_deg, res, patch,
-                       (bf16_t*)out, ray_pos);
-    return rf::check_launch("rf_ray_tokens");
+    RF_LAUNCH(patchify_rays_kernel, grid, dim3(256), 0, (hipStream_t)stream, rays_d, res, patch, (bf16_t*)out,
+              (int)(out_dtype == RF_DT_F16));
+    return rf::check_launch("rf_patchify_rays");
 }
 
 extern "C" int rf_patchify_rays(const float* rays_d, int n_views, int res, int patch, void* out, void* stream) {
-    RF_REQUIRE(rays_d && out, "rf_patchify_rays: null pointer");
-    RF_REQUIRE(res % patch == 0, "rf_patchify_rays: resolution %d not divisible by patch %d", res, patch);
-    if (n_views <= 0) return RF_OK;
-    dim3 grid((res * res + 255) / 256, n_views);
-    RF_LAUNCH(patchify_rays_kernel, grid, dim3(256), 0, (hipStream_t)stream, rays_d, res, patch, (bf16_t*)out);
-    return rf::check_launch("rf_patchify_rays");
+    return rf_patchify_rays_dt(rays_d, n_views, res, patch, out, RF_DT_BF16, stream);
 }
 
 extern "C" int rf_scene_pos(const float* tris, const int32_t* valid_idx, const int32_t* scene_off, const float* c2w,

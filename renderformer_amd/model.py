@@ -42,6 +42,9 @@ def _f32(t, device):
     return t.to(device=device, dtype=torch.float32).contiguous()
 
 
+OPERANDS = {"f16": torch.float16, "bf16": torch.bfloat16}  # 16-bit MFMA operand formats of the projections
+
+
 def _interleave_swiglu(w1: torch.Tensor, w3: torch.Tensor) -> torch.Tensor:
     """[F, D] x2 -> [2F, D] in 16-row groups (w1 block g, w3 block g) for the SwiGLU GEMM epilogue."""
     f, d = w1.shape
@@ -55,13 +58,18 @@ class _Layer:
 class _DeviceWeights:
     """Weights packed for the kernels: bf16 GEMM operands, fp32 norms/biases/tokens."""
 
-    def __init__(self, cfg: RenderFormerConfig, sd: Dict[str, torch.Tensor], device, dpt_precision: str = "f16"):
+    def __init__(self, cfg: RenderFormerConfig, sd: Dict[str, torch.Tensor], device, dpt_precision: str = "f16",
+                 operands: str = "f16"):
         d = cfg.latent_dim
+        # projection GEMM operands (weights, and the activations that feed them: RMSNorm outputs, attention
+        # outputs, SwiGLU outputs): fp16 by default; q/k/v of the attention kernels stay bf16
+        self.half = OPERANDS[operands]
+        hw = lambda t: t.to(device=device, dtype=self.half).contiguous()  # noqa: E731
         self.tri_token = _f32(sd["tri_token"].reshape(-1), device)
         self.reg_tokens = _f32(sd["reg_tokens"].reshape(cfg.num_register_tokens, d), device)
         vn_w = sd["vn_encoding_proj.weight"]
         self.vn_k = ((vn_w.shape[1] + 63) // 64) * 64
-        self.vn_w = _bf16(torch.nn.functional.pad(vn_w, (0, self.vn_k - vn_w.shape[1])), device)
+        self.vn_w = hw(torch.nn.functional.pad(vn_w, (0, self.vn_k - vn_w.shape[1])))
         self.vn_b = _f32(sd["vn_encoding_proj.bias"], device)
         self.vn_norm = _f32(sd["vn_encoder_norm.weight"], device)
         self.tex_w = _bf16(sd["texture_encoder.weight"], device)
@@ -85,18 +93,18 @@ class _DeviceWeights:
         for i in range(cfg.num_layers):
             p = f"transformer.layers.{i}."
             L = _Layer()
-            L.w_in = _bf16(sd[p + "multihead_attn.in_proj.weight"], device)
-            L.w_out = _bf16(sd[p + "multihead_attn.out_proj.weight"], device)
+            L.w_in = hw(sd[p + "multihead_attn.in_proj.weight"])
+            L.w_out = hw(sd[p + "multihead_attn.out_proj.weight"])
             L.qk_norm = _f32(torch.cat([sd[p + "multihead_attn.q_norm.weight"], sd[p + "multihead_attn.k_norm.weight"]]),
                              device)
             L.query_norm = _f32(sd[p + "query_norm.weight"], device)
-            L.w13 = _bf16(_interleave_swiglu(sd[p + "ffn.w1.weight"], sd[p + "ffn.w3.weight"]), device)
-            L.w2 = _bf16(sd[p + "ffn.w2.weight"], device)
+            L.w13 = hw(_interleave_swiglu(sd[p + "ffn.w1.weight"], sd[p + "ffn.w3.weight"]))
+            L.w2 = hw(sd[p + "ffn.w2.weight"])
             L.ffn_norm = _f32(sd[p + "ffn_norm.weight"], device)
             self.enc.append(L)
         vt = "view_transformer."
         self.patch_token = _f32(sd[vt + "ray_map_patch_token"].reshape(-1), device)
-        self.ray_w = _bf16(sd[vt + "ray_map_encoder.weight"], device)
+        self.ray_w = hw(sd[vt + "ray_map_encoder.weight"])
         self.ray_b = _f32(sd[vt + "ray_map_encoder.bias"], device)
         self.ray_norm = _f32(sd[vt + "ray_map_encoder_norm.weight"], device)
         self.dec_freqs = _f32(sd[vt + "transformer.rope_emb.freqs"], device)
@@ -105,21 +113,21 @@ class _DeviceWeights:
             p = f"{vt}transformer.layers.{i}."
             a = p + "multihead_attn."
             L = _Layer()
-            L.wq = _bf16(sd[a + "q_proj.weight"], device)
-            L.wkv = _bf16(torch.cat([sd[a + "k_proj.weight"], sd[a + "v_proj.weight"]], 0), device)
-            L.wo = _bf16(sd[a + "out_proj.weight"], device)
+            L.wq = hw(sd[a + "q_proj.weight"])
+            L.wkv = hw(torch.cat([sd[a + "k_proj.weight"], sd[a + "v_proj.weight"]], 0))
+            L.wo = hw(sd[a + "out_proj.weight"])
             L.q_norm = _f32(sd[a + "q_norm.weight"], device)
             L.k_norm = _f32(sd[a + "k_norm.weight"], device)
             L.query_norm = _f32(sd[p + "query_norm.weight"], device)
             L.kv_norm = _f32(sd[p + "kv_norm.weight"], device)
             if cfg.view_transformer_include_self_attn:
                 s = p + "self_attn."
-                L.ws_in = _bf16(sd[s + "in_proj.weight"], device)
-                L.ws_out = _bf16(sd[s + "out_proj.weight"], device)
+                L.ws_in = hw(sd[s + "in_proj.weight"])
+                L.ws_out = hw(sd[s + "out_proj.weight"])
                 L.sqk_norm = _f32(torch.cat([sd[s + "q_norm.weight"], sd[s + "k_norm.weight"]]), device)
                 L.self_norm = _f32(sd[p + "self_attn_norm.weight"], device)
-            L.w13 = _bf16(_interleave_swiglu(sd[p + "ffn.w1.weight"], sd[p + "ffn.w3.weight"]), device)
-            L.w2 = _bf16(sd[p + "ffn.w2.weight"], device)
+            L.w13 = hw(_interleave_swiglu(sd[p + "ffn.w1.weight"], sd[p + "ffn.w3.weight"]))
+            L.w2 = hw(sd[p + "ffn.w2.weight"])
             L.ffn_norm = _f32(sd[p + "ffn_norm.weight"], device)
             self.dec.append(L)
         # Cross-attention K/V of every decoder layer in ONE GEMM (their input, the stage-1 output, is the same
@@ -132,7 +140,7 @@ class _DeviceWeights:
             a = p + "multihead_attn."
             w = torch.cat([sd[a + "k_proj.weight"], sd[a + "v_proj.weight"]], 0).float()
             wkv_all.append(w * sd[p + "kv_norm.weight"].float()[None, :])
-        self.wkv_all = _bf16(torch.cat(wkv_all, 0), device)
+        self.wkv_all = hw(torch.cat(wkv_all, 0))
         # every layer's k_norm weight, for the one-launch key rotation of all layers (ops.qk_norm_rope_groups)
         self.k_norm_all = _f32(torch.cat([sd[f"{vt}transformer.layers.{i}.multihead_attn.k_norm.weight"]
                                           for i in range(cfg.view_transformer_n_layers)]), device)
@@ -256,7 +264,7 @@ class RenderFormer:
 
     def __init__(self, config: RenderFormerConfig, state_dict: Optional[Dict[str, torch.Tensor]] = None,
                  seed: int = 0, dpt_precision: Optional[str] = None, fp8: Optional[bool] = None,
-                 view_chunk: Optional[int] = None):
+                 view_chunk: Optional[int] = None, operands: Optional[str] = None):
         self.config = config
         # render_views: stage 2 + DPT over at most view_chunk views per pass (stage 1 once per scene); None = all
         # views of the batch in one pass.  A fixed chunk makes each view's image independent of the batching.
@@ -269,6 +277,14 @@ class RenderFormer:
         self.fp8_projections = set(os.environ.get("RF_FP8_PROJ", ",".join(FP8_PROJECTIONS)).split(","))
         # DPT operand precision (dpt.py): "f16" (default) or "bf16x3"; RF_DPT_PRECISION overrides the default
         self.dpt_precision = dpt_precision or os.environ.get("RF_DPT_PRECISION", "f16")
+        # 16-bit operands of the transformer projections (OPERANDS): fp16 by default (11-bit mantissa at the bf16
+        # MFMA rate: ~7x less rounding error end to end, tools/precision_budget.py); "bf16" (RF_OPERANDS=bf16)
+        # for checkpoints whose activations exceed fp16's range.  The fp8 mode quantises bf16 activations.
+        self.operands = operands or os.environ.get("RF_OPERANDS", "bf16" if self.fp8 else "f16")
+        if self.operands not in OPERANDS:
+            raise ValueError(f"operands must be one of {tuple(OPERANDS)}")
+        if self.fp8 and self.operands != "bf16":
+            raise ValueError("the fp8 mode quantises bf16 activations: operands must be 'bf16'")
         if self.dpt_precision not in DPT_PRECISIONS:
             raise ValueError(f"dpt_precision must be one of {DPT_PRECISIONS}")
         cfg = config
@@ -312,7 +328,7 @@ class RenderFormer:
         self._sd = {k: v.detach().float().cpu() for k, v in sd.items()}
         if self._w is not None:
             with torch.cuda.device(self._device):
-                self._w = _DeviceWeights(self.config, self._sd, self._device, self.dpt_precision)
+                self._w = _DeviceWeights(self.config, self._sd, self._device, self.dpt_precision, self.operands)
         return self
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
@@ -330,7 +346,7 @@ class RenderFormer:
             device = torch.device("cuda", torch.cuda.current_device())
         self._device = device
         with torch.cuda.device(device):
-            self._w = _DeviceWeights(self.config, self._sd, device, self.dpt_precision)
+            self._w = _DeviceWeights(self.config, self._sd, device, self.dpt_precision, self.operands)
         return self
 
     cuda = lambda self, i=None: self.to("cuda" if i is None else f"cuda:{i}")  # noqa: E731
@@ -403,7 +419,7 @@ class RenderFormer:
             ops.texture_pack(texture, log_ch, plan.dst_row, tex_in)
             if plan.T_tri:
                 ops.gemm(tex_in, W.tex_w, tex_lin, W.tex_b, ops.EPI_F32)
-        vn_in = torch.empty(plan.T_tri, W.vn_k, dtype=torch.bfloat16, device=dev)
+        vn_in = torch.empty(plan.T_tri, W.vn_k, dtype=W.half, device=dev)
         ops.vn_encode(vns, plan.dst_row, cfg.vn_pe_num_freqs, vn_in)
         vn_lin = torch.empty(plan.T_tri, D, dtype=torch.float32, device=dev)
         if plan.T_tri:
@@ -419,10 +435,10 @@ class RenderFormer:
         cfg, W, dev = self.config, self._w, self._device
         D, H, F = cfg.latent_dim, cfg.num_heads, cfg.dim_feedforward
         T = plan.T1
-        h = torch.empty(T, D, dtype=torch.bfloat16, device=dev)
-        qkv = torch.empty(T, 3 * D, dtype=torch.bfloat16, device=dev)
-        att = torch.empty(T, D, dtype=torch.bfloat16, device=dev)
-        g = torch.empty(T, F, dtype=torch.bfloat16, device=dev)
+        h = torch.empty(T, D, dtype=W.half, device=dev)      # GEMM operands: W.half (fp16 by default)
+        qkv = torch.empty(T, 3 * D, dtype=torch.bfloat16, device=dev)  # attention operands: bf16
+        att = torch.empty(T, D, dtype=W.half, device=dev)
+        g = torch.empty(T, F, dtype=W.half, device=dev)
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
         qk_pair = qkv[:, :2 * D]
         for L in W.enc:
@@ -450,11 +466,11 @@ class RenderFormer:
         D, H, F = cfg.view_transformer_latent_dim, cfg.view_transformer_n_heads, cfg.view_transformer_ffn_hidden_dim
         T2, R, P = x.shape[0], plan.R, plan.B * plan.V
         qk = cfg.qk_norm
-        h = torch.empty(T2, D, dtype=torch.bfloat16, device=dev)
+        h = torch.empty(T2, D, dtype=W.half, device=dev)
         q2 = torch.empty(T2, D, dtype=torch.bfloat16, device=dev)
-        att = torch.empty(T2, D, dtype=torch.bfloat16, device=dev)
-        g = torch.empty(T2, F, dtype=torch.bfloat16, device=dev)
-        hc = torch.empty(plan.T1, ctx.shape[1], dtype=torch.bfloat16, device=dev)
+        att = torch.empty(T2, D, dtype=W.half, device=dev)
+        g = torch.empty(T2, F, dtype=W.half, device=dev)
+        hc = torch.empty(plan.T1, ctx.shape[1], dtype=W.half, device=dev)
         n_dec = len(W.dec)
         # all layers' K/V in one GEMM (see _DeviceWeights.wkv_all) unless RF_KV_BATCH=0 or it would exceed 4 GiB
         kv_batch = (os.environ.get("RF_KV_BATCH", "1") != "0" and plan.T1 * n_dec * 2 * D * 2 <= (4 << 30))
@@ -612,7 +628,7 @@ class RenderFormer:
         c2w_v = c2w.reshape(P, 4, 4).float().contiguous()
         eye = torch.eye(4, dtype=torch.float32, device=dev).expand(P, 4, 4).contiguous()
         rays_c2w, pos_c2w = (eye, c2w_v) if cfg.turn_to_cam_coord else (c2w_v, eye)
-        ray_in = torch.empty(P * plan.R, 3 * cfg.patch_size ** 2, dtype=torch.bfloat16, device=dev)
+        ray_in = torch.empty(P * plan.R, 3 * cfg.patch_size ** 2, dtype=self._w.half, device=dev)
         ray_pos = torch.empty(P, 9, dtype=torch.float32, device=dev)
         ops.ray_tokens(rays_c2w, fov.reshape(P).float().contiguous(), resolution, cfg.patch_size, ray_in, ray_pos)
         x2 = self._ray_embed(plan, ray_in)
@@ -643,7 +659,7 @@ class RenderFormer:
                       max(plan.counts))
         x1 = self._stage1(plan, x1, pos1)
         P = B * V
-        ray_in = torch.empty(P * plan.R, 3 * cfg.patch_size ** 2, dtype=torch.bfloat16, device=dev)
+        ray_in = torch.empty(P * plan.R, 3 * cfg.patch_size ** 2, dtype=self._w.half, device=dev)
         ops.patchify_rays(rays_d.reshape(P, res, res, 3).float().contiguous(), cfg.patch_size, ray_in)
         ray_pos = rays_o.reshape(P, 1, 3).float().expand(P, 3, 3).reshape(P, 9).contiguous()
         x2 = self._ray_embed(plan, ray_in)

@@ -16,6 +16,9 @@ import torch
 from ._lib import call, load, ptr, stream
 
 EPI_BF16, EPI_F32, EPI_ADD_F32, EPI_SWIGLU = 0, 1, 2, 3
+_EPI_F16, _EPI_SWIGLU_F16 = 4, 5  # rf.h: the 16-bit epilogues with an fp16 C (chosen from out.dtype)
+DT_BF16, DT_F16 = 0, 1
+HALF = (torch.bfloat16, torch.float16)  # 16-bit operand formats of the MFMA path
 FLT_EPS = float(torch.finfo(torch.float32).eps)  # nn.RMSNorm(eps=None) on fp32 inputs
 CUS = 256  # MI355X compute units
 
@@ -92,25 +95,34 @@ def clear_device_error() -> None:
 
 def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias: Optional[torch.Tensor] = None,
          epilogue: int = EPI_BF16, tag: Optional[str] = None, flag: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out (epilogue)= a @ w.T ; a [M,K] bf16, w [N,K] bf16.  With ``flag`` (int32 device scalar) the HIP engine
-    runs it and the launch is a no-op unless the flag is non-zero when it runs (rf_gemm_bf16_if)."""
-    _dev(a, torch.bfloat16, "a")
-    _dev(w, torch.bfloat16, "w")
+    """out (epilogue)= a @ w.T ; a [M,K], w [N,K] both bf16 (rf_gemm_bf16) or both fp16 (rf_gemm_f16).  The
+    16-bit epilogues (EPI_BF16, EPI_SWIGLU) write out's dtype (bf16 or fp16).  With ``flag`` (int32 device
+    scalar; bf16 only) the launch is a no-op unless the flag is non-zero when it runs (rf_gemm_bf16_if)."""
+    _check(a.dtype in HALF and w.dtype == a.dtype, f"gemm: a/w must both be bf16 or both fp16 ({a.dtype}, {w.dtype})")
+    _dev(a, a.dtype, "a")
+    _dev(w, w.dtype, "w")
     m, k = a.shape
     n, k2 = w.shape
     _check(k == k2, f"gemm: K mismatch {k} vs {k2}")
-    want = torch.bfloat16 if epilogue in (EPI_BF16, EPI_SWIGLU) else torch.float32
-    _dev(out, want, "out")
+    if epilogue in (EPI_BF16, EPI_SWIGLU):
+        _check(out.dtype in HALF, "gemm: 16-bit epilogue needs a bf16 or fp16 out")
+        _dev(out, out.dtype, "out")
+    else:
+        _dev(out, torch.float32, "out")
     ncols = n // 2 if epilogue == EPI_SWIGLU else n
     _check(out.shape[0] == m and out.shape[1] == ncols, f"gemm: out shape {tuple(out.shape)} != ({m}, {ncols})")
     if bias is not None:
         _dev(bias, torch.float32, "bias")
     ws = _gemm_workspace(a.device)
+    epi = epilogue
+    if out.dtype == torch.float16:
+        epi = _EPI_F16 if epilogue == EPI_BF16 else _EPI_SWIGLU_F16
     _t0(tag)
     if flag is None:
-        call("rf_gemm_bf16", ptr(a), a.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), ptr(bias), m, n, k,
-             epilogue, ptr(ws), ws.numel(), stream())
+        call("rf_gemm_f16" if a.dtype == torch.float16 else "rf_gemm_bf16", ptr(a), a.stride(0), ptr(w), w.stride(0),
+             ptr(out), out.stride(0), ptr(bias), m, n, k, epi, ptr(ws), ws.numel(), stream())
     else:
+        _check(a.dtype == torch.bfloat16 and out.dtype != torch.float16, "gemm: the gated form is bf16 only")
         _dev(flag, torch.int32, "flag")
         call("rf_gemm_bf16_if", ptr(flag), ptr(a), a.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0),
              ptr(bias), m, n, k, epilogue, ptr(ws), ws.numel(), stream())
@@ -186,10 +198,13 @@ def mx8_quant_ref(x: torch.Tensor):
 
 
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor) -> torch.Tensor:
+    """out (bf16 or fp16, the next GEMM's operand format) = RMSNorm(x f32) * w."""
     _dev(x, torch.float32, "x")
-    _dev(out, torch.bfloat16, "out")
+    _check(out.dtype in HALF, "rmsnorm: out must be bf16 or fp16")
+    _dev(out, out.dtype, "out")
     _check(x.shape == out.shape and w.numel() == x.shape[1], "rmsnorm: shape mismatch")
-    call("rf_rmsnorm", ptr(x), x.stride(0), ptr(w), eps, ptr(out), out.stride(0), x.shape[0], x.shape[1], stream())
+    call("rf_rmsnorm_f16" if out.dtype == torch.float16 else "rf_rmsnorm", ptr(x), x.stride(0), ptr(w), eps, ptr(out),
+         out.stride(0), x.shape[0], x.shape[1], stream())
     return out
 
 
@@ -306,8 +321,10 @@ def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int
     workgroup ranges of `schedule` (attn_schedule of the same problems and heads) when given;
     n_split >= 1: the legacy per-unit kernel with flash-decoding splits + rf_attn_combine.
     q_prescaled: q already carries scale*log2(e) (qk_norm_rope q_scale=Q_LOG2_SCALE)."""
-    for t, nme in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
+    for t, nme in ((q, "q"), (k, "k"), (v, "v")):
         _dev(t, torch.bfloat16, nme)
+    _check(out.dtype in HALF, "attention: out must be bf16 or fp16")
+    _dev(out, out.dtype, "out")
     _dev(problems, torch.int32, "problems")
     _check(problems.dim() == 2 and problems.shape[1] == 5, "attention: problems must be [P, 5]")
     hd = q.shape[1] // n_heads
@@ -325,12 +342,15 @@ def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int
         nbytes = load().rf_attn_workspace_bytes(rows, n_heads, n_split)
         ws = torch.empty(nbytes // 4, dtype=torch.float32, device=out.device)
     _t0(tag)
-    if n_split == 0 and schedule is not None:
-        _dev(schedule, torch.int64, "schedule")
-        call("rf_attn_fwd_sched", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
-             out.stride(0), ptr(problems), problems.shape[0], n_heads, hd, scale, ptr(ws), ptr(schedule),
-             schedule.numel() - 1, stream())
+    if n_split == 0:
+        if schedule is not None:
+            _dev(schedule, torch.int64, "schedule")
+        call("rf_attn_fwd_sk", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+             out.stride(0), DT_F16 if out.dtype == torch.float16 else DT_BF16, ptr(problems), problems.shape[0],
+             n_heads, hd, scale, ptr(ws), ptr(schedule), schedule.numel() - 1 if schedule is not None else 0,
+             stream())
         return out
+    _check(out.dtype == torch.bfloat16, "attention: the legacy split kernels write bf16")
     call("rf_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out), out.stride(0),
          ptr(problems), problems.shape[0], max_q_len, n_heads, hd, scale, n_split, ptr(ws), rows, stream())
     if n_split > 1:
@@ -340,11 +360,14 @@ def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int
 
 def swin_attention(q, k, v, out, n_images: int, grid_h: int, grid_w: int, shift: int, n_heads: int,
                    window: int = 8, q_prescaled: bool = False) -> torch.Tensor:
-    for t, nme in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
+    for t, nme in ((q, "q"), (k, "k"), (v, "v")):
         _dev(t, torch.bfloat16, nme)
+    _check(out.dtype in HALF, "swin_attention: out must be bf16 or fp16")
+    _dev(out, out.dtype, "out")
     hd = q.shape[1] // n_heads
-    call("rf_swin_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out), out.stride(0),
-         n_images, grid_h, grid_w, window, shift, n_heads, hd, LN2 if q_prescaled else 1.0 / math.sqrt(hd), stream())
+    call("rf_swin_attn_fwd_dt", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+         out.stride(0), DT_F16 if out.dtype == torch.float16 else DT_BF16, n_images, grid_h, grid_w, window, shift,
+         n_heads, hd, LN2 if q_prescaled else 1.0 / math.sqrt(hd), stream())
     return out
 
 
@@ -408,10 +431,16 @@ def texture_linear(coef: torch.Tensor, wsum: torch.Tensor, bias: Optional[torch.
     return out
 
 
+def _dt(out: torch.Tensor) -> int:
+    _check(out.dtype in HALF, "16-bit output must be bf16 or fp16")
+    return DT_F16 if out.dtype == torch.float16 else DT_BF16
+
+
 def vn_encode(vn: torch.Tensor, dst_row: torch.Tensor, n_freqs: int, out: torch.Tensor):
     _dev(vn, torch.float32, "vn")
     _check(vn.is_contiguous() and vn.shape[-1] == 9, "vn must be contiguous [..., 9]")
-    call("rf_vn_encode", ptr(vn), vn.numel() // 9, ptr(dst_row), n_freqs, ptr(out), out.stride(0), stream())
+    call("rf_vn_encode_dt", ptr(vn), vn.numel() // 9, ptr(dst_row), n_freqs, ptr(out), out.stride(0), _dt(out),
+         stream())
     return out
 
 
@@ -419,7 +448,8 @@ def ray_tokens(c2w: torch.Tensor, fov_deg: torch.Tensor, res: int, patch: int, o
                ray_pos: torch.Tensor):
     _dev(c2w, torch.float32, "c2w")
     _check(c2w.is_contiguous() and fov_deg.is_contiguous(), "c2w/fov must be contiguous")
-    call("rf_ray_tokens", ptr(c2w), ptr(fov_deg), c2w.numel() // 16, res, patch, ptr(out), ptr(ray_pos), stream())
+    call("rf_ray_tokens_dt", ptr(c2w), ptr(fov_deg), c2w.numel() // 16, res, patch, ptr(out), ptr(ray_pos), _dt(out),
+         stream())
     return out
 
 
@@ -428,7 +458,8 @@ def patchify_rays(rays_d: torch.Tensor, patch: int, out: torch.Tensor):
     _check(rays_d.is_contiguous() and rays_d.shape[-1] == 3 and rays_d.shape[-2] == rays_d.shape[-3],
            "rays_d must be contiguous [*, res, res, 3]")
     res = rays_d.shape[-2]
-    call("rf_patchify_rays", ptr(rays_d), rays_d.numel() // (res * res * 3), res, patch, ptr(out), stream())
+    call("rf_patchify_rays_dt", ptr(rays_d), rays_d.numel() // (res * res * 3), res, patch, ptr(out), _dt(out),
+         stream())
     return out
 
 

@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load(require_device=False)
     for fn in header_functions():
         assert hasattr(lib, fn), fn
-    assert lib.rf_abi_version() == 9
+    assert lib.rf_abi_version() == 10
     # every int-returning entry point has a ctypes signature in the binding
     assert set(_lib.SIGNATURES) == set(header_functions()) - {"rf_last_error", "rf_abi_version",
                                                                "rf_attn_workspace_bytes", "rf_gemm_workspace_bytes",
@@ -245,7 +245,8 @@ def test_integration_binding_parses():
 def test_integration_binding_runs_against_reference_attention():
     """Execute INTEGRATION.md's reference-side binding verbatim (only the library path filled in) the way the
     reference's attention switch would call it — flash_attn's qkv-packed varlen layout [T, 3, H, 128] with
-    cu_seqlens — and compare with the fp64 softmax attention of every sequence."""
+    cu_seqlens (stage 1), and the kv-packed layout q [Tq, H, 128] / kv [Tk, 2, H, 128] with cu_seqlens_q /
+    cu_seqlens_k (stage-2 cross-attention, attention.py:183-198) — against fp64 softmax attention."""
     import math
     import torch
     from renderformer_amd import _lib
@@ -268,3 +269,20 @@ def test_integration_binding_runs_against_reference_attention():
         ref = torch.einsum("hqk,khd->qhd", torch.softmax(s, -1), v[a:b])
         err = ((o[a:b].double() - ref).norm() / ref.norm()).item()
         assert err < 6e-3, (a, b, err)
+    # the kv-packed binding: stage-2 cross-attention, 3 "views" of 256 rays over scenes of ragged lengths
+    Hc, R = 8, 256
+    klens = [700, 77, 1300]
+    cuq = torch.arange(0, R * (len(klens) + 1), R, dtype=torch.int32, device="cuda")
+    cuk = torch.tensor([0] + list(torch.tensor(klens).cumsum(0)), dtype=torch.int32, device="cuda")
+    qc = torch.randn(R * len(klens), Hc, hd, generator=g).bfloat16().cuda()
+    kv = torch.randn(sum(klens), 2, Hc, hd, generator=g).bfloat16().cuda()
+    oc = ns["rfhip_varlen_kvpacked"](qc, kv, cuq, cuk, R, max(klens))
+    torch.cuda.synchronize()
+    assert oc.shape == qc.shape
+    oc, qd, kd, vd = oc.float().cpu(), qc.double().cpu(), kv[:, 0].double().cpu(), kv[:, 1].double().cpu()
+    for i in range(len(klens)):
+        a, b, c0, c1 = cuq[i].item(), cuq[i + 1].item(), cuk[i].item(), cuk[i + 1].item()
+        s = torch.einsum("qhd,khd->hqk", qd[a:b], kd[c0:c1]) / math.sqrt(hd)
+        ref = torch.einsum("hqk,khd->qhd", torch.softmax(s, -1), vd[c0:c1])
+        err = ((oc[a:b].double() - ref).norm() / ref.norm()).item()
+        assert err < 6e-3, (i, err)

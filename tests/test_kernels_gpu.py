@@ -130,6 +130,91 @@ def test_gemm_256_tiles(monkeypatch, tile, m, n, k):
     assert relerr(outs.float(), refs) < 5e-3
 
 
+F16_TILES = {"auto": None, "256ph": "256", "128x256ph": "1282", "96x256ph3": "964", "64x256ph3": "645",
+             "128x256ph3": "1283", "96x256ring": "962", "128ring8wk64": "12884", "128ring": "128", "skph": "skph"}
+
+
+@pytest.mark.parametrize("tile", list(F16_TILES))
+@pytest.mark.parametrize("m,n,k", [(1, 256, 64), (777, 256, 192), (5649, 3072, 1024), (4096, 1024, 4096),
+                                   (5649, 1024, 1024), (4096, 8192, 1024)])
+def test_gemm_f16_operands(monkeypatch, tile, m, n, k):
+    """rf_gemm_f16 (fp16 A and W, fp16 MFMAs) on every loop the cost model can pick, every epilogue incl. the
+    fp16 outputs (RF_EPI_F16, RF_EPI_SWIGLU_F16) and the bf16 one, vs fp64 of the same fp16 operands."""
+    ops = _ops()
+    if F16_TILES[tile] == "skph":
+        if (m + 255) // 256 * (n // 256) < 512:
+            pytest.skip("the phased stream-K path needs >= 512 whole 256x256 tiles")
+        monkeypatch.setenv("RF_GEMM_SKPH", "1")
+    elif F16_TILES[tile]:
+        monkeypatch.setenv("RF_GEMM_TILE", F16_TILES[tile])
+    g = torch.Generator(device="cpu").manual_seed(m + 5 * n + k)
+    a = torch.randn(m, k, generator=g).half().to(dev)
+    w = (torch.randn(n, k, generator=g) / math.sqrt(k)).half().to(dev)
+    bias = torch.randn(n, generator=g).to(dev)
+    ref = a.double() @ w.double().t() + bias.double()
+    out = torch.empty(m, n, device=dev)
+    ops.gemm(a, w, out, bias, ops.EPI_F32)
+    assert relerr(out, ref) < 1e-5
+    acc = torch.randn(m, n, generator=g).to(dev)
+    ref2 = acc.double() + ref
+    ops.gemm(a, w, acc, bias, ops.EPI_ADD_F32)
+    assert relerr(acc, ref2) < 1e-5
+    for dt, tol in ((torch.float16, 6e-4), (torch.bfloat16, 4e-3)):
+        o16 = torch.empty(m, n, device=dev, dtype=dt)
+        ops.gemm(a, w, o16, bias, ops.EPI_BF16)
+        assert relerr(o16.float(), ref) < tol, dt
+    from renderformer_amd.model import _interleave_swiglu
+    refs = F.silu(a.double() @ w[: n // 2].double().t()) * (a.double() @ w[n // 2:].double().t())
+    for dt, tol in ((torch.float16, 8e-4), (torch.bfloat16, 5e-3)):
+        outs = torch.empty(m, n // 2, device=dev, dtype=dt)
+        ops.gemm(a, _interleave_swiglu(w[: n // 2].cpu(), w[n // 2:].cpu()).to(dev), outs, None, ops.EPI_SWIGLU)
+        assert relerr(outs.float(), refs) < tol, dt
+
+
+def test_rmsnorm_f16_and_attention_f16_out():
+    """The fp16-output forms feeding fp16 GEMMs: rf_rmsnorm_f16, and the stream-K / Swin attention writing O as
+    fp16 (q/k/v bf16): the same values as the bf16-output launches up to the output rounding."""
+    ops = _ops()
+    x = torch.randn(333, 1024, device=dev) * 3
+    w = torch.rand(1024, device=dev) + 0.5
+    ref = F.rms_norm(x.double(), (1024,), w.double(), 1e-6)
+    out = torch.empty(333, 1024, device=dev, dtype=torch.float16)
+    ops.rmsnorm(x, w, 1e-6, out)
+    assert relerr(out.float(), ref) < 6e-4
+    H, D = 8, 1024
+    g = torch.Generator(device="cpu").manual_seed(5)
+    lens = [700, 129, 65]
+    T = sum(lens)
+    qkv = torch.randn(T, 3 * D, generator=g).bfloat16().to(dev)
+    probs, off = [], 0
+    for n in lens:
+        probs.append([off, n, off, n, off])
+        off += n
+    pt = torch.tensor(probs, dtype=torch.int32, device=dev)
+    outs = {}
+    for dt in (torch.bfloat16, torch.float16):
+        o = torch.zeros(T, D, device=dev, dtype=dt)
+        ops.attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, pt, max(lens), H,
+                      schedule=ops.attn_schedule(probs, H, dev))
+        outs[dt] = o.float()
+    off = 0
+    for n in lens:
+        sl = slice(off, off + n)
+        r = _ref_attn(qkv[sl, :D].float().cpu(), qkv[sl, D:2 * D].float().cpu(), qkv[sl, 2 * D:].float().cpu(), H)
+        assert relerr(outs[torch.float16][sl].cpu(), r) < 2e-3
+        assert relerr(outs[torch.bfloat16][sl].cpu(), r) < 6e-3
+        off += n
+    n_img, gh = 2, 16
+    T2 = n_img * gh * gh
+    qkv2 = torch.randn(T2, 3 * D, generator=g).bfloat16().to(dev)
+    sw = {}
+    for dt in (torch.bfloat16, torch.float16):
+        o = torch.zeros(T2, D, device=dev, dtype=dt)
+        ops.swin_attention(qkv2[:, :D], qkv2[:, D:2 * D], qkv2[:, 2 * D:], o, n_img, gh, gh, 4, H)
+        sw[dt] = o.float()
+    assert relerr(sw[torch.float16], sw[torch.bfloat16]) < 4e-3
+
+
 def test_gemm_asymmetric_identity():
     """A = I with an asymmetric W catches a transposed C write (guide §3)."""
     ops = _ops()

@@ -14,6 +14,9 @@ from oracle import rf_ref
 
 pytestmark = pytest.mark.gpu
 HDR_TOL = 1e-3
+# deviation-from-the-mean bound at production size: the fp16-operand path measures 1-2e-4 (tools/
+# precision_budget.py predicts 1.2e-4); bf16 operands would be 6-8e-4
+AC_TOL = 4e-4
 
 
 def _pipeline(cfg, sd, dpt_precision=None):
@@ -232,7 +235,18 @@ def test_baseline_configs_match_reference(name):
     err, ac = rel_l2(got, ref), rel_l2_ac(got, ref)
     print(f"{name}: rel L2 {err:.3e} (deviation from the mean: {ac:.3e})")
     assert err < HDR_TOL
-    assert ac < 2e-2
+    assert ac < AC_TOL
+    # discrimination guard: the error must be far below the distance between two DIFFERENT frames
+    # of the fixtures, so a path that rendered the wrong view or scene cannot pass
+    if "view01_rel_l2_ac" in z.files:  # two camera views of the same scene
+        for v in range(1, got.shape[1]):
+            assert rel_l2_ac(got[:, v], ref[:, v]) <= 0.25 * float(z["view01_rel_l2_ac"]), v
+        assert rel_l2_ac(got[:, 1], ref[:, 0]) > 2.0 * rel_l2_ac(got[:, 0], ref[:, 0])  # view 1 is not view 0
+    if name in ("large_cbox_r512", "large_bunny_r512"):  # cbox (N=5,633) vs cbox-bunny (N=6,209)
+        other = load_case("large_bunny_r512" if name == "large_cbox_r512" else "large_cbox_r512")[4]["hdr"]
+        dist = rel_l2_ac(other, ref)
+        assert ac <= 0.25 * dist, (ac, dist)
+        assert rel_l2_ac(got, other) > 0.75 * dist  # the other scene's reference is far from this frame
     if "hdr_sum" in z.files:  # the whole image, not only the sampled pixels
         o64 = out.double()
         assert abs(float(o64.sum()) - float(z["hdr_sum"])) / abs(float(z["hdr_sum"])) < 1e-3
