@@ -74,7 +74,9 @@ const char* rf_last_error(void);
 int rf_abi_version(void);
 
 /* Device-side error word.  A stream-K owner (GEMM or attention) whose partner's partial does not arrive within
- * the spin bound (env RF_SPIN_LIMIT polls, default 2^24) stores a non-zero code into a host-mapped word instead
+ * the spin bound (env RF_SPIN_LIMIT polls, default 2^24; code 1 GEMM, 2 attention), a stream-K launch handed a
+ * range table that does not cover its tiles (code 3) or rf_scene_pos given a set above max_tris (code 4)
+ * stores a non-zero code into a host-mapped word instead
  * of failing silently; from then on every entry point returns RF_ERR_DEVICE (checked without a device sync)
  * until rf_clear_device_error(); the outputs of the reporting launch are invalid and the stream-K workspaces
  * must be re-zeroed.  rf_debug_raise_device_error launches a kernel that stores `code` (tests). */
@@ -266,7 +268,9 @@ int rf_patchify_rays_dt(const float* rays_d, int n_views, int res, int patch, vo
  * scene, offsets scene_off[B+1]).  For each set s (s = b when c2w == NULL, else s = b*n_views + v with the
  * camera transform p -> R^T (p - t)), writes n_reg centre rows then the n_b triangle rows to
  * pos_out[set_off[s] ...].  max_tris >= every n_b; partials: rf_scene_pos_partials(sets, max_tris) floats of
- * caller workspace (per-256-triangle sums, reduced in a fixed order: deterministic). */
+ * caller workspace (per-256-triangle sums, reduced in a fixed order: deterministic).  A set with n_b > max_tris
+ * (the kernel sees scene_off on the device only) is clamped to its own partial slots and raises device error 4
+ * (RF_ERR_DEVICE from the next call; its positions past ceil(max_tris/256)*256 are not written). */
 int rf_scene_pos(const float* tris, const int32_t* valid_idx, const int32_t* scene_off, const float* c2w,
                  int n_scenes, int n_views, int n_reg, float* pos_out, const int32_t* set_off, int max_tris,
                  float* partials, int64_t partial_floats, void* stream);

@@ -83,6 +83,7 @@ struct AttnArgs {
     const int64_t* bounds;
     int epoch;  // hand-off flag value of this launch (> 0, new every launch: no re-arm, stale flags never match)
     int o_f16;  // output O as fp16 (the A operand of an fp16 out-projection) instead of bf16
+    int ascend; // diagnostic (RF_SK_ASCEND=1): ascending blockIdx order inside a group (the round-2 layout), A/B only
 };
 
 // two f32 -> the 16-bit output pair: fp16 (OF16) or bf16, RNE
@@ -134,8 +135,9 @@ RF_DEV int sk_attn_block(const AttnArgs& p, int hw, int nwg, int& gend) {
     sk_attn_count(p, total, units);
     const SkLayout lay(nwg, units);
     int g = 0;
-    const int L = lay.logical(hw, &g);
+    int L = lay.logical(hw, &g);
     gend = lay.base(g) + lay.size(g);
+    if (p.ascend) L = lay.base(g) + gend - 1 - L;  // A/B diagnostic only (RF_SK_ASCEND=1): round-2 order, no progress guarantee
     const int64_t b = p.bounds[L], e = p.bounds[L + 1];
     const bool bad = b < 0 || e < b || e > total || (L == 0 && b != 0) || (L == nwg - 1 && e != total);
     return bad ? -1 : L;
@@ -1823,6 +1825,7 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
     a.part_o = (float*)workspace;
     a.flag = (int*)(a.part_o + (int64_t)SK5_MAX_GRID * PIECE_FLOATS);
     a.o_f16 = o_f16;
+    a.ascend = getenv("RF_SK_ASCEND") && atoi(getenv("RF_SK_ASCEND")) == 1;
     a.bounds = bounds;
     if (!bounds) {  // equal split per XCD group, written on the device ahead of the launch (stream-ordered)
         int64_t* eq = (int64_t*)(a.flag + SK5_MAX_GRID);

@@ -83,6 +83,7 @@ RF_DEV void report_device_error(int* err, int code) {
 #define RF_DEVERR_SK_GEMM 1
 #define RF_DEVERR_SK_ATTN 2
 #define RF_DEVERR_SK_SCHED 3  // a stream-K range table that does not cover the launch's tiles (rejected in-kernel)
+#define RF_DEVERR_SCENE_POS 4  // rf_scene_pos: a set holds more triangles than the max_tris it was launched for
 
 // ------------------------------------------------------------------------------------------------------
 // Stream-K block layout with forward progress (attention, GEMM and conv stream-K kernels).  The block that

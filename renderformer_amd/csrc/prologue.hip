@@ -261,11 +261,18 @@ __global__ __launch_bounds__(64) void scene_pos_center_kernel(const int32_t* __r
                                                               int has_c2w, int n_reg, int n_blocks,
                                                               const float* __restrict__ partial,
                                                               float* __restrict__ pos_out,
-                                                              const int32_t* __restrict__ set_off) {
+                                                              const int32_t* __restrict__ set_off, int* err) {
     const int set = blockIdx.x;
     const int scene = has_c2w ? set / n_views : set;
     const int n = scene_off[scene + 1] - scene_off[scene];
-    const int nb = (n + 255) / 256;  // blocks that held triangles of this set (the rest wrote zeros)
+    // blocks that held triangles of this set (the rest wrote zeros).  A set with more triangles than the
+    // max_tris the caller sized the launch for would read the next set's partials and leave positions past
+    // n_blocks * 256 unwritten: clamp to this set's slots and raise the device error word instead.
+    int nb = (n + 255) / 256;
+    if (nb > n_blocks) {
+        nb = n_blocks;
+        if (threadIdx.x == 0) report_device_error(err, RF_DEVERR_SCENE_POS);
+    }
     // the partials of 64 blocks at a time come in with one load round trip (lane b loads block b's 9 sums into
     // LDS), then lane c < 9 adds them in block order: the same sums in the same order as a serial loop (whose
     // ~200 dependent loads took 11 us), so the result is bit-identical to it
@@ -451,7 +458,7 @@ extern "C" int rf_scene_pos(const float* tris, const int32_t* valid_idx, const i
     RF_LAUNCH(scene_pos_tri_kernel, dim3(nb, sets), dim3(256), 0, (hipStream_t)stream, tris, valid_idx,
                        scene_off, c2w, n_views, n_reg, pos_out, set_off, partials);
     RF_LAUNCH(scene_pos_center_kernel, dim3(sets), dim3(64), 0, (hipStream_t)stream, scene_off, n_views,
-                       c2w ? 1 : 0, n_reg, nb, partials, pos_out, set_off);
+                       c2w ? 1 : 0, n_reg, nb, partials, pos_out, set_off, rf::device_error_word());
     return rf::check_launch("rf_scene_pos");
 }
 

@@ -675,6 +675,35 @@ def test_scene_pos_large_and_deterministic():
         assert torch.allclose(got, refp[b, :S[b]], atol=2e-6), b
 
 
+def test_scene_pos_undersized_max_tris_reports_device_error():
+    """max_tris below a set's triangle count: the centre kernel stays inside its set's partial slots
+    and raises device error 4 instead of reading the next set's sums; clear_device_error() recovers."""
+    from renderformer_amd._lib import DeviceError
+    from renderformer_amd.scenes import batch_scenes, synthetic_scene
+    ops = _ops()
+    counts = [700, 300]
+    bt = batch_scenes([synthetic_scene(n, 1, seed=50 + i) for i, n in enumerate(counts)], expand=False)
+    B, N = bt["mask"].shape
+    valid = torch.nonzero(bt["mask"].reshape(-1)).squeeze(1).to(torch.int32).to(dev)
+    scene_off = torch.tensor([0, counts[0], sum(counts)], dtype=torch.int32, device=dev)
+    S = [16 + c for c in counts]
+    set_off = torch.tensor([0, S[0], S[0] + S[1]], dtype=torch.int32, device=dev)
+    tris = bt["triangles"].reshape(B * N, 9).contiguous().to(dev)
+    pos = torch.zeros(sum(S), 9, device=dev)
+    ops.scene_pos(tris, valid, scene_off, None, B, 1, 16, pos, set_off, 300)  # 300 < 700: 2 blocks, not 3
+    torch.cuda.synchronize()
+    assert _lib_mod().rf_device_error() == 4
+    with pytest.raises(DeviceError, match="clear_device_error"):
+        ops.scene_pos(tris, valid, scene_off, None, B, 1, 16, pos, set_off, max(counts))
+    ops.clear_device_error()
+    ops.scene_pos(tris, valid, scene_off, None, B, 1, 16, pos, set_off, max(counts))
+    torch.cuda.synchronize()
+    assert _lib_mod().rf_device_error() == 0
+    refp, _ = rf_ref.center_pos(bt["triangles"].reshape(B, N, 9), bt["mask"], 16)
+    for b in range(B):
+        assert torch.allclose(pos[int(set_off[b]):int(set_off[b + 1])].cpu(), refp[b, :S[b]], atol=2e-6), b
+
+
 def test_hdr_output():
     ops = _ops()
     logits = torch.randn(2, 3, 16, 16, device=dev)

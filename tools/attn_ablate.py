@@ -34,7 +34,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "stamps":
         run()
     torch.cuda.synchronize()
     ws = ops._attn_workspace(out.device)
-    piece = (ws.numel() - 512) // 512
+    piece = 256 * 128 + 256 * 4  # PIECE_FLOATS (attention.hip): the debug stamps live in the last of 512 slots
     st = ws[511 * piece:511 * piece + 256 * 8 * 16].view(torch.int64).view(256, 8, 8).cpu().double()
     tiles = st[..., 7].clamp_min(1)
     names = ["top wait", "A (+K DMA, check)", "seam wait", "B (+V DMA)"]
@@ -85,8 +85,10 @@ VARIANTS = os.environ.get("ABL", "0,u,64,1,2,4,8,16,20").split(",")
 
 
 def timed(dbg, reps=20):
-    """dbg = an RF_ATTN_DBG value, or "u": the shipped kernel on equal tile counts (no schedule)"""
-    os.environ["RF_ATTN_DBG"] = "0" if dbg == "u" else dbg
+    """dbg = an RF_ATTN_DBG value, "u": the shipped kernel on equal tile counts (no schedule), "asc": the shipped
+    kernel with the round-2 block order (ascending blockIdx inside an XCD group; RF_SK_ASCEND=1, A/B only)"""
+    os.environ["RF_ATTN_DBG"] = "0" if dbg in ("u", "asc") else dbg
+    os.environ["RF_SK_ASCEND"] = "1" if dbg == "asc" else "0"
     sch = None if dbg == "u" else sched
     run(sch)
     torch.cuda.synchronize()
