@@ -342,11 +342,10 @@ def test_model_on_non_current_device():
 
 
 @pytest.mark.parametrize("name", ["large_cbox_r512", "large_cbox_r1024_v4"])
-def test_fp8_stage2_parity_report(name):
-    """The fp8 mode (stage-2 projections and FFN as MX fp8 GEMMs, BASELINE config 5's 'fp8 MFMA path') against
-    the same reference fixtures.  e4m3 keeps 3 mantissa bits (bf16: 7), so this mode is NOT inside the 1e-3
-    north-star bar that the default bf16 path meets; the measured error is printed and recorded in DESIGN.md,
-    and the test bounds it so that a broken kernel (not the format) fails."""
+def test_fp8_stage2_parity(name):
+    """The opt-in fp8 mode (its default subset: the stage-2 cross-attention Q and the FFN W2 as MX fp8 GEMMs)
+    against the same reference fixtures, at the north-star bar.  The other projections in fp8 miss it
+    (per-projection errors: tools/fp8_study.py), so the mode does not take them by default."""
     from renderformer_amd import RenderFormer, RenderFormerRenderingPipeline
     cfg, sd, inp, res, z = load_case(name)
     pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd, fp8=True)).to("cuda")
@@ -355,7 +354,7 @@ def test_fp8_stage2_parity_report(name):
     ref, st = reference_hdr(z)
     got = out[:, :, ::st, ::st].cpu()
     err, ac = rel_l2(got, ref), rel_l2_ac(got, ref)
-    print(f"fp8 stage 2, {name}: rel L2 {err:.3e} (deviation from the mean: {ac:.3e}); bf16 bar 1e-3")
-    assert err < 3e-2
+    print(f"fp8 stage 2, {name}: rel L2 {err:.3e} (deviation from the mean: {ac:.3e}); bar 1e-3")
+    assert err < 1e-3
     del pipe, out, d
     torch.cuda.empty_cache()

@@ -16,7 +16,7 @@ import torch  # noqa: E402
 
 from golden_util import load_case, reference_hdr, rel_l2, rel_l2_ac  # noqa: E402
 
-SUBSETS = [None, "q", "out", "self_in", "self_out", "w13", "w2", "w13,w2", "q,out,self_in,self_out",
+SUBSETS = ["f16", None, "q", "out", "self_in", "self_out", "w13", "w2", "w13,w2", "q,out,self_in,self_out",
            "q,out,self_in,self_out,w13,w2"]
 
 
@@ -29,11 +29,14 @@ def main():
         ref, st = reference_hdr(z)
         d = {k: v.cuda() for k, v in inp.items()}
         for sub in SUBSETS:
-            if sub is None:
-                os.environ.pop("RF_FP8_PROJ", None)
-            else:
+            # "f16": the default fp16 projection operands; None: bf16 operands (the base the fp8 mode runs on)
+            fp8 = sub not in ("f16", None)
+            if fp8:
                 os.environ["RF_FP8_PROJ"] = sub
-            pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd, fp8=sub is not None)).to("cuda")
+            else:
+                os.environ.pop("RF_FP8_PROJ", None)
+            operands = "f16" if sub == "f16" else "bf16"
+            pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd, fp8=fp8, operands=operands)).to("cuda")
             out = pipe(d["triangles"], d["texture"].clone(), d["mask"], d["vn"], d["c2w"], d["fov"], resolution=res)
             got = out[:, :, ::st, ::st].cpu()
             e, ac = rel_l2(got, ref), rel_l2_ac(got, ref)
