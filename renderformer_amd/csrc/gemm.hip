@@ -391,17 +391,28 @@ RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
     }
 }
 
-template <class C, int EPI>
+// TW2D = 0: the tile's rows are BM consecutive output rows from m0.  TW2D > 0 (convolutions, halo2_kernel):
+// the tile is a block TW2D pixels wide of one image (m0 = its top-left pixel, p.wo the image width), each
+// wave's MW pixels are MW / TW2D whole rows of it and fragment i covers 16 consecutive pixels of one row.
+// FINAL = false compiles out the fused-head path (RF_CONV_FINAL) for blocks that never take it: its silu
+// values are loop-invariant across the head's outputs, get hoisted, and double the accumulators' registers.
+template <class C, int EPI, int TW2D = 0, bool FINAL = true>
 RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&acc)[C::TI][C::TJ]) {
     constexpr int TI = C::TI, TJ = C::TJ;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int wm = wave / C::WGN, wn = wave % C::WGN;
+    static_assert(TW2D == 0 || (EPI == E_CONV && TW2D % 16 == 0 && C::MW % TW2D == 0), "2-D conv tile");
     // ------------------------------------------------------------------ epilogue
     // acc[i][j][e] = C[row][col + e], row = m0 + wm*MW + i*16 + (lane & 15),
     //                                  col = n0 + wn*NWD + j*16 + 4*(lane >> 4)
     const int rl = lane & 15, cq = 4 * (lane >> 4);
     const int rbase = m0 + wm * C::MW, cbase = n0 + wn * C::NWD;
+    // output row (pixel) of fragment i for this lane
+    auto frow = [&](int i) -> int {
+        if constexpr (TW2D == 0) return rbase + i * 16 + rl;
+        else return m0 + (wm * (C::MW / TW2D) + (i * 16) / TW2D) * p.wo + (i * 16) % TW2D + rl;
+    };
     if constexpr (EPI == E_SWIGLU) {
         bf16_t* c = reinterpret_cast<bf16_t*>(p.c);
 #pragma unroll
@@ -429,17 +440,17 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
         }
         return;
     } else if constexpr (EPI == E_CONV) {
-        if (p.flags & RF_CONV_FINAL) {
-            // SiLU -> 1x1 (cout <= NWD channels, all in the wn == 0 waves) -> ELU -> [10^x - 1]
-            f32x4 act[TI][TJ];  // silu(conv + bias), once per element; 0 in padded channels
+        if (FINAL && (p.flags & RF_CONV_FINAL)) {
+            // SiLU -> 1x1 (cout <= NWD channels, all in the wn == 0 waves) -> ELU -> [10^x - 1].  silu(conv +
+            // bias) is recomputed per output feature (n_fin = 3) rather than held in a TI x TJ array: that
+            // array doubled the accumulators' registers and made every conv tile with this epilogue spill
+            float bsum[TJ][4];  // bias, 0 in padded channels
 #pragma unroll
             for (int j = 0; j < TJ; ++j)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int col = cbase + j * 16 + cq + e;
-                    const float b = (p.bias && col < p.cout) ? p.bias[col] : 0.f;
-#pragma unroll
-                    for (int i = 0; i < TI; ++i) act[i][j][e] = col < p.cout ? silu_precise(acc[i][j][e] + b) : 0.f;
+                    bsum[j][e] = (p.bias && col < p.cout) ? p.bias[col] : 0.f;
                 }
             for (int f = 0; f < p.n_fin; ++f) {
                 float wf[TJ][4];
@@ -456,10 +467,10 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
 #pragma unroll
                     for (int j = 0; j < TJ; ++j)
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) s += act[i][j][e] * wf[j][e];
+                        for (int e = 0; e < 4; ++e) s += silu_precise(acc[i][j][e] + bsum[j][e]) * wf[j][e];
                     s += __shfl_xor(s, 16, 64);
                     s += __shfl_xor(s, 32, 64);
-                    const int m = rbase + i * 16 + rl;
+                    const int m = frow(i);
                     if (lane < 16 && wn == 0 && m < p.m) {
                         float y = s + p.b_fin[f];
                         y = y > 0.f ? y : p.elu_alpha * expm1f(y);
@@ -477,7 +488,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
         const int nreal = kk ? p.cout * kk * kk : p.cout;
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
-            const int m = rbase + i * 16 + rl;
+            const int m = frow(i);
             if (m >= p.m) continue;
             int img = 0, y = 0, x = 0;
             if (kk) {
@@ -1425,6 +1436,229 @@ __global__ __launch_bounds__(C::THREADS, C::BM == 256 ? 1 : 2) void halo_kernel(
     engine_epilogue<C, EPI>(p, tm * C::BM, tn * C::BN, acc);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Halo-tiled 3x3 convolution on 2-D output tiles: 16 x 32 pixels x 128 output channels per block (8 waves,
+// each 4 rows x 32 pixels x 64 channels = the phased 256x256 GEMM's 128x64 wave tile).  The 1-row-high
+// halo_kernel above re-reads the whole filter bank (K = 9 cin) for every 128 pixels, and at 512^2 that weight
+// stream (1.2 GB for output_conv1) bounds it; a 512-pixel block reads the bank 4x less often and its halo is
+// 1.2x the tile's pixels instead of 3x.  K runs chunk-major (32 input channels), tap-minor: per chunk the
+// 18 x 34 halo is staged once (40 x 1-KiB LDS-DMA pieces, 5 per wave, issued during the previous chunk into
+// the other of two buffers) and every tap reads its fragments at a shifted halo index (the XOR image of
+// lds_off is bank-conflict-free for 16 consecutive pixels from any start); the 8-KiB W slice of each
+// (chunk, tap) step streams through an S-deep ring.  Each step is two phases of 16 MFMAs (fragment rows 0-3,
+// then 4-7, sharing the step's four W fragments) in the phased loop's form: load section, barrier, MFMA
+// section, barrier, with waves 4-7 one section behind so each SIMD overlaps one wave's LDS reads with its
+// partner's MFMAs.  One counted vmcnt per step (h2_wait) publishes the next step's W slice, and at a chunk's
+// last tap also the next chunk's halo (issued before that W slice).
+namespace h2 {
+constexpr int TH = 16, TW = 32, HWID = TW + 2, HPIX = (TH + 2) * HWID;  // 612 halo pixels
+constexpr int PIECES = 40, PPW = PIECES / 8;                            // 1-KiB pieces per buffer, per wave
+constexpr int HBYTES = PIECES * 1024;                                   // 640 pixel slots x 64 B
+static_assert(PIECES * 16 >= HPIX, "halo buffer");
+// LDS-DMA left in flight when step t's wait must have landed W(t+1): the issue events after W(t+1) are, per
+// step j in [t + 2 - S, t], a halo piece (taps 0-4 of a chunk with a successor) and W(j + S) (if it exists;
+// steps before the loop stand for the prologue's W issues)
+constexpr int wait_count(int t, int S, bool last) {
+    int n = 0;
+    for (int j = t + 2 - S; j <= t; ++j) {
+        if (last) n += (j < 0 || j + S < 9) ? 1 : 0;
+        else n += 1 + ((j >= 0 && j < 5) ? 1 : 0);
+    }
+    return n;
+}
+}  // namespace h2
+// BN = 128 output channels: 4 x 2 waves of 4 rows x 64 channels; BN = 64 (output_conv2's 32 padded to 64):
+// 8 x 1 waves of 2 rows x 64 channels
+template <int S, int BN>
+struct H2Cfg {
+    static constexpr int WGN = BN / 64, WGM = 8 / WGN, RW = h2::TH / WGM;  // tile rows per wave
+    static constexpr int TI = 2 * RW, TJ = 4, WBYTES = BN * 64;            // fragments; W stage (BN x 32 ci x 2 B)
+    static constexpr int LDS = 2 * h2::HBYTES + S * WBYTES;
+    static_assert(BN == 64 || BN == 128, "halo2 channel tile");
+};
+// the epilogue's view of the block (engine_epilogue reads these members only)
+template <int BN>
+struct H2Tile {
+    static constexpr int WGN = BN / 64, WGM = 8 / WGN, MW = 512 / WGM, NWD = 64, TI = MW / 16, TJ = 4;
+};
+
+template <int N>
+RF_DEV void wait_vm_rt(int n) {  // vmcnt(n) for a wave-uniform n <= N (the unrolled callers pass constants)
+    if constexpr (N > 0) {
+        if (n >= N) {
+            wait_vm<N>();
+            return;
+        }
+        wait_vm_rt<N - 1>(n);
+    } else {
+        wait_vm<0>();
+    }
+}
+
+template <int S, int BN>
+RF_DEV void halo2_mainloop(const EngineArgs& p, char* smem, int img, int y0, int x0, int n0,
+                           f32x4 (&acc)[H2Cfg<S, BN>::TI][4]) {
+    using namespace h2;
+    using G = H2Cfg<S, BN>;
+    constexpr int TI = G::TI, HALF = TI / 2, WBYTES = G::WBYTES;
+    static_assert(S >= 2 && S <= 4, "W ring depth (the chunk's halo is issued at taps 0-4, before W(next chunk))");
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave / G::WGN, wn = wave % G::WGN;
+    // W stage: BN / 16 one-KiB pieces, one per wave of waves 0 .. BN / 16 - 1 (the rest stage no W and count
+    // only their halo pieces)
+    const bool has_w = BN == 128 || __builtin_amdgcn_readfirstlane(wave) < BN / 16;
+    const int nch = p.cin_pad / 32, nk = 9 * nch;
+    char* hbuf = smem;                    // two halo buffers
+    char* wring = smem + 2 * HBYTES;      // S W stages
+
+    // halo staging: piece wave + 8 t of a buffer holds halo pixels 16 (wave + 8 t) .. + 15 (64 B each, 16-B chunk
+    // XOR ((pixel >> 1) & 3), matching lds_off); pixels past the image or past the 612 in use read the zero row
+    int64_t hoff[PPW];
+#pragma unroll
+    for (int t = 0; t < PPW; ++t) {
+        const int hp = (wave + 8 * t) * 16 + (lane >> 2);
+        const int ch = (lane & 3) ^ ((hp >> 1) & 3);
+        int64_t off = -1;
+        if (hp < HPIX) {
+            const int hy = hp / HWID, hx = hp - hy * HWID;
+            const int iy = y0 + hy - 1, ix = x0 + hx - 1;
+            if (iy >= 0 && iy < p.hi && ix >= 0 && ix < p.wi)
+                off = ((int64_t)(img * p.hi + iy) * p.wi + ix) * p.cin_pad + ch * 8;
+        }
+        hoff[t] = off;
+    }
+    auto issue_halo = [&](int chunk, int t) {  // piece t of this wave, chunk's 32 channels, into buffer chunk & 1
+        const bf16_t* src = hoff[t] >= 0 ? p.a + hoff[t] + chunk * 32 : p.zero;
+        __builtin_amdgcn_global_load_lds(GLB_PTR(void, src),
+                                         LDS_PTR(void, hbuf + (chunk & 1) * HBYTES + (wave + 8 * t) * 1024), 16, 0, 0);
+    };
+    // W staging: wave w fills rows 16 w .. 16 w + 15 of a stage (one 1-KiB piece per lane-instruction)
+    const int wrow = 16 * wave + (lane >> 2);
+    const bf16_t* wsrc = p.w + (int64_t)(n0 + wrow) * p.ldw + (((lane & 3) ^ ((wrow >> 1) & 3)) * 8);
+    auto issue_w = [&](int kt) {
+        if (!has_w) return;
+        const int chunk = kt / 9, tap = kt - 9 * chunk;
+        __builtin_amdgcn_global_load_lds(GLB_PTR(void, wsrc + tap * p.cin_pad + chunk * 32),
+                                         LDS_PTR(void, wring + (kt % S) * WBYTES + wave * 1024), 16, 0, 0);
+    };
+
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int frow = lane & 15, fch = lane >> 4;
+    // halo index of fragment i's lane pixel at tap (0, 0): tile row RW wm + i / 2, column 16 (i & 1) + frow
+    int hbase[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) hbase[h] = (G::RW * wm) * HWID + 16 * h + frow;
+    bf16x8 fa[HALF], fb[4];
+    auto read_a = [&](const char* hb, int tap, int half) {  // fragments HALF half .. HALF half + HALF - 1
+        // opaque per use: otherwise the unrolled taps' 72 fragment addresses are hoisted out of the chunk
+        // loop and held in registers (78 VGPRs spilled)
+        int toff = (tap / 3) * HWID + tap % 3;
+        asm volatile("" : "+s"(toff));
+#pragma unroll
+        for (int r = 0; r < HALF; ++r) {
+            const int i = HALF * half + r;
+            const int hidx = hbase[i & 1] + (i >> 1) * HWID + toff;
+            fa[r] = *reinterpret_cast<const bf16x8*>(hb + lds_off(hidx, fch));
+        }
+    };
+    auto read_b = [&](int slot) {
+        int soff = slot * WBYTES;
+        asm volatile("" : "+s"(soff));
+        const char* ws = wring + soff;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            fb[j] = *reinterpret_cast<const bf16x8*>(ws + lds_off(wn * 64 + j * 16 + frow, fch));
+    };
+    auto mma = [&](int half) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int r = 0; r < HALF; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[HALF * half + r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                    __builtin_bit_cast(f16x8, fb[j]), __builtin_bit_cast(f16x8, fa[r]), acc[HALF * half + r][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto sync_in = [&]() {
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this section's fragments are in registers
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto sync_out = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // prologue: chunk 0's halo and W(0 .. S-1), all landed
+#pragma unroll
+    for (int t = 0; t < PPW; ++t) issue_halo(0, t);
+#pragma unroll
+    for (int kt = 0; kt < S; ++kt)
+        if (kt < nk) issue_w(kt);
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // waves 4-7: one section behind
+    if (late) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+
+    for (int c = 0; c < nch; ++c) {
+        const bool last = c + 1 == nch;
+        const char* hb = hbuf + (c & 1) * HBYTES;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int kt = 9 * c + t;
+            // phase 0: W fragments + A fragments 0 .. HALF - 1
+            read_b(kt % S);
+            read_a(hb, t, 0);
+            sync_in();
+            mma(0);
+            sync_out();
+            // phase 1: the other fragments; the next chunk's halo piece t (taps 0-4), W(kt + S), publish W(kt + 1)
+            read_a(hb, t, 1);
+            if (t < PPW && !last) issue_halo(c + 1, t);
+            if (kt + S < nk) issue_w(kt + S);
+            if (has_w) {
+                if (t < 8 || !last) {
+                    if (last) wait_vm_rt<4>(wait_count(t, S, true));
+                    else wait_vm_rt<8>(wait_count(t, S, false));
+                }
+            } else if (t == 8 && !last) {
+                wait_vm<0>();  // no W staged by this wave: only its pieces of the next chunk's halo
+            }
+            sync_in();
+            mma(1);
+            sync_out();
+        }
+    }
+    if (!late) __builtin_amdgcn_s_barrier();  // re-align the groups' barrier counts
+}
+
+template <int S, int BN>
+__global__ __launch_bounds__(512, 1) void halo2_kernel(EngineArgs p) {
+    __shared__ __attribute__((aligned(16))) char smem[H2Cfg<S, BN>::LDS];
+    // XCD-contiguous tile ids (consecutive ids share an XCD's L2: the two channel tiles of one pixel tile and
+    // neighbouring pixel tiles, whose halos overlap); tile id = pixel tile * n_tiles + channel tile
+    const int nwg = gridDim.x, hw = blockIdx.x;
+    const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
+    const int tiles_n = p.n / BN, tx_n = p.wo / h2::TW, ty_n = p.ho / h2::TH;
+    const int tn = wg % tiles_n, pt = wg / tiles_n;
+    const int tx = pt % tx_n, rest = pt / tx_n;
+    const int ty = rest % ty_n, img = rest / ty_n;
+    const int y0 = ty * h2::TH, x0 = tx * h2::TW;
+    f32x4 acc[H2Cfg<S, BN>::TI][4];
+    halo2_mainloop<S, BN>(p, smem, img, y0, x0, tn * BN, acc);
+    engine_epilogue<H2Tile<BN>, E_CONV, h2::TW, BN == 64>(p, (img * p.ho + y0) * p.wo + x0, tn * BN, acc);
+}
+
 // Tile configurations.  T128: 128x128, 4 waves of 64x64, 3-stage ring (48 KiB / 96 KiB LDS).
 // T256: 256x256, 8 waves of 128x64, 4-stage ring (128 KiB).  T256x128: 8 waves of 64x64, bf16x3 3-stage (144 KiB).
 using T128 = Tile<128, 128, 2, 2, 3>;
@@ -2273,11 +2507,41 @@ extern "C" int rf_quant_mx8(const void* x, int64_t ldx, int rows, int cols, void
     return rf::check_launch("rf_quant_mx8");
 }
 
+// halo2_kernel serves 3x3 / stride 1 / pad 1 fp16 convolutions on whole 16 x 32 tiles with a multiple of 128
+// output channels (or 64: output_conv2) when they make at least one block per CU (RF_CONV_HALO2=0: never,
+// 1: whenever it can)
+static bool halo2_ok(const EngineArgs& a) {
+    const char* env = getenv("RF_CONV_HALO2");
+    if (env && atoi(env) == 0) return false;
+    if (!env && getenv("RF_CONV_TILE")) return false;  // an explicit tile choice (A/B, tests) keeps its kernel
+    if (a.kw != 3 || a.k != 9 * a.cin_pad || a.stride != 1 || a.pad != 1 || a.ho != a.hi || a.wo != a.wi) return false;
+    if (a.cin_pad % 32 || (a.n % 128 && a.n != 64) || a.ho % h2::TH || a.wo % h2::TW || a.m % 512) return false;
+    const int64_t blocks = (int64_t)(a.m / 512) * (a.n == 64 ? 1 : a.n / 128);
+    return (env && atoi(env) == 1) || blocks >= 256;
+}
+
+static int launch_halo2(EngineArgs a, void* stream, const char* what) {
+    const bool n64 = a.n == 64;
+    const int nwg = (a.m / 512) * (n64 ? 1 : a.n / 128);
+    const char* env = getenv("RF_CONV_H2S");  // W ring depth: 4 (default) or 3
+    const bool s3 = env && atoi(env) == 3;
+    const hipStream_t st = (hipStream_t)stream;
+    if (n64) {
+        if (s3) RF_LAUNCH((halo2_kernel<3, 64>), dim3(nwg), dim3(512), 0, st, a);
+        else RF_LAUNCH((halo2_kernel<4, 64>), dim3(nwg), dim3(512), 0, st, a);
+    } else {
+        if (s3) RF_LAUNCH((halo2_kernel<3, 128>), dim3(nwg), dim3(512), 0, st, a);
+        else RF_LAUNCH((halo2_kernel<4, 128>), dim3(nwg), dim3(512), 0, st, a);
+    }
+    return rf::check_launch(what);
+}
+
 // fp16 convolutions (one MFMA per product): the 256x256 tile when the filter bank is a multiple of 256
 // wide and there is >= one tile per CU (the im2col gather of A is then read once per pixel tile),
 // 256x64 for <= 64 output channels, else 128x128 (faster than 256x128 on every DPT shape measured)
 template <bool GATHER>
 static int conv_f16_dp(EngineArgs& p, void* stream, const char* what) {
+    if (GATHER && halo2_ok(p)) return launch_halo2(p, stream, what);
     const char* env = getenv("RF_CONV_TILE");
     const int t = env ? atoi(env) : 0;
     // (RF_CONV_HALO=1 runs it halo-tiled: 90 -> 140 us at 512^2, 128 -> 32; a 128x64 tile at two blocks per

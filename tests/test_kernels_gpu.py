@@ -795,6 +795,40 @@ def test_conv_halo(cin, cout, hw, tile, monkeypatch):
     assert relerr(_planes_value(pl)[..., :cout].cpu(), F.silu(ref)) < 1e-3
 
 
+@pytest.mark.parametrize("h2s", ["3", "4"])
+@pytest.mark.parametrize("cin,cout,hh,ww,n_img", [(256, 128, 32, 64, 2), (128, 256, 48, 32, 1), (32, 128, 16, 32, 3),
+                                                  (96, 128, 16, 96, 1), (256, 256, 64, 64, 1), (128, 32, 32, 64, 2),
+                                                  (64, 64, 16, 32, 1)])
+def test_conv_halo2(cin, cout, hh, ww, n_img, h2s, monkeypatch):
+    """The 16 x 32-pixel halo-tiled 3x3 convolution (halo2_kernel; forced on with RF_CONV_HALO2=1, it is the
+    default at the 512^2 / 256^2 DPT levels): 1, 2, 3, 4 and 8 channel chunks (the next chunk's halo issued under
+    the current one), several images and tiles along both axes, non-square images, both W ring depths, the
+    128-channel block (1 or 2 channel tiles) and the 64-channel block (32 and 64 output channels), fused
+    bias + 2 residuals + SiLU fp16 planes with a padded row stride."""
+    monkeypatch.setenv("RF_CONV_HALO2", "1")
+    monkeypatch.setenv("RF_CONV_H2S", h2s)
+    from renderformer_amd.dpt import _Conv, split_planes
+    g = torch.Generator(device="cpu").manual_seed(cin * hh + cout + ww)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(cin * 9)
+    b = torch.randn(cout, generator=g)
+    x = torch.randn(n_img, cin, hh, ww, generator=g)
+    conv = _Conv(w, b, dev, f16=True)
+    xn = x.permute(0, 2, 3, 1).contiguous().to(dev)
+    r1 = torch.randn(n_img, hh, ww, cout, generator=g)
+    r2 = torch.randn(n_img, hh, ww, cout, generator=g)
+    out, pl = conv(split_planes(xn, conv.cin_pad, silu=True, f16=True), res1=r1.to(dev), res2=r2.to(dev),
+                   out_f32=True, planes_ld=cout + 32, planes_silu=True)
+    sx = _q(F.silu(x.double()).float(), "f16")
+    ref = F.conv2d(sx, _q(w, "f16"), b.double(), padding=1).permute(0, 2, 3, 1) + r1 + r2
+    assert relerr(out.cpu(), ref) < 2e-5
+    assert relerr(_planes_value(pl)[..., :cout].cpu(), F.silu(ref)) < 1e-3
+    assert (pl.hi[..., cout:] == 0).all()
+    # plain output (no residuals): the same kernel against the unfused conv
+    out2, _ = conv(split_planes(xn, conv.cin_pad, f16=True), out_f32=True)
+    ref2 = F.conv2d(_q(x, "f16"), _q(w, "f16"), b.double(), padding=1).permute(0, 2, 3, 1)
+    assert relerr(out2.cpu(), ref2) < 2e-5
+
+
 @pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("cin,cout,k", [(128, 128, 4), (256, 256, 2), (16, 16, 4), (32, 32, 2)])
 def test_deconv(cin, cout, k, prec):
@@ -833,16 +867,21 @@ def test_upsample_bilinear_align_corners(hi, ho, c, prec):
     assert out2 is None and torch.equal(pl2.hi, pl.hi) and (f16 or torch.equal(pl2.lo, pl.lo))
 
 
-@pytest.mark.parametrize("prec", PRECS)
-def test_conv_final_head(prec):
+@pytest.mark.parametrize("prec,hw", [("bf16x3", 24), ("f16", 24), ("f16h2", 32), ("f16h2", 64)])
+def test_conv_final_head(prec, hw, monkeypatch):
+    """output_conv2 + its fused head (SiLU, 1x1 32 -> 3, ELU, 10^x - 1); f16h2: on the 16 x 32-pixel halo kernel's
+    64-channel block (RF_CONV_HALO2=1; the default for 512^2 frames)."""
     from renderformer_amd.dpt import LOG_DECODE, NCHW_OUT, _Conv, split_planes
+    if prec == "f16h2":
+        monkeypatch.setenv("RF_CONV_HALO2", "1")
+        prec = "f16"
     f16 = prec == "f16"
     g = torch.Generator(device="cpu").manual_seed(9)
     w = torch.randn(32, 64, 3, 3, generator=g) / 24
     b = torch.randn(32, generator=g) * 0.1
     wf = torch.randn(3, 32, 1, 1, generator=g) / 6
     bf = torch.randn(3, generator=g) * 0.1
-    x = torch.randn(2, 64, 24, 24, generator=g)
+    x = torch.randn(2, 64, hw, hw, generator=g)
     conv = _Conv(w, b, dev, f16=f16)
     y = F.conv2d(F.silu(F.conv2d(_q(x, prec), _q(w, prec), b.double(), padding=1)), wf.double(), bf.double())
     y = F.elu(y, 1e-3)

@@ -189,7 +189,10 @@ def conv():
             for t in tiles:
                 os.environ["RF_CONV_PHASED"] = "1" if t == "256ph" else "0"
                 os.environ["RF_CONV_SKW8"] = "0" if t == "auto4w" else "1"
-                if not t.startswith("auto"):
+                # h2 / h2s4: the 16 x 32-pixel halo kernel (3- / 4-deep W ring); every other label runs without it
+                os.environ["RF_CONV_HALO2"] = "1" if t.startswith("h2") else "0"
+                os.environ["RF_CONV_H2S"] = "3" if t == "h2s3" else "4"
+                if not t.startswith("auto") and not t.startswith("h2"):
                     os.environ["RF_CONV_TILE"] = t.replace("ph", "")
                 ms = timeit(lambda: conv(x, out_f32=True), reps=10)
                 os.environ.pop("RF_CONV_TILE", None)
