@@ -23,6 +23,7 @@
 //   residual loads and SwiGLU pairs are 8-16 B vectors per lane.
 // * blockIdx is remapped so each XCD walks a contiguous band of tiles (T1).
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <math.h>
 #include <stdlib.h>
@@ -1495,13 +1496,17 @@ RF_DEV void wait_vm_rt(int n) {  // vmcnt(n) for a wave-uniform n <= N (the unro
     }
 }
 
-template <int S, int BN>
+// DBG (ablation timing only, wrong results): 1 = no MFMAs, 2 = no LDS-DMA after the prologue, 3 = no stagger.
+// One step = one load section {W fragments + all TI A fragments, the next chunk's halo piece (taps 0-4), W(kt + S - 1)
+// into the slot step kt - 1 read, counted wait for W(kt + 1)} and one MFMA section (4 TI MFMAs); with the two halves
+// of a step in separate sections (two barriers more per step) the 256^2 conv took 115 instead of 103 us.
+template <int S, int BN, int DBG = 0>
 RF_DEV void halo2_mainloop(const EngineArgs& p, char* smem, int img, int y0, int x0, int n0,
                            f32x4 (&acc)[H2Cfg<S, BN>::TI][4]) {
     using namespace h2;
     using G = H2Cfg<S, BN>;
-    constexpr int TI = G::TI, HALF = TI / 2, WBYTES = G::WBYTES;
-    static_assert(S >= 2 && S <= 4, "W ring depth (the chunk's halo is issued at taps 0-4, before W(next chunk))");
+    constexpr int TI = G::TI, WBYTES = G::WBYTES;
+    static_assert(S >= 3 && S <= 5, "W ring depth (S - 1 slices in flight; the chunk's halo must precede W(next chunk))");
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int wm = wave / G::WGN, wn = wave % G::WGN;
@@ -1514,22 +1519,21 @@ RF_DEV void halo2_mainloop(const EngineArgs& p, char* smem, int img, int y0, int
 
     // halo staging: piece wave + 8 t of a buffer holds halo pixels 16 (wave + 8 t) .. + 15 (64 B each, 16-B chunk
     // XOR ((pixel >> 1) & 3), matching lds_off); pixels past the image or past the 612 in use read the zero row
-    int64_t hoff[PPW];
+    int hpix[PPW], hch[PPW];
 #pragma unroll
     for (int t = 0; t < PPW; ++t) {
         const int hp = (wave + 8 * t) * 16 + (lane >> 2);
-        const int ch = (lane & 3) ^ ((hp >> 1) & 3);
-        int64_t off = -1;
+        hch[t] = (lane & 3) ^ ((hp >> 1) & 3);
+        int pix = -1;
         if (hp < HPIX) {
             const int hy = hp / HWID, hx = hp - hy * HWID;
             const int iy = y0 + hy - 1, ix = x0 + hx - 1;
-            if (iy >= 0 && iy < p.hi && ix >= 0 && ix < p.wi)
-                off = ((int64_t)(img * p.hi + iy) * p.wi + ix) * p.cin_pad + ch * 8;
+            if (iy >= 0 && iy < p.hi && ix >= 0 && ix < p.wi) pix = (img * p.hi + iy) * p.wi + ix;
         }
-        hoff[t] = off;
+        hpix[t] = pix;
     }
     auto issue_halo = [&](int chunk, int t) {  // piece t of this wave, chunk's 32 channels, into buffer chunk & 1
-        const bf16_t* src = hoff[t] >= 0 ? p.a + hoff[t] + chunk * 32 : p.zero;
+        const bf16_t* src = hpix[t] >= 0 ? p.a + (int64_t)hpix[t] * p.cin_pad + hch[t] * 8 + chunk * 32 : p.zero;
         __builtin_amdgcn_global_load_lds(GLB_PTR(void, src),
                                          LDS_PTR(void, hbuf + (chunk & 1) * HBYTES + (wave + 8 * t) * 1024), 16, 0, 0);
     };
@@ -1553,18 +1557,15 @@ RF_DEV void halo2_mainloop(const EngineArgs& p, char* smem, int img, int y0, int
     int hbase[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) hbase[h] = (G::RW * wm) * HWID + 16 * h + frow;
-    bf16x8 fa[HALF], fb[4];
-    auto read_a = [&](const char* hb, int tap, int half) {  // fragments HALF half .. HALF half + HALF - 1
+    bf16x8 fa[TI], fb[4];
+    auto read_a = [&](const char* hb, int tap) {
         // opaque per use: otherwise the unrolled taps' 72 fragment addresses are hoisted out of the chunk
         // loop and held in registers (78 VGPRs spilled)
         int toff = (tap / 3) * HWID + tap % 3;
         asm volatile("" : "+s"(toff));
 #pragma unroll
-        for (int r = 0; r < HALF; ++r) {
-            const int i = HALF * half + r;
-            const int hidx = hbase[i & 1] + (i >> 1) * HWID + toff;
-            fa[r] = *reinterpret_cast<const bf16x8*>(hb + lds_off(hidx, fch));
-        }
+        for (int i = 0; i < TI; ++i)
+            fa[i] = *reinterpret_cast<const bf16x8*>(hb + lds_off(hbase[i & 1] + (i >> 1) * HWID + toff, fch));
     };
     auto read_b = [&](int slot) {
         int soff = slot * WBYTES;
@@ -1574,14 +1575,15 @@ RF_DEV void halo2_mainloop(const EngineArgs& p, char* smem, int img, int y0, int
         for (int j = 0; j < 4; ++j)
             fb[j] = *reinterpret_cast<const bf16x8*>(ws + lds_off(wn * 64 + j * 16 + frow, fch));
     };
-    auto mma = [&](int half) {
+    auto mma = [&]() {
+        if constexpr (DBG == 1) return;
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int r = 0; r < HALF; ++r)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                acc[HALF * half + r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                    __builtin_bit_cast(f16x8, fb[j]), __builtin_bit_cast(f16x8, fa[r]), acc[HALF * half + r][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[j]),
+                                                                   __builtin_bit_cast(f16x8, fa[i]), acc[i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
     };
     auto sync_in = [&]() {
@@ -1596,16 +1598,16 @@ RF_DEV void halo2_mainloop(const EngineArgs& p, char* smem, int img, int y0, int
         __builtin_amdgcn_sched_barrier(0);
     };
 
-    // prologue: chunk 0's halo and W(0 .. S-1), all landed
+    // prologue: chunk 0's halo and W(0 .. S-2), all landed
 #pragma unroll
     for (int t = 0; t < PPW; ++t) issue_halo(0, t);
 #pragma unroll
-    for (int kt = 0; kt < S; ++kt)
+    for (int kt = 0; kt < S - 1; ++kt)
         if (kt < nk) issue_w(kt);
     wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // waves 4-7: one section behind
+    const bool late = DBG != 3 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // waves 4-7: one section behind
     if (late) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
 
@@ -1615,33 +1617,28 @@ RF_DEV void halo2_mainloop(const EngineArgs& p, char* smem, int img, int y0, int
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const int kt = 9 * c + t;
-            // phase 0: W fragments + A fragments 0 .. HALF - 1
             read_b(kt % S);
-            read_a(hb, t, 0);
-            sync_in();
-            mma(0);
-            sync_out();
-            // phase 1: the other fragments; the next chunk's halo piece t (taps 0-4), W(kt + S), publish W(kt + 1)
-            read_a(hb, t, 1);
-            if (t < PPW && !last) issue_halo(c + 1, t);
-            if (kt + S < nk) issue_w(kt + S);
+            read_a(hb, t);
+            // slot (kt - 1) % S was read by both wave groups before the barrier this section started after
+            if (DBG != 2 && t < PPW && !last) issue_halo(c + 1, t);
+            if (DBG != 2 && kt + S - 1 < nk) issue_w(kt + S - 1);
             if (has_w) {
-                if (t < 8 || !last) {
-                    if (last) wait_vm_rt<4>(wait_count(t, S, true));
-                    else wait_vm_rt<8>(wait_count(t, S, false));
+                if (t < 8 || !last) {  // W(kt + 1) landed: the same event count as an (S-1)-stage ring
+                    if (last) wait_vm_rt<4>(wait_count(t, S - 1, true));
+                    else wait_vm_rt<8>(wait_count(t, S - 1, false));
                 }
             } else if (t == 8 && !last) {
                 wait_vm<0>();  // no W staged by this wave: only its pieces of the next chunk's halo
             }
             sync_in();
-            mma(1);
+            mma();
             sync_out();
         }
     }
     if (!late) __builtin_amdgcn_s_barrier();  // re-align the groups' barrier counts
 }
 
-template <int S, int BN>
+template <int S, int BN, int DBG = 0>
 __global__ __launch_bounds__(512, 1) void halo2_kernel(EngineArgs p) {
     __shared__ __attribute__((aligned(16))) char smem[H2Cfg<S, BN>::LDS];
     // XCD-contiguous tile ids (consecutive ids share an XCD's L2: the two channel tiles of one pixel tile and
@@ -1655,7 +1652,7 @@ __global__ __launch_bounds__(512, 1) void halo2_kernel(EngineArgs p) {
     const int ty = rest % ty_n, img = rest / ty_n;
     const int y0 = ty * h2::TH, x0 = tx * h2::TW;
     f32x4 acc[H2Cfg<S, BN>::TI][4];
-    halo2_mainloop<S, BN>(p, smem, img, y0, x0, tn * BN, acc);
+    halo2_mainloop<S, BN, DBG>(p, smem, img, y0, x0, tn * BN, acc);
     engine_epilogue<H2Tile<BN>, E_CONV, h2::TW, BN == 64>(p, (img * p.ho + y0) * p.wo + x0, tn * BN, acc);
 }
 
@@ -2523,14 +2520,23 @@ static bool halo2_ok(const EngineArgs& a) {
 static int launch_halo2(EngineArgs a, void* stream, const char* what) {
     const bool n64 = a.n == 64;
     const int nwg = (a.m / 512) * (n64 ? 1 : a.n / 128);
-    const char* env = getenv("RF_CONV_H2S");  // W ring depth: 4 (default) or 3
-    const bool s3 = env && atoi(env) == 3;
+    const char* env = getenv("RF_CONV_H2S");  // W ring depth (slices in flight + 1): 4 (default), 3 or 5
+    const int ring = env ? atoi(env) : 4;
     const hipStream_t st = (hipStream_t)stream;
+    const int dbg = getenv("RF_H2_DBG") ? atoi(getenv("RF_H2_DBG")) : 0;  // ablation timing only
+    if (!n64 && ring == 4 && dbg >= 1 && dbg <= 3) {
+        if (dbg == 1) RF_LAUNCH((halo2_kernel<4, 128, 1>), dim3(nwg), dim3(512), 0, st, a);
+        if (dbg == 2) RF_LAUNCH((halo2_kernel<4, 128, 2>), dim3(nwg), dim3(512), 0, st, a);
+        if (dbg == 3) RF_LAUNCH((halo2_kernel<4, 128, 3>), dim3(nwg), dim3(512), 0, st, a);
+        return rf::check_launch(what);
+    }
     if (n64) {
-        if (s3) RF_LAUNCH((halo2_kernel<3, 64>), dim3(nwg), dim3(512), 0, st, a);
+        if (ring == 3) RF_LAUNCH((halo2_kernel<3, 64>), dim3(nwg), dim3(512), 0, st, a);
+        else if (ring == 5) RF_LAUNCH((halo2_kernel<5, 64>), dim3(nwg), dim3(512), 0, st, a);
         else RF_LAUNCH((halo2_kernel<4, 64>), dim3(nwg), dim3(512), 0, st, a);
     } else {
-        if (s3) RF_LAUNCH((halo2_kernel<3, 128>), dim3(nwg), dim3(512), 0, st, a);
+        if (ring == 3) RF_LAUNCH((halo2_kernel<3, 128>), dim3(nwg), dim3(512), 0, st, a);
+        else if (ring == 5) RF_LAUNCH((halo2_kernel<5, 128>), dim3(nwg), dim3(512), 0, st, a);
         else RF_LAUNCH((halo2_kernel<4, 128>), dim3(nwg), dim3(512), 0, st, a);
     }
     return rf::check_launch(what);

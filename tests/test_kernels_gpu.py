@@ -795,7 +795,7 @@ def test_conv_halo(cin, cout, hw, tile, monkeypatch):
     assert relerr(_planes_value(pl)[..., :cout].cpu(), F.silu(ref)) < 1e-3
 
 
-@pytest.mark.parametrize("h2s", ["3", "4"])
+@pytest.mark.parametrize("h2s", ["3", "4", "5"])
 @pytest.mark.parametrize("cin,cout,hh,ww,n_img", [(256, 128, 32, 64, 2), (128, 256, 48, 32, 1), (32, 128, 16, 32, 3),
                                                   (96, 128, 16, 96, 1), (256, 256, 64, 64, 1), (128, 32, 32, 64, 2),
                                                   (64, 64, 16, 32, 1)])

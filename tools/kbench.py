@@ -189,9 +189,10 @@ def conv():
             for t in tiles:
                 os.environ["RF_CONV_PHASED"] = "1" if t == "256ph" else "0"
                 os.environ["RF_CONV_SKW8"] = "0" if t == "auto4w" else "1"
-                # h2 / h2s4: the 16 x 32-pixel halo kernel (3- / 4-deep W ring); every other label runs without it
+                # h2 / h2s3 / h2s5: the 16 x 32-pixel halo kernel (4- / 3- / 5-deep W ring); other labels run without it
                 os.environ["RF_CONV_HALO2"] = "1" if t.startswith("h2") else "0"
-                os.environ["RF_CONV_H2S"] = "3" if t == "h2s3" else "4"
+                os.environ["RF_CONV_H2S"] = t[4:] if t.startswith("h2s") else "4"
+                os.environ["RF_H2_DBG"] = t[4:] if t.startswith("h2db") else "0"  # h2db1/2/3: ablations
                 if not t.startswith("auto") and not t.startswith("h2"):
                     os.environ["RF_CONV_TILE"] = t.replace("ph", "")
                 ms = timeit(lambda: conv(x, out_f32=True), reps=10)
