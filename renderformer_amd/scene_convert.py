@@ -13,9 +13,11 @@ This module does the same in numpy with no trimesh/h5py/dacite (none is installe
   are kept as written, nothing is merged.
 * Transforms exactly as scene_mesh.py:41-55: unit-sphere normalisation (:13-18), rotations about x, y, z in that
   order, per-axis scale, translation.
-* Smooth shading: faces are grouped by edge adjacency across dihedral angles below 30 degrees; every group gets
-  its own copy of its vertices and angle-weighted vertex normals.  This restates what trimesh.graph.smooth_shade
-  does, but trimesh is third-party and absent, so the group order and the normal weighting are PARITY UNPINNED
+* Smooth shading: faces are grouped by edge adjacency across dihedral angles below 30 degrees, with
+  trimesh's large-facet rule (coplanar facets over 1/10 of the mesh area are shaded alone, ``smooth_groups``);
+  every group gets its own copy of its vertices and angle-weighted vertex normals.  This restates what
+  trimesh.graph.smooth_shade does, but trimesh is third-party and absent, so the grouping details (facet
+  coplanarity test, group order) and the normal weighting are PARITY UNPINNED
   (for the planar-walled example scenes such as cbox every group is planar and the normals are the plane
   normals under any weighting).  Flat shading: per-face vertices, normals = face normals.
 * The OBJ round trip of the reference (export at 8 decimals, reload) is reproduced by rounding vertices and
@@ -202,15 +204,18 @@ def _face_angles(tris: np.ndarray) -> np.ndarray:
     return out
 
 
-def smooth_groups(v: np.ndarray, f: np.ndarray, angle: float = SMOOTH_ANGLE) -> List[np.ndarray]:
-    """Face groups connected through shared edges whose dihedral angle is below `angle` (union-find),
-    ordered by their first face."""
-    fn = _face_normals(v[f])
-    edges = {}
-    for fi, (a, b, c) in enumerate(f):
-        for e in ((a, b), (b, c), (c, a)):
-            edges.setdefault((min(e), max(e)), []).append(fi)
-    parent = np.arange(len(f))
+# trimesh.graph.facets declares two adjacent faces coplanar when (face_adjacency_radius / span)^2 exceeds
+# tol.facet_threshold = 5000; with radius = span / (2 sin(theta / 2)) that is a dihedral angle below
+# 2 asin(1 / (2 sqrt(5000))) = 0.81 degrees (restated from trimesh's published source, which is not installed
+# here: PARITY UNPINNED, like the rest of the smooth-shading restatement)
+FACET_ANGLE = 2.0 * math.asin(1.0 / (2.0 * math.sqrt(5000.0)))
+FACET_MINAREA = 10.0  # smooth_shade's default: facets larger than mesh.area / 10 are shaded on their own
+
+
+def _components(n: int, pairs, keep=None) -> List[List[int]]:
+    """Connected components of faces 0..n-1 over the given adjacency pairs (union-find), ordered by their first
+    face; with ``keep`` only those faces take part."""
+    parent = np.arange(n)
 
     def find(x):
         while parent[x] != x:
@@ -218,23 +223,68 @@ def smooth_groups(v: np.ndarray, f: np.ndarray, angle: float = SMOOTH_ANGLE) -> 
             x = parent[x]
         return x
 
-    for fs in edges.values():
-        for i in range(len(fs)):
-            for j in range(i + 1, len(fs)):
-                a, b = fs[i], fs[j]
-                if math.acos(max(-1.0, min(1.0, float(fn[a] @ fn[b])))) < angle:
-                    ra, rb = find(a), find(b)
-                    if ra != rb:
-                        parent[max(ra, rb)] = min(ra, rb)
-    roots = np.array([find(i) for i in range(len(f))])
-    order = []
-    seen = {}
-    for fi, r in enumerate(roots):
+    for a, b in pairs:
+        ra, rb = find(a), find(b)
+        if ra != rb:
+            parent[max(ra, rb)] = min(ra, rb)
+    order, seen = [], {}
+    for fi in range(n):
+        if keep is not None and not keep[fi]:
+            continue
+        r = find(fi)
         if r not in seen:
             seen[r] = len(order)
             order.append([])
         order[seen[r]].append(fi)
-    return [np.asarray(g, dtype=np.int64) for g in order]
+    return order
+
+
+def smooth_groups(v: np.ndarray, f: np.ndarray, angle: float = SMOOTH_ANGLE,
+                  facet_minarea: Optional[float] = FACET_MINAREA) -> List[np.ndarray]:
+    """Shading groups of trimesh.graph.smooth_shade(mesh, angle, facet_minarea) (scene_mesh.py:58):
+    faces joined through shared edges whose dihedral angle is below `angle`, except that every facet (a
+    connected set of >= 2 coplanar faces) with more than 1/facet_minarea of the mesh's area is cut out of that
+    adjacency and becomes a group of its own, so large flat regions keep their plane normals and do not bend
+    their neighbours' normals.  Order: the smoothed components, then the large facets, then faces left alone.
+    Group order only orders triangles in the output (the renderer is invariant to it); the seeded random
+    colours follow it."""
+    tris = v[f]
+    fn = _face_normals(tris)
+    edges = {}
+    for fi, (a, b, c) in enumerate(f):
+        for e in ((a, b), (b, c), (c, a)):
+            edges.setdefault((min(e), max(e)), []).append(fi)
+    adj, dih = [], []
+    for fs in edges.values():
+        for i in range(len(fs)):
+            for j in range(i + 1, len(fs)):
+                a, b = fs[i], fs[j]
+                adj.append((a, b))
+                dih.append(math.acos(max(-1.0, min(1.0, float(fn[a] @ fn[b])))))
+    n = len(f)
+    smooth = [p for p, d in zip(adj, dih) if d < angle]
+    facets = []
+    if facet_minarea is not None and smooth:
+        area = 0.5 * np.linalg.norm(np.cross(tris[:, 1] - tris[:, 0], tris[:, 2] - tris[:, 0]), axis=-1)
+        flat = [p for p, d in zip(adj, dih) if d < FACET_ANGLE]
+        cand = [g for g in _components(n, flat) if len(g) >= 2]
+        facets = [g for g in cand if area[g].sum() > area.sum() / facet_minarea]
+    if not facets:
+        return [np.asarray(g, dtype=np.int64) for g in _components(n, smooth)]
+    free = np.ones(n, dtype=bool)
+    for g in facets:
+        free[g] = False
+    smooth = [(a, b) for a, b in smooth if free[a] and free[b]]
+    in_pair = np.zeros(n, dtype=bool)
+    for a, b in smooth:
+        in_pair[a] = in_pair[b] = True
+    groups = _components(n, smooth, keep=in_pair)  # connected_components(min_len=2) over the remaining pairs
+    groups += facets
+    covered = np.zeros(n, dtype=bool)
+    for g in groups:
+        covered[g] = True
+    groups += [[int(i)] for i in np.flatnonzero(~covered)]  # loose faces, one group each
+    return [np.asarray(g, dtype=np.int64) for g in groups]
 
 
 def vertex_normals(v: np.ndarray, f: np.ndarray) -> np.ndarray:
@@ -256,7 +306,7 @@ def shade(v: np.ndarray, f: np.ndarray, smooth: bool):
         fn = _face_normals(tris)
         return tris, np.repeat(fn[:, None], 3, axis=1), np.arange(len(f))
     tris, vns, gid = [], [], []
-    for g, faces in enumerate(smooth_groups(v, f)):
+    for g, faces in enumerate(smooth_groups(v, f, facet_minarea=FACET_MINAREA)):
         used, local = np.unique(f[faces], return_inverse=True)
         lf = local.reshape(-1, 3)
         lv = v[used]

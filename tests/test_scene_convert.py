@@ -8,6 +8,7 @@ come from trimesh in the reference (absent here): parity unpinned, checked only 
 weighting gives the plane normal.
 """
 import json
+import math
 import os
 
 import numpy as np
@@ -83,6 +84,34 @@ def test_smooth_shading_cube_and_flat(tmp_path):
     t2, vn2, _ = sc.shade(verts, faces, False)
     assert np.allclose(vn2, np.cross(t2[:, 1] - t2[:, 0], t2[:, 2] - t2[:, 0])[:, None, :].repeat(3, 1) /
                        np.linalg.norm(np.cross(t2[:, 1] - t2[:, 0], t2[:, 2] - t2[:, 0]), axis=-1)[:, None, None])
+
+
+def test_smooth_shading_large_facet_kept_flat():
+    """trimesh's smooth_shade facet rule (restated, parity unpinned): a coplanar facet over 1/10 of the mesh
+    area next to a gently curved 15-20 degree bend is shaded on its own (plane normals), while without the
+    rule the bend (below 30 degrees) joins it into one group and bends its boundary normals."""
+    t20, t15 = math.tan(math.radians(20.0)), math.tan(math.radians(15.0))
+    v = [(0, 4, 0), (0, 0, 0)]                                              # 0, 1: far corners of the square
+    v += [(4, y, 0) for y in range(5)]                                      # 2..6: shared edge x = 4
+    v += [(5, y, t20 if y % 2 == 0 else t15) for y in range(5)]             # 7..11: strip's outer edge
+    f = [(0, 1, 2)] + [(0, 2 + y, 3 + y) for y in range(4)]                 # flat square (area 16) as a fan
+    for y in range(4):
+        f += [(2 + y, 7 + y, 8 + y), (2 + y, 8 + y, 3 + y)]                 # strip faces 5..12, not coplanar
+    verts, faces = np.asarray(v, dtype=np.float64), np.asarray(f, dtype=np.int64)
+    groups = sorted(sorted(g.tolist()) for g in sc.smooth_groups(verts, faces))
+    assert groups == [[0, 1, 2, 3, 4], list(range(5, 13))]
+    assert len(sc.smooth_groups(verts, faces, facet_minarea=None)) == 1
+    tris, vn, _ = sc.shade(verts, faces, True)
+    flat = np.isclose(tris[..., 2], 0).all(-1)
+    assert flat.sum() == 5 and np.allclose(vn[flat], [0.0, 0.0, 1.0])
+    # without the rule the shared-edge vertices average in the strip's normals
+    old = sc.FACET_MINAREA
+    try:
+        sc.FACET_MINAREA = None
+        _, vn0, _ = sc.shade(verts, faces, True)
+    finally:
+        sc.FACET_MINAREA = old
+    assert not np.allclose(vn0[flat], [0.0, 0.0, 1.0])
 
 
 def test_schema_is_strict(tmp_path):

@@ -257,10 +257,13 @@ def coldgemm():
     shapes = [("s1 qkv", S, 3 * D, D, ops.EPI_BF16), ("s1 out", S, D, D, ops.EPI_ADD_F32),
               ("s1 w2", S, D, F, ops.EPI_ADD_F32), ("s2 q", R, D, D, ops.EPI_BF16),
               ("s2 qkv", R, 3 * D, D, ops.EPI_BF16), ("s2 out", R, D, D, ops.EPI_ADD_F32),
-              ("s2 w2", R, D, F, ops.EPI_ADD_F32), ("kvall", S, 20 * D, D, ops.EPI_BF16)]
+              ("s2 w2", R, D, F, ops.EPI_ADD_F32), ("kvall", S, 20 * D, D, ops.EPI_BF16),
+              ("s1 w13", S, 2 * F, D, ops.EPI_SWIGLU), ("s2 w13", R, 2 * F, D, ops.EPI_SWIGLU)]
     if os.environ.get("KB_SHAPES"):
         shapes = [x for x in shapes if x[0] in os.environ["KB_SHAPES"].split(",")]
     tiles = os.environ.get("KB_TILES", "auto").split(",")
+    # KB_GROUP_M: comma list of RF_GEMM_GROUP_M raster overrides tried for every tile code (- = the host's pick)
+    groups = os.environ.get("KB_GROUP_M", "-").split(",")
     for name, m, n, k, epi in shapes:
         per = m * k * 2 + n * k * 2 + m * n * 4
         nrot = max(2, int((768 << 20) // per) + 1)
@@ -269,6 +272,7 @@ def coldgemm():
             a = torch.randn(m, k, device=dev).bfloat16()
             w = (torch.randn(n, k, device=dev) / math.sqrt(k)).bfloat16()
             c = (torch.empty(m, n, device=dev, dtype=torch.bfloat16) if epi == ops.EPI_BF16
+                 else torch.empty(m, n // 2, device=dev, dtype=torch.bfloat16) if epi == ops.EPI_SWIGLU
                  else torch.zeros(m, n, device=dev))
             sets.append((a, w, c))
         for t in tiles:
@@ -276,17 +280,23 @@ def coldgemm():
                 os.environ.pop("RF_GEMM_TILE", None)
             else:
                 os.environ["RF_GEMM_TILE"] = t
-            i = [0]
+            for gm in groups:
+                if gm == "-":
+                    os.environ.pop("RF_GEMM_GROUP_M", None)
+                else:
+                    os.environ["RF_GEMM_GROUP_M"] = gm
+                i = [0]
 
-            def run():
-                a, w, c = sets[i[0] % nrot]
-                i[0] += 1
-                ops.gemm(a, w, c, None, epi)
-            ms = timeit(run, reps=3 * nrot)
-            err = check(sets[0][0], sets[0][1], epi)
-            print(f"cold gemm {name:7s} {m}x{n}x{k} tile={t:5s}: {ms*1e3:8.1f} us  {2*m*n*k/ms/1e9:7.1f} TF  "
-                  f"relerr {err:.1e}  ({nrot} rotating operand sets)", flush=True)
+                def run():
+                    a, w, c = sets[i[0] % nrot]
+                    i[0] += 1
+                    ops.gemm(a, w, c, None, epi)
+                ms = timeit(run, reps=3 * nrot)
+                err = check(sets[0][0], sets[0][1], epi)
+                print(f"cold gemm {name:7s} {m}x{n}x{k} tile={t:5s} group_m={gm:>3s}: {ms*1e3:8.1f} us  "
+                      f"{2*m*n*k/ms/1e9:7.1f} TF  relerr {err:.1e}  ({nrot} rotating operand sets)", flush=True)
         os.environ.pop("RF_GEMM_TILE", None)
+        os.environ.pop("RF_GEMM_GROUP_M", None)
         del sets
         torch.cuda.empty_cache()
 
