@@ -1496,7 +1496,8 @@ RF_DEV void wait_vm_rt(int n) {  // vmcnt(n) for a wave-uniform n <= N (the unro
     }
 }
 
-// DBG (ablation timing only, wrong results): 1 = no MFMAs, 2 = no LDS-DMA after the prologue, 3 = no stagger.
+// DBG (ablation timing only, wrong results): 1 = no MFMAs, 2 = no LDS-DMA after the prologue, 3 = no stagger;
+// (right results) 4 = no static priority for the MFMA section, 8 = priority for the load section instead.
 // One step = one load section {W fragments + all TI A fragments, the next chunk's halo piece (taps 0-4), W(kt + S - 1)
 // into the slot step kt - 1 read, counted wait for W(kt + 1)} and one MFMA section (4 TI MFMAs); with the two halves
 // of a step in separate sections (two barriers more per step) the 256^2 conv took 115 instead of 103 us.
@@ -1518,12 +1519,16 @@ RF_DEV void halo2_mainloop(const EngineArgs& p, char* smem, int img, int y0, int
     char* wring = smem + 2 * HBYTES;      // S W stages
 
     // halo staging: piece wave + 8 t of a buffer holds halo pixels 16 (wave + 8 t) .. + 15 (64 B each, 16-B chunk
-    // XOR ((pixel >> 1) & 3), matching lds_off); pixels past the image or past the 612 in use read the zero row
+    // XOR hkey(column) = ((hp mod HWID) >> 2) & 3: a function of the halo column only, so one halo row down is a
+    // constant HWID * 64 bytes for every lane and a tap's fragment address is a per-(column half, tap column)
+    // register plus an immediate (no per-tap address VALU); any 16 consecutive columns of a row still cover the
+    // 16 (pixel mod 4, chunk) bank groups once, so the fragment reads stay conflict-free).  Pixels past the
+    // image or past the 612 in use read the zero row
     int hpix[PPW], hch[PPW];
 #pragma unroll
     for (int t = 0; t < PPW; ++t) {
         const int hp = (wave + 8 * t) * 16 + (lane >> 2);
-        hch[t] = (lane & 3) ^ ((hp >> 1) & 3);
+        hch[t] = (lane & 3) ^ (((hp % HWID) >> 2) & 3);
         int pix = -1;
         if (hp < HPIX) {
             const int hy = hp / HWID, hx = hp - hy * HWID;
@@ -1553,19 +1558,23 @@ RF_DEV void halo2_mainloop(const EngineArgs& p, char* smem, int img, int y0, int
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int frow = lane & 15, fch = lane >> 4;
-    // halo index of fragment i's lane pixel at tap (0, 0): tile row RW wm + i / 2, column 16 (i & 1) + frow
-    int hbase[2];
+    // LDS byte address (in the current halo buffer) of fragment i's lane pixel at tap (ty, tx): tile row
+    // RW wm + i / 2 + ty, halo column hx = 16 (i & 1) + frow + tx; = hadr[i & 1][tx] + (i / 2 + ty) HWID 64,
+    // the second term an immediate of the unrolled loops.  hadr moves between the two halo buffers per chunk.
+    uint32_t hadr[2][3];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) hbase[h] = (G::RW * wm) * HWID + 16 * h + frow;
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) {
+            const int hx = 16 * h + frow + tx;
+            hadr[h][tx] = (uint32_t)(uintptr_t)LDS_PTR(char, hbuf) + ((G::RW * wm) * HWID + hx) * 64 +
+                          ((fch ^ ((hx >> 2) & 3)) << 4);
+        }
     bf16x8 fa[TI], fb[4];
-    auto read_a = [&](const char* hb, int tap) {
-        // opaque per use: otherwise the unrolled taps' 72 fragment addresses are hoisted out of the chunk
-        // loop and held in registers (78 VGPRs spilled)
-        int toff = (tap / 3) * HWID + tap % 3;
-        asm volatile("" : "+s"(toff));
+    auto read_a = [&](int tap) {
 #pragma unroll
         for (int i = 0; i < TI; ++i)
-            fa[i] = *reinterpret_cast<const bf16x8*>(hb + lds_off(hbase[i & 1] + (i >> 1) * HWID + toff, fch));
+            fa[i] = *LDS_PTR(const bf16x8, (uintptr_t)(hadr[i & 1][tap % 3] + ((i >> 1) + tap / 3) * HWID * 64));
     };
     auto read_b = [&](int slot) {
         int soff = slot * WBYTES;
@@ -1577,14 +1586,14 @@ RF_DEV void halo2_mainloop(const EngineArgs& p, char* smem, int img, int y0, int
     };
     auto mma = [&]() {
         if constexpr (DBG == 1) return;
-        __builtin_amdgcn_s_setprio(1);
+        if constexpr (DBG != 4 && DBG != 8) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[j]),
                                                                    __builtin_bit_cast(f16x8, fa[i]), acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
+        if constexpr (DBG != 4 && DBG != 8) __builtin_amdgcn_s_setprio(0);
     };
     auto sync_in = [&]() {
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this section's fragments are in registers
@@ -1613,12 +1622,12 @@ RF_DEV void halo2_mainloop(const EngineArgs& p, char* smem, int img, int y0, int
 
     for (int c = 0; c < nch; ++c) {
         const bool last = c + 1 == nch;
-        const char* hb = hbuf + (c & 1) * HBYTES;
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const int kt = 9 * c + t;
+            if constexpr (DBG == 8) __builtin_amdgcn_s_setprio(1);  // ablation: the load section outranks the MFMAs
             read_b(kt % S);
-            read_a(hb, t);
+            read_a(t);
             // slot (kt - 1) % S was read by both wave groups before the barrier this section started after
             if (DBG != 2 && t < PPW && !last) issue_halo(c + 1, t);
             if (DBG != 2 && kt + S - 1 < nk) issue_w(kt + S - 1);
@@ -1630,10 +1639,16 @@ RF_DEV void halo2_mainloop(const EngineArgs& p, char* smem, int img, int y0, int
             } else if (t == 8 && !last) {
                 wait_vm<0>();  // no W staged by this wave: only its pieces of the next chunk's halo
             }
+            if constexpr (DBG == 8) __builtin_amdgcn_s_setprio(0);
             sync_in();
             mma();
             sync_out();
         }
+        const uint32_t step = (c & 1) ? (uint32_t)-HBYTES : (uint32_t)HBYTES;  // next chunk: the other halo buffer
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int tx = 0; tx < 3; ++tx) hadr[h][tx] += step;
     }
     if (!late) __builtin_amdgcn_s_barrier();  // re-align the groups' barrier counts
 }
@@ -2524,10 +2539,12 @@ static int launch_halo2(EngineArgs a, void* stream, const char* what) {
     const int ring = env ? atoi(env) : 4;
     const hipStream_t st = (hipStream_t)stream;
     const int dbg = getenv("RF_H2_DBG") ? atoi(getenv("RF_H2_DBG")) : 0;  // ablation timing only
-    if (!n64 && ring == 4 && dbg >= 1 && dbg <= 3) {
+    if (!n64 && ring == 4 && dbg >= 1 && dbg <= 8) {
         if (dbg == 1) RF_LAUNCH((halo2_kernel<4, 128, 1>), dim3(nwg), dim3(512), 0, st, a);
         if (dbg == 2) RF_LAUNCH((halo2_kernel<4, 128, 2>), dim3(nwg), dim3(512), 0, st, a);
         if (dbg == 3) RF_LAUNCH((halo2_kernel<4, 128, 3>), dim3(nwg), dim3(512), 0, st, a);
+        if (dbg == 4) RF_LAUNCH((halo2_kernel<4, 128, 4>), dim3(nwg), dim3(512), 0, st, a);
+        if (dbg == 8) RF_LAUNCH((halo2_kernel<4, 128, 8>), dim3(nwg), dim3(512), 0, st, a);
         return rf::check_launch(what);
     }
     if (n64) {
