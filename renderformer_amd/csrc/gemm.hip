@@ -1696,6 +1696,10 @@ using T128w8k2s4 = Tile<128, 128, 2, 4, 4, 2>;
 using T96x256k2 = Tile<96, 256, 2, 4, 3, 2>;
 using T64x256k2 = Tile<64, 256, 2, 4, 3, 2>;
 using T64x256w4k2 = Tile<64, 256, 1, 4, 3, 2>;
+// small DPT levels (64^2 / 32^2 / 128^2 convolutions): 4 waves of 32 x 32 (64 x 64) or 32 x 64 (64 x 128) with an
+// 8- / 6-deep ring, data-parallel (A/B against the stream-K 128x128 default: RF_CONV_TILE=64 / 6412)
+using T64c = Tile<64, 64, 2, 2, 8>;
+using T64x128c = Tile<64, 128, 2, 2, 6>;
 
 int pick_group_m(int tiles_m, int tiles_n, int bm, int bn, int64_t per_xcd) {
     if (const char* env = getenv("RF_GEMM_GROUP_M")) return std::max(1, std::min(tiles_m, atoi(env)));
@@ -2563,13 +2567,15 @@ static int launch_halo2(EngineArgs a, void* stream, const char* what) {
 // wide and there is >= one tile per CU (the im2col gather of A is then read once per pixel tile),
 // 256x64 for <= 64 output channels, else 128x128 (faster than 256x128 on every DPT shape measured)
 template <bool GATHER>
-static int conv_f16_dp(EngineArgs& p, void* stream, const char* what) {
+static int conv_f16_dp(EngineArgs& p, void* stream, const char* what, int tile = 0) {
     if (GATHER && halo2_ok(p)) return launch_halo2(p, stream, what);
     const char* env = getenv("RF_CONV_TILE");
-    const int t = env ? atoi(env) : 0;
+    const int t = tile ? tile : env ? atoi(env) : 0;
     // (RF_CONV_HALO=1 runs it halo-tiled: 90 -> 140 us at 512^2, 128 -> 32; a 128x64 tile at two blocks per
     // CU measured the same 90 us with or without the halo, so the gathered 256x64 launch stays the default)
     if (p.n == 64) return launch_conv<T256x64, P_F16, GATHER>(p, stream, what);
+    if (t == 64 || t == 6464) return launch_conv<T64c, P_F16, GATHER>(p, stream, what);
+    if (t == 6412) return launch_conv<T64x128c, P_F16, GATHER>(p, stream, what);
     if (t == 128) return launch_conv<T128, P_F16, GATHER>(p, stream, what);
     if (t == 1288) return launch_conv<T128w8, P_F16, GATHER>(p, stream, what);
     if (p.n % 256 == 0 && (t == 256 || (!t && ((p.m + 255) / 256) * (p.n / 256) >= 256)))
@@ -2586,9 +2592,10 @@ static int conv_f16_dp(EngineArgs& p, void* stream, const char* what) {
 
 template <int NT>
 static int conv_dispatch(EngineArgs& p, bool gather, bool big, int64_t sk_grid_n, void* workspace, void* stream,
-                         const char* what) {
+                         const char* what, int tile = 0) {
     if constexpr (NT == P_F16) {
-        if (!sk_grid_n) return gather ? conv_f16_dp<true>(p, stream, what) : conv_f16_dp<false>(p, stream, what);
+        if (!sk_grid_n)
+            return gather ? conv_f16_dp<true>(p, stream, what, tile) : conv_f16_dp<false>(p, stream, what, tile);
     }
     if (sk_grid_n) {
         sk_setup(p, workspace);
@@ -2648,13 +2655,33 @@ static int conv_common(EngineArgs& p, int nterm, bool gather, const void* w_hi, 
     // keeping >= 8 K-steps.
     const char* sk_env = getenv("RF_CONV_SK");
     int64_t skg = 0;
-    if (!big && p.n % 128 == 0 && workspace && ws_bytes >= SK_WS_BYTES && !(sk_env && atoi(sk_env) == 0)) {
+    int ct = env ? atoi(env) : 0;
+    // small DPT levels (<= 4,096 output pixels per launch: the 64^2 / 32^2 refinenets and their rn convs): the
+    // 64x64 tile, data-parallel at K <= 2,304 and stream-K above (GPU time per launch, rocprofv3 over
+    // tools/kbench.py conv: 256->256 @32 32.4 -> 26.6 us, @64 30.1 -> 27.6 us, 1024->256 @32 50.4 -> 41.4 us;
+    // 1024->256 @64 stays on the default, 54.4 vs 68.1 us).  RF_CONV_SMALL=0 keeps the default tiles.
+    static const bool small_on = !getenv("RF_CONV_SMALL") || atoi(getenv("RF_CONV_SMALL")) != 0;
+    if (!ct && small_on && nterm == P_F16 && gather && p.kw == 3 && p.n % 64 == 0 && p.m <= 4096 &&
+        (p.k <= 2304 || p.m <= 1024))
+        ct = p.k <= 2304 ? 64 : 6464;
+    if (nterm == P_F16 && ct == 6464 && p.n % 64 == 0 && workspace && ws_bytes >= SK_WS_BYTES) {
+        // A/B: stream-K over the 64x64 small-level tile, up to two blocks per CU, >= 12 K-steps per block
+        const int64_t tiles = (int64_t)((p.m + 63) / 64) * (p.n / 64);
+        const int64_t grid = std::min<int64_t>(512, tiles * (p.k / BK) / 12);
+        if (grid > tiles) {
+            sk_setup(p, workspace);
+            return gather ? launch_sk<T64c, E_CONV, P_F16, true>(p, (int)grid, stream, what)
+                          : launch_sk<T64c, E_CONV, P_F16, false>(p, (int)grid, stream, what);
+        }
+    }
+    if (!big && p.n % 128 == 0 && workspace && ws_bytes >= SK_WS_BYTES && !(sk_env && atoi(sk_env) == 0) &&
+        !(nterm == P_F16 && (ct == 64 || ct == 6412 || ct == 6464))) {
         const int64_t tiles = (int64_t)((p.m + 127) / 128) * (p.n / 128);
         const int64_t work = tiles * (p.k / BK);
         const int64_t grid = std::min<int64_t>(256, work / 8);
         if (tiles < 192 && grid > tiles) skg = grid;
     }
-    return nterm == P_F16 ? conv_dispatch<P_F16>(p, gather, big, skg, workspace, stream, what)
+    return nterm == P_F16 ? conv_dispatch<P_F16>(p, gather, big, skg, workspace, stream, what, ct == 64 ? 64 : 0)
                           : conv_dispatch<3>(p, gather, big, skg, workspace, stream, what);
 }
 

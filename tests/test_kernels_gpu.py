@@ -728,15 +728,20 @@ def _planes_value(pl):
     return pl.hi.float() if pl.f16 else pl.hi.float() + pl.lo.float()
 
 
-@pytest.mark.parametrize("tile", ["auto", "4w"])
+@pytest.mark.parametrize("tile", ["auto", "4w", "64", "6412", "6464"])
 @pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("cin,cout,k,stride,hw", [(64, 128, 3, 1, 17), (256, 256, 3, 1, 32), (16, 32, 3, 1, 20),
                                                    (1024, 128, 1, 1, 16), (128, 128, 3, 2, 16), (48, 200, 3, 1, 9)])
 def test_conv_matches_fp64(cin, cout, k, stride, hw, prec, tile, monkeypatch):
-    """auto: small grids on the 8-wave 128x128 tile (data-parallel or stream-K); 4w: the 4-wave tile."""
+    """auto: small grids on the 8-wave 128x128 tile (data-parallel or stream-K); 4w: the 4-wave tile; 64 / 6412:
+    the data-parallel 64x64 / 64x128 small-level tiles, 6464: stream-K over the 64x64 tile (fp16 only)."""
+    if tile in ("64", "6412", "6464") and prec != "f16":
+        pytest.skip("the small-level tiles serve fp16 operands")
     if tile == "4w":
         monkeypatch.setenv("RF_CONV_SKW8", "0")
         monkeypatch.setenv("RF_CONV_TILE", "128")
+    elif tile != "auto":
+        monkeypatch.setenv("RF_CONV_TILE", tile)
     from renderformer_amd.dpt import _Conv, split_planes
     f16 = prec == "f16"
     g = torch.Generator(device="cpu").manual_seed(cin + cout)

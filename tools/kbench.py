@@ -179,8 +179,11 @@ def norms():
 def conv():
     from renderformer_amd.dpt import _Conv, split_planes
     for f16 in (True,) if os.environ.get("KB_F16_ONLY") else (True, False):
-        for cin, cout, hw in [(256, 256, 256), (256, 128, 512), (256, 256, 128), (256, 256, 64), (256, 256, 32),
-                              (128, 256, 256), (128, 32, 512)]:
+        shapes = [(256, 256, 256), (256, 128, 512), (256, 256, 128), (256, 256, 64), (256, 256, 32),
+                  (128, 256, 256), (128, 32, 512), (512, 256, 128), (1024, 256, 64), (1024, 256, 32)]
+        if os.environ.get("KB_CONV_HW"):  # only these output resolutions
+            shapes = [x for x in shapes if str(x[2]) in os.environ["KB_CONV_HW"].split(",")]
+        for cin, cout, hw in shapes:
             conv = _Conv(torch.randn(cout, cin, 3, 3) / 48, torch.randn(cout), dev, f16=f16)
             x = split_planes(torch.randn(1, hw, hw, cin, device=dev), conv.cin_pad, f16=f16)
             fl = 2 * hw * hw * cin * cout * 9
