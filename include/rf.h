@@ -39,6 +39,8 @@
  *   rf_split_planes    (operand preparation for the above; no reference counterpart)
  *   rf_deconv2d_bf16x3 DPT nn.ConvTranspose2d kernel == stride (dpt.py:195-206; aten conv_transpose2d)
  *   rf_upsample_bilinear F.interpolate(bilinear, align_corners=True) (dpt.py:154-155, 269-270)
+ *   rf_upsample_bilinear_h  the same resize on fp16 planes: refinenet1's output straight into output_conv1,
+ *                      whose weights hold the folded 1x1 out_conv (dpt.py:157-159, 268-271; RF_CONV_BORDER_BIAS)
  */
 #ifndef RF_H
 #define RF_H
@@ -55,7 +57,7 @@ extern "C" {
 #define RF_ERR_UNSUPPORTED 3
 #define RF_ERR_DEVICE 4       /* an earlier launch reported a device-side error (see rf_device_error) */
 
-#define RF_ABI_VERSION 10
+#define RF_ABI_VERSION 11
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -293,12 +295,16 @@ int rf_hdr_output(const float* logits, float* out, int n, int c, int h, int w, f
  * RF_CONV_SILU_OUT; v is stored to `out` (f32, may be NULL) and/or split into the output planes
  * p_hi/p_lo (channel stride p_ld), of silu(v) when RF_CONV_PLANE_SILU.
  * RF_CONV_FINAL (cout <= 64): out[pixel, f] = elu(sum_c silu(v_c) * w_fin[f, c] + b_fin[f], alpha),
- * then 10^x - 1 with RF_CONV_LOG_DECODE; [n, n_fin, h, w] layout with RF_CONV_NCHW_OUT. */
+ * then 10^x - 1 with RF_CONV_LOG_DECODE; [n, n_fin, h, w] layout with RF_CONV_NCHW_OUT.
+ * RF_CONV_BORDER_BIAS (3x3, pad 1, stride 1): `bias` holds 9 rows of cout, row 3 ry + rx with ry / rx = 0 on the
+ * first image row / column, 2 on the last, 1 elsewhere: the bias of a convolution whose input carried a constant
+ * that zero padding cuts at the border (an affine 1x1 folded into the 3x3 weights, dpt.py output_conv1). */
 #define RF_CONV_PLANE_SILU 1
 #define RF_CONV_SILU_OUT 2
 #define RF_CONV_FINAL 4
 #define RF_CONV_LOG_DECODE 8
 #define RF_CONV_NCHW_OUT 16
+#define RF_CONV_BORDER_BIAS 32
 int rf_conv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, int wi, int cin_pad, const void* w_hi,
                      const void* w_lo, int cout, int cout_pad, int kh, int kw, int stride, int pad, const float* bias,
                      const float* res1, const float* res2, float* out, void* p_hi, void* p_lo, int p_ld, int flags,
@@ -333,6 +339,12 @@ int rf_split_planes(const float* x, int64_t rows, int c, int64_t ldx, void* p_hi
  * (p_lo == NULL: one fp16 plane, as rf_split_planes). */
 int rf_upsample_bilinear(const float* in, int n_img, int hi, int wi, int c, float* out, int ho, int wo, void* p_hi,
                          void* p_lo, int p_ld, void* stream);
+
+/* The same resize from one fp16 plane (channel stride in_ld, c % 8 == 0) into one fp16 plane (channel stride
+ * p_ld): values widened to f32, blended as rf_upsample_bilinear, rounded once (F.interpolate of the plane's
+ * values; dpt.py:268-271 with output_conv1's preceding 1x1 folded into its weights). */
+int rf_upsample_bilinear_h(const void* in, int in_ld, int n_img, int hi, int wi, int c, int ho, int wo, void* p_out,
+                           int p_ld, void* stream);
 
 #ifdef __cplusplus
 }

@@ -49,6 +49,9 @@ RF_DEV uint32_t pack_f16x2(float lo, float hi) {
     return (uint32_t)*reinterpret_cast<uint16_t*>(&a) | ((uint32_t)*reinterpret_cast<uint16_t*>(&b) << 16);
 }
 
+// fp16 bits -> f32 (exact)
+RF_DEV float f16_bits_to_f32(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
+
 RF_DEV float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -136,7 +136,62 @@ __global__ __launch_bounds__(256) void upsample8_kernel(const float* __restrict_
     }
 }
 
+// fp16 plane in (channel stride in_ld) -> fp16 plane out, 8 channels per thread, the blend of upsample8_kernel
+__global__ __launch_bounds__(256) void upsample8h_kernel(const uint16_t* __restrict__ in, int in_ld,
+                                                         uint16_t* __restrict__ p_out, int p_ld, int hi, int wi, int c,
+                                                         int ho, int wo, float sh, float sw) {
+    const int c8n = c >> 3;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= wo * c8n) return;
+    const int row = blockIdx.y;  // img * ho + oy
+    const int img = row / ho, oy = row - img * ho;
+    const int ox = i / c8n;
+    const int cc = (i - ox * c8n) * 8;
+    const float fy = sh * (float)oy, fx = sw * (float)ox;
+    const int y0 = (int)fy, x0 = (int)fx;
+    const int y1 = y0 + (y0 < hi - 1 ? 1 : 0), x1 = x0 + (x0 < wi - 1 ? 1 : 0);
+    const float ly1 = fy - (float)y0, lx1 = fx - (float)x0;
+    const float ly0 = 1.0f - ly1, lx0 = 1.0f - lx1;
+    const uint16_t* base = in + (int64_t)img * hi * wi * in_ld + cc;
+    const uint4 qa = *reinterpret_cast<const uint4*>(base + (int64_t)(y0 * wi + x0) * in_ld);
+    const uint4 qb = *reinterpret_cast<const uint4*>(base + (int64_t)(y0 * wi + x1) * in_ld);
+    const uint4 qd = *reinterpret_cast<const uint4*>(base + (int64_t)(y1 * wi + x0) * in_ld);
+    const uint4 qe = *reinterpret_cast<const uint4*>(base + (int64_t)(y1 * wi + x1) * in_ld);
+    const uint32_t wa[4] = {qa.x, qa.y, qa.z, qa.w}, wb[4] = {qb.x, qb.y, qb.z, qb.w};
+    const uint32_t wd[4] = {qd.x, qd.y, qd.z, qd.w}, we[4] = {qe.x, qe.y, qe.z, qe.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float r[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float a = f16_bits_to_f32((uint16_t)(wa[k] >> (16 * h))), b = f16_bits_to_f32((uint16_t)(wb[k] >> (16 * h)));
+            const float d = f16_bits_to_f32((uint16_t)(wd[k] >> (16 * h))), e = f16_bits_to_f32((uint16_t)(we[k] >> (16 * h)));
+            r[h] = ly0 * (lx0 * a + lx1 * b) + ly1 * (lx0 * d + lx1 * e);
+        }
+        o[k] = pack_f16x2(r[0], r[1]);
+    }
+    *reinterpret_cast<uint4*>(p_out + ((int64_t)row * wo + ox) * p_ld + cc) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 }  // namespace
+
+extern "C" int rf_upsample_bilinear_h(const void* in, int in_ld, int n_img, int hi, int wi, int c, int ho, int wo,
+                                      void* p_out, int p_ld, void* stream) {
+    RF_REQUIRE(in && p_out, "rf_upsample_bilinear_h: null pointer");
+    RF_REQUIRE(c % 8 == 0 && in_ld % 8 == 0 && p_ld % 8 == 0 && in_ld >= c && p_ld >= c,
+               "rf_upsample_bilinear_h: bad widths (c, in_ld, p_ld multiples of 8)");
+    RF_REQUIRE(((uintptr_t)in & 15) == 0 && ((uintptr_t)p_out & 15) == 0, "rf_upsample_bilinear_h: 16-B alignment");
+    if ((int64_t)n_img * ho * wo <= 0) return RF_OK;
+    RF_REQUIRE((int64_t)wo * (c / 8) < (1 << 30) && (int64_t)n_img * ho < 65536 && (int64_t)hi * wi < (1 << 30),
+               "rf_upsample_bilinear_h: image too large");
+    const float sh = ho > 1 ? (float)(hi - 1) / (float)(ho - 1) : 0.f;
+    const float sw = wo > 1 ? (float)(wi - 1) / (float)(wo - 1) : 0.f;
+    const dim3 grid((unsigned)((wo * (c / 8) + 255) / 256), (unsigned)(n_img * ho));
+    RF_LAUNCH(upsample8h_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const uint16_t*)in, in_ld,
+              (uint16_t*)p_out, p_ld, hi, wi, c, ho, wo, sh, sw);
+    return rf::check_launch("rf_upsample_bilinear_h");
+}
 
 extern "C" int rf_split_planes(const float* x, int64_t rows, int c, int64_t ldx, void* p_hi, void* p_lo, int p_ld,
                                int silu_act, void* stream) {

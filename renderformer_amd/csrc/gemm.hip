@@ -487,17 +487,22 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
         }
         const int kk = p.deconv;
         const int nreal = kk ? p.cout * kk * kk : p.cout;
+        const bool border = (p.flags & RF_CONV_BORDER_BIAS) && !kk;
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
             const int m = frow(i);
             if (m >= p.m) continue;
             int img = 0, y = 0, x = 0;
-            if (kk) {
+            if (kk || border) {
                 x = m % p.wo;
                 const int t = m / p.wo;
                 y = t % p.ho;
                 img = t / p.ho;
             }
+            // RF_CONV_BORDER_BIAS: bias row 3 ry + rx of the pixel's border class (rf.h)
+            const float* brow = p.bias;
+            if (border && brow)
+                brow += (3 * (y == 0 ? 0 : y == p.ho - 1 ? 2 : 1) + (x == 0 ? 0 : x == p.wo - 1 ? 2 : 1)) * p.cout;
             float4 r1[TJ], r2[TJ];
             int64_t pixv[TJ];
             int cov[TJ];
@@ -531,7 +536,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                 const float rr2[4] = {r2[j].x, r2[j].y, r2[j].z, r2[j].w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    if (p.bias) v[e] += p.bias[co + e];
+                    if (brow) v[e] += brow[co + e];
                     v[e] = (v[e] + rr1[e]) + rr2[e];
                     if (p.flags & RF_CONV_SILU_OUT) v[e] = silu_precise(v[e]);
                 }
@@ -2622,6 +2627,10 @@ static int conv_common(EngineArgs& p, int nterm, bool gather, const void* w_hi, 
     RF_REQUIRE(!p_hi || ((p_lo || nterm == P_F16) && p_ld % 4 == 0 && p_ld >= cout), "%s: bad plane output", what);
     RF_REQUIRE(!(flags & RF_CONV_FINAL) || (cout <= 64 && w_fin && b_fin && n_fin > 0 && out),
                "%s: final head needs cout <= 64 and w_fin/b_fin", what);
+    RF_REQUIRE(!(flags & RF_CONV_BORDER_BIAS) ||
+                   (bias && !(flags & RF_CONV_FINAL) && p.kw == 3 && p.k == 9 * p.cin_pad && p.stride == 1 &&
+                    p.pad == 1 && p.ho == p.hi && p.wo == p.wi && p.deconv == 0),
+               "%s: RF_CONV_BORDER_BIAS needs a 3x3 stride-1 pad-1 convolution with its 9-row bias", what);
     static void* z = nullptr;  // device address of the zero row (per process; single device per process)
     if (!z && hipGetSymbolAddress(&z, HIP_SYMBOL(g_zero_row)) != hipSuccess) {
         z = nullptr;

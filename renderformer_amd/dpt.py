@@ -20,9 +20,15 @@ Graph with two exact rewrites:
 * The final ``F.interpolate`` to (hp*patch, wp*patch) is the identity (path_1 is
   already 8*hp for patch 8, align_corners=True) and is skipped; output_conv2's
   SiLU + 1x1 + the ELU + 10^x - 1 decode are fused into the last 3x3 conv.
+* (fp16 mode) refinenet1's 1x1 ``out_conv`` is folded into ``output_conv1``:
+  conv3x3(up(W1 y + b1)) = conv3x3'(up(y)) + a border-class bias, with conv3x3' =
+  W3 (x) W1 per tap (``fold_affine_1x1``).  The resize then reads refinenet1's fp16
+  planes directly and neither the 1x1 launch nor its fp32 output remain
+  (``RF_DPT_FOLD=0`` restores the unfolded path).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -30,7 +36,7 @@ import torch
 
 from ._lib import call, ptr, stream
 
-PLANE_SILU, SILU_OUT, FINAL, LOG_DECODE, NCHW_OUT = 1, 2, 4, 8, 16
+PLANE_SILU, SILU_OUT, FINAL, LOG_DECODE, NCHW_OUT, BORDER_BIAS = 1, 2, 4, 8, 16, 32
 BK, BN = 32, 128
 
 
@@ -85,6 +91,34 @@ def upsample(x: torch.Tensor, ho: int, wo: int, out_f32: bool = True, planes_ld:
     return out, pl
 
 
+def upsample_planes(x: Planes, ho: int, wo: int, planes_ld: int) -> Planes:
+    """fp16 planes -> bilinear (align_corners=True) fp16 planes of ho x wo (rf_upsample_bilinear_h)."""
+    n, h, w, ld = x.shape
+    c = _pad(x.c, 8)
+    pl = Planes.empty(n, ho, wo, x.c, planes_ld, x.hi.device, True)
+    call("rf_upsample_bilinear_h", ptr(x.hi), ld, n, h, w, c, ho, wo, ptr(pl.hi), planes_ld, stream())
+    return pl
+
+
+def fold_affine_1x1(w3: torch.Tensor, b3: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor):
+    """conv3x3(W3, b3, pad 1)(up(conv1x1(W1, b1)(y))) == conv3x3(W, pad 1)(up(y)) + B[border class]  (exact):
+    the per-pixel affine 1x1 commutes with the bilinear resize (which reproduces constants), so the 3x3 sees
+    W3 (x) W1 applied to up(y) plus the constant b1, and zero padding cuts b1 out of the taps that fall outside
+    the image -- the bias depends on whether the pixel is on the first / last row and column.
+    Returns W [cout, cin1, 3, 3] and B [9, cout] (row 3 ry + rx, rf.h RF_CONV_BORDER_BIAS), float64."""
+    w3 = w3.detach().double().cpu()
+    w1 = w1.detach().double().cpu().reshape(w1.shape[0], w1.shape[1])
+    w = torch.einsum("ocyx,ci->oiyx", w3, w1)
+    tap = torch.einsum("ocyx,c->oyx", w3, b1.detach().double().cpu())  # b1 through each tap
+    keep = {0: [1, 2], 1: [0, 1, 2], 2: [0, 1]}  # class 0: tap 0 reads row / column -1; class 2: tap 2 reads the end
+    b = torch.empty(9, w3.shape[0], dtype=torch.float64)
+    b3 = b3.detach().double().cpu()
+    for ry in range(3):
+        for rx in range(3):
+            b[3 * ry + rx] = b3 + tap[:, keep[ry]][:, :, keep[rx]].sum((1, 2))
+    return w, b
+
+
 class _Conv:
     """One nn.Conv2d / nn.ConvTranspose2d(kernel == stride) with weights laid out for the engine
     (bf16 hi/lo planes, or one fp16 plane with ``f16``)."""
@@ -117,7 +151,8 @@ class _Conv:
         self.b = None if b is None else b.detach().float().to(device).contiguous()
 
     def __call__(self, x: Planes, stride=1, pad=None, res1=None, res2=None, out_f32=False,
-                 planes_ld: Optional[int] = None, planes_silu=False, final=None, final_flags=0):
+                 planes_ld: Optional[int] = None, planes_silu=False, final=None, final_flags=0,
+                 border_bias: Optional[torch.Tensor] = None):
         n, h, w, ld = x.shape
         if ld != self.cin_pad or x.c != self.cin:
             raise ValueError(f"conv input planes must have {self.cin} channels padded to {self.cin_pad}, got "
@@ -153,12 +188,17 @@ class _Conv:
             if r is not None and (tuple(r.shape) != (n, ho, wo, self.cout) or not r.is_contiguous()):
                 raise ValueError("residual must match the conv output")
         flags = PLANE_SILU if planes_silu else 0
+        bias = self.b
+        if border_bias is not None:  # [9, cout] rows by border class (fold_affine_1x1)
+            if not (self.f16 and not self.k and self.kh == 3 and stride == 1 and pad == 1):
+                raise ValueError("border_bias needs an fp16 3x3 stride-1 pad-1 convolution")
+            bias, flags = border_bias, flags | BORDER_BIAS
         if self.f16 and self.k:
             call("rf_deconv2d_f16", ptr(x.hi), n, h, w, ld, ptr(self.w_hi), self.cout, self.k, ptr(self.b), ptr(out),
                  ptr(pl.hi if pl else None), planes_ld or 0, ptr(ws), ws.numel(), stream())
         elif self.f16:
             call("rf_conv2d_f16", ptr(x.hi), n, h, w, ld, ptr(self.w_hi), self.cout, self.cout_pad, self.kh, self.kw,
-                 stride, pad, ptr(self.b), ptr(res1), ptr(res2), ptr(out), ptr(pl.hi if pl else None), planes_ld or 0,
+                 stride, pad, ptr(bias), ptr(res1), ptr(res2), ptr(out), ptr(pl.hi if pl else None), planes_ld or 0,
                  flags, 0, 0, 0, 0.0, ptr(ws), ws.numel(), stream())
         elif self.k:
             call("rf_deconv2d_bf16x3", ptr(x.hi), ptr(x.lo), n, h, w, ld, ptr(self.w_hi), ptr(self.w_lo), self.cout,
@@ -204,6 +244,13 @@ class DPTHead:
         if self.out2.cout > 64:
             raise ValueError("output_conv2 must have <= 64 channels for the fused head")
         self.feat_ld = self.refine[1][0][2][0].cin_pad
+        # refinenet1's 1x1 out_conv folded into output_conv1 (fp16 mode; module docstring)
+        self.fold = f16 and os.environ.get("RF_DPT_FOLD", "1") != "0"
+        if self.fold:
+            w, b = fold_affine_1x1(g("scratch.output_conv1.weight"), g("scratch.output_conv1.bias"),
+                                   g("scratch.refinenet1.out_conv.weight"), g("scratch.refinenet1.out_conv.bias"))
+            self.out1_fold = C(w.float(), None)
+            self.out1_fold_bias = b.float().to(device).contiguous()
 
     def _rcu(self, convs, x32, xs: Planes, extra=None, want_f32=False, next_silu=True, next_ld=None):
         """ResidualConvUnit (dpt.py:76-92): conv2(silu(conv1(silu(x)))) + x (+ extra = fusion-block x0)."""
@@ -218,6 +265,8 @@ class DPTHead:
         else:
             out, outs = self._rcu(units[1], x1, x1s, extra=x0, want_f32=True, next_ld=self.feat_ld)
         _, y = self._rcu(units[2], out, outs, next_silu=False, next_ld=out_conv.cin_pad)
+        if last and self.fold:  # out_conv lives in output_conv1's folded weights
+            return upsample_planes(y, *size, planes_ld=self.out1_fold.cin_pad)
         y32, _ = out_conv(y, out_f32=True)
         if last:
             return upsample(y32, *size, out_f32=False, planes_ld=self.out1.cin_pad, f16=self.f16)[1]
@@ -258,6 +307,9 @@ class DPTHead:
         p1 = self._fuse(1, p2, rn[0], rns[0], (2 * rn[0].shape[1], 2 * rn[0].shape[2]), last=True)
         if (p1.shape[1], p1.shape[2]) != (hp * patch, wp * patch):
             raise ValueError("DPT output size mismatch (patch size must be 8)")
-        _, o1 = self.out1(p1, planes_ld=self.out2.cin_pad)
+        if self.fold:
+            _, o1 = self.out1_fold(p1, planes_ld=self.out2.cin_pad, border_bias=self.out1_fold_bias)
+        else:
+            _, o1 = self.out1(p1, planes_ld=self.out2.cin_pad)
         flags = (LOG_DECODE if log_decode else 0) | (0 if channels_last else NCHW_OUT)
         return self.out2(o1, final=(self.w_fin, self.b_fin, elu_alpha), final_flags=flags)

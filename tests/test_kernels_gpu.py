@@ -872,6 +872,48 @@ def test_upsample_bilinear_align_corners(hi, ho, c, prec):
     assert out2 is None and torch.equal(pl2.hi, pl.hi) and (f16 or torch.equal(pl2.lo, pl.lo))
 
 
+@pytest.mark.parametrize("hi,ho,c,ld_in,ld_out", [(4, 9, 16, 16, 32), (256, 512, 256, 256, 256), (33, 64, 40, 48, 40)])
+def test_upsample_planes_f16_in(hi, ho, c, ld_in, ld_out):
+    """rf_upsample_bilinear_h (fp16 planes in and out, the folded DPT tail): the fp32 blend of the plane's
+    fp16 values rounded once, vs F.interpolate on the same values; padded channels stay zero."""
+    from renderformer_amd.dpt import Planes, upsample_planes
+    g = torch.Generator(device="cpu").manual_seed(hi + c)
+    x = torch.randn(2, hi, hi, c, generator=g).half()
+    pin = Planes.empty(2, hi, hi, c, ld_in, dev, True)
+    pin.hi[..., :c] = x.to(dev)
+    pl = upsample_planes(pin, ho, ho, planes_ld=ld_out)
+    ref = F.interpolate(x.float().permute(0, 3, 1, 2), size=(ho, ho), mode="bilinear",
+                        align_corners=True).permute(0, 2, 3, 1)
+    got = pl.hi[..., :c].float().cpu()
+    assert float((got - ref).abs().max()) <= float(ref.abs().max()) * 2.0 ** -10  # one fp16 rounding
+    assert relerr(got, ref) < 4e-4
+    assert (pl.hi[..., c:] == 0).all()
+
+
+@pytest.mark.parametrize("hw,halo2", [(24, "0"), (64, "1")])
+def test_conv_border_bias(hw, halo2, monkeypatch):
+    """RF_CONV_BORDER_BIAS: per-pixel bias row by border class (3 ry + rx), on the engine tile and on the halo
+    kernel (the folded output_conv1), vs torch conv + the class bias."""
+    from renderformer_amd.dpt import _Conv, split_planes
+    monkeypatch.setenv("RF_CONV_HALO2", halo2)
+    g = torch.Generator(device="cpu").manual_seed(hw)
+    cin, cout = 64, 128
+    w = torch.randn(cout, cin, 3, 3, generator=g) / 24
+    b9 = torch.randn(9, cout, generator=g)
+    x = torch.randn(2, cin, hw, hw, generator=g)
+    conv = _Conv(w, None, dev, f16=True)
+    _, pl = conv(split_planes(x.permute(0, 2, 3, 1).contiguous().to(dev), conv.cin_pad, f16=True), planes_ld=cout,
+                 border_bias=b9.to(dev).contiguous())
+    ref = F.conv2d(_q(x, "f16"), _q(w, "f16"), None, padding=1)
+    ry = torch.ones(hw, dtype=torch.long)
+    ry[0], ry[-1] = 0, 2
+    ref = (ref + b9.double()[3 * ry[:, None] + ry[None, :]].permute(2, 0, 1)[None]).permute(0, 2, 3, 1)
+    assert relerr(pl.hi.float().cpu(), ref) < 1e-3
+    with pytest.raises(Exception):  # the flag needs a 3x3 stride-1 pad-1 convolution
+        conv(split_planes(x.permute(0, 2, 3, 1).contiguous().to(dev), conv.cin_pad, f16=True), stride=2, pad=1,
+             planes_ld=cout, border_bias=b9.to(dev).contiguous())
+
+
 @pytest.mark.parametrize("prec,hw", [("bf16x3", 24), ("f16", 24), ("f16h2", 32), ("f16h2", 64)])
 def test_conv_final_head(prec, hw, monkeypatch):
     """output_conv2 + its fused head (SiLU, 1x1 32 -> 3, ELU, 10^x - 1); f16h2: on the 16 x 32-pixel halo kernel's

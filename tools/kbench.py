@@ -184,9 +184,10 @@ def conv():
         if os.environ.get("KB_CONV_HW"):  # only these output resolutions
             shapes = [x for x in shapes if str(x[2]) in os.environ["KB_CONV_HW"].split(",")]
         for cin, cout, hw in shapes:
-            conv = _Conv(torch.randn(cout, cin, 3, 3) / 48, torch.randn(cout), dev, f16=f16)
+            ks = int(os.environ.get("KB_CONV_K", "3"))  # kernel size (1: the 1x1 out_conv / projections)
+            conv = _Conv(torch.randn(cout, cin, ks, ks) / 48, torch.randn(cout), dev, f16=f16)
             x = split_planes(torch.randn(1, hw, hw, cin, device=dev), conv.cin_pad, f16=f16)
-            fl = 2 * hw * hw * cin * cout * 9
+            fl = 2 * hw * hw * cin * cout * ks * ks
             mf = 1 if f16 else 3
             tiles = os.environ.get("KB_CONV_TILES", "128,1288,256,2561,auto4w,auto").split(",") if f16 else ("128", "256")
             for t in tiles:
@@ -200,7 +201,7 @@ def conv():
                     os.environ["RF_CONV_TILE"] = t.replace("ph", "")
                 ms = timeit(lambda: conv(x, out_f32=True), reps=10)
                 os.environ.pop("RF_CONV_TILE", None)
-                print(f"conv3x3 {'f16 ' if f16 else 'bf16x3'} {cin}->{cout} @{hw} tile={t}: "
+                print(f"conv{ks}x{ks} {'f16 ' if f16 else 'bf16x3'} {cin}->{cout} @{hw} tile={t}: "
                       f"{ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF(algorithmic)  {mf*fl/ms/1e9:7.1f} TF(MFMA issued)")
             if f16 and os.environ.get("KB_CONV_GEMM"):  # the same M, N, K as a plain bf16 GEMM (no gather)
                 a = torch.randn(hw * hw, 9 * cin, device=dev).bfloat16()
