@@ -12,6 +12,9 @@
 #   configs          the other SURVEY 8d configurations (bunny, 1024^2, 4 views, 4 scenes, v1-base 256^2)
 #   c5               config 5 (24 views at 1024^2), bf16 and MX fp8
 #   pmc <script args...>   SQ counter passes (one rocprofv3 run each) over one python command
+#   l2               per-kernel L2 hit rates of a short bench run (TCC_HIT_sum / TCC_MISS_sum, tools/pmc_l2.py)
+#   attnab           attention GPU tests, then interleaved ablation timings of the RF_ATTN_DBG variants in $ABL
+#   fold             the DPT fold A/B: kernel-trace of the frame with RF_DPT_FOLD=1 and 0, then the bench A/B
 # Every GPU step runs under its own timeout and the steps are chained with && (set -e): the first failure
 # (fault, abort, time limit) ends the job.
 set -e
@@ -72,6 +75,17 @@ pmc)
         i=$((i+1))
         prof_run timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $O/p$i -o run -- python3 "$@" > $O/p$i.log 2>&1
     done ;;
+l2)
+    prof_run timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $O/pmc -o run -- python3 $R/bench.py --profile --steps 2 --warmup 1 > $O/pmc.log 2>&1
+    python tools/pmc_l2.py $(find $O/pmc -name '*counter_collection.csv' -print -quit) 30 > $O/l2.txt ;;
+attnab)
+    timeout -k 10 300 $T tests/test_kernels_gpu.py -k "attention or attn" > $O/t_attn.log 2>&1
+    ABL=${ABL:-0,1024} timeout -k 10 300 python -u tools/attn_ablate.py > $O/ablate.log 2>&1 ;;
+fold)
+    for v in 1 0; do
+        (export RF_DPT_FOLD=$v; prof_run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof$v -o run -- python3 $R/bench.py --profile --steps 5 --warmup 2 --no-cpu-baseline > $O/prof$v.log 2>&1)
+    done
+    bash tools/gpu.sh ab $TAG "RF_DPT_FOLD=1" "RF_DPT_FOLD=0" ;;
 *)
     echo "unknown task $TASK" >&2; exit 2 ;;
 esac
