@@ -36,6 +36,7 @@
  *                      the ResidualConvUnit SiLU/skip (dpt.py:86-92) and fusion sum (:141-143) fused; FINAL mode
  *                      also fuses output_conv2 SiLU + 1x1 (dpt.py:234-240), ELU and the log decode
  *   rf_conv2d_f16 / rf_deconv2d_f16  the same two DPT convolutions with fp16 operands (one MFMA per product)
+ *   rf_conv1x1_f16_group  the four DPT tap projections (dpt.py:197-199, 244-249) as one launch
  *   rf_split_planes    (operand preparation for the above; no reference counterpart)
  *   rf_deconv2d_bf16x3 DPT nn.ConvTranspose2d kernel == stride (dpt.py:195-206; aten conv_transpose2d)
  *   rf_upsample_bilinear F.interpolate(bilinear, align_corners=True) (dpt.py:154-155, 269-270)
@@ -326,6 +327,13 @@ int rf_conv2d_f16(const void* in, int n_img, int hi, int wi, int cin_pad, const 
                   int kw, int stride, int pad, const float* bias, const float* res1, const float* res2, float* out,
                   void* p_out, int p_ld, int flags, const float* w_fin, const float* b_fin, int n_fin, float elu_alpha,
                   void* workspace, int64_t ws_bytes, void* stream);
+/* Up to 4 independent 1x1 fp16 convolutions over images of the same n_img x hi x wi (the DPT's four tap
+ * projections, dpt.py:197-199 / 244-249) in ONE launch: conv q reads in[q] (channel stride cin_pad[q]) and
+ * writes out plane p_out[q] (channel stride p_ld[q]) = in . W_q^T + bias[q] (bias may be NULL, or any entry);
+ * W_q fp16 [cout_pad[q]][cin_pad[q]], cout_pad a multiple of 128.  Same results as rf_conv2d_f16 per conv. */
+int rf_conv1x1_f16_group(int n_conv, const void* const* in, const int* cin_pad, const void* const* w, const int* cout,
+                         const int* cout_pad, const float* const* bias, void* const* p_out, const int* p_ld, int n_img,
+                         int hi, int wi, void* stream);
 int rf_deconv2d_f16(const void* in, int n_img, int hi, int wi, int cin_pad, const void* w, int cout, int k,
                     const float* bias, float* out, void* p_out, int p_ld, void* workspace, int64_t ws_bytes,
                     void* stream);

@@ -1281,6 +1281,37 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
     }
 }
 
+// Several independent data-parallel launches of one tile configuration as ONE grid (the DPT's four tap
+// projections): problem q owns blocks [first[q], first[q + 1]); each block reads its problem's arguments
+// from the kernel-argument segment at a wave-uniform index and runs the engine's tile unchanged.  Short
+// launches at the DPT's 64^2 level are latency-bound (a fixed ~15 us each), so one grid overlaps them.
+constexpr int GROUP_MAX = 4;
+struct GroupArgs {
+    EngineArgs p[GROUP_MAX];
+    int first[GROUP_MAX + 1];
+    int n;
+};
+
+template <class C, int EPI, int NTERM, bool GATHER>
+__global__ __launch_bounds__(C::THREADS, 2) void engine_group_kernel(GroupArgs g) {
+    constexpr int BM = C::BM, BN = C::BN, TI = C::TI, TJ = C::TJ;
+    __shared__ __attribute__((aligned(16))) char smem[C::STAGES * stage_bytes<C, NTERM>()];
+    const int nwg = gridDim.x, hw = blockIdx.x;
+    const int xcd = hw & 7, qd = nwg >> 3, rd = nwg & 7;
+    const int wg = (xcd < rd ? xcd * (qd + 1) : rd * (qd + 1) + (xcd - rd) * qd) + (hw >> 3);
+    int q = 0;
+#pragma unroll
+    for (int i = 1; i < GROUP_MAX; ++i) q += (i < g.n && wg >= g.first[i]) ? 1 : 0;
+    const EngineArgs& p = g.p[q];
+    const int local = wg - g.first[q];
+    const int tiles_m = (p.m + BM - 1) / BM;
+    int tm, tn;
+    tile_coords(local, tiles_m, p.n / BN, p.group_m, tm, tn);
+    f32x4 acc[TI][TJ];
+    engine_mainloop<C, NTERM, GATHER, EPI == E_ADD>(p, smem, tm * BM, tn * BN, 0, p.k / (BK * C::KH), acc);
+    engine_epilogue<C, EPI>(p, tm * BM, tn * BN, acc);
+}
+
 // ---------------------------------------------------------------------------------------------------
 // Halo-tiled 3x3 convolution (stride 1, pad 1, fp16 operands).  The im2col gather of engine_mainloop
 // stages every input pixel once per tap (9x the input through L2 -> LDS per output tile); here an output
@@ -2751,6 +2782,60 @@ extern "C" int rf_conv2d_f16(const void* in, int n_img, int hi, int wi, int cin_
     p.ldw = p.k;
     return conv_common(p, P_F16, true, w, nullptr, cout, cout_pad, out, bias, res1, res2, p_out, nullptr, p_ld, flags,
                        w_fin, b_fin, n_fin, elu_alpha, workspace, ws_bytes, stream, "rf_conv2d_f16");
+}
+
+extern "C" int rf_conv1x1_f16_group(int n_conv, const void* const* in, const int* cin_pad, const void* const* w,
+                                    const int* cout, const int* cout_pad, const float* const* bias,
+                                    void* const* p_out, const int* p_ld, int n_img, int hi, int wi, void* stream) {
+    RF_REQUIRE(n_conv >= 1 && n_conv <= GROUP_MAX, "rf_conv1x1_f16_group: 1..%d convolutions", GROUP_MAX);
+    RF_REQUIRE(in && cin_pad && w && cout && cout_pad && p_out && p_ld, "rf_conv1x1_f16_group: null array");
+    static void* z = nullptr;
+    if (!z && hipGetSymbolAddress(&z, HIP_SYMBOL(g_zero_row)) != hipSuccess) {
+        z = nullptr;
+        rf::set_error("rf_conv1x1_f16_group: zero row symbol");
+        return RF_ERR_LAUNCH;
+    }
+    using C = T128w8;
+    GroupArgs g{};
+    g.n = n_conv;
+    int blocks = 0;
+    for (int q = 0; q < n_conv; ++q) {
+        RF_REQUIRE(in[q] && w[q] && p_out[q], "rf_conv1x1_f16_group: null pointer in conv %d", q);
+        RF_REQUIRE(cin_pad[q] % BK == 0 && cout_pad[q] % C::BN == 0 && cout_pad[q] >= cout[q] && cout[q] % 4 == 0,
+                   "rf_conv1x1_f16_group: conv %d: cin_pad %% 32, cout_pad %% 128, cout %% 4", q);
+        RF_REQUIRE(p_ld[q] % 4 == 0 && p_ld[q] >= cout[q], "rf_conv1x1_f16_group: conv %d: bad p_ld", q);
+        EngineArgs& p = g.p[q];
+        p.a = (const bf16_t*)in[q];
+        p.hi = hi;
+        p.wi = wi;
+        p.cin_pad = cin_pad[q];
+        p.cin_m = udiv_magic(cin_pad[q]);
+        p.ho = hi;
+        p.wo = wi;
+        p.kw = 1;
+        p.kw_m = udiv_magic(1);
+        p.stride = 1;
+        p.pad = 0;
+        p.m = n_img * hi * wi;
+        p.k = cin_pad[q];
+        p.ldw = p.k;
+        p.zero = (const bf16_t*)z;
+        p.w = (const bf16_t*)w[q];
+        p.n = cout_pad[q];
+        p.bias = bias ? bias[q] : nullptr;
+        p.p_hi = (bf16_t*)p_out[q];
+        p.p_ld = p_ld[q];
+        p.plane_f16 = 1;
+        p.cout = cout[q];
+        const int tiles_m = (p.m + C::BM - 1) / C::BM, tiles_n = p.n / C::BN;
+        p.group_m = pick_group_m(tiles_m, tiles_n, C::BM, C::BN, ((int64_t)tiles_m * tiles_n + 7) / 8);
+        g.first[q] = blocks;
+        blocks += tiles_m * tiles_n;
+    }
+    g.first[n_conv] = blocks;
+    if (blocks == 0) return RF_OK;
+    RF_LAUNCH((engine_group_kernel<C, E_CONV, P_F16, true>), dim3(blocks), dim3(C::THREADS), 0, (hipStream_t)stream, g);
+    return rf::check_launch("rf_conv1x1_f16_group");
 }
 
 extern "C" int rf_deconv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, int wi, int cin_pad,

@@ -34,6 +34,8 @@ from typing import Dict, List, Optional
 
 import torch
 
+import ctypes
+
 from ._lib import call, ptr, stream
 
 PLANE_SILU, SILU_OUT, FINAL, LOG_DECODE, NCHW_OUT, BORDER_BIAS = 1, 2, 4, 8, 16, 32
@@ -98,6 +100,29 @@ def upsample_planes(x: Planes, ho: int, wo: int, planes_ld: int) -> Planes:
     pl = Planes.empty(n, ho, wo, x.c, planes_ld, x.hi.device, True)
     call("rf_upsample_bilinear_h", ptr(x.hi), ld, n, h, w, c, ho, wo, ptr(pl.hi), planes_ld, stream())
     return pl
+
+
+def conv1x1_group(convs: List["_Conv"], xs: List[Planes], planes_ld: List[int]) -> List[Planes]:
+    """Independent fp16 1x1 convolutions over images of one size as ONE launch (rf_conv1x1_f16_group): the
+    DPT's four tap projections.  Same results as calling each conv with ``planes_ld``."""
+    n, h, w, _ = xs[0].shape
+    for c, x in zip(convs, xs):
+        if not (c.f16 and x.f16 and c.kh == c.kw == 1 and not c.k and x.shape[:3] == (n, h, w) and
+                x.shape[3] == c.cin_pad and x.c == c.cin):
+            raise ValueError("conv1x1_group: fp16 1x1 convolutions over equally sized input planes of cin_pad")
+    outs = [Planes.empty(n, h, w, c.cout, ld, xs[0].hi.device, True) for c, ld in zip(convs, planes_ld)]
+    k = len(convs)
+
+    def arr(ct, vals):
+        a = (ct * k)(*vals)
+        return ctypes.cast(a, ctypes.c_void_p), a  # (pointer, keep-alive)
+
+    args = [arr(ctypes.c_void_p, [ptr(x.hi) for x in xs]), arr(ctypes.c_int, [c.cin_pad for c in convs]),
+            arr(ctypes.c_void_p, [ptr(c.w_hi) for c in convs]), arr(ctypes.c_int, [c.cout for c in convs]),
+            arr(ctypes.c_int, [c.cout_pad for c in convs]), arr(ctypes.c_void_p, [ptr(c.b) for c in convs]),
+            arr(ctypes.c_void_p, [ptr(o.hi) for o in outs]), arr(ctypes.c_int, list(planes_ld))]
+    call("rf_conv1x1_f16_group", k, *[a[0] for a in args], n, h, w, stream())
+    return outs
 
 
 def fold_affine_1x1(w3: torch.Tensor, b3: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor):
@@ -244,6 +269,9 @@ class DPTHead:
         if self.out2.cout > 64:
             raise ValueError("output_conv2 must have <= 64 channels for the fused head")
         self.feat_ld = self.refine[1][0][2][0].cin_pad
+        # the tap projections as one grouped launch (fp16 mode; RF_DPT_GROUP=0: one launch each)
+        self.group_proj = (f16 and os.environ.get("RF_DPT_GROUP", "1") != "0" and len(self.projects) <= 4 and
+                           all(c.kh == 1 and c.kw == 1 and not c.k and c.cout_pad % 128 == 0 for c in self.projects))
         # refinenet1's 1x1 out_conv folded into output_conv1 (fp16 mode; module docstring)
         self.fold = f16 and os.environ.get("RF_DPT_FOLD", "1") != "0"
         if self.fold:
@@ -283,10 +311,13 @@ class DPTHead:
                  log_decode: bool, channels_last: bool) -> torch.Tensor:
         """taps: the four decoder outputs, as fp32 rows or as their tap_planes()."""
         layers = []
-        for i, t in enumerate(taps):
-            x = t if isinstance(t, Planes) else self.tap_planes(i, t, n_img, hp, wp)
-            nxt = self.resize[i] if i in self.resize else self.rn[i]
-            _, x = self.projects[i](x, planes_ld=nxt.cin_pad)
+        xs = [t if isinstance(t, Planes) else self.tap_planes(i, t, n_img, hp, wp) for i, t in enumerate(taps)]
+        nxt_ld = [(self.resize[i] if i in self.resize else self.rn[i]).cin_pad for i in range(len(xs))]
+        if self.group_proj:  # the four projections as one launch (their 64^2 GEMMs are latency-bound)
+            xs = conv1x1_group(self.projects[:len(xs)], xs, nxt_ld)
+        for i, x in enumerate(xs):
+            if not self.group_proj:
+                _, x = self.projects[i](x, planes_ld=nxt_ld[i])
             if i in self.resize:
                 _, x = self.resize[i](x, stride=2 if i == 3 else 1, pad=1 if i == 3 else None,
                                       planes_ld=self.rn[i].cin_pad)

@@ -890,6 +890,33 @@ def test_upsample_planes_f16_in(hi, ho, c, ld_in, ld_out):
     assert (pl.hi[..., c:] == 0).all()
 
 
+def test_conv1x1_group_matches_single_convs():
+    """rf_conv1x1_f16_group (the DPT tap projections as one launch) vs the fp64 convolution of each, and vs
+    one rf_conv2d_f16 call each; one conv without bias."""
+    from renderformer_amd.dpt import _Conv, conv1x1_group, split_planes
+    g = torch.Generator(device="cpu").manual_seed(3)
+    couts, cin, hw = (128, 256, 512, 1024), 1024, 24
+    convs, xs, refs = [], [], []
+    for q, co in enumerate(couts):
+        w = torch.randn(co, cin, 1, 1, generator=g) / 32
+        b = None if q == 2 else torch.randn(co, generator=g)
+        x = torch.randn(1, cin, hw, hw, generator=g)
+        conv = _Conv(w, b, dev, f16=True)
+        convs.append(conv)
+        xs.append(split_planes(x.permute(0, 2, 3, 1).contiguous().to(dev), conv.cin_pad, f16=True))
+        refs.append(F.conv2d(_q(x, "f16"), _q(w, "f16"), None if b is None else b.double()).permute(0, 2, 3, 1))
+    lds = [c + 32 for c in couts]
+    outs = conv1x1_group(convs, xs, lds)
+    for conv, x, o, ref, ld in zip(convs, xs, outs, refs, lds):
+        assert o.shape[-1] == ld and (o.hi[..., conv.cout:] == 0).all()
+        assert relerr(o.hi[..., :conv.cout].float().cpu(), ref) < 1e-3
+        _, single = conv(x, planes_ld=ld)
+        assert relerr(o.hi.float(), single.hi.float()) < 1e-3
+    bad = split_planes(torch.randn(1, hw, hw, 512, device=dev), 512, f16=True)  # wrong channel count
+    with pytest.raises(ValueError):
+        conv1x1_group(convs[:2], [xs[0], bad], lds[:2])
+
+
 @pytest.mark.parametrize("hw,halo2", [(24, "0"), (64, "1")])
 def test_conv_border_bias(hw, halo2, monkeypatch):
     """RF_CONV_BORDER_BIAS: per-pixel bias row by border class (3 ry + rx), on the engine tile and on the halo
