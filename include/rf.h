@@ -37,6 +37,7 @@
  *                      also fuses output_conv2 SiLU + 1x1 (dpt.py:234-240), ELU and the log decode
  *   rf_conv2d_f16 / rf_deconv2d_f16  the same two DPT convolutions with fp16 operands (one MFMA per product)
  *   rf_conv1x1_f16_group  the four DPT tap projections (dpt.py:197-199, 244-249) as one launch
+ *   rf_conv2d_f16_group   independent DPT convolutions / deconvolutions (resize layers, layer*_rn) as one launch
  *   rf_split_planes    (operand preparation for the above; no reference counterpart)
  *   rf_deconv2d_bf16x3 DPT nn.ConvTranspose2d kernel == stride (dpt.py:195-206; aten conv_transpose2d)
  *   rf_upsample_bilinear F.interpolate(bilinear, align_corners=True) (dpt.py:154-155, 269-270)
@@ -327,6 +328,22 @@ int rf_conv2d_f16(const void* in, int n_img, int hi, int wi, int cin_pad, const 
                   int kw, int stride, int pad, const float* bias, const float* res1, const float* res2, float* out,
                   void* p_out, int p_ld, int flags, const float* w_fin, const float* b_fin, int n_fin, float elu_alpha,
                   void* workspace, int64_t ws_bytes, void* stream);
+/* Up to 4 independent fp16 convolutions / deconvolutions (kernel == stride) as ONE launch on the 128 x 128
+ * tile: the DPT's resize layers (dpt.py:195-216) and its layer*_rn convolutions (dpt.py:228-231), whose 64^2 /
+ * 32^2 launches are latency-bound.  Member q is what rf_conv2d_f16 (deconv_k == 0: in, n_img, hi, wi, cin_pad,
+ * w, cout, cout_pad, kh, kw, stride, pad, bias, out, p_out, p_ld, flags) or rf_deconv2d_f16 (deconv_k = k;
+ * cout_pad, kh, kw, stride, pad and flags unused) computes, except RF_CONV_FINAL; output channels (cout_pad, or
+ * k*k*cout) a multiple of 128. */
+typedef struct {
+    const void* in;
+    const void* w;
+    const float* bias;
+    float* out;
+    void* p_out;
+    int n_img, hi, wi, cin_pad, cout, cout_pad, kh, kw, stride, pad, deconv_k, p_ld, flags;
+} rf_conv_desc;
+int rf_conv2d_f16_group(int n_conv, const rf_conv_desc* convs, void* stream);
+
 /* Up to 4 independent 1x1 fp16 convolutions over images of the same n_img x hi x wi (the DPT's four tap
  * projections, dpt.py:197-199 / 244-249) in ONE launch: conv q reads in[q] (channel stride cin_pad[q]) and
  * writes out plane p_out[q] (channel stride p_ld[q]) = in . W_q^T + bias[q] (bias may be NULL, or any entry);

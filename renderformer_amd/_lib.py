@@ -75,6 +75,7 @@ SIGNATURES = {
     "rf_upsample_bilinear": [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _I, _P],
     "rf_upsample_bilinear_h": [_P, _I, _I, _I, _I, _I, _I, _I, _P, _I, _P],
     "rf_conv1x1_f16_group": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "rf_conv2d_f16_group": [_I, _P, _P],
     "rf_gemm_mx8": [_P, _L, _P, _L, _P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _P],
     "rf_quant_mx8": [_P, _L, _I, _I, _P, _L, _P, _L, _P],
     "rf_device_error": [],

@@ -2784,15 +2784,64 @@ extern "C" int rf_conv2d_f16(const void* in, int n_img, int hi, int wi, int cin_
                        w_fin, b_fin, n_fin, elu_alpha, workspace, ws_bytes, stream, "rf_conv2d_f16");
 }
 
-extern "C" int rf_conv1x1_f16_group(int n_conv, const void* const* in, const int* cin_pad, const void* const* w,
-                                    const int* cout, const int* cout_pad, const float* const* bias,
-                                    void* const* p_out, const int* p_ld, int n_img, int hi, int wi, void* stream) {
-    RF_REQUIRE(n_conv >= 1 && n_conv <= GROUP_MAX, "rf_conv1x1_f16_group: 1..%d convolutions", GROUP_MAX);
-    RF_REQUIRE(in && cin_pad && w && cout && cout_pad && p_out && p_ld, "rf_conv1x1_f16_group: null array");
+// one grouped-launch member: the fields rf_conv2d_f16 / rf_deconv2d_f16 and conv_common set (the deconvolution
+// runs its dense A as a 1x1 gather: the same row addresses), or an error message
+static const char* group_member(EngineArgs& p, const rf_conv_desc& d, const void* zero) {
+    if (!d.in || !d.w || !(d.out || d.p_out)) return "null pointer";
+    if (d.cin_pad % BK) return "cin_pad must be a multiple of 32";
+    if (d.cout % 4) return "cout must be a multiple of 4";
+    if (d.p_out && (d.p_ld % 4 || d.p_ld < d.cout)) return "bad p_ld";
+    if (d.flags & RF_CONV_FINAL) return "the fused final head runs on its own launch";
+    p = EngineArgs{};
+    p.a = (const bf16_t*)d.in;
+    p.cin_pad = d.cin_pad;
+    p.cin_m = udiv_magic(d.cin_pad);
+    p.zero = (const bf16_t*)zero;
+    if (d.deconv_k > 0) {
+        p.hi = p.ho = d.hi;
+        p.wi = p.wo = d.wi;
+        p.kw = 1;
+        p.stride = 1;
+        p.pad = 0;
+        p.deconv = d.deconv_k;
+        p.n = d.deconv_k * d.deconv_k * d.cout;
+        if (d.flags) return "a deconvolution takes no flags";
+    } else {
+        p.hi = d.hi;
+        p.wi = d.wi;
+        p.ho = (d.hi + 2 * d.pad - d.kh) / d.stride + 1;
+        p.wo = (d.wi + 2 * d.pad - d.kw) / d.stride + 1;
+        p.kw = d.kw;
+        p.stride = d.stride;
+        p.pad = d.pad;
+        p.n = d.cout_pad;
+        if (d.cout_pad < d.cout) return "cout_pad < cout";
+        if ((d.flags & RF_CONV_BORDER_BIAS) && !(d.bias && d.kh == 3 && d.kw == 3 && d.stride == 1 && d.pad == 1))
+            return "RF_CONV_BORDER_BIAS needs a 3x3 stride-1 pad-1 convolution with its 9-row bias";
+    }
+    p.kw_m = udiv_magic(p.kw);
+    p.m = d.n_img * p.ho * p.wo;
+    p.k = (d.deconv_k > 0 ? 1 : d.kh * d.kw) * d.cin_pad;
+    if (p.k >= 65536) return "kh*kw*cin_pad must be < 65536";
+    if (p.n % T128w8::BN) return "output channels (k*k*cout for a deconvolution) must be a multiple of 128";
+    p.ldw = p.k;
+    p.w = (const bf16_t*)d.w;
+    p.c = d.out;
+    p.bias = d.bias;
+    p.p_hi = (bf16_t*)d.p_out;
+    p.p_ld = d.p_ld;
+    p.plane_f16 = 1;
+    p.cout = d.cout;
+    p.flags = d.flags;
+    return nullptr;
+}
+
+extern "C" int rf_conv2d_f16_group(int n_conv, const rf_conv_desc* convs, void* stream) {
+    RF_REQUIRE(n_conv >= 1 && n_conv <= GROUP_MAX && convs, "rf_conv2d_f16_group: 1..%d convolutions", GROUP_MAX);
     static void* z = nullptr;
     if (!z && hipGetSymbolAddress(&z, HIP_SYMBOL(g_zero_row)) != hipSuccess) {
         z = nullptr;
-        rf::set_error("rf_conv1x1_f16_group: zero row symbol");
+        rf::set_error("rf_conv2d_f16_group: zero row symbol");
         return RF_ERR_LAUNCH;
     }
     using C = T128w8;
@@ -2800,33 +2849,9 @@ extern "C" int rf_conv1x1_f16_group(int n_conv, const void* const* in, const int
     g.n = n_conv;
     int blocks = 0;
     for (int q = 0; q < n_conv; ++q) {
-        RF_REQUIRE(in[q] && w[q] && p_out[q], "rf_conv1x1_f16_group: null pointer in conv %d", q);
-        RF_REQUIRE(cin_pad[q] % BK == 0 && cout_pad[q] % C::BN == 0 && cout_pad[q] >= cout[q] && cout[q] % 4 == 0,
-                   "rf_conv1x1_f16_group: conv %d: cin_pad %% 32, cout_pad %% 128, cout %% 4", q);
-        RF_REQUIRE(p_ld[q] % 4 == 0 && p_ld[q] >= cout[q], "rf_conv1x1_f16_group: conv %d: bad p_ld", q);
+        const char* err = group_member(g.p[q], convs[q], z);
+        RF_REQUIRE(!err, "rf_conv2d_f16_group: conv %d: %s", q, err ? err : "");
         EngineArgs& p = g.p[q];
-        p.a = (const bf16_t*)in[q];
-        p.hi = hi;
-        p.wi = wi;
-        p.cin_pad = cin_pad[q];
-        p.cin_m = udiv_magic(cin_pad[q]);
-        p.ho = hi;
-        p.wo = wi;
-        p.kw = 1;
-        p.kw_m = udiv_magic(1);
-        p.stride = 1;
-        p.pad = 0;
-        p.m = n_img * hi * wi;
-        p.k = cin_pad[q];
-        p.ldw = p.k;
-        p.zero = (const bf16_t*)z;
-        p.w = (const bf16_t*)w[q];
-        p.n = cout_pad[q];
-        p.bias = bias ? bias[q] : nullptr;
-        p.p_hi = (bf16_t*)p_out[q];
-        p.p_ld = p_ld[q];
-        p.plane_f16 = 1;
-        p.cout = cout[q];
         const int tiles_m = (p.m + C::BM - 1) / C::BM, tiles_n = p.n / C::BN;
         p.group_m = pick_group_m(tiles_m, tiles_n, C::BM, C::BN, ((int64_t)tiles_m * tiles_n + 7) / 8);
         g.first[q] = blocks;
@@ -2835,7 +2860,30 @@ extern "C" int rf_conv1x1_f16_group(int n_conv, const void* const* in, const int
     g.first[n_conv] = blocks;
     if (blocks == 0) return RF_OK;
     RF_LAUNCH((engine_group_kernel<C, E_CONV, P_F16, true>), dim3(blocks), dim3(C::THREADS), 0, (hipStream_t)stream, g);
-    return rf::check_launch("rf_conv1x1_f16_group");
+    return rf::check_launch("rf_conv2d_f16_group");
+}
+
+extern "C" int rf_conv1x1_f16_group(int n_conv, const void* const* in, const int* cin_pad, const void* const* w,
+                                    const int* cout, const int* cout_pad, const float* const* bias,
+                                    void* const* p_out, const int* p_ld, int n_img, int hi, int wi, void* stream) {
+    RF_REQUIRE(n_conv >= 1 && n_conv <= GROUP_MAX, "rf_conv1x1_f16_group: 1..%d convolutions", GROUP_MAX);
+    RF_REQUIRE(in && cin_pad && w && cout && cout_pad && p_out && p_ld, "rf_conv1x1_f16_group: null array");
+    rf_conv_desc d[GROUP_MAX] = {};
+    for (int q = 0; q < n_conv; ++q) {
+        d[q].in = in[q];
+        d[q].w = w[q];
+        d[q].bias = bias ? bias[q] : nullptr;
+        d[q].p_out = p_out[q];
+        d[q].n_img = n_img;
+        d[q].hi = hi;
+        d[q].wi = wi;
+        d[q].cin_pad = cin_pad[q];
+        d[q].cout = cout[q];
+        d[q].cout_pad = cout_pad[q];
+        d[q].kh = d[q].kw = d[q].stride = 1;
+        d[q].p_ld = p_ld[q];
+    }
+    return rf_conv2d_f16_group(n_conv, d, stream);
 }
 
 extern "C" int rf_deconv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, int wi, int cin_pad,

@@ -125,6 +125,43 @@ def conv1x1_group(convs: List["_Conv"], xs: List[Planes], planes_ld: List[int]) 
     return outs
 
 
+class _ConvDesc(ctypes.Structure):
+    """rf.h rf_conv_desc"""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("in_", "w", "bias", "out", "p_out")] + \
+               [(n, ctypes.c_int) for n in ("n_img", "hi", "wi", "cin_pad", "cout", "cout_pad", "kh", "kw", "stride",
+                                            "pad", "deconv_k", "p_ld", "flags")]
+
+
+def conv_group(jobs: List[dict]) -> List[tuple]:
+    """Independent fp16 convolutions / deconvolutions as ONE launch (rf_conv2d_f16_group).  A job is
+    dict(conv=_Conv, x=Planes, stride=1, pad=None, out_f32=False, planes_ld=None, planes_silu=False); the
+    result per job is (out f32 or None, planes or None), as _Conv.__call__ returns them."""
+    descs = (_ConvDesc * len(jobs))()
+    results = []
+    for d, j in zip(descs, jobs):
+        c, x = j["conv"], j["x"]
+        n, h, w, ld = x.shape
+        if not (c.f16 and x.f16) or ld != c.cin_pad or x.c != c.cin:
+            raise ValueError("conv_group: fp16 convolutions whose input planes have cin channels padded to cin_pad")
+        stride = j.get("stride", 1)
+        pad = c.kh // 2 if j.get("pad") is None else j["pad"]
+        if c.k:
+            ho, wo = h * c.k, w * c.k
+        else:
+            ho, wo = (h + 2 * pad - c.kh) // stride + 1, (w + 2 * pad - c.kw) // stride + 1
+        out = torch.empty(n, ho, wo, c.cout, device=x.hi.device) if j.get("out_f32") else None
+        ld_out = j.get("planes_ld")
+        pl = Planes.empty(n, ho, wo, c.cout, ld_out, x.hi.device, True) if ld_out else None
+        d.in_, d.w, d.bias, d.out, d.p_out = ptr(x.hi), ptr(c.w_hi), ptr(c.b), ptr(out), ptr(pl.hi if pl else None)
+        d.n_img, d.hi, d.wi, d.cin_pad, d.cout, d.cout_pad = n, h, w, c.cin_pad, c.cout, c.cout_pad
+        d.kh, d.kw, d.stride, d.pad, d.deconv_k = c.kh, c.kw, stride, pad, c.k
+        d.p_ld = ld_out or 0
+        d.flags = PLANE_SILU if j.get("planes_silu") else 0
+        results.append((out, pl))
+    call("rf_conv2d_f16_group", len(jobs), ctypes.cast(descs, ctypes.c_void_p), stream())
+    return results
+
+
 def fold_affine_1x1(w3: torch.Tensor, b3: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor):
     """conv3x3(W3, b3, pad 1)(up(conv1x1(W1, b1)(y))) == conv3x3(W, pad 1)(up(y)) + B[border class]  (exact):
     the per-pixel affine 1x1 commutes with the bilinear resize (which reproduces constants), so the 3x3 sees
@@ -315,6 +352,9 @@ class DPTHead:
         nxt_ld = [(self.resize[i] if i in self.resize else self.rn[i]).cin_pad for i in range(len(xs))]
         if self.group_proj:  # the four projections as one launch (their 64^2 GEMMs are latency-bound)
             xs = conv1x1_group(self.projects[:len(xs)], xs, nxt_ld)
+        # (the resize layers and layer2-4_rn as grouped launches measured slower: their 32^2 / 64^2 members have
+        # K = 4,608 - 9,216, which the stream-K launches spread over the chip and one data-parallel grid does not;
+        # same-box frame 83.6 -> 81.3 frames/s, profiles/r3_dpt_group_ab.txt)
         for i, x in enumerate(xs):
             if not self.group_proj:
                 _, x = self.projects[i](x, planes_ld=nxt_ld[i])

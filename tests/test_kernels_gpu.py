@@ -917,6 +917,36 @@ def test_conv1x1_group_matches_single_convs():
         conv1x1_group(convs[:2], [xs[0], bad], lds[:2])
 
 
+def test_conv_group_matches_single_launches():
+    """rf_conv2d_f16_group: a deconvolution (k = 4), a stride-2 3x3 convolution with bias, and two 3x3
+    convolutions of different sizes with fp32 + SiLU-plane outputs in one launch, each vs its own launch."""
+    from renderformer_amd.dpt import _Conv, conv_group, split_planes
+    g = torch.Generator(device="cpu").manual_seed(4)
+
+    def planes(c, hw):
+        return split_planes(torch.randn(1, hw, hw, c, generator=g).to(dev), c, f16=True)
+
+    dec = _Conv(torch.randn(64, 128, 4, 4, generator=g) / 16, torch.randn(128, generator=g), dev, deconv=True, f16=True)
+    s2 = _Conv(torch.randn(128, 96, 3, 3, generator=g) / 30, torch.randn(128, generator=g), dev, f16=True)
+    c1 = _Conv(torch.randn(256, 64, 3, 3, generator=g) / 24, None, dev, f16=True)
+    c2 = _Conv(torch.randn(256, 256, 3, 3, generator=g) / 48, None, dev, f16=True)
+    jobs = [dict(conv=dec, x=planes(64, 12), planes_ld=128),
+            dict(conv=s2, x=planes(96, 20), stride=2, pad=1, planes_ld=160),
+            dict(conv=c1, x=planes(64, 24), out_f32=True, planes_ld=256, planes_silu=True),
+            dict(conv=c2, x=planes(256, 9), out_f32=True, planes_ld=256, planes_silu=True)]
+    got = conv_group(jobs)
+    for j, (out, pl) in zip(jobs, got):
+        kw = {k: v for k, v in j.items() if k not in ("conv", "x")}
+        if j["conv"].k:
+            kw.pop("stride", None), kw.pop("pad", None)
+        ref_out, ref_pl = j["conv"](j["x"], **kw)
+        assert relerr(pl.hi.float(), ref_pl.hi.float()) < 1e-3
+        if out is not None:
+            assert relerr(out, ref_out) < 1e-5
+    with pytest.raises(ValueError):
+        conv_group([dict(conv=c2, x=planes(64, 9))])  # input planes of the wrong width
+
+
 @pytest.mark.parametrize("hw,halo2", [(24, "0"), (64, "1")])
 def test_conv_border_bias(hw, halo2, monkeypatch):
     """RF_CONV_BORDER_BIAS: per-pixel bias row by border class (3 ry + rx), on the engine tile and on the halo
