@@ -2836,22 +2836,32 @@ static const char* group_member(EngineArgs& p, const rf_conv_desc& d, const void
     return nullptr;
 }
 
-extern "C" int rf_conv2d_f16_group(int n_conv, const rf_conv_desc* convs, void* stream) {
-    RF_REQUIRE(n_conv >= 1 && n_conv <= GROUP_MAX && convs, "rf_conv2d_f16_group: 1..%d convolutions", GROUP_MAX);
+// dense: every member is a 1x1 stride-1 convolution over unpadded pixels (A = dense rows of cin_pad, K a
+// multiple of 64): the 128x128 tile with 64-deep steps on plain rows (the stage-2 projections' loop) instead of
+// the gathered 32-deep one
+template <bool DENSE>
+static int conv_group_launch(int n_conv, const rf_conv_desc* convs, void* stream, const char* what) {
+    RF_REQUIRE(n_conv >= 1 && n_conv <= GROUP_MAX && convs, "%s: 1..%d convolutions", what, GROUP_MAX);
     static void* z = nullptr;
     if (!z && hipGetSymbolAddress(&z, HIP_SYMBOL(g_zero_row)) != hipSuccess) {
         z = nullptr;
-        rf::set_error("rf_conv2d_f16_group: zero row symbol");
+        rf::set_error("%s: zero row symbol", what);
         return RF_ERR_LAUNCH;
     }
-    using C = T128w8;
+    using C = std::conditional_t<DENSE, T128w8k2s4, T128w8>;
     GroupArgs g{};
     g.n = n_conv;
     int blocks = 0;
     for (int q = 0; q < n_conv; ++q) {
         const char* err = group_member(g.p[q], convs[q], z);
-        RF_REQUIRE(!err, "rf_conv2d_f16_group: conv %d: %s", q, err ? err : "");
+        RF_REQUIRE(!err, "%s: conv %d: %s", what, q, err ? err : "");
         EngineArgs& p = g.p[q];
+        if constexpr (DENSE) {
+            RF_REQUIRE(convs[q].kh == 1 && convs[q].kw == 1 && convs[q].stride == 1 && convs[q].pad == 0 &&
+                           !convs[q].deconv_k && p.k % (BK * C::KH) == 0,
+                       "%s: conv %d: dense members are 1x1 stride-1 convolutions with cin_pad %% 64 == 0", what, q);
+            p.lda = p.cin_pad;
+        }
         const int tiles_m = (p.m + C::BM - 1) / C::BM, tiles_n = p.n / C::BN;
         p.group_m = pick_group_m(tiles_m, tiles_n, C::BM, C::BN, ((int64_t)tiles_m * tiles_n + 7) / 8);
         g.first[q] = blocks;
@@ -2859,8 +2869,13 @@ extern "C" int rf_conv2d_f16_group(int n_conv, const rf_conv_desc* convs, void* 
     }
     g.first[n_conv] = blocks;
     if (blocks == 0) return RF_OK;
-    RF_LAUNCH((engine_group_kernel<C, E_CONV, P_F16, true>), dim3(blocks), dim3(C::THREADS), 0, (hipStream_t)stream, g);
-    return rf::check_launch("rf_conv2d_f16_group");
+    RF_LAUNCH((engine_group_kernel<C, E_CONV, P_F16, !DENSE>), dim3(blocks), dim3(C::THREADS), 0, (hipStream_t)stream,
+              g);
+    return rf::check_launch(what);
+}
+
+extern "C" int rf_conv2d_f16_group(int n_conv, const rf_conv_desc* convs, void* stream) {
+    return conv_group_launch<false>(n_conv, convs, stream, "rf_conv2d_f16_group");
 }
 
 extern "C" int rf_conv1x1_f16_group(int n_conv, const void* const* in, const int* cin_pad, const void* const* w,
@@ -2883,7 +2898,12 @@ extern "C" int rf_conv1x1_f16_group(int n_conv, const void* const* in, const int
         d[q].kh = d[q].kw = d[q].stride = 1;
         d[q].p_ld = p_ld[q];
     }
-    return rf_conv2d_f16_group(n_conv, d, stream);
+    // (RF_CONV_GROUP_DENSE=0: the gathered 32-deep loop, A/B)
+    static const bool dense = !getenv("RF_CONV_GROUP_DENSE") || atoi(getenv("RF_CONV_GROUP_DENSE")) != 0;
+    bool ok = dense;
+    for (int q = 0; q < n_conv; ++q) ok = ok && cin_pad[q] % 64 == 0;
+    return ok ? conv_group_launch<true>(n_conv, d, stream, "rf_conv1x1_f16_group")
+              : conv_group_launch<false>(n_conv, d, stream, "rf_conv1x1_f16_group");
 }
 
 extern "C" int rf_deconv2d_bf16x3(const void* in_hi, const void* in_lo, int n_img, int hi, int wi, int cin_pad,
