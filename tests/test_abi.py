@@ -286,3 +286,26 @@ def test_integration_binding_runs_against_reference_attention():
         ref = torch.einsum("hqk,khd->qhd", torch.softmax(s, -1), vd[c0:c1])
         err = ((oc[a:b].double() - ref).norm() / ref.norm()).item()
         assert err < 6e-3, (i, err)
+
+
+def test_conv_desc_layout_matches_header(tmp_path):
+    """dpt._ConvDesc (ctypes) has the size and field offsets of rf.h's rf_conv_desc (checked with the host C
+    compiler on the header itself)."""
+    import ctypes
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no host C compiler")
+    from renderformer_amd.dpt import _ConvDesc
+    names = [f[0] for f in _ConvDesc._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "rf.h"\nint main(void) {\n'
+                   '  printf("%zu", sizeof(rf_conv_desc));\n' +
+                   "".join(f'  printf(" %zu", offsetof(rf_conv_desc, {"in" if n == "in_" else n}));\n' for n in names) +
+                   "  return 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.run([cc, "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    want = [ctypes.sizeof(_ConvDesc)] + [getattr(_ConvDesc, n).offset for n in names]
+    assert got == want
