@@ -182,20 +182,22 @@ def main():
     from renderformer_amd import RenderFormer, RenderFormerRenderingPipeline, ops
     from renderformer_amd.config import named_config
     from renderformer_amd.flops import frame_flops
-    from renderformer_amd.parallel import assign_units, gather_frames, max_over_ranks, scene_cost, shard_views
+    from renderformer_amd.parallel import FrameGather, PendingFrames, assign_units, max_over_ranks, scene_cost, shard_views
     from renderformer_amd.scenes import batch_scenes, synthetic_scene
     from renderformer_amd.weights import synthetic_state_dict
 
     cfg = named_config(args.config)
     sd = synthetic_state_dict(cfg, seed=0)
-    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd, fp8=args.fp8, view_chunk=args.view_chunk)).to(dev)
+    # fp16 range check deferred: no per-frame host wait in the timed loop; checked once after it (check_range)
+    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd, fp8=args.fp8, view_chunk=args.view_chunk,
+                                                      range_check="deferred")).to(dev)
 
     # ---- the units of one step: (batch tensors on the device, global frame ids)
     if args.workload == "cbox":
         scenes = [synthetic_scene(args.tris, args.views, seed=1 + rank * args.scenes + i) for i in range(args.scenes)]
         hosts = [batch_scenes(scenes)]
         n_per_rank = args.scenes * args.views
-        ids = [list(range(rank * n_per_rank, (rank + 1) * n_per_rank))]
+        rank_ids = [list(range(r * n_per_rank, (r + 1) * n_per_rank)) for r in range(world)]
         n_frames_step = n_per_rank * world
         scaling = "weak"
     elif args.workload == "c4":
@@ -204,12 +206,17 @@ def main():
         from renderformer_amd.examples import convert_all, example_names
         from renderformer_amd.h5io import load_single_h5_data
         names = example_names()
-        files = convert_all(names, workers=8)
+        if world > 1:  # rank 0 converts (8 processes), the others wait and then only find the cached files
+            if rank == 0:
+                convert_all(names, workers=8)
+            dist.barrier()
+        files = convert_all(names, workers=8 if world == 1 else 1)
         step_names = [names[i % len(names)] for i in range(args.scenes)]
         scene_data = {n: load_single_h5_data(files[n]) for n in set(step_names)}
         counts = [int(scene_data[n]["triangles"].shape[0]) for n in step_names]
         costs = [scene_cost(cfg, n, args.views, args.res) for n in counts]
-        mine = assign_units(costs, world)[rank]
+        plan = assign_units(costs, world)
+        mine = plan[rank]
         hosts = []
         for i in mine:
             d = scene_data[step_names[i]]
@@ -217,15 +224,16 @@ def main():
             vsel = [v % nv for v in range(args.views)]  # --views views of the scene's cameras (cycled)
             hosts.append({"triangles": d["triangles"][None], "texture": d["texture"][None], "mask": d["mask"][None],
                           "vn": d["vn"][None], "c2w": d["c2w"][vsel][None], "fov": d["fov"][vsel].reshape(1, -1, 1)})
-        ids = [[i * args.views + v for v in range(args.views)] for i in mine]
+        rank_ids = [[i * args.views + v for i in plan[r] for v in range(args.views)] for r in range(world)]
         n_frames_step = args.scenes * args.views
         scaling = "strong"
     else:  # c5
         sc = synthetic_scene(args.tris, args.views, seed=1)
-        vr = shard_views(args.views, world)[rank]
+        shards = shard_views(args.views, world)
+        vr = shards[rank]
         sc.c2w, sc.fov = sc.c2w[vr.start:vr.stop], sc.fov[vr.start:vr.stop]
         hosts = [batch_scenes([sc])] if len(vr) else []
-        ids = [list(vr)] if len(vr) else []
+        rank_ids = [list(r) for r in shards]
         n_frames_step = args.views
         scaling = "strong"
     batches = [{k: v.to(dev) for k, v in h.items() if k != "tex_channels"} for h in hosts]
@@ -240,6 +248,9 @@ def main():
     calls = [0]
     chans = 4 if cfg.include_alpha else 3
     frame_shape = (args.res, args.res, chans)
+    # finished frames to every rank: ONE RCCL all_gather per step with the static per-rank counts / ids above (no
+    # host sync), issued asynchronously so it overlaps the next step's launches (parallel.FrameGather)
+    gather = FrameGather(rank_ids, frame_shape, dev) if world > 1 else None
 
     def step():
         frames = []
@@ -257,12 +268,12 @@ def main():
             local = frames[0]
         else:
             local = torch.cat(frames) if frames else torch.empty((0,) + frame_shape, device=dev)
-        if world > 1:  # finished frames to every rank (RCCL all_gather over xGMI)
-            return gather_frames(local, [i for u in ids for i in u], n_frames_step)
-        return local
+        if world > 1:  # finished frames to every rank (RCCL all_gather over xGMI), completed by .result()
+            return gather.start(local)
+        return PendingFrames(out=local)
 
     for _ in range(args.warmup):
-        step()
+        step().result()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -275,15 +286,21 @@ def main():
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
+    pend = None
     for i in range(args.steps):
         if i == args.steps - 1:
             ops.TIMER = timer
-        out = step()
+        nxt = step()
+        if pend is not None:  # the previous step's gather ran beside this step's launches; the stream waits for it
+            pend.result()
+        pend = nxt
+    out = pend.result()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ops.TIMER = None
+    pipe.check_range()  # every timed frame has completed: raise if one overflowed fp16 (DeviceError)
     elapsed = max_over_ranks(elapsed, device=dev if args.backend == "nccl" else None)
     if not torch.isfinite(out).all():
         raise RuntimeError("non-finite output")
@@ -358,7 +375,8 @@ def main():
                                f"{cfg.view_transformer_use_swin_attn} dpt={cfg.dpt_features}/{cfg.dpt_out_channels}",
                 "global_batch": n_frames_step, "seq_len": s_len, "res": args.res,
                 "parallelism": f"dp{world}" + ("" if args.workload != "c5" else " (views)"),
-                "gather": "RCCL all_gather of the HDR frames" if world > 1 and args.backend == "nccl" else
+                "gather": "one async RCCL all_gather of the HDR frames per step (static counts, overlaps the next step)"
+                          if world > 1 and args.backend == "nccl" else
                           (f"{args.backend} all_gather" if world > 1 else "none (1 rank)"),
                 "weights": "synthetic seed 0 (no checkpoint offline)",
                 "precision": ("stage-2 cross-attention Q and FFN W2 MX fp8 (e4m3, E8M0 per 32) on bf16 operands, "

@@ -59,7 +59,7 @@ extern "C" {
 #define RF_ERR_UNSUPPORTED 3
 #define RF_ERR_DEVICE 4       /* an earlier launch reported a device-side error (see rf_device_error) */
 
-#define RF_ABI_VERSION 11
+#define RF_ABI_VERSION 12
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -86,6 +86,14 @@ int rf_abi_version(void);
  * must be re-zeroed.  rf_debug_raise_device_error launches a kernel that stores `code` (tests). */
 int rf_device_error(void);
 int rf_clear_device_error(void);
+/* fp16 range flag.  Every writer of fp16 operands (RF_EPI_F16 / RF_EPI_SWIGLU_F16 GEMM outputs, rf_rmsnorm_f16,
+ * fp16 attention / Swin O, fp16 DPT planes of the convolutions and rf_split_planes) stores a non-zero code (1 GEMM,
+ * 2 RMSNorm, 4 attention, 8 DPT plane) into a second host-mapped word when it meets a value beyond fp16's range
+ * (|x| > 65504, inf included; NaN operands are not flagged): the values it wrote are inf.  Read with
+ * rf_f16_range_flag() (no device sync: read it after the launches in question have completed), reset with
+ * rf_clear_f16_range_flag().  The model re-renders such a frame with bf16 operands (RenderFormer.range_check). */
+int rf_f16_range_flag(void);
+int rf_clear_f16_range_flag(void);
 int rf_debug_raise_device_error(int code, void* stream);
 
 /* Kernel timer (measurement only; bench.py's roofline).  rf_ktimer_arm() creates a start/stop event pair on the
@@ -209,6 +217,16 @@ int rf_attn_combine(const void* workspace, int64_t ws_rows, int n_split, int n_h
 int rf_attn_fwd_sk(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                    void* o, int64_t ldo, int o_dtype, const int32_t* problems, int n_problems, int n_heads,
                    int head_dim, float scale, void* workspace, const int64_t* bounds, int grid, void* stream);
+/* The stream-K attention with the q/k/v element type as an argument: qkv_dtype RF_DT_F16 runs fp16 operands on
+ * v_mfma_f32_32x32x16_f16 (the bf16 rate; P is fp16 too), RF_DT_BF16 the bf16 kernel; O is o_dtype.  Replaces
+ * flash_attn_varlen_qkvpacked_func / flash_attn_varlen_kvpacked_func (renderformer/layers/attention.py:166-172,
+ * 193-195) for EITHER half type the reference hands them: its default torch_dtype=torch.float16
+ * (rendering_pipeline.py:37, infer.py:37, batch_infer.py:65) makes q/k/v fp16, bf16 runs make them bf16.  bounds
+ * NULL = equal ranges (then grid is ignored), else an rf_attn_schedule table for `grid` workgroups. */
+int rf_attn_fwd_dt(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                   void* o, int64_t ldo, int qkv_dtype, int o_dtype, const int32_t* problems, int n_problems,
+                   int n_heads, int head_dim, float scale, void* workspace, const int64_t* bounds, int grid,
+                   void* stream);
 
 /* Shifted-window attention over n_images patch grids [grid_h, grid_w] stored row-major (token
  * r = img*gh*gw + y*gw + x); windows of window x window tokens on the grid rolled by -shift,
@@ -298,7 +316,7 @@ int rf_hdr_output(const float* logits, float* out, int n, int c, int h, int w, f
  * p_hi/p_lo (channel stride p_ld), of silu(v) when RF_CONV_PLANE_SILU.
  * RF_CONV_FINAL (cout <= 64): out[pixel, f] = elu(sum_c silu(v_c) * w_fin[f, c] + b_fin[f], alpha),
  * then 10^x - 1 with RF_CONV_LOG_DECODE; [n, n_fin, h, w] layout with RF_CONV_NCHW_OUT.
- * RF_CONV_BORDER_BIAS (3x3, pad 1, stride 1): `bias` holds 9 rows of cout, row 3 ry + rx with ry / rx = 0 on the
+ * RF_CONV_BORDER_BIAS (3x3, pad 1, stride 1, images of at least 2 x 2 pixels): `bias` holds 9 rows of cout, row 3 ry + rx with ry / rx = 0 on the
  * first image row / column, 2 on the last, 1 elsewhere: the bias of a convolution whose input carried a constant
  * that zero padding cuts at the border (an affine 1x1 folded into the 3x3 weights, dpt.py output_conv1). */
 #define RF_CONV_PLANE_SILU 1

@@ -40,6 +40,7 @@ SIGNATURES = {
     "rf_gemm_f16": [_P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _L, _P],
     "rf_rmsnorm_f16": [_P, _L, _P, _F, _P, _L, _I, _I, _P],
     "rf_attn_fwd_sk": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _P, _I, _I, _I, _F, _P, _P, _I, _P],
+    "rf_attn_fwd_dt": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _P, _I, _I, _I, _F, _P, _P, _I, _P],
     "rf_swin_attn_fwd_dt": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P],
     "rf_rmsnorm": [_P, _L, _P, _F, _P, _L, _I, _I, _P],
     "rf_qk_norm_rope": [_P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _F, _F, _P, _L, _I, _P, _I, _P],
@@ -80,6 +81,8 @@ SIGNATURES = {
     "rf_quant_mx8": [_P, _L, _I, _I, _P, _L, _P, _L, _P],
     "rf_device_error": [],
     "rf_clear_device_error": [],
+    "rf_f16_range_flag": [],
+    "rf_clear_f16_range_flag": [],
     "rf_debug_raise_device_error": [_I, _P],
     "rf_ktimer_arm": [],
     "rf_ktimer_read": [_P, _I],
@@ -97,7 +100,9 @@ class HipLibraryError(RuntimeError):
 class DeviceError(RuntimeError):
     """A kernel reported a device-side failure (a stream-K hand-off that timed out, or a range table that does not
     fit its launch): the outputs of that launch are invalid.  ``renderformer_amd.ops.clear_device_error()``
-    recovers (it drains the device, clears the error word and drops the stream-K workspaces)."""
+    recovers (it drains the device, clears the error word and drops the stream-K workspaces).  Also raised by a
+    deferred fp16 range check (``RenderFormer(range_check="deferred")``) that finds a frame whose fp16 operands
+    overflowed."""
 
 
 def load(require_device: bool = True):

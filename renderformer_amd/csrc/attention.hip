@@ -83,6 +83,7 @@ struct AttnArgs {
     const int64_t* bounds;
     int epoch;  // hand-off flag value of this launch (> 0, new every launch: no re-arm, stale flags never match)
     int o_f16;  // output O as fp16 (the A operand of an fp16 out-projection) instead of bf16
+    int* range; // o_f16: the mapped fp16 range flag (|O| > 65504), else null
     int ascend; // diagnostic (RF_SK_ASCEND=1): ascending blockIdx order inside a group (the round-2 layout), A/B only
 };
 
@@ -438,6 +439,14 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_fwd_kernel(Attn
     }
     const float inv = l_tot > 0.f ? 1.0f / l_tot : 0.f;
     bf16_t* dst = p.o + (int64_t)orow * p.ldo + hoff;
+    if constexpr (OF16) {  // fp16 O (Swin): range flag as in the stream-K epilogue
+        float amax = 0.f;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) amax = amax3(amax, o[dt][r] * inv, o[dt][r + 1] * inv);
+        if (p.range && !f16_in_range(amax)) report_f16_range(p.range, RF_RANGE_ATTN);
+    }
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
@@ -736,6 +745,30 @@ RF_DEV uint32_t cvt_pk_bf16(float lo, float hi) {
     asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
     return r;
 }
+// two f32 -> one packed fp16x2 (RNE), pinned like cvt_pk_bf16
+RF_DEV uint32_t cvt_pk_f16(float lo, float hi) {
+    uint32_t r;
+    asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+    return r;
+}
+// the P operand format of the stream-K kernel follows its q/k/v format (F16: fp16, else bf16).  Fragments are
+// carried as bf16x8 bit containers either way and re-typed at the MFMA (mfma32).
+template <bool F16>
+RF_DEV uint32_t cvt_pk_p(float lo, float hi) { return F16 ? cvt_pk_f16(lo, hi) : cvt_pk_bf16(lo, hi); }
+template <bool F16>
+RF_DEV __bf16 to_p16(float e) {
+    if constexpr (F16) return __builtin_bit_cast(__bf16, (_Float16)e);
+    else return (__bf16)e;
+}
+// v_mfma_f32_32x32x16_bf16 / _f16 (same cycles) on 8 x 16-bit fragments
+template <bool F16>
+RF_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+    if constexpr (F16)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                      0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
 // dword w (0..3) of an MFMA bf16x8 operand
 RF_DEV void set_pk(bf16x8& f, int w, uint32_t v) {
     u32x4 u = __builtin_bit_cast(u32x4, f);
@@ -755,7 +788,10 @@ RF_DEV void dma_piece(const bf16_t* g, uint32_t lds) {
 // 2 = no top-of-tile wait + barrier, 4 = no PV MFMAs, 8 = no exp2 (P = bf16(S)), 16 = no QK MFMAs,
 // 32 = s_memtime stamps per segment (cycles summed over tiles) into the workspace's last piece slot,
 // 64 = no static priority for waves 4-7
-template <bool UNIT, int DBG = 0, bool OF16 = false>
+// IF16: q, k, v (and P) as fp16 on v_mfma_f32_32x32x16_f16 — the reference's default half precision hands
+// flash_attn_varlen_* fp16 operands (rendering_pipeline.py:37, attention.py:166-172); else bf16.  P <= 2^thr
+// (= 2^12 by default) stays inside fp16's range.
+template <bool UNIT, int DBG = 0, bool OF16 = false, bool IF16 = false>
 __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     // SPLIT: half of each tile's softmax (keys 32-63) moves from phase A (QK^T, VALU-heavy) into the first
     // half of phase B (PV, VALU-light), balancing the two phases that share each SIMD; DBG & 128 = unsplit
@@ -904,7 +940,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 for (int st = 0; st < 8; ++st) {
                     const bf16x8 a = *reinterpret_cast<const bf16x8*>(smem + koff + (st & 1 ? kb_odd : kb_even) +
                                                                       8192 * b + 512 * (st >> 1));
-                    s[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[st], st == 0 ? minit : s[b], 0, 0, 0);
+                    s[b] = mfma32<IF16>(a, qf[st], st == 0 ? minit : s[b]);
                 }
         };
         auto mask_tail = [&](f32x16* sv, int t) {  // keys >= k_len of tile t -> -inf (tail tile only)
@@ -1028,7 +1064,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                     if (st == 0) sn[b] = minit;
                     asm volatile("" : "+v"(kf[j % 3]));
                 } else {
-                    sn[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[j % 3], qf[st], st == 0 ? minit : sn[b], 0, 0, 0);
+                    sn[b] = mfma32<IF16>(kf[j % 3], qf[st], st == 0 ? minit : sn[b]);
                 }
                 if (!SPLIT || j < 8) {
                     float e[2];
@@ -1041,10 +1077,10 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                         asm volatile("" : "+v"(ls[x & 3]));  // keep the add in this gap (IR passes sink it)
                     }
                     if constexpr (CVT_PIN) {
-                        set_pk(pf[j >> 3][(j >> 2) & 1], j & 3, cvt_pk_bf16(e[0], e[1]));
+                        set_pk(pf[j >> 3][(j >> 2) & 1], j & 3, cvt_pk_p<IF16>(e[0], e[1]));
                     } else {
-                        pf[j >> 3][(j >> 2) & 1][2 * (j & 3)] = (__bf16)e[0];
-                        pf[j >> 3][(j >> 2) & 1][2 * (j & 3) + 1] = (__bf16)e[1];
+                        pf[j >> 3][(j >> 2) & 1][2 * (j & 3)] = to_p16<IF16>(e[0]);
+                        pf[j >> 3][(j >> 2) & 1][2 * (j & 3) + 1] = to_p16<IF16>(e[1]);
                     }
                 }
                 if constexpr (!(DBG & 1)) {
@@ -1067,7 +1103,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                     const float v = s[x >> 4][x & 15];
                     const float e = fast_exp2(UNIT ? v : v * c);
                     l_tile += e;
-                    pf[x >> 4][(x >> 3) & 1][x & 7] = (__bf16)e;
+                    pf[x >> 4][(x >> 3) & 1][x & 7] = to_p16<IF16>(e);
                 }
             }
             l_run += l_tile;
@@ -1103,7 +1139,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                             const float v = s[x >> 4][x & 15];
                             const float e = fast_exp2(UNIT ? v : v * c);
                             l2 += e;
-                            pf[x >> 4][(x >> 3) & 1][x & 7] = (__bf16)e;
+                            pf[x >> 4][(x >> 3) & 1][x & 7] = to_p16<IF16>(e);
                         }
                     }
                     l_run += l2;
@@ -1111,7 +1147,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 if constexpr (DBG & 4) {
                     asm volatile("" : "+v"(vf[j % 3]), "+v"(pf[b][sp]));
                 } else {
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[j % 3], pf[b][sp], o[dt], 0, 0, 0);
+                    o[dt] = mfma32<IF16>(vf[j % 3], pf[b][sp], o[dt]);
                 }
                 if (SPLIT && j < 8) {
                     float e[2];
@@ -1124,10 +1160,10 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                         asm volatile("" : "+v"(ls[x & 3]));
                     }
                     if constexpr (CVT_PIN) {
-                        set_pk(pf[x_blk(16 + 2 * j)][x_sp(16 + 2 * j)], j & 3, cvt_pk_bf16(e[0], e[1]));
+                        set_pk(pf[x_blk(16 + 2 * j)][x_sp(16 + 2 * j)], j & 3, cvt_pk_p<IF16>(e[0], e[1]));
                     } else {
-                        pf[x_blk(16 + 2 * j)][x_sp(16 + 2 * j)][(2 * j) & 7] = (__bf16)e[0];
-                        pf[x_blk(16 + 2 * j)][x_sp(16 + 2 * j)][(2 * j + 1) & 7] = (__bf16)e[1];
+                        pf[x_blk(16 + 2 * j)][x_sp(16 + 2 * j)][(2 * j) & 7] = to_p16<IF16>(e[0]);
+                        pf[x_blk(16 + 2 * j)][x_sp(16 + 2 * j)][(2 * j + 1) & 7] = to_p16<IF16>(e[1]);
                     }
                 } else if (SPLIT) {
 #pragma unroll
@@ -1246,6 +1282,14 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         const int qrow_o = q0 + qi;
         if (qrow_o < q1) {  // (lanes l and l + 32 hold the same query row: both store or neither)
             bf16_t* dst = p.o + (int64_t)(q_start + qrow_o) * p.ldo + hoff;
+            if constexpr (OF16) {  // fp16 O: |O| <= max |V| row-wise, but V (bf16) may exceed fp16's range
+                float amax = 0.f;
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int r = 0; r < 16; r += 2) amax = amax3(amax, o[dt][r] * inv, o[dt][r + 1] * inv);
+                if (p.range && !f16_in_range(amax)) report_f16_range(p.range, RF_RANGE_ATTN);
+            }
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
@@ -1802,13 +1846,15 @@ int cu_count() {  // per-device, queried once
 
 int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv, void* o,
                    int64_t ldo, const int32_t* problems, int n_problems, int n_heads, float scale, void* workspace,
-                   void* stream, const int64_t* bounds = nullptr, int grid = 0, bool o_f16 = false) {
+                   void* stream, const int64_t* bounds = nullptr, int grid = 0, bool o_f16 = false,
+                   bool i_f16 = false) {
     RF_REQUIRE(workspace, "rf_attn_fwd: stream-K mode needs the workspace (rf_attn_workspace_bytes(0, H, 0))");
     if (!bounds) {
         grid = cu_count();
         if (const char* env = getenv("RF_ATTN_GRID")) grid = atoi(env);  // tests: force many cut units
     }
     RF_REQUIRE(grid >= 1 && grid <= SK5_MAX_GRID, "rf_attn_fwd: grid %d out of range", grid);
+    hipStream_t st0 = (hipStream_t)stream;
     AttnArgs a{};
     a.q = (const bf16_t*)q;
     a.k = (const bf16_t*)k;
@@ -1825,6 +1871,7 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
     a.part_o = (float*)workspace;
     a.flag = (int*)(a.part_o + (int64_t)SK5_MAX_GRID * PIECE_FLOATS);
     a.o_f16 = o_f16;
+    a.range = o_f16 ? rf::range_word() : nullptr;
     a.ascend = getenv("RF_SK_ASCEND") && atoi(getenv("RF_SK_ASCEND")) == 1;
     a.bounds = bounds;
     if (!bounds) {  // equal split per XCD group, written on the device ahead of the launch (stream-ordered)
@@ -1837,14 +1884,24 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
     a.spin = rf::spin_limit();
     // a fresh flag value per launch: a publisher's flag from an earlier launch (even one that timed out and left
     // a late flag behind) never equals this launch's, so flags need no re-arm and no memset
-    static std::atomic<int> epoch{0};
-    a.epoch = 1 + (epoch.fetch_add(1) & 0x3fffffff);
+    a.epoch = rf::next_epoch(a.flag, SK5_MAX_GRID * sizeof(int), st0);
     // (the grid may exceed the CUs: the SkLayout waits only go to earlier-dispatched blocks)
     // q pre-scaled by scale*log2(e) upstream (scale = ln 2): scores are already exp2 exponents
     const bool unit = fabsf(a.c - 1.0f) < 1e-6f;
     const int dbg = getenv("RF_ATTN_DBG") ? atoi(getenv("RF_ATTN_DBG")) : 0;
     const dim3 g(grid), b(NW5 * 64);
     hipStream_t st = (hipStream_t)stream;
+    if (i_f16) {  // fp16 q/k/v (rf_attn_fwd_dt): the production kernel only, no diagnostic variants
+        if (unit && o_f16)
+            RF_LAUNCH((attn_sk_kernel<true, 0, true, true>), g, b, 0, st, a);
+        else if (unit)
+            RF_LAUNCH((attn_sk_kernel<true, 0, false, true>), g, b, 0, st, a);
+        else if (o_f16)
+            RF_LAUNCH((attn_sk_kernel<false, 0, true, true>), g, b, 0, st, a);
+        else
+            RF_LAUNCH((attn_sk_kernel<false, 0, false, true>), g, b, 0, st, a);
+        return rf::check_launch("rf_attn_fwd_dt");
+    }
     if (getenv("RF_ATTN_P4") && atoi(getenv("RF_ATTN_P4")) == 1) {  // one-wave-per-SIMD kernel
         a.thr = getenv("RF_ATTN_THR") ? (float)atof(getenv("RF_ATTN_THR")) : P4_SUM_THR_LOG2;
         if (unit)
@@ -2179,6 +2236,21 @@ extern "C" int rf_attn_fwd_sk(const void* q, int64_t ldq, const void* k, int64_t
                           bounds, bounds ? grid : 0, o_dtype == RF_DT_F16);
 }
 
+extern "C" int rf_attn_fwd_dt(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                              void* o, int64_t ldo, int qkv_dtype, int o_dtype, const int32_t* problems,
+                              int n_problems, int n_heads, int head_dim, float scale, void* workspace,
+                              const int64_t* bounds, int grid, void* stream) {
+    RF_REQUIRE(q && k && v && o && problems && workspace, "rf_attn_fwd_dt: null pointer");
+    RF_REQUIRE(head_dim == HD, "rf_attn_fwd_dt: head_dim must be 128 (got %d)", head_dim);
+    RF_REQUIRE(qkv_dtype == RF_DT_BF16 || qkv_dtype == RF_DT_F16, "rf_attn_fwd_dt: qkv_dtype must be RF_DT_BF16/F16");
+    RF_REQUIRE(o_dtype == RF_DT_BF16 || o_dtype == RF_DT_F16, "rf_attn_fwd_dt: o_dtype must be RF_DT_BF16/F16");
+    RF_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0, "rf_attn_fwd_dt: strides must be 16-B aligned");
+    RF_REQUIRE(n_heads >= 1, "rf_attn_fwd_dt: n_heads must be >= 1");
+    if (n_problems <= 0) return RF_OK;
+    return attn_sk_launch(q, ldq, k, ldk, v, ldv, o, ldo, problems, n_problems, n_heads, scale, workspace, stream,
+                          bounds, bounds ? grid : 0, o_dtype == RF_DT_F16, qkv_dtype == RF_DT_F16);
+}
+
 extern "C" int64_t rf_attn_workspace_bytes(int64_t rows, int n_heads, int n_split) {
     if (n_split == 0)  // partial slots, flags, the device-built equal range table
         return (int64_t)SK5_MAX_GRID * PIECE_FLOATS * 4 + SK5_MAX_GRID * 4 + (SK5_MAX_GRID + 1) * 8;
@@ -2225,6 +2297,7 @@ extern "C" int rf_swin_attn_fwd_dt(const void* q, int64_t ldq, const void* k, in
     a.n_split = 1;
     dim3 grid((grid_h / window) * (grid_w / window), n_heads, n_images);
     RF_REQUIRE(o_dtype == RF_DT_BF16 || o_dtype == RF_DT_F16, "rf_swin_attn_fwd: o_dtype must be RF_DT_BF16/F16");
+    a.range = o_dtype == RF_DT_F16 ? rf::range_word() : nullptr;
     if (o_dtype == RF_DT_F16)
         RF_LAUNCH((attn_fwd_kernel<true, 2, true>), grid, dim3(128), 0, (hipStream_t)stream, a);
     else

@@ -5,7 +5,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "common.h"
@@ -38,6 +40,37 @@ int* device_error_word() {
         g_dev_err_dev = (int*)d;
     });
     return g_dev_err_dev;
+}
+
+// word 1 of the same mapped allocation: the fp16 range flag (rf_f16_range_flag)
+int* range_word() {
+    int* w = device_error_word();
+    return w ? w + 1 : nullptr;
+}
+
+// Hand-off flag epochs of the stream-K kernels (attention and GEMM/conv): every launch gets a fresh flag value,
+// so flags need no re-arm and no memset between launches.  Values are 1 + (counter mod 2^B) (B = 30, or
+// RF_EPOCH_BITS for tests), i.e. they repeat every 2^B launches; a flag slot written 2^B launches ago and never
+// since could then equal the current value and let an owner fold a stale partial.  So per flag area the
+// generation (counter >> B) of its last launch is remembered, and the first launch of a new generation on an area
+// re-zeroes the area first (stream-ordered hipMemsetAsync; zero is never an epoch).  Thread-safe; 64-bit counter.
+int next_epoch(void* flags, size_t bytes, hipStream_t st) {
+    static std::mutex mu;
+    static uint64_t counter = 0;
+    static std::unordered_map<void*, uint64_t> gen_of;
+    const char* env = getenv("RF_EPOCH_BITS");  // (read per launch: tests shrink the period to force wraps)
+    const int bits = env ? std::min(30, std::max(2, atoi(env))) : 30;
+    std::lock_guard<std::mutex> lk(mu);
+    const uint64_t c = counter++;
+    const uint64_t gen = c >> bits;
+    auto it = gen_of.find(flags);
+    if (it == gen_of.end()) {
+        gen_of.emplace(flags, gen);  // a new area is zero-filled by its owner (rf.h workspace contract)
+    } else if (it->second != gen) {
+        (void)hipMemsetAsync(flags, 0, bytes, st);
+        it->second = gen;
+    }
+    return 1 + (int)(c & ((1ull << bits) - 1));
 }
 
 int spin_limit() {
@@ -93,6 +126,17 @@ extern "C" int rf_device_error(void) {
 extern "C" int rf_clear_device_error(void) {
     rf::device_error_word();
     if (rf::g_dev_err_host) *rf::g_dev_err_host = 0;
+    return RF_OK;
+}
+
+extern "C" int rf_f16_range_flag(void) {
+    rf::device_error_word();
+    return rf::g_dev_err_host ? rf::g_dev_err_host[1] : 0;
+}
+
+extern "C" int rf_clear_f16_range_flag(void) {
+    rf::device_error_word();
+    if (rf::g_dev_err_host) rf::g_dev_err_host[1] = 0;
     return RF_OK;
 }
 

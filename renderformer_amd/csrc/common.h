@@ -12,6 +12,7 @@ typedef uint16_t bf16_t;  // raw bf16 bits in memory
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;  // MFMA A/B fragment (4 VGPRs)
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;  // fp16 MFMA A/B fragment
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
@@ -83,6 +84,24 @@ RF_DEV float silu_precise(float x) { return x / (1.0f + expf(-x)); }
 RF_DEV void report_device_error(int* err, int code) {
     if (err) __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// fp16 range flag (rf_f16_range_flag): a writer of fp16 operands that met a value it cannot represent (|x| >
+// 65504, inf included) stores its code; the values it wrote are inf.  Plain vector system-scope store, like the
+// error word (only ever taken on the failing path).
+RF_DEV void report_f16_range(int* w, int code) {
+    if (w) __hip_atomic_store(w, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// |x| <= 65504 (fp16's largest finite value) for a running max of |x| (an inf input fails it)
+RF_DEV bool f16_in_range(float amax) { return amax <= 65504.0f; }
+// running max of |a|, |b| (v_max3_f32 with abs source modifiers).  A NaN operand is ignored: NaNs come from NaN
+// inputs (the reference propagates them too, and bf16 operands would not remove them), while an overflow is caught
+// where the finite value that exceeds fp16's range is produced
+RF_DEV float amax3(float m, float a, float b) {
+    return __builtin_fmaxf(__builtin_fmaxf(m, __builtin_fabsf(a)), __builtin_fabsf(b));
+}
+#define RF_RANGE_GEMM 1      // rf_gemm_f16 / rf_gemm_bf16 RF_EPI_F16 / RF_EPI_SWIGLU_F16 outputs
+#define RF_RANGE_RMSNORM 2   // rf_rmsnorm_f16
+#define RF_RANGE_ATTN 4      // attention / Swin O written as fp16
+#define RF_RANGE_CONV 8      // DPT fp16 planes (conv epilogue plane, rf_split_planes)
 #define RF_DEVERR_SK_GEMM 1
 #define RF_DEVERR_SK_ATTN 2
 #define RF_DEVERR_SK_SCHED 3  // a stream-K range table that does not cover the launch's tiles (rejected in-kernel)
@@ -148,7 +167,11 @@ namespace rf {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 int* device_error_word();  // device pointer of the mapped error word (nullptr if it could not be allocated)
+int* range_word();         // device pointer of the mapped fp16 range flag (rf_f16_range_flag)
 int spin_limit();          // stream-K hand-off spin bound (RF_SPIN_LIMIT, default 2^24 polls)
+// fresh hand-off flag value (>= 1) for a stream-K launch on the flag area [flags, flags + bytes); re-zeroes the
+// area on the stream when the epoch sequence wraps (capi.cpp)
+int next_epoch(void* flags, size_t bytes, hipStream_t st);
 // Kernel timer (rf_ktimer_arm / rf_ktimer_read): when armed, the next library launch takes a start/stop event
 // pair that the dispatch packet itself timestamps (hipExtLaunchKernel), so the measured duration is the
 // kernel's own, as in a rocprofv3 kernel trace, with no extra packets in the queue.

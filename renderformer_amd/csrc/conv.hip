@@ -12,7 +12,8 @@
 namespace {
 
 
-RF_DEV void store_split4(bf16_t* p_hi, bf16_t* p_lo, int64_t off, float4 v, bool act) {
+// returns max |value| written to an fp16 plane (0 for hi/lo planes): the range flag's input
+RF_DEV float store_split4(bf16_t* p_hi, bf16_t* p_lo, int64_t off, float4 v, bool act) {
     float x[4] = {v.x, v.y, v.z, v.w};
     if (!p_lo) {
         if (act) {
@@ -20,7 +21,7 @@ RF_DEV void store_split4(bf16_t* p_hi, bf16_t* p_lo, int64_t off, float4 v, bool
             for (int e = 0; e < 4; ++e) x[e] = silu(x[e]);
         }
         *reinterpret_cast<uint2*>(p_hi + off) = make_uint2(pack_f16x2(x[0], x[1]), pack_f16x2(x[2], x[3]));
-        return;
+        return amax3(amax3(0.f, x[0], x[1]), x[2], x[3]);
     }
     uint32_t h[2], l[2];
 #pragma unroll
@@ -36,18 +37,21 @@ RF_DEV void store_split4(bf16_t* p_hi, bf16_t* p_lo, int64_t off, float4 v, bool
     }
     *reinterpret_cast<uint2*>(p_hi + off) = make_uint2(h[0], h[1]);
     *reinterpret_cast<uint2*>(p_lo + off) = make_uint2(l[0], l[1]);
+    return 0.f;
 }
 
 __global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ x, int rows, int c, int64_t ldx,
                                                     bf16_t* __restrict__ p_hi, bf16_t* __restrict__ p_lo, int p_ld,
-                                                    int act) {
+                                                    int act, int* range) {
     const int c4 = c / 4;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;  // rows * c4 < 2^31 (host check)
     if (i >= rows * c4) return;
     const int r32 = i / c4;
     const int64_t r = r32;
     const int cc = (i - r32 * c4) * 4;
-    store_split4(p_hi, p_lo, r * p_ld + cc, *reinterpret_cast<const float4*>(x + r * ldx + cc), act);
+    const float am = store_split4(p_hi, p_lo, r * p_ld + cc, *reinterpret_cast<const float4*>(x + r * ldx + cc), act);
+    // one fp16 plane (p_lo == NULL): the decoder taps cast to fp16 must fit its range
+    if (range && !f16_in_range(am)) report_f16_range(range, RF_RANGE_CONV);
 }
 
 // bilinear, align_corners=True (torch upsample_bilinear2d); scale passed from the host.  One block row per
@@ -201,7 +205,7 @@ extern "C" int rf_split_planes(const float* x, int64_t rows, int c, int64_t ldx,
     if (n <= 0) return RF_OK;
     RF_REQUIRE(n < (1ll << 31) - 256, "rf_split_planes: too many elements");
     RF_LAUNCH(split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, (int)rows, c,
-                       ldx, (bf16_t*)p_hi, (bf16_t*)p_lo, p_ld, silu_act);
+                       ldx, (bf16_t*)p_hi, (bf16_t*)p_lo, p_ld, silu_act, p_lo ? nullptr : rf::range_word());
     return rf::check_launch("rf_split_planes");
 }
 

@@ -35,7 +35,6 @@ namespace {
 
 constexpr int BK = 32;
 constexpr int P_F16 = 2;  // NTERM value of the fp16-operand mode
-typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 
 enum Epi { E_BF16 = RF_EPI_BF16, E_F32 = RF_EPI_F32, E_ADD = RF_EPI_ADD_F32, E_SWIGLU = RF_EPI_SWIGLU, E_CONV = 16 };
 
@@ -99,6 +98,7 @@ struct EngineArgs {
     int ld_sa, ld_sw;
     int persist;  // phased_sk_kernel: whole tiles strided over the grid, next tile's first K-tiles prefetched
     int out_f16;  // E_BF16 / E_SWIGLU: 16-bit output as fp16 instead of bf16 (rf_gemm_f16's RF_EPI_*_F16)
+    int* range;   // fp16 outputs (out_f16, fp16 conv planes): the mapped range flag, raised on |x| > 65504
 };
 
 // two f32 -> the kernel's 16-bit output pair (RNE): fp16 when the launch asks for it, else bf16
@@ -414,6 +414,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
         if constexpr (TW2D == 0) return rbase + i * 16 + rl;
         else return m0 + (wm * (C::MW / TW2D) + (i * 16) / TW2D) * p.wo + (i * 16) % TW2D + rl;
     };
+    float amax = 0.f;  // fp16 outputs: running max |value| (NaN-propagating) for the range flag
     if constexpr (EPI == E_SWIGLU) {
         bf16_t* c = reinterpret_cast<bf16_t*>(p.c);
 #pragma unroll
@@ -434,11 +435,13 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                         }
                         o[e] = silu(g) * u;
                     }
+                    amax = amax3(amax3(amax, o[0], o[1]), o[2], o[3]);
                     *reinterpret_cast<uint2*>(c + (int64_t)row * p.ldc + ocol) =
                         make_uint2(pack16(p, o[0], o[1]), pack16(p, o[2], o[3]));
                 }
             }
         }
+        if (p.range && !f16_in_range(amax)) report_f16_range(p.range, RF_RANGE_GEMM);
         return;
     } else if constexpr (EPI == E_CONV) {
         if (FINAL && (p.flags & RF_CONV_FINAL)) {
@@ -549,6 +552,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
 #pragma unroll
                         for (int e = 0; e < 4; ++e) a[e] = silu_precise(a[e]);
                     }
+                    amax = amax3(amax3(amax, a[0], a[1]), a[2], a[3]);
                     *reinterpret_cast<uint2*>(p.p_hi + pix * p.p_ld + co) = make_uint2(pack_f16x2(a[0], a[1]),
                                                                                        pack_f16x2(a[2], a[3]));
                 } else if (p.p_hi) {
@@ -569,6 +573,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                 }
             }
         }
+        if (p.range && !f16_in_range(amax)) report_f16_range(p.range, RF_RANGE_CONV);
         return;
     } else {
 #pragma unroll
@@ -588,6 +593,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                 }
                 const int64_t o = (int64_t)row * p.ldc + col;
                 if constexpr (EPI == E_BF16) {
+                    amax = amax3(amax3(amax, v[0], v[1]), v[2], v[3]);
                     *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.c) + o) =
                         make_uint2(pack16(p, v[0], v[1]), pack16(p, v[2], v[3]));
                 } else {  // E_F32, or E_ADD whose accumulators started from the C tile (load_c_acc)
@@ -595,6 +601,8 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                 }
             }
         }
+        if constexpr (EPI == E_BF16)
+            if (p.range && !f16_in_range(amax)) report_f16_range(p.range, RF_RANGE_GEMM);
     }
 }
 
@@ -1806,12 +1814,11 @@ int launch_sk(EngineArgs a, int grid, void* stream, const char* what) {
     return rf::check_launch(what);
 }
 
-int g_sk_epoch = 0;  // flags from earlier launches never equal the current epoch (workspace zeroed once)
-
-void sk_setup(EngineArgs& p, void* workspace) {
+void sk_setup(EngineArgs& p, void* workspace, void* stream) {
     p.sk_part = (float*)workspace;
     p.sk_flag = (int*)(p.sk_part + SK_PART_FLOATS);
-    p.sk_epoch = ++g_sk_epoch;
+    // flags from earlier launches never equal the current epoch (rf::next_epoch re-zeroes the area on a wrap)
+    p.sk_epoch = rf::next_epoch(p.sk_flag, SK_MAX_GRID * sizeof(int), (hipStream_t)stream);
     p.err = rf::device_error_word();
     p.spin = rf::spin_limit();
     // diagnostics: stamps in the last 256 KiB of the partial area (tools/kbench.py skstamps)
@@ -2426,8 +2433,9 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
     p.bias = bias;
     p.gate = gate;
     p.out_f16 = out_f16;
+    p.range = out_f16 ? rf::range_word() : nullptr;
     if (workspace && ws_bytes >= SK_WS_BYTES && skph(m, n, k)) {
-        sk_setup(p, workspace);
+        sk_setup(p, workspace, stream);
         const int64_t tiles = (int64_t)((m + 255) / 256) * (n / 256);
         p.persist = tiles % 256 == 0 && persist_on();  // whole tiles per block either way: prefetching form
         if (f16) {
@@ -2450,7 +2458,7 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
     const bool big = cfg != 128;
     const int grid = (!big && workspace && ws_bytes >= SK_WS_BYTES) ? sk_grid(m, n, k) : 0;
     if (grid) {
-        sk_setup(p, workspace);
+        sk_setup(p, workspace, stream);
         switch (epilogue) {
             case RF_EPI_BF16: return launch_sk<T128, E_BF16>(p, grid, stream, "rf_gemm_bf16");
             case RF_EPI_F32: return launch_sk<T128, E_F32>(p, grid, stream, "rf_gemm_bf16");
@@ -2461,7 +2469,7 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
     // 256x256 tiles at one 512-thread block per CU reach ~1.2 PF/s when every CU has work; when the tile count
     // would leave a ragged last round, stream-K the K loop over exactly 256 blocks instead.
     if (workspace && ws_bytes >= SK_WS_BYTES && n % 256 == 0 && sk256(m, n, k)) {
-        sk_setup(p, workspace);
+        sk_setup(p, workspace, stream);
         switch (epilogue) {
             case RF_EPI_BF16: return launch_sk<T256, E_BF16>(p, 256, stream, "rf_gemm_bf16");
             case RF_EPI_F32: return launch_sk<T256, E_F32>(p, 256, stream, "rf_gemm_bf16");
@@ -2634,7 +2642,7 @@ static int conv_dispatch(EngineArgs& p, bool gather, bool big, int64_t sk_grid_n
             return gather ? conv_f16_dp<true>(p, stream, what, tile) : conv_f16_dp<false>(p, stream, what, tile);
     }
     if (sk_grid_n) {
-        sk_setup(p, workspace);
+        sk_setup(p, workspace, stream);
         // fp16 convolutions stream-K over the 8-wave 128x128 tile (64^2 / 32^2 DPT levels: 1.6x / 2.1x)
         if (NT == P_F16 && !(getenv("RF_CONV_SKW8") && atoi(getenv("RF_CONV_SKW8")) == 0))
             return gather ? launch_sk<T128w8, E_CONV, NT, true>(p, (int)sk_grid_n, stream, what)
@@ -2660,8 +2668,9 @@ static int conv_common(EngineArgs& p, int nterm, bool gather, const void* w_hi, 
                "%s: final head needs cout <= 64 and w_fin/b_fin", what);
     RF_REQUIRE(!(flags & RF_CONV_BORDER_BIAS) ||
                    (bias && !(flags & RF_CONV_FINAL) && p.kw == 3 && p.k == 9 * p.cin_pad && p.stride == 1 &&
-                    p.pad == 1 && p.ho == p.hi && p.wo == p.wi && p.deconv == 0),
-               "%s: RF_CONV_BORDER_BIAS needs a 3x3 stride-1 pad-1 convolution with its 9-row bias", what);
+                    p.pad == 1 && p.ho == p.hi && p.wo == p.wi && p.deconv == 0 && p.ho >= 2 && p.wo >= 2),
+               "%s: RF_CONV_BORDER_BIAS needs a 3x3 stride-1 pad-1 convolution of an image of at least 2 x 2 pixels "
+               "with its 9-row bias", what);
     static void* z = nullptr;  // device address of the zero row (per process; single device per process)
     if (!z && hipGetSymbolAddress(&z, HIP_SYMBOL(g_zero_row)) != hipSuccess) {
         z = nullptr;
@@ -2680,6 +2689,7 @@ static int conv_common(EngineArgs& p, int nterm, bool gather, const void* w_hi, 
     p.p_lo = (bf16_t*)p_lo;
     p.p_ld = p_ld;
     p.plane_f16 = nterm == P_F16;
+    p.range = (p_hi && nterm == P_F16) ? rf::range_word() : nullptr;
     p.cout = cout;
     p.flags = flags;
     p.w_fin = w_fin;
@@ -2709,7 +2719,7 @@ static int conv_common(EngineArgs& p, int nterm, bool gather, const void* w_hi, 
         const int64_t tiles = (int64_t)((p.m + 63) / 64) * (p.n / 64);
         const int64_t grid = std::min<int64_t>(512, tiles * (p.k / BK) / 12);
         if (grid > tiles) {
-            sk_setup(p, workspace);
+            sk_setup(p, workspace, stream);
             return gather ? launch_sk<T64c, E_CONV, P_F16, true>(p, (int)grid, stream, what)
                           : launch_sk<T64c, E_CONV, P_F16, false>(p, (int)grid, stream, what);
         }
@@ -2816,8 +2826,10 @@ static const char* group_member(EngineArgs& p, const rf_conv_desc& d, const void
         p.pad = d.pad;
         p.n = d.cout_pad;
         if (d.cout_pad < d.cout) return "cout_pad < cout";
-        if ((d.flags & RF_CONV_BORDER_BIAS) && !(d.bias && d.kh == 3 && d.kw == 3 && d.stride == 1 && d.pad == 1))
-            return "RF_CONV_BORDER_BIAS needs a 3x3 stride-1 pad-1 convolution with its 9-row bias";
+        if ((d.flags & RF_CONV_BORDER_BIAS) &&
+            !(d.bias && d.kh == 3 && d.kw == 3 && d.stride == 1 && d.pad == 1 && d.hi >= 2 && d.wi >= 2))
+            return "RF_CONV_BORDER_BIAS needs a 3x3 stride-1 pad-1 convolution of an image of at least 2 x 2 pixels "
+                   "with its 9-row bias";
     }
     p.kw_m = udiv_magic(p.kw);
     p.m = d.n_img * p.ho * p.wo;
@@ -2831,6 +2843,7 @@ static const char* group_member(EngineArgs& p, const rf_conv_desc& d, const void
     p.p_hi = (bf16_t*)d.p_out;
     p.p_ld = d.p_ld;
     p.plane_f16 = 1;
+    p.range = d.p_out ? rf::range_word() : nullptr;
     p.cout = d.cout;
     p.flags = d.flags;
     return nullptr;

@@ -20,7 +20,8 @@ RF_DEV uint32_t pack_out(float lo, float hi) { return F16 ? pack_f16x2(lo, hi) :
 template <bool F16>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ x, int64_t ldx,
                                                       const float* __restrict__ w, float eps,
-                                                      bf16_t* __restrict__ out, int64_t ldo, int rows, int dim) {
+                                                      bf16_t* __restrict__ out, int64_t ldo, int rows, int dim,
+                                                      int* range) {
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
     if (row >= rows) return;
@@ -33,14 +34,18 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
     ss = wave_sum(ss);
     const float inv = 1.0f / sqrtf(ss / (float)dim + eps);
     bf16_t* orow = out + (int64_t)row * ldo;
+    float amax = 0.f;
     for (int c = lane * 4; c < dim; c += 256) {
         const float4 v = *reinterpret_cast<const float4*>(xr + c);
         const float4 g = *reinterpret_cast<const float4*>(w + c);
+        const float o0 = v.x * inv * g.x, o1 = v.y * inv * g.y, o2 = v.z * inv * g.z, o3 = v.w * inv * g.w;
+        if constexpr (F16) amax = amax3(amax3(amax, o0, o1), o2, o3);
         uint2 pk;
-        pk.x = pack_out<F16>(v.x * inv * g.x, v.y * inv * g.y);
-        pk.y = pack_out<F16>(v.z * inv * g.z, v.w * inv * g.w);
+        pk.x = pack_out<F16>(o0, o1);
+        pk.y = pack_out<F16>(o2, o3);
         *reinterpret_cast<uint2*>(orow + c) = pk;
     }
+    if (F16 && range && !f16_in_range(amax)) report_f16_range(range, RF_RANGE_RMSNORM);
 }
 
 // dim = 256 * NV: the whole row and its weights are loaded up front (NV float4 per lane each, all in
@@ -48,7 +53,8 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
 template <int NV, bool F16>
 __global__ __launch_bounds__(256) void rmsnorm_v_kernel(const float* __restrict__ x, int64_t ldx,
                                                         const float* __restrict__ w, float eps,
-                                                        bf16_t* __restrict__ out, int64_t ldo, int rows) {
+                                                        bf16_t* __restrict__ out, int64_t ldo, int rows,
+                                                        int* range) {
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
     if (row >= rows) return;
@@ -64,13 +70,18 @@ __global__ __launch_bounds__(256) void rmsnorm_v_kernel(const float* __restrict_
     ss = wave_sum(ss);
     const float inv = 1.0f / sqrtf(ss / (float)(256 * NV) + eps);
     bf16_t* orow = out + (int64_t)row * ldo + 4 * lane;
+    float amax = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
+        const float o0 = v[i].x * inv * g[i].x, o1 = v[i].y * inv * g[i].y;
+        const float o2 = v[i].z * inv * g[i].z, o3 = v[i].w * inv * g[i].w;
+        if constexpr (F16) amax = amax3(amax3(amax, o0, o1), o2, o3);
         uint2 pk;
-        pk.x = pack_out<F16>(v[i].x * inv * g[i].x, v[i].y * inv * g[i].y);
-        pk.y = pack_out<F16>(v[i].z * inv * g[i].z, v[i].w * inv * g[i].w);
+        pk.x = pack_out<F16>(o0, o1);
+        pk.y = pack_out<F16>(o2, o3);
         *reinterpret_cast<uint2*>(orow + 256 * i) = pk;
     }
+    if (F16 && range && !f16_in_range(amax)) report_f16_range(range, RF_RANGE_RMSNORM);
 }
 
 // ----------------------------------------------------------------------------- q/k norm + RoPE
@@ -433,14 +444,15 @@ int rmsnorm_launch(const float* x, int64_t ldx, const float* weight, float eps, 
     const bool al = ((uintptr_t)x & 15) == 0 && ((uintptr_t)weight & 15) == 0 && ((uintptr_t)out & 7) == 0;
     static const bool generic = getenv("RF_RMSNORM_GENERIC") && atoi(getenv("RF_RMSNORM_GENERIC"));  // A/B only
     bf16_t* o = (bf16_t*)out;
+    int* rg = F16 ? rf::range_word() : nullptr;  // fp16 out: raise the range flag on |x| > 65504 / NaN
     switch (al && !generic && dim % 256 == 0 ? dim / 256 : 0) {
-        case 2: RF_LAUNCH((rmsnorm_v_kernel<2, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows); break;
-        case 3: RF_LAUNCH((rmsnorm_v_kernel<3, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows); break;
-        case 4: RF_LAUNCH((rmsnorm_v_kernel<4, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows); break;
-        case 6: RF_LAUNCH((rmsnorm_v_kernel<6, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows); break;
-        case 8: RF_LAUNCH((rmsnorm_v_kernel<8, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows); break;
+        case 2: RF_LAUNCH((rmsnorm_v_kernel<2, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows, rg); break;
+        case 3: RF_LAUNCH((rmsnorm_v_kernel<3, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows, rg); break;
+        case 4: RF_LAUNCH((rmsnorm_v_kernel<4, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows, rg); break;
+        case 6: RF_LAUNCH((rmsnorm_v_kernel<6, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows, rg); break;
+        case 8: RF_LAUNCH((rmsnorm_v_kernel<8, F16>), grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows, rg); break;
         default:
-            RF_LAUNCH(rmsnorm_kernel<F16>, grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows, dim);
+            RF_LAUNCH(rmsnorm_kernel<F16>, grid, dim3(256), 0, st, x, ldx, weight, eps, o, ldo, rows, dim, rg);
     }
     return rf::check_launch(what);
 }

@@ -35,11 +35,23 @@ def cache_dir() -> str:
     return os.environ.get("RF_EXAMPLES_CACHE", os.path.join(os.environ.get("TMPDIR", "/tmp"), "rf_examples_h5"))
 
 
+def _converter_digest() -> bytes:
+    """sha256 of the converter's own sources (scene_convert.py, h5io.py, scenes.py): a converter change (e.g. the
+    smooth-shading facet rule) invalidates every cached .h5."""
+    h = hashlib.sha256()
+    here = os.path.dirname(os.path.abspath(__file__))
+    for f in ("scene_convert.py", "h5io.py", "scenes.py"):
+        h.update(open(os.path.join(here, f), "rb").read())
+    return h.digest()
+
+
 def _source_digest(name: str) -> str:
-    """sha256 of the scene JSON and every OBJ it names: a cached .h5 is reused only for the same sources."""
+    """sha256 of the converter sources, the scene JSON and every OBJ it names: a cached .h5 is reused only when
+    all of them are unchanged."""
     import json
     path = os.path.join(EXAMPLES_DIR, name + ".json")
-    h = hashlib.sha256(open(path, "rb").read())
+    h = hashlib.sha256(_converter_digest())
+    h.update(open(path, "rb").read())
     for obj in json.load(open(path)).get("objects", {}).values():
         h.update(open(os.path.join(EXAMPLES_DIR, obj["mesh_path"]), "rb").read())
     return h.hexdigest()[:16]

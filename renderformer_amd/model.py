@@ -10,8 +10,13 @@ Execution model: every scene is *unpadded* into a packed token
 matrix — stage 1 holds ``16 + n_b`` rows per scene (register tokens then the
 valid triangles), stage 2 ``R = (res/8)^2`` ray-token rows per (scene, view).
 All GEMMs run over the packed rows of the whole batch at once; attention
-kernels receive per-problem row ranges.  The residual streams are fp32,
-GEMM operands bf16, attention softmax fp32, the DPT head fp32.
+kernels receive per-problem row ranges.  The residual streams are fp32; the
+projection GEMMs take fp16 operands (RMSNorm / SwiGLU / attention outputs and
+weights; ``operands="bf16"`` selects bf16), attention q/k/v are bf16 with an fp32
+softmax, and the DPT convolutions take fp16 operands with fp32 accumulation.
+fp16 operands are range-checked on the device (every fp16 writer raises a flag on
+|x| > 65504; ``range_check``): a frame that overflowed is rendered again
+with bf16 operands, or reported as a DeviceError in the deferred mode.
 """
 from __future__ import annotations
 
@@ -243,6 +248,13 @@ def _build_plan(mask: torch.Tensor, V: int, res: int, patch: int, n_reg: int, de
                  sched2=ops.attn_schedule(prob2, n_heads, device) if n_heads else None)
 
 
+class PrecisionWarning(UserWarning):
+    pass
+
+
+RANGE_CHECKS = ("sync", "deferred", "off")
+
+
 def _hf_cache_snapshot(model_id: str) -> Optional[str]:
     """Newest snapshot directory of a hub model id in the local Hugging Face cache that holds config.json and
     model.safetensors (the files PyTorchModelHubMixin downloads), or None."""
@@ -268,8 +280,19 @@ class RenderFormer:
 
     def __init__(self, config: RenderFormerConfig, state_dict: Optional[Dict[str, torch.Tensor]] = None,
                  seed: int = 0, dpt_precision: Optional[str] = None, fp8: Optional[bool] = None,
-                 view_chunk: Optional[int] = None, operands: Optional[str] = None):
+                 view_chunk: Optional[int] = None, operands: Optional[str] = None,
+                 range_check: Optional[str] = None):
         self.config = config
+        # fp16 range check (RF_RANGE_CHECK): the fp16-writing kernels raise a host-mapped flag on |x| > 65504 (inf included)
+        # (a checkpoint whose activations exceed fp16's range).  "sync" (default): after each frame the host waits for
+        # THAT frame's end event (no device sync) and reads the flag; an overflowed frame is rendered again with bf16
+        # operands, which the model then keeps (PrecisionWarning).  "deferred": no wait per frame (bench.py's timed
+        # loop); check_range() — called after a synchronize, and at the start of the next render — raises DeviceError
+        # for an overflowed frame.  "off": no check.
+        self.range_check = range_check or os.environ.get("RF_RANGE_CHECK", "sync")
+        if self.range_check not in RANGE_CHECKS:
+            raise ValueError(f"range_check must be one of {RANGE_CHECKS}")
+        self.range_fallbacks = 0  # frames rendered again with bf16 operands after an fp16 overflow
         # render_views: stage 2 + DPT over at most view_chunk views per pass (stage 1 once per scene); None = all
         # views of the batch in one pass.  A fixed chunk makes each view's image independent of the batching.
         self.view_chunk = view_chunk if view_chunk is not None else (int(os.environ.get("RF_VIEW_CHUNK", "0")) or None)
@@ -305,7 +328,7 @@ class RenderFormer:
         # texture encoder fast path for to_h5-format textures (proven per call on the device; RF_TEX_FAST=0
         # forces the general pack + GEMM path)
         self._tex_fast = os.environ.get("RF_TEX_FAST", "1") != "0"
-        self._last_plan = None
+        self._last_plan: Dict = {}  # (V, res) -> (mask object, mask version, plan): the no-read-back fast path
         self._w: Optional[_DeviceWeights] = None
         self._plans: Dict = {}
         self._capture: Optional[dict] = None
@@ -374,8 +397,10 @@ class RenderFormer:
         # same mask tensor object, unmodified since the last call (torch's version counter): reuse that plan
         # without reading the mask back (the host sync below stalls the queue at the start of every frame).
         # The reference is held, so the object (and its storage) cannot be recycled under the same id.
-        last = self._last_plan
-        if last is not None and last[0] is mask and last[1] == (mask._version, V, res):
+        # one entry per (views, resolution): a view-chunked render alternates between two chunk sizes when V is not a
+        # multiple of view_chunk, and each keeps its fast path
+        last = self._last_plan.get((V, res))
+        if last is not None and last[0] is mask and last[1] == mask._version:
             return last[2]
         key = (tuple(mask.shape), mask.sum(1).cpu().numpy().tobytes(), mask.cpu().numpy().tobytes(), V, res)
         plan = self._plans.get(key)
@@ -385,7 +410,9 @@ class RenderFormer:
             plan = _build_plan(mask, V, res, self.config.patch_size, self.config.num_register_tokens, self._device,
                                self.config.num_heads)
             self._plans[key] = plan
-        self._last_plan = (mask, (mask._version, V, res), plan)
+        if len(self._last_plan) > 8:
+            self._last_plan.clear()
+        self._last_plan[(V, res)] = (mask, mask._version, plan)
         return plan
 
     def capture_taps(self, enc_rows=None, dec_rows=None, dec_views=None) -> dict:
@@ -394,6 +421,9 @@ class RenderFormer:
         order, = the reference's sequence) and their row norms, and for every decoder layer the ray-token rows
         `dec_rows` of views `dec_views` of scene 0.  Returns the dict the render fills (device fp32 tensors:
         'enc_rows' [n, D], 'enc_rownorm' [S], 'dec_rows' [layers, views, n, D])."""
+        if self.view_chunk and any(int(v) >= int(self.view_chunk) for v in (dec_views or [])):
+            # the capture is one-shot and filled by the first pass over the views (stage 2 runs per chunk)
+            raise ValueError(f"capture_taps: dec_views must be < view_chunk ({self.view_chunk})")
         out: dict = {}
         dev = self._device
         as_idx = lambda x: None if x is None else torch.as_tensor(x, dtype=torch.long).to(dev)  # noqa: E731
@@ -592,7 +622,65 @@ class RenderFormer:
         caller (the reference's own infer.py places the model on cuda:1, infer.py:43)."""
         self._require()
         with torch.cuda.device(self._device):
-            return self._render_views(triangles, texture, mask, vn, c2w, fov, resolution, log_encode)
+            self._range_enter()
+            out = self._render_views(triangles, texture, mask, vn, c2w, fov, resolution, log_encode)
+            if self._range_overflowed():
+                # the texture was log-encoded in place by the first render: the second one must not encode again
+                out = self._render_views(triangles, texture, mask, vn, c2w, fov, resolution, False)
+            return out
+
+    # ------------------------------------------------------------------ fp16 range check
+    def _range_active(self) -> bool:
+        return self.operands == "f16" and self.range_check != "off"
+
+    def _range_enter(self):
+        if not self._range_active():
+            return
+        if self.range_check == "deferred":
+            self.check_range()  # an earlier deferred frame (its completion already observed) overflowed: raise
+        else:
+            ops.clear_f16_range_flag()
+
+    def check_range(self):
+        """Deferred mode: raise DeviceError if a frame rendered with fp16 operands overflowed fp16's range.  Reads
+        the host-mapped flag without a device sync, so call it after the frames in question have completed (e.g.
+        after torch.cuda.synchronize())."""
+        if self._range_active() and ops.f16_range_flag():
+            code = ops.f16_range_flag()
+            ops.clear_f16_range_flag()
+            from ._lib import DeviceError
+            raise DeviceError(f"fp16 operand overflow (range flag {code}: |x| > 65504 in an fp16 operand) -- "
+                              "this checkpoint's activations exceed fp16's range: render with operands='bf16' "
+                              "(RF_OPERANDS=bf16) or range_check='sync' (re-renders such frames in bf16)")
+
+    def _range_overflowed(self) -> bool:
+        """sync mode: wait for this frame's end event (host-side, no device sync), read the flag; on overflow switch
+        the projections to bf16 operands for good and return True (the caller renders the frame again)."""
+        if not self._range_active() or self.range_check != "sync":
+            return False
+        ev = torch.cuda.Event()
+        ev.record()
+        ev.synchronize()
+        code = ops.f16_range_flag()
+        if not code:
+            return False
+        import warnings
+        warnings.warn(f"fp16 operand overflow (range flag {code}): this checkpoint's activations exceed fp16's range; "
+                      "the frame is rendered again and the model keeps bf16 projection operands from now on",
+                      PrecisionWarning, stacklevel=3)
+        ops.clear_f16_range_flag()
+        self.operands = "bf16"
+        self._w = _DeviceWeights(self.config, self._sd, self._device, self.dpt_precision, self.operands)
+        self.range_fallbacks += 1
+        return True
+
+    @property
+    def precision(self) -> str:
+        """What the projections and attention compute with (the pipeline's last_precision["computed"])."""
+        proj = {"f16": "fp16", "bf16": "bf16"}[self.operands]
+        fp8 = f"; stage-2 {', '.join(sorted(self.fp8_projections))} as MX fp8" if self.fp8 else ""
+        return (f"{proj} projection operands{fp8}, bf16 attention q/k/v, fp32 accumulate/softmax/residual; DPT "
+                f"{'fp16' if self.dpt_precision == 'f16' else 'bf16x3'} operands, fp32 accumulate")
 
     def _render_views(self, triangles, texture, mask, vn, c2w, fov, resolution, log_encode):
         cfg, dev = self.config, self._device
@@ -651,7 +739,12 @@ class RenderFormer:
         """Reference signature (renderformer.py:171-206).  Returns ELU'd log-space images [B, V, C, H, W]."""
         self._require()
         with torch.cuda.device(self._device):
-            return self._forward(tri_vpos_list, texture_patch_list, valid_mask, vns, rays_o, rays_d, tri_vpos_view_tf)
+            self._range_enter()
+            out = self._forward(tri_vpos_list, texture_patch_list, valid_mask, vns, rays_o, rays_d, tri_vpos_view_tf)
+            if self._range_overflowed():
+                out = self._forward(tri_vpos_list, texture_patch_list, valid_mask, vns, rays_o, rays_d,
+                                    tri_vpos_view_tf)
+            return out
 
     def _forward(self, tri_vpos_list, texture_patch_list, valid_mask, vns, rays_o, rays_d, tri_vpos_view_tf):
         cfg, dev = self.config, self._device

@@ -93,6 +93,17 @@ def clear_device_error() -> None:
     _ATTN_WS.clear()
 
 
+def f16_range_flag() -> int:
+    """The library's fp16 range flag (rf_f16_range_flag, a host-mapped word: no device sync): non-zero once a
+    writer of fp16 operands (GEMM epilogue 1, RMSNorm 2, attention O 4, DPT plane 8) met |x| > 65504 (inf included)
+    since the last clear.  Read it after the launches in question have completed."""
+    return int(load(require_device=False).rf_f16_range_flag())
+
+
+def clear_f16_range_flag() -> None:
+    load(require_device=False).rf_clear_f16_range_flag()
+
+
 def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias: Optional[torch.Tensor] = None,
          epilogue: int = EPI_BF16, tag: Optional[str] = None, flag: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out (epilogue)= a @ w.T ; a [M,K], w [N,K] both bf16 (rf_gemm_bf16) or both fp16 (rf_gemm_f16).  The
@@ -322,9 +333,12 @@ def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int
     n_split None/0: the stream-K kernel (balanced over the CUs, cut units merged in-kernel), with the
     workgroup ranges of `schedule` (attn_schedule of the same problems and heads) when given;
     n_split >= 1: the legacy per-unit kernel with flash-decoding splits + rf_attn_combine.
-    q_prescaled: q already carries scale*log2(e) (qk_norm_rope q_scale=Q_LOG2_SCALE)."""
+    q_prescaled: q already carries scale*log2(e) (qk_norm_rope q_scale=Q_LOG2_SCALE).  q/k/v are bf16 or
+    all fp16 (rf_attn_fwd_dt: the fp16 operands the reference's default half precision hands flash_attn; the
+    stream-K kernel only)."""
+    _check(q.dtype in HALF, f"attention: q/k/v must be bf16 or fp16, got {q.dtype}")
     for t, nme in ((q, "q"), (k, "k"), (v, "v")):
-        _dev(t, torch.bfloat16, nme)
+        _dev(t, q.dtype, nme)
     _check(out.dtype in HALF, "attention: out must be bf16 or fp16")
     _dev(out, out.dtype, "out")
     _dev(problems, torch.int32, "problems")
@@ -347,12 +361,13 @@ def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int
     if n_split == 0:
         if schedule is not None:
             _dev(schedule, torch.int64, "schedule")
-        call("rf_attn_fwd_sk", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
-             out.stride(0), DT_F16 if out.dtype == torch.float16 else DT_BF16, ptr(problems), problems.shape[0],
+        call("rf_attn_fwd_dt", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+             out.stride(0), DT_F16 if q.dtype == torch.float16 else DT_BF16,
+             DT_F16 if out.dtype == torch.float16 else DT_BF16, ptr(problems), problems.shape[0],
              n_heads, hd, scale, ptr(ws), ptr(schedule), schedule.numel() - 1 if schedule is not None else 0,
              stream())
         return out
-    _check(out.dtype == torch.bfloat16, "attention: the legacy split kernels write bf16")
+    _check(q.dtype == torch.bfloat16 and out.dtype == torch.bfloat16, "attention: the legacy split kernels are bf16")
     call("rf_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out), out.stride(0),
          ptr(problems), problems.shape[0], max_q_len, n_heads, hd, scale, n_split, ptr(ws), rows, stream())
     if n_split > 1:

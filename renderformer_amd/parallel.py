@@ -6,7 +6,8 @@ disjoint units with no collective on the data path.  Scenes differ a lot in
 cost (N from ~0.5k to ~12k triangles, stage 1 is O(S^2)), so units are assigned
 by greedy longest-processing-time on the analytic FLOP model, not round-robin.
 The only collective is the optional gather of finished HDR frames to every
-rank (RCCL all_gather over xGMI on GPUs, gloo in the CPU tests).
+rank: one RCCL all_gather over xGMI per step with static per-rank counts (no
+host sync), overlapping the next step (FrameGather; gloo in the CPU tests).
 """
 from __future__ import annotations
 
@@ -50,40 +51,94 @@ def max_over_ranks(value: float, device=None) -> float:
     return float(t.item())
 
 
-def gather_frames(local: torch.Tensor, local_ids: Sequence[int], n_total: int) -> torch.Tensor:
-    """all_gather per-rank frame stacks [n_local, ...] into [n_total, ...] in global unit order.
+class PendingFrames:
+    """An all-gather in flight (FrameGather.start): ``result()`` makes the caller's current stream wait for it (no
+    host block on RCCL) and returns the frames [n_total, ...] in global order."""
 
-    Every rank must call it, including ranks with no units (n_local = 0, but the trailing frame shape
-    still given): the collective needs every member.  On RCCL the frames stay on the device (xGMI);
-    under gloo (CPU tests) device tensors are moved to the host for the exchange."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-        out = local.new_empty((n_total,) + tuple(local.shape[1:]))
-        if len(local_ids):
-            out[torch.as_tensor(list(local_ids), dtype=torch.long, device=local.device)] = local
-        return out
-    world = dist.get_world_size()
-    dev = local.device
-    xdev = torch.device("cpu") if dist.get_backend() == "gloo" else dev
-    n_loc = torch.tensor([local.shape[0]], device=xdev)
-    counts = [torch.zeros_like(n_loc) for _ in range(world)]
-    dist.all_gather(counts, n_loc)
-    cmax = int(max(int(c.item()) for c in counts))
-    if cmax == 0:
-        return local.new_empty((n_total,) + tuple(local.shape[1:]))
-    pad = torch.zeros((cmax,) + tuple(local.shape[1:]), dtype=local.dtype, device=xdev)
-    pad[: local.shape[0]] = local.to(xdev)
-    ids = torch.full((cmax,), -1, dtype=torch.long, device=xdev)
-    if len(local_ids):
-        ids[: len(local_ids)] = torch.as_tensor(list(local_ids), dtype=torch.long, device=xdev)
-    bufs = [torch.empty_like(pad) for _ in range(world)]
-    id_bufs = [torch.empty_like(ids) for _ in range(world)]
-    dist.all_gather(bufs, pad)
-    dist.all_gather(id_bufs, ids)
-    out = torch.empty((n_total,) + tuple(local.shape[1:]), dtype=local.dtype, device=xdev)
-    for b, i in zip(bufs, id_bufs):
-        keep = i >= 0
-        out[i[keep]] = b[keep]
-    return out.to(dev)
+    def __init__(self, out=None, work=None, finish=None):
+        self._out, self._work, self._finish = out, work, finish
+
+    def result(self) -> torch.Tensor:
+        if self._work is not None:
+            self._work.wait()  # RCCL: the current stream waits on the collective's stream (no host sync)
+            self._work = None
+        if self._finish is not None:
+            self._out = self._finish()
+            self._finish = None
+        return self._out
+
+
+class FrameGather:
+    """All-gather of finished HDR frames with STATIC per-rank counts and ids: every rank knows every rank's frame
+    ids up front (``assign_units`` / ``shard_views`` are deterministic), so one step needs exactly one collective —
+    an ``all_gather_into_tensor`` of the ranks' frame stacks padded to the largest count — and no host sync (no
+    count or id exchange, no ``.item()``).  On RCCL the collective is issued asynchronously (``async_op``): it runs
+    on the process group's own stream, after the frames' producer on the current stream, and overlaps whatever the
+    caller launches next (the next step's render) until ``result()``.  Under gloo (CPU-side tests) the frames go
+    through the host synchronously.  The gathered order is global: slot (rank r, j) holds frame rank_ids[r][j]."""
+
+    def __init__(self, rank_ids: Sequence[Sequence[int]], frame_shape, device, dtype=torch.float32):
+        self.rank_ids = [list(r) for r in rank_ids]
+        self.world = len(self.rank_ids)
+        self.n_total = sum(len(r) for r in self.rank_ids)
+        ids = sorted(i for r in self.rank_ids for i in r)
+        if ids != list(range(self.n_total)):
+            raise ValueError("rank_ids must cover 0..n_total-1 exactly once")
+        self.cmax = max(1, max(len(r) for r in self.rank_ids))
+        self.frame_shape = tuple(frame_shape)
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        if self.distributed and dist.get_world_size() != self.world:
+            raise ValueError(f"rank_ids for {self.world} ranks, world size {dist.get_world_size()}")
+        self.rank = dist.get_rank() if self.distributed else 0
+        self.gloo = self.distributed and dist.get_backend() == "gloo"
+        perm = [0] * self.n_total  # perm[global id] = slot of the gathered [world * cmax] buffer
+        for r, rid in enumerate(self.rank_ids):
+            for j, i in enumerate(rid):
+                perm[i] = r * self.cmax + j
+        xdev = torch.device("cpu") if self.gloo else self.device
+        # the gathered buffer IS the global order when every rank holds cmax consecutive ids in rank order
+        self.identity = perm == list(range(self.world * self.cmax))
+        self.perm = None if self.identity else torch.tensor(perm, dtype=torch.long, device=xdev)
+
+    def start(self, local: torch.Tensor) -> PendingFrames:
+        mine = self.rank_ids[self.rank]
+        if tuple(local.shape) != (len(mine),) + self.frame_shape:
+            raise ValueError(f"local frames {tuple(local.shape)} != {(len(mine),) + self.frame_shape}")
+        if not self.distributed:
+            if self.identity:
+                return PendingFrames(out=local)
+            out = local.new_empty((self.n_total,) + self.frame_shape)
+            out[torch.as_tensor(mine, dtype=torch.long, device=local.device)] = local
+            return PendingFrames(out=out)
+        xdev = torch.device("cpu") if self.gloo else self.device
+        if local.shape[0] == self.cmax:
+            pad = local.to(xdev).contiguous()
+        else:
+            pad = torch.zeros((self.cmax,) + self.frame_shape, dtype=local.dtype, device=xdev)
+            pad[: local.shape[0]] = local.to(xdev)
+        buf = torch.empty((self.world * self.cmax,) + self.frame_shape, dtype=local.dtype, device=xdev)
+        perm, dev = self.perm, self.device
+
+        def finish():
+            out = buf if perm is None else buf.index_select(0, perm)
+            return out.to(dev)
+        if self.gloo:
+            dist.all_gather_into_tensor(buf, pad)
+            return PendingFrames(out=finish())
+        work = dist.all_gather_into_tensor(buf, pad, async_op=True)
+        return PendingFrames(work=work, finish=finish)
+
+    def __call__(self, local: torch.Tensor) -> torch.Tensor:
+        return self.start(local).result()
+
+
+def gather_frames(local: torch.Tensor, rank_ids: Sequence[Sequence[int]]) -> torch.Tensor:
+    """All-gather per-rank frame stacks [n_local, ...] into [n_total, ...] in global order (FrameGather, one
+    collective).  ``rank_ids`` lists EVERY rank's global frame ids (identical on all ranks); every rank must call
+    it, including ranks with no frames (n_local = 0, the trailing frame shape still given)."""
+    return FrameGather(rank_ids, tuple(local.shape[1:]), local.device, local.dtype)(local)
 
 
 def shard_views(n_views: int, world: int) -> List[range]:
@@ -124,20 +179,22 @@ class ShardedRenderer:
         views = {int(s["c2w"].shape[1]) for s in scenes}
         if len(views) != 1:
             raise ValueError("all scenes of one call must have the same view count")
-        mine = self.plan(scenes, res)[self.rank]
+        plan = self.plan(scenes, res)
+        mine = plan[self.rank]
         frames = [self.pipeline(**scenes[i], resolution=res, **kw)[0] for i in mine]  # [V, H, W, C] each
         shape = self._frame_shape(views.pop(), res)
         local = (torch.stack(frames) if frames
                  else torch.empty((0,) + shape, dtype=torch.float32, device=self.pipeline.device))
         if not gather:
             return mine, local
-        return gather_frames(local, mine, len(scenes))
+        return gather_frames(local, plan)
 
     def render_views(self, scene: dict, res: int = 512, gather: bool = True, **kw):
         """One scene, its views split across ranks (shard_views); returns [V, res, res, C] on every rank
         (gather) or (my view range, my frames)."""
         n_views = int(scene["c2w"].shape[1])
-        vr = shard_views(n_views, self.world)[self.rank]
+        shards = shard_views(n_views, self.world)
+        vr = shards[self.rank]
         shape = self._frame_shape(n_views, res)[1:]
         if len(vr):
             sub = dict(scene)
@@ -148,4 +205,4 @@ class ShardedRenderer:
             local = torch.empty((0,) + shape, dtype=torch.float32, device=self.pipeline.device)
         if not gather:
             return vr, local
-        return gather_frames(local, list(vr), n_views)
+        return gather_frames(local, [list(r) for r in shards])

@@ -9,14 +9,16 @@ log-encodes the emission channels of ``texture`` **in place**
 Precision: the reference GPU path switches stage precision with
 ``torch_dtype`` (rendering_pipeline.py:98-99, view_transformer.py:119: half ->
 stage 1 half, stage 2 fp32, DPT half; fp32 -> stage 1 fp32, stage 2 bf16).  This
-path runs ONE policy for every ``torch_dtype``: bf16 MFMA operands with fp32
-accumulation / softmax / residual streams in both transformer stages and
-fp16-operand, fp32-accumulate DPT convolutions — the policy measured within the
-1e-3 relative-L2 parity budget of the reference CPU fp32 output at every
+path runs ONE policy for every ``torch_dtype``: fp16 projection operands (bf16 with
+``operands="bf16"``, or after an fp16 overflow: ``RenderFormer.range_check``), bf16
+attention q/k/v, fp32 accumulation / softmax / residual streams in both transformer
+stages, and fp16-operand, fp32-accumulate DPT convolutions — the policy measured
+within the 1e-3 relative-L2 parity budget of the reference CPU fp32 output at every
 BASELINE configuration (tests/test_parity_gpu.py).  The argument is validated
 exactly like the reference; ``torch.float32`` (which in the reference selects
 fp32 stage-1 arithmetic) emits a one-time ``PrecisionWarning`` saying so, and
-``last_precision`` records what ran.
+``last_precision`` records what ran (``RenderFormer.precision``, read after the
+frame, so an fp16-overflow fallback to bf16 shows).
 """
 from __future__ import annotations
 
@@ -24,14 +26,7 @@ import warnings
 
 import torch
 
-from .model import RenderFormer
-
-
-class PrecisionWarning(UserWarning):
-    pass
-
-
-POLICY = "bf16 MFMA operands, fp32 accumulate/softmax/residual; DPT fp16 operands, fp32 accumulate"
+from .model import PrecisionWarning, RenderFormer  # noqa: F401  (PrecisionWarning re-exported)
 
 
 class RenderFormerRenderingPipeline:
@@ -63,9 +58,8 @@ class RenderFormerRenderingPipeline:
         if torch_dtype == torch.float32 and not self._warned_fp32:
             self._warned_fp32 = True
             warnings.warn("torch_dtype=torch.float32: this MI355X path has no fp32-operand mode; it computes with "
-                          f"{POLICY} (within 1e-3 relative L2 of the reference's CPU fp32 output)", PrecisionWarning,
-                          stacklevel=2)
-        self.last_precision = {"requested": str(torch_dtype), "computed": POLICY}
+                          f"{self.model.precision} (within 1e-3 relative L2 of the reference's CPU fp32 output)",
+                          PrecisionWarning, stacklevel=2)
         cfg = self.config
         if cfg.texture_encode_patch_size == 1 and texture.dim() == 5:
             texture = texture[:, :, :, 0, 0].contiguous()
@@ -73,8 +67,13 @@ class RenderFormerRenderingPipeline:
             raise ValueError("texture must be contiguous (it is log-encoded in place)")
         if texture.dtype != torch.float32:
             raise ValueError("texture must be float32 (it is log-encoded in place)")
-        return self.model.render_views(triangles, texture, mask, vn, c2w, fov, resolution,
-                                       log_encode=not cfg.use_ldr)
+        out = self.model.render_views(triangles, texture, mask, vn, c2w, fov, resolution, log_encode=not cfg.use_ldr)
+        self.last_precision = {"requested": str(torch_dtype), "computed": self.model.precision}
+        return out
+
+    def check_range(self):
+        """RenderFormer.check_range (deferred fp16 range check): raise DeviceError if a completed frame overflowed."""
+        self.model.check_range()
 
     def __call__(self, *args, **kwargs):
         return self.render(*args, **kwargs)

@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load(require_device=False)
     for fn in header_functions():
         assert hasattr(lib, fn), fn
-    assert lib.rf_abi_version() == 11
+    assert lib.rf_abi_version() == 12
     # every int-returning entry point has a ctypes signature in the binding
     assert set(_lib.SIGNATURES) == set(header_functions()) - {"rf_last_error", "rf_abi_version",
                                                                "rf_attn_workspace_bytes", "rf_gemm_workspace_bytes",
@@ -242,14 +242,19 @@ def test_integration_binding_parses():
 
 
 @pytest.mark.gpu
-def test_integration_binding_runs_against_reference_attention():
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
+def test_integration_binding_runs_against_reference_attention(dtype):
     """Execute INTEGRATION.md's reference-side binding verbatim (only the library path filled in) the way the
     reference's attention switch would call it — flash_attn's qkv-packed varlen layout [T, 3, H, 128] with
     cu_seqlens (stage 1), and the kv-packed layout q [Tq, H, 128] / kv [Tk, 2, H, 128] with cu_seqlens_q /
-    cu_seqlens_k (stage-2 cross-attention, attention.py:183-198) — against fp64 softmax attention."""
+    cu_seqlens_k (stage-2 cross-attention, attention.py:183-198) — against fp64 softmax attention, with the
+    reference's default fp16 operands (torch_dtype=torch.float16, rendering_pipeline.py:37) and with bf16; the
+    output keeps the input's type, and fp32 q/k/v are refused (as flash_attn refuses them)."""
     import math
     import torch
     from renderformer_amd import _lib
+    dt = getattr(torch, dtype)
+    tol = 2e-3 if dt == torch.float16 else 6e-3  # fp16 operands and P carry 3 more mantissa bits than bf16
     src = _integration_binding_source().replace('ctypes.CDLL("librfhip.so")', f'ctypes.CDLL({_lib.LIB_PATH!r})')
     ns = {}
     exec(compile(src, "INTEGRATION.md", "exec"), ns)
@@ -258,34 +263,36 @@ def test_integration_binding_runs_against_reference_attention():
     cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device="cuda")
     T = sum(lens)
     g = torch.Generator(device="cpu").manual_seed(2)
-    qkv = torch.randn(T, 3, H, hd, generator=g).bfloat16().cuda()
+    qkv = torch.randn(T, 3, H, hd, generator=g).to(dt).cuda()
     out = ns["rfhip_varlen_qkvpacked"](qkv, cu, max(lens))
     torch.cuda.synchronize()
-    assert out.shape == (T, H, hd)
+    assert out.shape == (T, H, hd) and out.dtype == dt
     o = out.float().cpu()
     q, k, v = (qkv[:, i].double().cpu() for i in range(3))
     for a, b in zip(cu.tolist(), cu.tolist()[1:]):
         s = torch.einsum("qhd,khd->hqk", q[a:b], k[a:b]) / math.sqrt(hd)
         ref = torch.einsum("hqk,khd->qhd", torch.softmax(s, -1), v[a:b])
         err = ((o[a:b].double() - ref).norm() / ref.norm()).item()
-        assert err < 6e-3, (a, b, err)
+        assert err < tol, (a, b, err)
     # the kv-packed binding: stage-2 cross-attention, 3 "views" of 256 rays over scenes of ragged lengths
     Hc, R = 8, 256
     klens = [700, 77, 1300]
     cuq = torch.arange(0, R * (len(klens) + 1), R, dtype=torch.int32, device="cuda")
     cuk = torch.tensor([0] + list(torch.tensor(klens).cumsum(0)), dtype=torch.int32, device="cuda")
-    qc = torch.randn(R * len(klens), Hc, hd, generator=g).bfloat16().cuda()
-    kv = torch.randn(sum(klens), 2, Hc, hd, generator=g).bfloat16().cuda()
+    qc = torch.randn(R * len(klens), Hc, hd, generator=g).to(dt).cuda()
+    kv = torch.randn(sum(klens), 2, Hc, hd, generator=g).to(dt).cuda()
     oc = ns["rfhip_varlen_kvpacked"](qc, kv, cuq, cuk, R, max(klens))
     torch.cuda.synchronize()
-    assert oc.shape == qc.shape
+    assert oc.shape == qc.shape and oc.dtype == dt
     oc, qd, kd, vd = oc.float().cpu(), qc.double().cpu(), kv[:, 0].double().cpu(), kv[:, 1].double().cpu()
     for i in range(len(klens)):
         a, b, c0, c1 = cuq[i].item(), cuq[i + 1].item(), cuk[i].item(), cuk[i + 1].item()
         s = torch.einsum("qhd,khd->hqk", qd[a:b], kd[c0:c1]) / math.sqrt(hd)
         ref = torch.einsum("hqk,khd->qhd", torch.softmax(s, -1), vd[c0:c1])
         err = ((oc[a:b].double() - ref).norm() / ref.norm()).item()
-        assert err < 6e-3, (i, err)
+        assert err < tol, (i, err)
+    with pytest.raises(TypeError, match="fp16 and bf16"):
+        ns["rfhip_varlen_qkvpacked"](qkv.float(), cu, max(lens))
 
 
 def test_conv_desc_layout_matches_header(tmp_path):

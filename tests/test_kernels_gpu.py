@@ -215,6 +215,58 @@ def test_rmsnorm_f16_and_attention_f16_out():
     assert relerr(sw[torch.float16], sw[torch.bfloat16]) < 4e-3
 
 
+def test_f16_range_flag_writers():
+    """Every fp16 writer raises the range flag on a value beyond fp16's range (|x| > 65504, inf included) and
+    only then: the fp16 GEMM epilogues (plain and SwiGLU), rf_rmsnorm_f16, the attention / Swin fp16 O and the
+    fp16 plane of rf_split_planes; bf16 outputs of the same values never raise it."""
+    from renderformer_amd import ops
+    ops.clear_f16_range_flag()
+    g = torch.Generator(device="cpu").manual_seed(99)
+    a = torch.randn(300, 256, generator=g).half().to(dev)
+    w = (torch.randn(512, 256, generator=g) / 16).half().to(dev)
+
+    def flag_after(fn):
+        ops.clear_f16_range_flag()
+        fn()
+        torch.cuda.synchronize()
+        f = ops.f16_range_flag()
+        ops.clear_f16_range_flag()
+        return f
+
+    o16 = torch.empty(300, 512, device=dev, dtype=torch.float16)
+    assert flag_after(lambda: ops.gemm(a, w, o16)) == 0
+    assert flag_after(lambda: ops.gemm(a, w * 4096, o16)) != 0                     # |x| up to ~1e5
+    assert flag_after(lambda: ops.gemm(a, w * 4096, torch.empty_like(o16, dtype=torch.bfloat16))) == 0
+    sw = torch.empty(300, 256, device=dev, dtype=torch.float16)
+    assert flag_after(lambda: ops.gemm(a, w, sw, None, ops.EPI_SWIGLU)) == 0
+    assert flag_after(lambda: ops.gemm(a, w * 300, sw, None, ops.EPI_SWIGLU)) != 0  # silu(g) u ~ 1e5
+    x = torch.randn(64, 1024, generator=g).to(dev)
+    h = torch.empty(64, 1024, device=dev, dtype=torch.float16)
+    assert flag_after(lambda: ops.rmsnorm(x, torch.ones(1024, device=dev), 1e-6, h)) == 0
+    assert flag_after(lambda: ops.rmsnorm(x, torch.full((1024,), 1e4, device=dev), 1e-6, h)) != 0
+    H, D, S = 2, 256, 200
+    q = torch.randn(S, D, generator=g).bfloat16().to(dev)
+    k = torch.randn(S, D, generator=g).bfloat16().to(dev)
+    v = torch.randn(S, D, generator=g).bfloat16().to(dev)
+    pt = torch.tensor([[0, S, 0, S, 0]], dtype=torch.int32, device=dev)
+    oa = torch.empty(S, D, device=dev, dtype=torch.float16)
+    assert flag_after(lambda: ops.attention(q, k, v, oa, pt, S, H)) == 0
+    assert flag_after(lambda: ops.attention(q, k, (v.float() * 1e5).bfloat16(), oa, pt, S, H)) != 0
+    assert flag_after(lambda: ops.attention(q, k, (v.float() * 1e5).bfloat16(), oa.bfloat16(), pt, S, H)) == 0
+    n_img, gs = 1, 8
+    qs = torch.randn(n_img * gs * gs, D, generator=g).bfloat16().to(dev)
+    os_ = torch.empty(n_img * gs * gs, D, device=dev, dtype=torch.float16)
+    assert flag_after(lambda: ops.swin_attention(qs, qs, qs, os_, n_img, gs, gs, 0, H)) == 0
+    assert flag_after(lambda: ops.swin_attention(qs, qs, (qs.float() * 1e5).bfloat16(), os_, n_img, gs, gs, 0, H)) != 0
+    from renderformer_amd import _lib
+    xs = torch.randn(128, 64, generator=g).to(dev)
+    plane = torch.empty(128, 64, device=dev, dtype=torch.float16)
+    split = lambda t: _lib.call("rf_split_planes", t.data_ptr(), 128, 64, 64, plane.data_ptr(), None, 64, 0,  # noqa: E731
+                                _lib.stream())
+    assert flag_after(lambda: split(xs)) == 0
+    assert flag_after(lambda: split(xs * 1e5)) != 0
+
+
 def test_gemm_asymmetric_identity():
     """A = I with an asymmetric W catches a transposed C write (guide §3)."""
     ops = _ops()
@@ -476,6 +528,74 @@ def test_attention_stream_k_prescaled_rescale(thr, grid, sched, sk_kernel, monke
             ref = _ref_attn(qref, qkv[sl, D:2 * D].float(), qkv[sl, 2 * D:].float(), H)
             assert relerr(o[sl], ref) < 6e-3, (thr, grid, n)
             off += n
+
+
+@pytest.mark.parametrize("prescaled", [False, True])
+@pytest.mark.parametrize("thr", ["12", "0"])
+@pytest.mark.parametrize("grid", [None, "5", "23"])
+def test_attention_f16_operands(grid, thr, prescaled, monkeypatch):
+    """rf_attn_fwd_dt with fp16 q/k/v (the operands the reference's default torch_dtype=float16 hands
+    flash_attn_varlen_*): ragged problems with tail tiles, key spikes that force the deferred rescale (THR=0: at
+    every growth), cut units merged by their owners (small grids), fp16 and bf16 O; checked against fp64 at a
+    tighter bar than bf16 (fp16 operands and P keep 3 more mantissa bits), and fp16 beats bf16 on the same data."""
+    monkeypatch.setenv("RF_ATTN_THR", thr)
+    if grid:
+        monkeypatch.setenv("RF_ATTN_GRID", grid)
+    ops = _ops()
+    H = 4
+    D = H * 128
+    lens = [1000, 129, 700, 65]
+    T = sum(lens)
+    g = torch.Generator(device="cpu").manual_seed(17)
+    qkv = torch.randn(T, 3 * D, generator=g)
+    for r in (5, 640, 960, 1129 + 64, 1129 + 699):
+        qkv[r, D:2 * D] *= 6.0
+    qkv[:, 2 * D:] *= 1000.0  # values far outside bf16's 8-bit mantissa comfort, well inside fp16's range
+    probs, off = [], 0
+    for n in lens:
+        probs.append([off, n, off, n, off])
+        off += n
+    pt = torch.tensor(probs, dtype=torch.int32, device=dev)
+    errs = {}
+    for dt in (torch.float16, torch.bfloat16):
+        d = qkv.to(dt).to(dev)
+        q = (d[:, :D].float() * ops.Q_LOG2_SCALE).to(dt) if prescaled else d[:, :D]
+        for odt in (dt, torch.float16 if dt == torch.bfloat16 else torch.bfloat16):
+            out = torch.zeros(T, D, device=dev, dtype=odt)
+            ops.attention(q, d[:, D:2 * D], d[:, 2 * D:], out, pt, max(lens), H, q_prescaled=prescaled)
+            o = out.float().cpu()
+            off, tot = 0, []
+            for n in lens:
+                sl = slice(off, off + n)
+                qref = q[sl].float().cpu() / (ops.Q_LOG2_SCALE if prescaled else 1.0)
+                ref = _ref_attn(qref, d[sl, D:2 * D].float().cpu(), d[sl, 2 * D:].float().cpu(), H)
+                tot.append(relerr(o[sl], ref))
+                off += n
+            errs[(dt, odt)] = max(tot)
+    assert errs[(torch.float16, torch.float16)] < 2e-3, errs
+    assert errs[(torch.float16, torch.bfloat16)] < 6e-3, errs
+    assert errs[(torch.bfloat16, torch.bfloat16)] < 6e-3, errs
+    assert errs[(torch.float16, torch.float16)] < errs[(torch.bfloat16, torch.bfloat16)], errs
+
+
+def test_attention_f16_operands_bench_shape():
+    """fp16 q/k/v at the stage-1 bench shape (S = 5,649, 8 heads, the cost-balanced schedule over the full grid:
+    every one of the 184 units cut), sampled rows vs fp64."""
+    ops = _ops()
+    H, S = 8, 5649
+    D = H * 128
+    g = torch.Generator(device="cpu").manual_seed(5649)
+    qkv = torch.randn(S, 3 * D, generator=g).half()
+    d = qkv.to(dev)
+    probs = [[0, S, 0, S, 0]]
+    out = torch.zeros(S, D, device=dev, dtype=torch.float16)
+    ops.attention(d[:, :D], d[:, D:2 * D], d[:, 2 * D:], out, torch.tensor(probs, dtype=torch.int32, device=dev), S, H,
+                  schedule=ops.attn_schedule(probs, H, dev))
+    torch.cuda.synchronize()
+    assert _lib_mod().rf_device_error() == 0
+    rows = torch.cat([torch.arange(0, 16), torch.randperm(S, generator=g)[:496].sort().values, torch.tensor([S - 1])])
+    ref = _ref_attn(qkv[rows, :D].float(), qkv[:, D:2 * D].float(), qkv[:, 2 * D:].float(), H)
+    assert relerr(out.float().cpu()[rows], ref) < 2e-3
 
 
 @pytest.mark.parametrize("sched", [False, True])
@@ -1168,3 +1288,40 @@ def test_attention_schedule_matches_equal_ranges_at_bench_shape():
     ref = _ref_attn(qs[rows].float().cpu() / ops.Q_LOG2_SCALE, qkv[:, D:2 * D].float().cpu(), qkv[:, 2 * D:].float().cpu(), H)
     e_sched, e_equal = relerr(outs[1][rows].cpu(), ref), relerr(outs[0][rows].cpu(), ref)
     assert e_sched < 6e-3 and e_sched < 1.25 * e_equal, (e_sched, e_equal)
+
+
+def test_stream_k_epoch_wrap(monkeypatch):
+    """stream-K hand-off flags compare against a per-launch epoch that repeats every 2^B launches; on
+    each wrap the flag area is re-zeroed on the stream (rf::next_epoch), so a flag left from 2^B launches ago can
+    never pass for the current launch's.  With B = 2 (a wrap every 4 launches) repeated attention and stream-K
+    GEMM launches with cut units stay correct and raise no device error."""
+    monkeypatch.setenv("RF_EPOCH_BITS", "2")
+    monkeypatch.setenv("RF_ATTN_GRID", "23")
+    ops = _ops()
+    H, D = 2, 256
+    lens = [700, 129]
+    T = sum(lens)
+    g = torch.Generator(device="cpu").manual_seed(4)
+    qkv = torch.randn(T, 3 * D, generator=g).bfloat16()
+    d = qkv.to(dev)
+    probs = [[0, 700, 0, 700, 0], [700, 129, 700, 129, 700]]
+    pt = torch.tensor(probs, dtype=torch.int32, device=dev)
+    a = torch.randn(1000, 1024, generator=g).bfloat16().to(dev)
+    w = (torch.randn(1024, 1024, generator=g) / 32).bfloat16().to(dev)
+    ref_g = a.double() @ w.double().t()
+    monkeypatch.setenv("RF_GEMM_SKPH", "1")
+    for it in range(11):
+        out = torch.zeros(T, D, device=dev, dtype=torch.bfloat16)
+        ops.attention(d[:, :D], d[:, D:2 * D], d[:, 2 * D:], out, pt, 700, H)
+        c = torch.empty(1000, 1024, device=dev)
+        ops.gemm(a, w, c, None, ops.EPI_F32)
+        o = out.float().cpu()
+        off = 0
+        for n in lens:
+            sl = slice(off, off + n)
+            ref = _ref_attn(qkv[sl, :D].float(), qkv[sl, D:2 * D].float(), qkv[sl, 2 * D:].float(), H)
+            assert relerr(o[sl], ref) < 6e-3, (it, n)
+            off += n
+        assert relerr(c, ref_g) < 1e-5, it
+    torch.cuda.synchronize()
+    assert _lib_mod().rf_device_error() == 0

@@ -35,10 +35,12 @@ def _worker(rank, world, port, q):
     try:
         n_total = 7
         costs = [float(c) for c in (5, 1, 3, 3, 8, 2, 2)]
-        mine = assign_units(costs, world)[rank]
+        plan = assign_units(costs, world)
+        mine = plan[rank]
         # each "frame" encodes its global id so the gather order can be checked
         local = torch.stack([torch.full((4, 4, 3), float(i)) for i in mine])
-        allf = gather_frames(local, mine, n_total)
+        allf = gather_frames(local, plan)
+        assert allf.shape[0] == n_total
         t = max_over_ranks(float(rank + 1))
         q.put((rank, [float(allf[i, 0, 0, 0]) for i in range(n_total)], t))
     finally:
@@ -64,9 +66,22 @@ def test_gather_and_timing_world2_gloo():
 
 
 def test_single_process_gather_identity():
-    local = torch.arange(6.0).view(2, 3)
-    out = gather_frames(local, [3, 0], 4)
-    assert torch.equal(out[3], local[0]) and torch.equal(out[0], local[1])
+    local = torch.arange(12.0).view(4, 3)
+    out = gather_frames(local, [[3, 0, 1, 2]])
+    assert torch.equal(out[3], local[0]) and torch.equal(out[0], local[1]) and torch.equal(out[2], local[3])
+    assert gather_frames(local, [[0, 1, 2, 3]]) is local  # identity order: no copy
+
+
+def test_frame_gather_static_slots():
+    """Slot layout of the one-collective gather: rank r's j-th frame sits at r * cmax + j of the padded buffer,
+    and the permutation back to global order is precomputed (no id exchange at run time)."""
+    from renderformer_amd.parallel import FrameGather
+    g = FrameGather([[4, 0], [1], [2, 3]], (2,), "cpu")
+    assert g.cmax == 2 and not g.identity
+    assert g.perm.tolist() == [1, 2, 4, 5, 0]
+    assert FrameGather([[0, 1], [2, 3]], (2,), "cpu").identity  # shard_views' equal contiguous ranges
+    with pytest.raises(ValueError):
+        FrameGather([[0, 1], [1]], (2,), "cpu")
 
 
 class _OraclePipeline:
