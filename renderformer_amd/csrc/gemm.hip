@@ -1715,6 +1715,164 @@ __global__ __launch_bounds__(512, 1) void halo2_kernel(EngineArgs p) {
     engine_epilogue<H2Tile<BN>, E_CONV, h2::TW, BN == 64>(p, (img * p.ho + y0) * p.wo + x0, tn * BN, acc);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// The DPT's last 3x3 convolution (output_conv2, dpt.py:234-240: <= 32 filters, fp16) with its fused head
+// (SiLU -> 1x1 to n_fin -> ELU -> 10^x - 1).  The halo2 kernel pads the 32-filter bank to a 64-wide tile (half
+// its MFMAs multiply zeros) and runs 16 MFMAs per barrier-delimited section, which left it bound by its section
+// overheads (68 us for 19.3 GFLOP at 512^2).  Here a block is 4 waves (one per SIMD) over a 16 x 32
+// pixel tile with exactly 32 output channels: each wave owns 4 tile rows (8 fragments of 16 pixels) x 32
+// channels, so one (chunk, tap) step is 16 useful MFMAs per wave, and a whole 32-channel chunk (9 taps, 144
+// MFMAs per wave) runs between two barriers.  Per chunk the 18 x 34 halo (40 KiB, halo2's column-keyed XOR
+// image: conflict-free fragment reads) and the chunk's 9 W slices (18 KiB) land by LDS-DMA in one of two
+// buffers while the previous chunk computes.  The input plane is read ~1.2x (the halo), the bank once per block.
+namespace c32 {
+constexpr int TH = 16, TW = 32, HWID = TW + 2, HPIX = (TH + 2) * HWID;  // 612 halo pixels
+constexpr int HPIECES = 40, WPIECES = 18;                               // 1-KiB pieces per chunk
+constexpr int HBYTES = HPIECES * 1024, WBYTES = WPIECES * 1024, BUF = HBYTES + WBYTES;
+constexpr int NWAVE = 4, HPW = HPIECES / NWAVE;                         // 10 halo pieces per wave
+constexpr int LDS = 2 * BUF;                                             // 116 KiB: one block per CU
+}  // namespace c32
+
+__global__ __launch_bounds__(256, 1) void conv3x3_c32_kernel(EngineArgs p) {
+    using namespace c32;
+    __shared__ __attribute__((aligned(16))) char smem[LDS];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // XCD-contiguous tile ids (neighbouring tiles, whose halos overlap, share an XCD's L2)
+    const int nwg = gridDim.x, hw = blockIdx.x;
+    const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
+    const int tx_n = p.wo / TW, ty_n = p.ho / TH;
+    const int tx = wg % tx_n, rest = wg / tx_n;
+    const int ty = rest % ty_n, img = rest / ty_n;
+    const int y0 = ty * TH, x0 = tx * TW;
+    const int nch = p.cin_pad / 32;
+
+    // halo piece t of this wave = halo pixels 16 (wave + 4 t) .. + 15, 64 B each (16-B chunk ^ column key)
+    int hpix[HPW], hch[HPW];
+#pragma unroll
+    for (int t = 0; t < HPW; ++t) {
+        const int hp = (wave + NWAVE * t) * 16 + (lane >> 2);
+        hch[t] = (lane & 3) ^ (((hp % HWID) >> 2) & 3);
+        int pix = -1;
+        if (hp < HPIX) {
+            const int hy = hp / HWID, hx = hp - hy * HWID;
+            const int iy = y0 + hy - 1, ix = x0 + hx - 1;
+            if (iy >= 0 && iy < p.hi && ix >= 0 && ix < p.wi) pix = (img * p.hi + iy) * p.wi + ix;
+        }
+        hpix[t] = pix;
+    }
+    // W piece v (0..17) = tap v / 2, output channels 16 (v & 1) .. + 15 (rows of the [cout_pad][9][cin_pad] bank)
+    const int wr = lane >> 2;
+    auto issue = [&](int chunk, int buf) {
+        char* b = smem + buf * BUF;
+#pragma unroll
+        for (int t = 0; t < HPW; ++t) {
+            const bf16_t* src = hpix[t] >= 0 ? p.a + (int64_t)hpix[t] * p.cin_pad + hch[t] * 8 + chunk * 32 : p.zero;
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, src), LDS_PTR(void, b + (wave + NWAVE * t) * 1024), 16, 0, 0);
+        }
+        for (int v = wave; v < WPIECES; v += NWAVE) {  // waves 0, 1: 5 pieces; 2, 3: 4 (wave-uniform)
+            const int tap = v >> 1, row = 16 * (v & 1) + wr;
+            const bf16_t* src = p.w + (int64_t)row * p.ldw + tap * p.cin_pad + chunk * 32 + (((lane & 3) ^ ((row >> 1) & 3)) * 8);
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, src), LDS_PTR(void, b + HBYTES + v * 1024), 16, 0, 0);
+        }
+    };
+    const int n_issue = HPW + (WPIECES - wave + NWAVE - 1) / NWAVE;  // LDS-DMA per wave per chunk (14 or 15)
+
+    f32x4 acc[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int frow = lane & 15, fch = lane >> 4;
+    // fragment i = tile row 4 wave + i / 2, columns 16 (i & 1) .. + 15; at tap (ty, tx) its lane's halo pixel is
+    // row 4 wave + i / 2 + ty, column hx = 16 (i & 1) + frow + tx: hadr[i & 1][tx] + (i / 2 + ty) HWID 64
+    uint32_t hadr[2][3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int hx = 16 * h + frow + t;
+            hadr[h][t] = (uint32_t)(uintptr_t)LDS_PTR(char, smem) + ((4 * wave) * HWID + hx) * 64 +
+                         ((fch ^ ((hx >> 2) & 3)) << 4);
+        }
+    const uint32_t wadr = (uint32_t)(uintptr_t)LDS_PTR(char, smem) + HBYTES + lds_off(frow, fch);
+
+    issue(0, 0);
+    for (int c = 0; c < nch; ++c) {
+        const int buf = c & 1;
+        if (c + 1 < nch) {
+            issue(c + 1, buf ^ 1);  // lands under this chunk's MFMAs
+            wait_vm_rt<16>(n_issue);  // this wave's pieces of chunk c landed (chunk c + 1's still in flight)
+        } else {
+            wait_vm<0>();
+        }
+        __builtin_amdgcn_s_barrier();  // every wave's pieces of chunk c landed
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t bo = buf * BUF;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            bf16x8 fa[8], fb[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                fb[j] = *LDS_PTR(const bf16x8, (uintptr_t)(wadr + bo + tap * 2048 + j * 1024));
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                fa[i] = *LDS_PTR(const bf16x8, (uintptr_t)(hadr[i & 1][tap % 3] + bo + ((i >> 1) + tap / 3) * HWID * 64));
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[j]),
+                                                                       __builtin_bit_cast(f16x8, fa[i]), acc[i][j], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();  // buffer `buf` is free for chunk c + 2
+    }
+
+    // fused head: acc[i][j][e] = conv channel 16 j + 4 (lane >> 4) + e of pixel (tile row 4 wave + i / 2, column
+    // 16 (i & 1) + (lane & 15)); s_f = sum_c silu(conv_c + b_c) w_fin[f, c], the 32 channels of a pixel summed over
+    // the lane's 8 and the four lane groups
+    float bsum[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int col = j * 16 + 4 * (lane >> 4) + e;
+            bsum[j][e] = (p.bias && col < p.cout) ? p.bias[col] : 0.f;
+        }
+    const int hwp = p.ho * p.wo;
+    for (int f = 0; f < p.n_fin; ++f) {
+        float wf[2][4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int col = j * 16 + 4 * (lane >> 4) + e;
+                wf[j][e] = col < p.cout ? p.w_fin[f * p.cout + col] : 0.f;
+            }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) s += silu_precise(acc[i][j][e] + bsum[j][e]) * wf[j][e];
+            s += __shfl_xor(s, 16, 64);
+            s += __shfl_xor(s, 32, 64);
+            if (lane < 16) {
+                const int m = (img * p.ho + y0 + 4 * wave + (i >> 1)) * p.wo + x0 + 16 * (i & 1) + lane;
+                float y = s + p.b_fin[f];
+                y = y > 0.f ? y : p.elu_alpha * expm1f(y);
+                if (p.flags & RF_CONV_LOG_DECODE) y = powf(10.0f, y) - 1.0f;
+                const int64_t o = (p.flags & RF_CONV_NCHW_OUT) ? ((int64_t)(m / hwp) * p.n_fin + f) * hwp + (m % hwp)
+                                                              : (int64_t)m * p.n_fin + f;
+                reinterpret_cast<float*>(p.c)[o] = y;
+            }
+        }
+    }
+}
+
 // Tile configurations.  T128: 128x128, 4 waves of 64x64, 3-stage ring (48 KiB / 96 KiB LDS).
 // T256: 256x256, 8 waves of 128x64, 4-stage ring (128 KiB).  T256x128: 8 waves of 64x64, bf16x3 3-stage (144 KiB).
 using T128 = Tile<128, 128, 2, 2, 3>;
@@ -2607,11 +2765,27 @@ static int launch_halo2(EngineArgs a, void* stream, const char* what) {
     return rf::check_launch(what);
 }
 
+// conv3x3_c32_kernel serves the fused-head 3x3 convolution with <= 32 filters (output_conv2) on whole 16 x 32
+// tiles (RF_CONV_C32=0: the halo2 / engine paths instead)
+static bool c32_ok(const EngineArgs& a) {
+    const char* env = getenv("RF_CONV_C32");
+    if ((env && atoi(env) == 0) || !(a.flags & RF_CONV_FINAL) || a.cout > 32 || a.n < 32) return false;
+    if (a.kw != 3 || a.k != 9 * a.cin_pad || a.stride != 1 || a.pad != 1 || a.ho != a.hi || a.wo != a.wi) return false;
+    return a.cin_pad % 32 == 0 && a.ho % c32::TH == 0 && a.wo % c32::TW == 0 && a.m > 0;
+}
+
+static int launch_c32(EngineArgs a, void* stream, const char* what) {
+    const int nwg = a.m / (c32::TH * c32::TW);
+    RF_LAUNCH(conv3x3_c32_kernel, dim3(nwg), dim3(256), 0, (hipStream_t)stream, a);
+    return rf::check_launch(what);
+}
+
 // fp16 convolutions (one MFMA per product): the 256x256 tile when the filter bank is a multiple of 256
 // wide and there is >= one tile per CU (the im2col gather of A is then read once per pixel tile),
 // 256x64 for <= 64 output channels, else 128x128 (faster than 256x128 on every DPT shape measured)
 template <bool GATHER>
 static int conv_f16_dp(EngineArgs& p, void* stream, const char* what, int tile = 0) {
+    if (GATHER && c32_ok(p)) return launch_c32(p, stream, what);
     if (GATHER && halo2_ok(p)) return launch_halo2(p, stream, what);
     const char* env = getenv("RF_CONV_TILE");
     const int t = tile ? tile : env ? atoi(env) : 0;

@@ -307,3 +307,43 @@ def coldgemm():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "coldgemm":
     coldgemm()
+
+
+def vendor():
+    """STUDY ONLY (never linked into librfhip): the vendor GEMM library (torch.nn.functional.linear on fp16, i.e.
+    hipBLASLt / rocBLAS) against the engine on the frame's projection shapes with fp16 operands and cold rotating
+    operand sets (as coldgemm).  Run it under rocprofv3 --kernel-trace --stats to get the library's kernel names
+    (tile shape, stream-K or not) and durations, and under --pmc FETCH_SIZE / TCC_HIT_sum,TCC_MISS_sum passes for its
+    traffic.  The engine rows use 16-bit outputs (RF_EPI_F16) so both write the same bytes."""
+    shapes = [("s1 qkv", S, 3 * D, D), ("s1 out", S, D, D), ("s1 w2", S, D, F), ("s1 w13", S, 2 * F, D),
+              ("s2 q", R, D, D), ("s2 w2", R, D, F), ("s2 w13", R, 2 * F, D), ("s2 qkv", R, 3 * D, D),
+              ("kvall", S, 20 * D, D)]
+    if os.environ.get("KB_SHAPES"):
+        shapes = [x for x in shapes if x[0] in os.environ["KB_SHAPES"].split(",")]
+    for name, m, n, k in shapes:
+        per = m * k * 2 + n * k * 2 + m * n * 2
+        nrot = max(2, int((768 << 20) // per) + 1)
+        sets = [(torch.randn(m, k, device=dev).half(), (torch.randn(n, k, device=dev) / math.sqrt(k)).half(),
+                 torch.empty(m, n, device=dev, dtype=torch.float16)) for _ in range(nrot)]
+        i = [0]
+
+        def eng():
+            a, w, c = sets[i[0] % nrot]
+            i[0] += 1
+            ops.gemm(a, w, c)
+
+        def lib():
+            a, w, c = sets[i[0] % nrot]
+            i[0] += 1
+            torch.nn.functional.linear(a, w)  # fp16 [m, n] out (torch's caching allocator: no malloc per call)
+        fl = 2 * m * n * k
+        for label, fn in (("engine", eng), ("vendor", lib)):
+            ms = timeit(fn, reps=3 * nrot)
+            print(f"vendor-study {name:7s} {m}x{n}x{k} {label}: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF "
+                  f"({nrot} rotating operand sets, fp16 in, fp16 out)", flush=True)
+        del sets
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "vendor":
+    vendor()
