@@ -15,6 +15,8 @@
 #   l2               per-kernel L2 hit rates of a short bench run (TCC_HIT_sum / TCC_MISS_sum, tools/pmc_l2.py)
 #   attnab           attention GPU tests, then interleaved ablation timings of the RF_ATTN_DBG variants in $ABL
 #   fold             the DPT fold A/B: kernel-trace of the frame with RF_DPT_FOLD=1 and 0, then the bench A/B
+#   vendor           kernel-trace of the vendor GEMM library vs the engine on the frame's projection shapes
+#                    (tools/kbench.py vendor: study only, nothing of it is linked into librfhip)
 # Every GPU step runs under its own timeout and the steps are chained with && (set -e): the first failure
 # (fault, abort, time limit) ends the job.
 set -e
@@ -86,6 +88,8 @@ fold)
         (export RF_DPT_FOLD=$v; prof_run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof$v -o run -- python3 $R/bench.py --profile --steps 5 --warmup 2 --no-cpu-baseline > $O/prof$v.log 2>&1)
     done
     bash tools/gpu.sh ab $TAG "RF_DPT_FOLD=1" "RF_DPT_FOLD=0" ;;
+vendor)
+    prof_run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/vend -o run -- python3 $R/tools/kbench.py vendor > $O/vendor.log 2>&1 ;;
 *)
     echo "unknown task $TASK" >&2; exit 2 ;;
 esac
