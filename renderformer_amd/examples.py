@@ -61,9 +61,9 @@ def example_h5(name: str, out_dir: Optional[str] = None, compression_level: int 
     """Path of examples/<name>.json converted to HDF5 (converted on first use, reused while the sources match)."""
     from .scene_convert import convert_scene
     out_dir = out_dir or cache_dir()
-    path = os.path.join(out_dir, name + ".h5")
+    path = os.path.join(out_dir, name + (".h5" if compression_level == 1 else f".gzip{compression_level}.h5"))
     stamp = path + ".src"
-    digest = _source_digest(name)
+    digest = f"{_source_digest(name)}:gzip{compression_level}"
     if not (os.path.exists(path) and os.path.exists(stamp) and open(stamp).read() == digest):
         os.makedirs(out_dir, exist_ok=True)
         tmp = path + f".tmp{os.getpid()}"

@@ -1,32 +1,44 @@
-"""End-to-end batch_infer throughput: HDF5 decode + render + EXR/PNG writes for a
-folder of cbox-sized synthetic scenes, inline vs pipelined.  python tools/batch_e2e.py [n_scenes]  (GPU box)"""
+"""End-to-end batch_infer throughput (BASELINE config 4's data path): HDF5 decode + render + EXR/PNG
+writes for a folder of the reference's example scenes (examples/*.json converted by the package's converter,
+cycled to n scenes), inline vs pipelined.  python tools/batch_e2e.py [n_scenes] [batch_size]  (GPU box)
+
+Every scene is a new mask pattern for the model, so each pays the per-scene plan (mask read-back + the host
+stream-K attention schedule, ~1 ms) that bench.py's repeated frame reuses."""
+import json
 import os
+import shutil
 import sys
 import tempfile
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import numpy as np  # noqa: E402
 
 import batch_infer  # noqa: E402
-from renderformer_amd import h5io  # noqa: E402
-from renderformer_amd.scenes import expand_texture, synthetic_scene  # noqa: E402
+from renderformer_amd.examples import convert_all, example_names  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+bs = sys.argv[2] if len(sys.argv) > 2 else "1"
 root = tempfile.mkdtemp(prefix="rf_e2e_")
 scenes = os.path.join(root, "scenes")
 os.makedirs(scenes)
+names = example_names()
+files = convert_all(names, workers=8, compression_level=9)  # the reference converter's gzip level (to_h5.py:88)
 for i in range(n):
-    sc = synthetic_scene(5633, 1, seed=100 + i)
-    h5io.write_scene(os.path.join(scenes, f"s{i}.h5"), sc.triangles, sc.vn,
-                     expand_texture(sc.tex_channels).astype(np.float16), sc.c2w, sc.fov)
+    shutil.copy(files[names[i % len(names)]], os.path.join(scenes, f"s{i:03d}_{names[i % len(names)]}.h5"))
 args = ["--h5_folder", scenes, "--model_id", "renderformer-v1.1-swin-large", "--synthetic_seed", "0",
-        "--resolution", "512", "--batch_size", "1", "--precision", "bf16"]
-batch_infer.main(args + ["--output_dir", os.path.join(root, "warm")])  # build + tune
-for mode in ("1", "0", "1", "0"):
+        "--resolution", "512", "--batch_size", bs, "--precision", "fp16"]
+batch_infer.main(args + ["--output_dir", os.path.join(root, "warm")])  # model build + first-touch allocations
+res = {}
+for mode in ("0", "1", "0"):
     os.environ["RF_BATCH_INLINE"] = mode
+    out = os.path.join(root, "out" + mode)
     t0 = time.perf_counter()
-    batch_infer.main(args + ["--output_dir", os.path.join(root, "out" + mode)])
+    batch_infer.main(args + ["--output_dir", out])
     dt = time.perf_counter() - t0
-    print(f"{'inline' if mode == '1' else 'pipelined'}: {n / dt:.2f} frames/s end to end ({dt:.2f} s for {n})",
-          flush=True)
+    key = "inline" if mode == "1" else "pipelined"
+    res[key] = max(res.get(key, 0.0), n / dt)
+    print(f"{key}: {n / dt:.2f} frames/s end to end ({dt:.2f} s for {n} scenes, batch_size {bs})", flush=True)
+print(json.dumps({"batch_infer_e2e_frames_per_s": res, "scenes": n, "batch_size": int(bs), "res": 512,
+                  "data": "the reference's 16 example scenes converted to HDF5 (gzip 9), cycled",
+                  "host_threads": __import__("renderformer_amd.h5io", fromlist=["host_threads"]).host_threads()}))
+shutil.rmtree(root, ignore_errors=True)
