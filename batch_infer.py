@@ -94,7 +94,11 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
     dev = pipeline.device
     kw = dict(resolution=args.resolution, torch_dtype=PRECISION[args.precision])
 
-    def render(batch):
+    model = getattr(pipeline, "model", None)
+
+    def render(batch, host=None):
+        if host is not None and hasattr(model, "plan_hint"):  # a new scene's plan from the host mask: no read-back
+            model.plan_hint(batch["mask"], host["mask"].numpy())
         tex = batch["texture"]
         if tex.dtype != torch.float32:  # the file's dtype, widened on the device like the inline path's host cast
             tex = tex.float()
@@ -104,7 +108,7 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
     if not pipelined or dev.type != "cuda":
         for idx in batches:
             items, host = _load_batch(files, idx, args.padding_length, False)
-            yield items, render({k: v.to(dev) for k, v in host.items()}).cpu()
+            yield items, render({k: v.to(dev) for k, v in host.items()}, host).cpu()
         return
     # HDF5 decode (zlib releases the GIL) runs LOADERS batches ahead on a thread pool, consumed in order
     pool = ThreadPoolExecutor(max_workers=LOADERS)
@@ -143,7 +147,7 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
             compute.wait_stream(h2d)
             for v in batch.values():  # allocated on the copy stream, used on the compute stream
                 v.record_stream(compute)
-            imgs = render(batch)
+            imgs = render(batch, host)
             # the result goes back on its own stream right behind this batch, not behind the next one
             d2h.wait_stream(compute)
             with torch.cuda.stream(d2h):

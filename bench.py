@@ -237,6 +237,8 @@ def main():
         n_frames_step = args.views
         scaling = "strong"
     batches = [{k: v.to(dev) for k, v in h.items() if k != "tex_channels"} for h in hosts]
+    for b, h in zip(batches, hosts):  # plans from the host masks: a new scene never reads its mask back
+        pipe.model.plan_hint(b["mask"], h["mask"].numpy() if torch.is_tensor(h["mask"]) else h["mask"])
     tex0 = [b["texture"][:, :, -3:].clone() for b in batches]
     # the pipeline log-encodes the 3 emission channels in place (reference semantics): every step gets a
     # fresh input texture staged in HBM before the timed region (or, past 32 GiB of copies, the emission

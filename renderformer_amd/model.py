@@ -206,46 +206,59 @@ class _Plan:
     view_off: Optional[torch.Tensor] = None
 
 
-def _build_plan(mask: torch.Tensor, V: int, res: int, patch: int, n_reg: int, device, n_heads: int = 0) -> _Plan:
-    B, N = mask.shape
-    counts = [int(c) for c in mask.sum(dim=1).tolist()]  # host sync (like flash_attn unpad_input)
-    flat = mask.reshape(-1)
-    valid_flat = torch.nonzero(flat).squeeze(1).to(torch.int32)
-    T_tri = int(valid_flat.numel())
-    dst_row = torch.full((B * N,), -1, dtype=torch.int32, device=device)
-    dst_row[valid_flat.long()] = torch.arange(T_tri, dtype=torch.int32, device=device)
+def _build_plan(mask_host, V: int, res: int, patch: int, n_reg: int, device, n_heads: int = 0) -> _Plan:
+    """The plan from a HOST copy of the mask (numpy bool [B, N]): every index table is built with numpy and reaches
+    the device in ONE pinned, non-blocking copy (plus one for the two stream-K range tables), so building a plan
+    never waits for the device (the frames queued before it keep running).  Only a device-only mask needs a
+    read-back first (RenderFormer._plan: like flash_attn's unpad_input)."""
+    import numpy as np
+    m = np.asarray(mask_host, dtype=bool)
+    B, N = m.shape
+    counts = [int(c) for c in m.sum(axis=1)]
+    valid_flat = np.flatnonzero(m.reshape(-1)).astype(np.int32)
+    T_tri = int(valid_flat.size)
+    dst_row = np.full(B * N, -1, dtype=np.int32)
+    dst_row[valid_flat] = np.arange(T_tri, dtype=np.int32)
     S = [n_reg + c for c in counts]
-    cu1 = [0]
-    for s in S:
-        cu1.append(cu1[-1] + s)
-    tri_rows, reg_rows, prob1 = [], [], []
-    for b in range(B):
-        tri_rows.append(torch.arange(cu1[b] + n_reg, cu1[b + 1], dtype=torch.int32))
-        reg_rows.append(torch.arange(cu1[b], cu1[b] + n_reg, dtype=torch.int32))
-        prob1.append([cu1[b], S[b], cu1[b], S[b], cu1[b]])
-    scene_off = [0]
-    for c in counts:
-        scene_off.append(scene_off[-1] + c)
+    cu1 = np.concatenate([[0], np.cumsum(S)]).astype(np.int64)
+    tri_rows = np.concatenate([np.arange(cu1[b] + n_reg, cu1[b + 1]) for b in range(B)] or [np.zeros(0)])
+    reg_rows = np.concatenate([np.arange(cu1[b], cu1[b] + n_reg) for b in range(B)] or [np.zeros(0)])
+    prob1 = [[int(cu1[b]), S[b], int(cu1[b]), S[b], int(cu1[b])] for b in range(B)]
+    scene_off = np.concatenate([[0], np.cumsum(counts)])
     hp = wp = res // patch
     R = hp * wp
     P = B * V
     kv_off, kv_src, prob2, prob_self = [0], [], [], []
     for p in range(P):
         b = p // V
-        kv_src.append(torch.arange(cu1[b], cu1[b + 1], dtype=torch.int32))
-        prob2.append([p * R, R, kv_off[-1], S[b], cu1[b]])
+        kv_src.append(np.arange(cu1[b], cu1[b + 1]))
+        prob2.append([p * R, R, kv_off[-1], S[b], int(cu1[b])])
         prob_self.append([p * R, R, p * R, R, p * R])
         kv_off.append(kv_off[-1] + S[b])
-
-    def dev(x):
-        return (torch.cat(x) if isinstance(x, list) and x and torch.is_tensor(x[0]) else torch.tensor(x, dtype=torch.int32)).to(device)
-
-    return _Plan(B=B, V=V, res=res, counts=counts, T_tri=T_tri, T1=cu1[-1], T_kv=kv_off[-1], R=R, hp=hp, wp=wp,
-                 max_s=max(S), valid_flat=valid_flat, dst_row=dst_row, tri_rows=dev(tri_rows), reg_rows=dev(reg_rows),
-                 scene_off=dev(scene_off), cu1=dev(cu1), kv_off=dev(kv_off), kv_src_rows=dev(kv_src),
-                 prob1=dev(prob1).view(-1, 5), prob2=dev(prob2).view(-1, 5), prob_self=dev(prob_self).view(-1, 5),
-                 sched1=ops.attn_schedule(prob1, n_heads, device) if n_heads else None,
-                 sched2=ops.attn_schedule(prob2, n_heads, device) if n_heads else None)
+    parts = {"valid_flat": valid_flat, "dst_row": dst_row, "tri_rows": tri_rows, "reg_rows": reg_rows,
+             "scene_off": scene_off, "cu1": cu1, "kv_off": np.asarray(kv_off),
+             "kv_src_rows": np.concatenate(kv_src) if kv_src else np.zeros(0), "prob1": np.asarray(prob1).reshape(-1),
+             "prob2": np.asarray(prob2).reshape(-1), "prob_self": np.asarray(prob_self).reshape(-1)}
+    offs, o = {}, 0
+    for k, a in parts.items():
+        offs[k] = (o, int(a.size))
+        o += int(a.size)
+    buf = np.empty(max(o, 1), dtype=np.int32)
+    for k, a in parts.items():
+        buf[offs[k][0]:offs[k][0] + offs[k][1]] = a
+    dbuf = torch.from_numpy(buf).pin_memory().to(device, non_blocking=True)
+    t = {k: dbuf[a:a + n] for k, (a, n) in offs.items()}
+    sched1 = sched2 = None
+    if n_heads and ops.attn_schedule_enabled():
+        grid = ops.attn_grid(device)
+        sc = np.concatenate([ops.attn_schedule_host(prob1, n_heads, grid), ops.attn_schedule_host(prob2, n_heads, grid)])
+        dsc = torch.from_numpy(sc).pin_memory().to(device, non_blocking=True)
+        sched1, sched2 = dsc[:grid + 1], dsc[grid + 1:]
+    return _Plan(B=B, V=V, res=res, counts=counts, T_tri=T_tri, T1=int(cu1[-1]), T_kv=kv_off[-1], R=R, hp=hp, wp=wp,
+                 max_s=max(S), valid_flat=t["valid_flat"], dst_row=t["dst_row"], tri_rows=t["tri_rows"],
+                 reg_rows=t["reg_rows"], scene_off=t["scene_off"], cu1=t["cu1"], kv_off=t["kv_off"],
+                 kv_src_rows=t["kv_src_rows"], prob1=t["prob1"].view(-1, 5), prob2=t["prob2"].view(-1, 5),
+                 prob_self=t["prob_self"].view(-1, 5), sched1=sched1, sched2=sched2)
 
 
 class PrecisionWarning(UserWarning):
@@ -328,7 +341,10 @@ class RenderFormer:
         # texture encoder fast path for to_h5-format textures (proven per call on the device; RF_TEX_FAST=0
         # forces the general pack + GEMM path)
         self._tex_fast = os.environ.get("RF_TEX_FAST", "1") != "0"
-        self._last_plan: Dict = {}  # (V, res) -> (mask object, mask version, plan): the no-read-back fast path
+        # (id(mask), V, res) -> (mask object, mask version, plan): the no-read-back fast path for a mask tensor seen
+        # before (bench.py c4 cycles 64 fixed device masks; a view-chunked render alternates two chunk sizes)
+        self._last_plan: Dict = {}
+        self._host_masks: Dict = {}  # id(device mask) -> (mask, version, host copy): plan_hint
         self._w: Optional[_DeviceWeights] = None
         self._plans: Dict = {}
         self._capture: Optional[dict] = None
@@ -393,26 +409,39 @@ class RenderFormer:
             raise RuntimeError("call .to('cuda') before running the model")
         _load_lib()
 
+    def plan_hint(self, mask: torch.Tensor, mask_host) -> None:
+        """Register the host copy of a device mask (batch_infer.py has it: it uploaded the batch), so the plan for a
+        NEW mask pattern is built without reading the mask back (no device sync in front of the frame).  Valid for
+        this mask object at its current version (an in-place edit invalidates it)."""
+        if len(self._host_masks) > 64:
+            self._host_masks.clear()
+        self._host_masks[id(mask)] = (mask, mask._version, mask_host)
+
     def _plan(self, mask, V, res):
-        # same mask tensor object, unmodified since the last call (torch's version counter): reuse that plan
-        # without reading the mask back (the host sync below stalls the queue at the start of every frame).
-        # The reference is held, so the object (and its storage) cannot be recycled under the same id.
-        # one entry per (views, resolution): a view-chunked render alternates between two chunk sizes when V is not a
-        # multiple of view_chunk, and each keeps its fast path
-        last = self._last_plan.get((V, res))
+        # the same mask tensor object, unmodified since it was planned (torch's version counter): reuse that plan
+        # without reading the mask back (the host sync stalls the queue at the start of every frame).  The
+        # reference is held, so the object (and its storage) cannot be recycled under the same id.
+        ko = (id(mask), V, res)
+        last = self._last_plan.get(ko)
         if last is not None and last[0] is mask and last[1] == mask._version:
             return last[2]
-        key = (tuple(mask.shape), mask.sum(1).cpu().numpy().tobytes(), mask.cpu().numpy().tobytes(), V, res)
+        hint = self._host_masks.get(id(mask))
+        if hint is not None and hint[0] is mask and hint[1] == mask._version:
+            import numpy as np
+            host = np.asarray(hint[2], dtype=bool)
+        else:
+            host = mask.cpu().numpy().astype(bool)  # (device-only mask: one read-back, like unpad_input)
+        key = (tuple(mask.shape), host.tobytes(), V, res)
         plan = self._plans.get(key)
         if plan is None:
-            if len(self._plans) > 16:
+            if len(self._plans) > 64:
                 self._plans.clear()
-            plan = _build_plan(mask, V, res, self.config.patch_size, self.config.num_register_tokens, self._device,
+            plan = _build_plan(host, V, res, self.config.patch_size, self.config.num_register_tokens, self._device,
                                self.config.num_heads)
             self._plans[key] = plan
-        if len(self._last_plan) > 8:
+        if len(self._last_plan) > 128:
             self._last_plan.clear()
-        self._last_plan[(V, res)] = (mask, mask._version, plan)
+        self._last_plan[ko] = (mask, mask._version, plan)
         return plan
 
     def capture_taps(self, enc_rows=None, dec_rows=None, dec_views=None) -> dict:

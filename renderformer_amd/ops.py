@@ -314,12 +314,17 @@ def attn_schedule_host(problems, n_heads: int, grid: int):
     return out
 
 
+def attn_schedule_enabled() -> bool:
+    """The cost-balanced ranges are used unless RF_ATTN_SCHED=0 or the one-wave-per-SIMD kernel runs (attn_schedule)."""
+    return os.environ.get("RF_ATTN_SCHED", "1") != "0" and os.environ.get("RF_ATTN_P4") != "1"
+
+
 def attn_schedule(problems, n_heads: int, device) -> Optional[torch.Tensor]:
     """Device copy of the cost-balanced ranges for `problems` (host [P, 5] list/array), built once per plan;
     None when RF_ATTN_SCHED=0 (equal tile counts per workgroup, for A/B), and under RF_ATTN_P4=1: the schedule
     prices the 8-wave kernel's merge order (last partial first, publish deferred to the next prologue), which the
     one-wave-per-SIMD kernel does not share, so it runs on the equal split of each XCD group instead."""
-    if os.environ.get("RF_ATTN_SCHED", "1") == "0" or os.environ.get("RF_ATTN_P4") == "1":
+    if not attn_schedule_enabled():
         return None
     return torch.from_numpy(attn_schedule_host(problems, n_heads, attn_grid(device))).to(device)
 

@@ -427,3 +427,28 @@ def test_f16_overflow_deferred_check_raises():
     ok(d["triangles"], d["texture"].clone(), d["mask"], d["vn"], d["c2w"], d["fov"], resolution=res)
     torch.cuda.synchronize()
     ok.check_range()  # no overflow: no error
+
+
+def test_plan_hint_matches_read_back():
+    """plan_hint (the host copy of a device mask, batch_infer.py / bench.py): a new mask pattern's plan is built
+    from the host copy without reading the mask back, and the frame equals the one planned from the read-back;
+    a hint is ignored once the device mask is edited in place."""
+    from renderformer_amd.scenes import batch_scenes, synthetic_scene
+    cfg, sd, _, _, _ = load_case("tiny_swin")
+    b = {k: v for k, v in batch_scenes([synthetic_scene(60, 2, seed=8), synthetic_scene(41, 2, seed=9)],
+                                         padding_length=64).items() if k != "tex_channels"}
+    d = {k: v.cuda() for k, v in b.items()}
+    ref = _pipeline(cfg, sd)(d["triangles"], d["texture"].clone(), d["mask"].clone(), d["vn"], d["c2w"], d["fov"],
+                             resolution=64).cpu()
+    pipe = _pipeline(cfg, sd)
+    pipe.model.plan_hint(d["mask"], b["mask"].numpy())
+    got = pipe(d["triangles"], d["texture"].clone(), d["mask"], d["vn"], d["c2w"], d["fov"], resolution=64).cpu()
+    assert torch.equal(got, ref)
+    wrong = b["mask"].numpy().copy()
+    wrong[0, :] = True  # a stale hint: must not be used after the in-place edit below
+    pipe.model.plan_hint(d["mask"], wrong)
+    d["mask"][1, 30:] = False
+    edited = pipe(d["triangles"], d["texture"].clone(), d["mask"], d["vn"], d["c2w"], d["fov"], resolution=64).cpu()
+    fresh = _pipeline(cfg, sd)(d["triangles"], d["texture"].clone(), d["mask"].clone(), d["vn"], d["c2w"], d["fov"],
+                               resolution=64).cpu()
+    assert torch.equal(edited, fresh)

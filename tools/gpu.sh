@@ -15,6 +15,7 @@
 #   l2               per-kernel L2 hit rates of a short bench run (TCC_HIT_sum / TCC_MISS_sum, tools/pmc_l2.py)
 #   attnab           attention GPU tests, then interleaved ablation timings of the RF_ATTN_DBG variants in $ABL
 #   fold             the DPT fold A/B: kernel-trace of the frame with RF_DPT_FOLD=1 and 0, then the bench A/B
+#   c4               config 4: bench.py --workload c4 (64 example scenes) and batch_infer.py end to end (tools/batch_e2e.py)
 #   vendor           kernel-trace of the vendor GEMM library vs the engine on the frame's projection shapes
 #                    (tools/kbench.py vendor: study only, nothing of it is linked into librfhip)
 # Every GPU step runs under its own timeout and the steps are chained with && (set -e): the first failure
@@ -88,6 +89,9 @@ fold)
         (export RF_DPT_FOLD=$v; prof_run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof$v -o run -- python3 $R/bench.py --profile --steps 5 --warmup 2 --no-cpu-baseline > $O/prof$v.log 2>&1)
     done
     bash tools/gpu.sh ab $TAG "RF_DPT_FOLD=1" "RF_DPT_FOLD=0" ;;
+c4)
+    timeout -k 10 400 python bench.py --workload c4 --steps 3 --warmup 1 > $O/c4.json 2> $O/c4.err
+    timeout -k 10 500 python -u tools/batch_e2e.py 64 1 > $O/e2e.log 2>&1 ;;
 vendor)
     prof_run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/vend -o run -- python3 $R/tools/kbench.py vendor > $O/vendor.log 2>&1 ;;
 *)
