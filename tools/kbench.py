@@ -317,7 +317,7 @@ def vendor():
     traffic.  The engine rows use 16-bit outputs (RF_EPI_F16) so both write the same bytes."""
     shapes = [("s1 qkv", S, 3 * D, D), ("s1 out", S, D, D), ("s1 w2", S, D, F), ("s1 w13", S, 2 * F, D),
               ("s2 q", R, D, D), ("s2 w2", R, D, F), ("s2 w13", R, 2 * F, D), ("s2 qkv", R, 3 * D, D),
-              ("kvall", S, 20 * D, D)]
+              ("kvall", S, 20 * D, D), ("sq8k", 8192, 8192, 8192)]
     if os.environ.get("KB_SHAPES"):
         shapes = [x for x in shapes if x[0] in os.environ["KB_SHAPES"].split(",")]
     for name, m, n, k in shapes:
