@@ -787,8 +787,8 @@ RF_DEV void dma_piece(const bf16_t* g, uint32_t lds) {
 // DBG (diagnostic builds only, RF_ATTN_DBG; results are garbage): 1 = no K/V DMA in the loop,
 // 2 = no top-of-tile wait + barrier, 4 = no PV MFMAs, 8 = no exp2 (P = bf16(S)), 16 = no QK MFMAs,
 // 32 = s_memtime stamps per segment (cycles summed over tiles) into the workspace's last piece slot,
-// 64 = no static priority for waves 4-7, 1024 = rebuild the QK^T chains' C operand (-m) in every phase B (the
-// round-3 form; now it is rewritten only where m moves: rebase)
+// 64 = no static priority for waves 4-7, 1024 = keep the QK^T chains' C operand (-m) live across tiles and
+// rewrite it only where m moves (rebase) — valid results, but it spills, see MINIT_EVERY
 // IF16: q, k, v (and P) as fp16 on v_mfma_f32_32x32x16_f16 — the reference's default half precision hands
 // flash_attn_varlen_* fp16 operands (rendering_pipeline.py:37, attention.py:166-172); else bf16.  P <= 2^thr
 // (= 2^12 by default) stays inside fp16's range.
@@ -800,9 +800,10 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     // CVT_PIN: the bf16 packs of P are inline-asm v_cvt_pk_bf16_f32 in their MFMA gaps (hipcc otherwise
     // sinks all 16 of them into one VALU burst after the last QK^T MFMA); DBG & 256 = compiler casts
     constexpr bool CVT_PIN = !(DBG & 256);
-    // MINIT_EVERY: -m is a per-lane constant of the piece except where rebase moves m (rare), so the 16 C-operand
-    // registers are rewritten there instead of by 16 v_mov per tile in phase B (DBG & 1024: the per-tile form)
-    constexpr bool MINIT_EVERY = (DBG & 1024) != 0;
+    // MINIT_EVERY: the 16 C-operand registers (-m) are rebuilt by one v_mov per PV gap each tile.  DBG & 1024
+    // keeps them live across tiles and rewrites them only on rebase: 16 more live VGPRs, which spill (17-23 VGPRs
+    // to scratch at 2 waves/SIMD), so the per-tile form stays the default
+    constexpr bool MINIT_EVERY = (DBG & 1024) == 0;
     constexpr auto x_blk = [](int x) { return x >> 4; };
     constexpr auto x_sp = [](int x) { return (x >> 3) & 1; };
     __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // 64 KiB

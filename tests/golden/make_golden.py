@@ -74,6 +74,8 @@ REAL_CASES = {
     "real_shader-ball_r512": ("shader-ball", LARGE, 512, 0, False),
     "real_cbox-teapot_r512": ("cbox-teapot", LARGE, 512, 0, False),
     "real_init-template_r512": ("init-template", LARGE, 512, 0, False),
+    "real_room_r512": ("room", LARGE, 512, 0, False),
+    "real_crystals_r512": ("crystals", LARGE, 512, 0, False),
 }
 # 1024^2 x 4 views is 50 MB of fp32 HDR: such fixtures keep every SUB-th pixel row and column (plus the
 # full-image sum and sum of squares), the GPU test compares the same sample

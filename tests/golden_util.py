@@ -16,7 +16,8 @@ CASES = ["tiny_swin", "tiny_swin_r128", "tiny_full", "tiny_large", "cbox_base"]
 BIG_CASES = ["large_cbox_r512", "large_bunny_r512", "base_cbox_r256", "large_cbox_r1024_v4"]
 # the reference's own example scenes (examples/*.json through the package's converter), large-proxy at 512^2:
 # config 4's scenes, incl. the longest triangle sequence (cbox-lucy, S = 11,819)
-REAL_CASES = ["real_cbox-lucy_r512", "real_shader-ball_r512", "real_cbox-teapot_r512", "real_init-template_r512"]
+REAL_CASES = ["real_cbox-lucy_r512", "real_shader-ball_r512", "real_cbox-teapot_r512", "real_init-template_r512",
+              "real_room_r512", "real_crystals_r512"]
 # cases whose fixture holds production-size intermediate taps (make_golden.PROD_TAPS)
 PROD_TAP_CASES = BIG_CASES + ["real_cbox-lucy_r512"]
 
