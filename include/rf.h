@@ -43,6 +43,8 @@
  *   rf_upsample_bilinear F.interpolate(bilinear, align_corners=True) (dpt.py:154-155, 269-270)
  *   rf_upsample_bilinear_h  the same resize on fp16 planes: refinenet1's output straight into output_conv1,
  *                      whose weights hold the folded 1x1 out_conv (dpt.py:157-159, 268-271; RF_CONV_BORDER_BIAS)
+ *   rf_encoder_forward TransformerEncoder.forward (attention.py:579-590): the whole stage-1 stack in one call
+ *   rf_decoder_forward TransformerDecoder.forward (attention.py:673-688) + the DPT taps (view_transformer.py:85)
  */
 #ifndef RF_H
 #define RF_H
@@ -59,7 +61,7 @@ extern "C" {
 #define RF_ERR_UNSUPPORTED 3
 #define RF_ERR_DEVICE 4       /* an earlier launch reported a device-side error (see rf_device_error) */
 
-#define RF_ABI_VERSION 12
+#define RF_ABI_VERSION 13
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -388,6 +390,128 @@ int rf_upsample_bilinear(const float* in, int n_img, int hi, int wi, int c, floa
  * values; dpt.py:268-271 with output_conv1's preceding 1x1 folded into its weights). */
 int rf_upsample_bilinear_h(const void* in, int in_ld, int n_img, int hi, int wi, int c, int ho, int wo, void* p_out,
                            int p_ld, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Stage-level entry points: a whole transformer stack in one call (stage.cpp: host code that issues the unit entry
+ * points above in the order the Python model does, so results are bit-identical to it).  Weight pointers are device
+ * pointers in the operand type (RF_DT_F16 or RF_DT_BF16 = the model's `operands`), norm weights f32.  The struct
+ * arrays themselves live in host memory.  Workspaces are caller-owned: `workspace` holds the stack's activations
+ * (rf_*_workspace_bytes), gemm_ws / attn_ws are the GEMM / stream-K attention workspaces of the unit entry points.
+ * --------------------------------------------------------------------------------------------------------------- */
+
+/* One layer of TransformerEncoder (renderformer/layers/attention.py:579-590 -> AttentionLayer.forward :484-527,
+ * MultiHeadAttention :115-202, FeedForwardSwiGLU :51-57). */
+typedef struct {
+    const float* attn_norm;  /* [D]   pre-norm of the attention block (norm1) */
+    const void* w_qkv;       /* [3D, D] in-projection, rows q | k | v */
+    const float* qk_norm;    /* [2D]  full-width q then k RMSNorm weights, or NULL (no q/k norm) */
+    const void* w_out;       /* [D, D] out-projection */
+    const float* ffn_norm;   /* [D]   pre-norm of the FFN block (norm2) */
+    const void* w13;         /* [2F, D] w1 / w3 interleaved in 16-row groups (RF_EPI_SWIGLU layout) */
+    const void* w2;          /* [D, F] */
+} rf_encoder_layer;
+
+typedef struct {
+    int n_layers, rows, dim, n_heads, ffn_dim;  /* rows = packed tokens of the batch (registers + triangles) */
+    int operand_dtype;                          /* RF_DT_F16 / RF_DT_BF16: weights and GEMM operands */
+    float eps;                                  /* RMSNorm eps (1e-6) */
+    const rf_encoder_layer* layers;             /* host array [n_layers] */
+    const float* pos;                           /* [rows, 9] triangle vertex positions (RoPE), NULL = no RoPE */
+    int64_t ld_pos;
+    const float* freqs;                         /* RoPE frequencies [n_freqs] (rope.py:152-206) */
+    int n_freqs;
+    const int32_t* problems;                    /* device [n_problems][5] attention units (rf_attn_fwd), one per scene */
+    int n_problems;
+    const int64_t* bounds;                      /* rf_attn_schedule table (device) for `grid` workgroups, or NULL */
+    int grid;
+    void* workspace;                            /* rf_encoder_workspace_bytes() bytes (activations; no zeroing) */
+    void* gemm_ws;                              /* rf_gemm_workspace_bytes() bytes, zeroed once (may be NULL) */
+    int64_t gemm_ws_bytes;
+    void* attn_ws;                              /* rf_attn_workspace_bytes(0, H, 0) bytes, zeroed once */
+    int timer_attn;                             /* measurement: rf_ktimer_arm() before every attention launch */
+} rf_encoder_desc;
+
+/* x[rows, dim] (f32 residual stream, row stride ldx) through the encoder stack in place: per layer
+ * x += W_out attn(rope(qk_norm(W_qkv rmsnorm(x)))) ; x += W2 swiglu(W13 rmsnorm(x)).  Replaces
+ * TransformerEncoder.forward (attention.py:579-590) on the packed, unpadded rows.  dim = n_heads * 128. */
+int rf_encoder_forward(float* x, int64_t ldx, const rf_encoder_desc* desc, void* stream);
+int64_t rf_encoder_workspace_bytes(int rows, int dim, int ffn_dim, int operand_dtype);
+
+/* One layer of TransformerDecoder (attention.py:673-688 -> AttentionLayer.forward :484-527 with cross-attention,
+ * :436-482): cross-attention rays -> triangles, self-attention between ray tokens (Swin windows :316-370 or full),
+ * SwiGLU FFN, each pre-norm and residual. */
+typedef struct {
+    const float* query_norm;   /* [D] pre-norm of the cross-attention block */
+    const void* w_q;           /* [D, D] */
+    const float* q_norm;       /* [D] full-width q RMSNorm, or NULL */
+    const float* kv_norm;      /* [Dc] context norm (per-layer K/V form only; unused with w_kv_all) */
+    const void* w_kv;          /* [2D, Dc] K rows then V rows (per-layer K/V form only) */
+    const float* k_norm;       /* [D] full-width k RMSNorm, or NULL (per-layer key form only) */
+    const void* w_out;         /* [D, D] */
+    const float* self_norm;    /* [D] pre-norm of the self-attention block; NULL = no self-attention */
+    const void* w_self_in;     /* [3D, D] */
+    const float* self_qk_norm; /* [2D] or NULL */
+    const void* w_self_out;    /* [D, D] */
+    const float* ffn_norm;     /* [D] */
+    const void* w13;           /* [2F, D] (RF_EPI_SWIGLU layout) */
+    const void* w2;            /* [D, F] */
+} rf_decoder_layer;
+
+/* A decoder output handed to the DPT head (view_transformer.py:85 out_layers): after layer `layer`, x is written
+ * as operand planes (rf_split_planes: p_lo NULL = one fp16 plane) with channel stride p_ld. */
+typedef struct {
+    int layer, p_ld;
+    void* p_hi;
+    void* p_lo;
+} rf_decoder_tap;
+
+typedef struct {
+    int n_layers, rows, dim, n_heads, ffn_dim;  /* rows = ray tokens of all (scene, view) images */
+    int operand_dtype;
+    float eps;
+    const rf_decoder_layer* layers;             /* host array [n_layers] */
+    /* context (the stage-1 output) and its K/V: one GEMM for every layer when w_kv_all != NULL (rows of layer i:
+       K then V at 2*D*i; ctx_norm = unit weights, each layer's kv_norm folded into its rows), else per layer */
+    const float* ctx;
+    int64_t ld_ctx;
+    int ctx_rows, ctx_dim;
+    const float* ctx_norm;
+    const void* w_kv_all;
+    /* keys of each view: row r of the rotated keys reads context row kv_src_rows[r] with camera-frame triangle
+       position kv_pos[r]; k_batch = 1 rotates every layer's keys in one launch (needs w_kv_all; k_norm_all =
+       [n_layers * D] or NULL) */
+    int kv_rows;
+    const int32_t* kv_src_rows;
+    const float* kv_pos;
+    int64_t ld_kv_pos;
+    int k_batch;
+    const float* k_norm_all;
+    const float* freqs;                         /* RoPE frequencies [n_freqs] */
+    int n_freqs;
+    const float* ray_pos;                       /* [images, 9] ray-origin positions, one per image (row / ray_pos_div) */
+    int64_t ld_ray_pos;
+    int ray_pos_div;                            /* ray tokens per image */
+    const int32_t* cross_problems;              /* device [n_cross][5]: (q rows of an image, its scene's keys) */
+    int n_cross;
+    const int64_t* cross_bounds;                /* rf_attn_schedule table or NULL */
+    int cross_grid;
+    /* self-attention: Swin windows (swin = 1; shift on odd layers) or full attention over self_problems */
+    int swin, n_images, grid_h, grid_w, window, shift;
+    const int32_t* self_problems;
+    int n_self;
+    const rf_decoder_tap* taps;                 /* host array [n_taps], in layer order */
+    int n_taps;
+    void* workspace;                            /* rf_decoder_workspace_bytes(desc) bytes */
+    void* gemm_ws;
+    int64_t gemm_ws_bytes;
+    void* attn_ws;
+    int timer_cross;                            /* measurement: rf_ktimer_arm() before every cross-attention launch */
+} rf_decoder_desc;
+
+/* x[rows, dim] (f32 ray-token residual stream) through the decoder stack in place; the DPT taps are written as
+ * they are produced.  Replaces TransformerDecoder.forward (attention.py:673-688) on packed rows. */
+int rf_decoder_forward(float* x, int64_t ldx, const rf_decoder_desc* desc, void* stream);
+int64_t rf_decoder_workspace_bytes(const rf_decoder_desc* desc);
 
 #ifdef __cplusplus
 }

@@ -86,11 +86,51 @@ SIGNATURES = {
     "rf_debug_raise_device_error": [_I, _P],
     "rf_ktimer_arm": [],
     "rf_ktimer_read": [_P, _I],
+    "rf_encoder_forward": [_P, _L, _P, _P],
+    "rf_decoder_forward": [_P, _L, _P, _P],
 }
 RF_ERR_DEVICE = 4
 
 _lock = threading.Lock()
 _lib = None
+
+
+class EncoderLayer(ctypes.Structure):
+    """rf.h rf_encoder_layer (device pointers of one TransformerEncoder layer's weights)"""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("attn_norm", "w_qkv", "qk_norm", "w_out", "ffn_norm", "w13", "w2")]
+
+
+class EncoderDesc(ctypes.Structure):
+    """rf.h rf_encoder_desc"""
+    _fields_ = [("n_layers", _I), ("rows", _I), ("dim", _I), ("n_heads", _I), ("ffn_dim", _I),
+                ("operand_dtype", _I), ("eps", _F), ("layers", _P), ("pos", _P), ("ld_pos", _L), ("freqs", _P),
+                ("n_freqs", _I), ("problems", _P), ("n_problems", _I), ("bounds", _P), ("grid", _I),
+                ("workspace", _P), ("gemm_ws", _P), ("gemm_ws_bytes", _L), ("attn_ws", _P), ("timer_attn", _I)]
+
+
+class DecoderLayer(ctypes.Structure):
+    """rf.h rf_decoder_layer"""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("query_norm", "w_q", "q_norm", "kv_norm", "w_kv", "k_norm", "w_out",
+                                               "self_norm", "w_self_in", "self_qk_norm", "w_self_out", "ffn_norm",
+                                               "w13", "w2")]
+
+
+class DecoderTap(ctypes.Structure):
+    """rf.h rf_decoder_tap"""
+    _fields_ = [("layer", _I), ("p_ld", _I), ("p_hi", _P), ("p_lo", _P)]
+
+
+class DecoderDesc(ctypes.Structure):
+    """rf.h rf_decoder_desc"""
+    _fields_ = [("n_layers", _I), ("rows", _I), ("dim", _I), ("n_heads", _I), ("ffn_dim", _I),
+                ("operand_dtype", _I), ("eps", _F), ("layers", _P), ("ctx", _P), ("ld_ctx", _L), ("ctx_rows", _I),
+                ("ctx_dim", _I), ("ctx_norm", _P), ("w_kv_all", _P), ("kv_rows", _I), ("kv_src_rows", _P),
+                ("kv_pos", _P), ("ld_kv_pos", _L), ("k_batch", _I), ("k_norm_all", _P), ("freqs", _P),
+                ("n_freqs", _I), ("ray_pos", _P), ("ld_ray_pos", _L), ("ray_pos_div", _I), ("cross_problems", _P),
+                ("n_cross", _I), ("cross_bounds", _P), ("cross_grid", _I), ("swin", _I), ("n_images", _I),
+                ("grid_h", _I), ("grid_w", _I), ("window", _I), ("shift", _I), ("self_problems", _P), ("n_self", _I),
+                ("taps", _P), ("n_taps", _I), ("workspace", _P), ("gemm_ws", _P), ("gemm_ws_bytes", _L),
+                ("attn_ws", _P), ("timer_cross", _I)]
 
 
 class HipLibraryError(RuntimeError):
@@ -128,6 +168,10 @@ def load(require_device: bool = True):
             lib.rf_scene_pos_partials.argtypes = [_I, _I]
             lib.rf_attn_workspace_bytes.argtypes = [_L, _I, _I]
             lib.rf_attn_grid.argtypes = []
+            lib.rf_encoder_workspace_bytes.restype = ctypes.c_int64
+            lib.rf_encoder_workspace_bytes.argtypes = [_I, _I, _I, _I]
+            lib.rf_decoder_workspace_bytes.restype = ctypes.c_int64
+            lib.rf_decoder_workspace_bytes.argtypes = [_P]
             _lib = lib
     if require_device and not torch.cuda.is_available():
         raise HipLibraryError("renderformer_amd needs a HIP device (MI355X); none is visible")

@@ -343,6 +343,11 @@ class DPTHead:
         stream is never cloned (4 x 33.6 MB of copy traffic per 512^2 frame at D = 1024)."""
         return split_planes(t.view(n_img, hp, wp, t.shape[-1]), self.projects[i].cin_pad, f16=self.f16)
 
+    def empty_tap_planes(self, i: int, n_img: int, hp: int, wp: int, c: int, device) -> Planes:
+        """The (unfilled) operand planes tap_planes(i, ...) would return, for a producer that writes them itself
+        (rf_decoder_forward's taps)."""
+        return Planes.empty(n_img, hp, wp, c, self.projects[i].cin_pad, device, self.f16)
+
     @torch.no_grad()
     def __call__(self, taps: List, n_img: int, hp: int, wp: int, patch: int, elu_alpha: float,
                  log_decode: bool, channels_last: bool) -> torch.Tensor:

@@ -313,6 +313,9 @@ class RenderFormer:
         # quantised per 32-element block.  Not config 5's path: the subset inside the 1e-3 bar (FP8_DEFAULT) buys no
         # frame time, and the full set misses the bar 3x
         self.fp8 = (os.environ.get("RF_FP8", "0") != "0") if fp8 is None else bool(fp8)
+        # stage 1 as ONE library call (rf_encoder_forward: the same launches in the same order, so the same bits)
+        # instead of 8 Python-issued calls per layer; RF_NATIVE_STAGES=0 issues them from Python
+        self.native_stages = os.environ.get("RF_NATIVE_STAGES", "1") != "0"
         # which stage-2 projections the fp8 mode quantises (RF_FP8_PROJ, comma list of FP8_PROJECTIONS)
         self.fp8_projections = set(os.environ.get("RF_FP8_PROJ", ",".join(FP8_DEFAULT)).split(","))
         unknown = self.fp8_projections - set(FP8_PROJECTIONS)
@@ -501,6 +504,13 @@ class RenderFormer:
         cfg, W, dev = self.config, self._w, self._device
         D, H, F = cfg.latent_dim, cfg.num_heads, cfg.dim_feedforward
         T = plan.T1
+        if self._native_ok() and T > 0:
+            if getattr(W, "enc_desc", None) is None:  # host array of the layers' device pointers, built once
+                W.enc_desc = ops.encoder_layers(W.enc, cfg.view_indep_qk_norm)
+            ops.encoder_forward(x, W.enc_desc, len(W.enc), H, F, W.half, EPS, pos1, W.enc_freqs, plan.prob1,
+                                schedule=plan.sched1, tag="attn_stage1")
+            self._capture_stage1(plan, x)
+            return x
         h = torch.empty(T, D, dtype=W.half, device=dev)      # GEMM operands: W.half (fp16 by default)
         qkv = torch.empty(T, 3 * D, dtype=torch.bfloat16, device=dev)  # attention operands: bf16
         att = torch.empty(T, D, dtype=W.half, device=dev)
@@ -518,13 +528,21 @@ class RenderFormer:
             ops.rmsnorm(x, L.ffn_norm, EPS, h)
             ops.gemm(h, L.w13, g, None, ops.EPI_SWIGLU, tag="gemm_w13_stage1")
             ops.gemm(g, L.w2, x, None, ops.EPI_ADD_F32)
+        self._capture_stage1(plan, x)
+        return x
+
+    def _native_ok(self) -> bool:
+        """Stages run as one library call each (rf_encoder_forward / rf_decoder_forward) unless RF_NATIVE_STAGES=0
+        or the legacy split-KV attention is selected (RF_ATTN_SPLIT, a per-op diagnostic mode)."""
+        return self.native_stages and int(os.environ.get("RF_ATTN_SPLIT", "0") or 0) == 0
+
+    def _capture_stage1(self, plan: _Plan, x: torch.Tensor):
         cap = self._capture
         if cap is not None:  # (test capture, capture_taps): scene 0's rows of the stage-1 output
-            s0 = cfg.num_register_tokens + plan.counts[0]
+            s0 = self.config.num_register_tokens + plan.counts[0]
             cap["out"]["enc_rownorm"] = x[:s0].norm(dim=-1)
             if cap["enc"] is not None:
                 cap["out"]["enc_rows"] = x.index_select(0, cap["enc"]).clone()
-        return x
 
     def _stage2(self, plan: _Plan, x: torch.Tensor, ctx: torch.Tensor, pos2: torch.Tensor, ray_pos: torch.Tensor):
         """TransformerDecoder (attention.py:673-688): cross-attn rays->triangles, Swin/full self-attn, SwiGLU."""
@@ -532,22 +550,40 @@ class RenderFormer:
         D, H, F = cfg.view_transformer_latent_dim, cfg.view_transformer_n_heads, cfg.view_transformer_ffn_hidden_dim
         T2, R, P = x.shape[0], plan.R, plan.B * plan.V
         qk = cfg.qk_norm
+        n_dec = len(W.dec)
+        # all layers' K/V in one GEMM (see _DeviceWeights.wkv_all) unless RF_KV_BATCH=0 or it would exceed 4 GiB
+        kv_batch = (os.environ.get("RF_KV_BATCH", "1") != "0" and plan.T1 * n_dec * 2 * D * 2 <= (4 << 30))
+        # (the rotated keys of all layers are kept when they fit in 4 GiB: T_kv grows with the view count)
+        k_batch = kv_batch and os.environ.get("RF_K_BATCH", "1") != "0" and plan.T_kv * n_dec * D * 2 <= (4 << 30)
+        swin = cfg.view_transformer_use_swin_attn
+        cap = self._capture
+        if self._native_ok() and not self.fp8 and not (cap is not None and cap["dec"] is not None):
+            # the whole stack as ONE library call (rf_decoder_forward): the same launches in the same order
+            if getattr(W, "dec_desc", None) is None:
+                W.dec_desc = ops.decoder_layers(W.dec, qk)
+            out_idx = sorted(i for i in set(cfg.out_layers) if 0 <= i < n_dec)
+            planes = [W.dpt.empty_tap_planes(j, P, plan.hp, plan.wp, D, dev) for j in range(len(out_idx))]
+            kv = dict(ctx_norm=W.ctx_unit if kv_batch else None, w_kv_all=W.wkv_all if kv_batch else None,
+                      k_batch=k_batch, k_norm_all=W.k_norm_all if qk else None, kv_src_rows=plan.kv_src_rows,
+                      kv_pos=pos2, freqs=W.dec_freqs)
+            cross = dict(ray_pos=ray_pos, ray_pos_div=R, problems=plan.prob2, schedule=plan.sched2)
+            sa = dict(swin=swin, n_images=P, grid_h=plan.hp, grid_w=plan.wp, window=SWIN_WINDOW, shift=SWIN_SHIFT,
+                      problems=None if swin else plan.prob_self)
+            ops.decoder_forward(x, W.dec_desc, n_dec, H, F, W.half, EPS, ctx, kv, cross, sa,
+                                [(i, pl.hi, pl.lo, pl.hi.shape[-1]) for i, pl in zip(out_idx, planes)], tag="attn_cross")
+            self._capture = None  # (one-shot; a decoder-row capture takes the per-op path below)
+            return planes
         h = torch.empty(T2, D, dtype=W.half, device=dev)
         q2 = torch.empty(T2, D, dtype=torch.bfloat16, device=dev)
         att = torch.empty(T2, D, dtype=W.half, device=dev)
         g = torch.empty(T2, F, dtype=W.half, device=dev)
         hc = torch.empty(plan.T1, ctx.shape[1], dtype=W.half, device=dev)
-        n_dec = len(W.dec)
-        # all layers' K/V in one GEMM (see _DeviceWeights.wkv_all) unless RF_KV_BATCH=0 or it would exceed 4 GiB
-        kv_batch = (os.environ.get("RF_KV_BATCH", "1") != "0" and plan.T1 * n_dec * 2 * D * 2 <= (4 << 30))
         if kv_batch:
             ops.rmsnorm(ctx, W.ctx_unit, EPS, hc)
             kv_all = torch.empty(plan.T1, n_dec * 2 * D, dtype=torch.bfloat16, device=dev)
             ops.gemm(hc, W.wkv_all, kv_all)
         else:
             kv = torch.empty(plan.T1, 2 * D, dtype=torch.bfloat16, device=dev)
-        # (the rotated keys of all layers are kept when they fit in 4 GiB: T_kv grows with the view count)
-        k_batch = kv_batch and os.environ.get("RF_K_BATCH", "1") != "0" and plan.T_kv * n_dec * D * 2 <= (4 << 30)
         if k_batch:
             # keys of all layers normed + rotated in one launch: layer i's K is the D columns at 2*D*i of kv_all,
             # its rotated copy the D columns at D*i of kview_all
@@ -557,7 +593,6 @@ class RenderFormer:
         else:
             kview = torch.empty(plan.T_kv, D, dtype=torch.bfloat16, device=dev)
         qkv = torch.empty(T2, 3 * D, dtype=torch.bfloat16, device=dev) if cfg.view_transformer_include_self_attn else None
-        swin = cfg.view_transformer_use_swin_attn
         fp8 = self.fp8
         if fp8:
             W.make_fp8()

@@ -51,6 +51,15 @@ class KernelTimer:
 TIMER: Optional[KernelTimer] = None
 
 
+def _timer_takes(tag: Optional[str], n: int) -> bool:
+    """Whether the armed KernelTimer times launches tagged `tag`; if so it counts the n launches that a stage-level
+    entry point arms itself (rf_encoder_desc.timer_attn)."""
+    if TIMER is None or tag is None or TIMER.tag != tag:
+        return False
+    TIMER.n += n
+    return True
+
+
 def _t0(tag):
     return TIMER.start(tag) if TIMER is not None and tag is not None else None
 
@@ -378,6 +387,120 @@ def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int
     if n_split > 1:
         call("rf_attn_combine", ptr(ws), rows, n_split, n_heads, None, rows, ptr(out), out.stride(0), stream())
     return out
+
+
+def encoder_layers(layers, qk_norm: bool):
+    """Host array of rf_encoder_layer (device pointers) for the encoder stack's weights (model._Layer objects with
+    query_norm, w_in, qk_norm, w_out, ffn_norm, w13, w2).  The caller keeps the tensors alive."""
+    from ._lib import EncoderLayer
+    arr = (EncoderLayer * len(layers))()
+    for e, L in zip(arr, layers):
+        e.attn_norm, e.w_qkv, e.w_out = ptr(L.query_norm), ptr(L.w_in), ptr(L.w_out)
+        e.qk_norm = ptr(L.qk_norm) if qk_norm else None
+        e.ffn_norm, e.w13, e.w2 = ptr(L.ffn_norm), ptr(L.w13), ptr(L.w2)
+    return arr
+
+
+def encoder_forward(x: torch.Tensor, layers, n_layers: int, n_heads: int, ffn_dim: int, operands: torch.dtype,
+                    eps: float, pos: Optional[torch.Tensor], freqs: Optional[torch.Tensor], problems: torch.Tensor,
+                    schedule: Optional[torch.Tensor] = None, tag: Optional[str] = None) -> torch.Tensor:
+    """x [T, D] f32 through the whole encoder stack in place, one C call (rf_encoder_forward; `layers` from
+    encoder_layers).  Same launches, same order and so the same bits as the per-op sequence of model._stage1."""
+    from ._lib import EncoderDesc
+    import ctypes
+    _dev(x, torch.float32, "x")
+    _check(operands in HALF, "encoder_forward: operands must be bf16 or fp16")
+    _dev(problems, torch.int32, "problems")
+    rows, dim = x.shape
+    _check(dim == n_heads * 128, "encoder_forward: dim must be n_heads * 128")
+    if pos is not None:
+        _dev(pos, torch.float32, "pos")
+        _check(pos.shape[0] >= rows and pos.shape[1] == 9 and freqs is not None, "encoder_forward: pos [T, 9] + freqs")
+    if schedule is not None:
+        _dev(schedule, torch.int64, "schedule")
+    odt = DT_F16 if operands == torch.float16 else DT_BF16
+    lib = load()
+    ws = torch.empty(int(lib.rf_encoder_workspace_bytes(rows, dim, ffn_dim, odt)), dtype=torch.uint8, device=x.device)
+    gws = _gemm_workspace(x.device)
+    d = EncoderDesc(n_layers=n_layers, rows=rows, dim=dim, n_heads=n_heads, ffn_dim=ffn_dim, operand_dtype=odt, eps=eps,
+                    layers=ctypes.addressof(layers), pos=ptr(pos), ld_pos=pos.stride(0) if pos is not None else 0,
+                    freqs=ptr(freqs), n_freqs=freqs.numel() if freqs is not None else 0, problems=ptr(problems),
+                    n_problems=problems.shape[0], bounds=ptr(schedule),
+                    grid=schedule.numel() - 1 if schedule is not None else 0, workspace=ptr(ws), gemm_ws=ptr(gws),
+                    gemm_ws_bytes=gws.numel(), attn_ws=ptr(_attn_workspace(x.device)),
+                    timer_attn=int(_timer_takes(tag, n_layers)))
+    call("rf_encoder_forward", ptr(x), x.stride(0), ctypes.addressof(d), stream())
+    return x
+
+
+def decoder_layers(layers, qk_norm: bool):
+    """Host array of rf_decoder_layer (device pointers) for the decoder stack's weights (model._Layer objects)."""
+    from ._lib import DecoderLayer
+    arr = (DecoderLayer * len(layers))()
+    for e, L in zip(arr, layers):
+        e.query_norm, e.w_q, e.kv_norm, e.w_kv, e.w_out = (ptr(L.query_norm), ptr(L.wq), ptr(L.kv_norm), ptr(L.wkv),
+                                                           ptr(L.wo))
+        e.q_norm = ptr(L.q_norm) if qk_norm else None
+        e.k_norm = ptr(L.k_norm) if qk_norm else None
+        if hasattr(L, "ws_in"):
+            e.self_norm, e.w_self_in, e.w_self_out = ptr(L.self_norm), ptr(L.ws_in), ptr(L.ws_out)
+            e.self_qk_norm = ptr(L.sqk_norm) if qk_norm else None
+        e.ffn_norm, e.w13, e.w2 = ptr(L.ffn_norm), ptr(L.w13), ptr(L.w2)
+    return arr
+
+
+def decoder_forward(x: torch.Tensor, layers, n_layers: int, n_heads: int, ffn_dim: int, operands: torch.dtype,
+                    eps: float, ctx: torch.Tensor, kv: dict, cross: dict, self_attn: dict, taps=(),
+                    tag: Optional[str] = None) -> torch.Tensor:
+    """x [T2, D] f32 through the whole decoder stack in place, one C call (rf_decoder_forward; `layers` from
+    decoder_layers).  kv: ctx_norm, w_kv_all (None = per-layer K/V), k_batch, k_norm_all, kv_src_rows, kv_pos,
+    freqs; cross: ray_pos, ray_pos_div, problems, schedule; self_attn: swin, n_images, grid_h, grid_w, window, shift,
+    problems; taps: (layer, planes_hi, planes_lo or None, ld) in layer order."""
+    from ._lib import DecoderDesc, DecoderTap
+    import ctypes
+    _dev(x, torch.float32, "x")
+    _dev(ctx, torch.float32, "ctx")
+    _check(operands in HALF, "decoder_forward: operands must be bf16 or fp16")
+    rows, dim = x.shape
+    _check(dim == n_heads * 128, "decoder_forward: dim must be n_heads * 128")
+    _dev(cross["problems"], torch.int32, "cross problems")
+    _dev(kv["kv_src_rows"], torch.int32, "kv_src_rows")
+    for key in ("kv_pos", "freqs"):
+        if kv.get(key) is not None:
+            _dev(kv[key], torch.float32, key)
+    if cross.get("ray_pos") is not None:
+        _dev(cross["ray_pos"], torch.float32, "ray_pos")
+    if cross.get("schedule") is not None:
+        _dev(cross["schedule"], torch.int64, "schedule")
+    tarr = (DecoderTap * max(1, len(taps)))()
+    for e, (layer, hi, lo, ld) in zip(tarr, taps):
+        e.layer, e.p_hi, e.p_lo, e.p_ld = layer, ptr(hi), ptr(lo), ld
+    gws = _gemm_workspace(x.device)
+    sch = cross.get("schedule")
+    pos, rpos, freqs = kv.get("kv_pos"), cross.get("ray_pos"), kv.get("freqs")
+    sp = self_attn.get("problems")
+    d = DecoderDesc(n_layers=n_layers, rows=rows, dim=dim, n_heads=n_heads, ffn_dim=ffn_dim,
+                    operand_dtype=DT_F16 if operands == torch.float16 else DT_BF16, eps=eps,
+                    layers=ctypes.addressof(layers), ctx=ptr(ctx), ld_ctx=ctx.stride(0), ctx_rows=ctx.shape[0],
+                    ctx_dim=ctx.shape[1], ctx_norm=ptr(kv.get("ctx_norm")), w_kv_all=ptr(kv.get("w_kv_all")),
+                    kv_rows=kv["kv_src_rows"].numel(), kv_src_rows=ptr(kv["kv_src_rows"]), kv_pos=ptr(pos),
+                    ld_kv_pos=pos.stride(0) if pos is not None else 0, k_batch=int(bool(kv.get("k_batch"))),
+                    k_norm_all=ptr(kv.get("k_norm_all")), freqs=ptr(freqs),
+                    n_freqs=freqs.numel() if freqs is not None else 0, ray_pos=ptr(rpos),
+                    ld_ray_pos=rpos.stride(0) if rpos is not None else 0, ray_pos_div=cross.get("ray_pos_div", 1),
+                    cross_problems=ptr(cross["problems"]), n_cross=cross["problems"].shape[0], cross_bounds=ptr(sch),
+                    cross_grid=sch.numel() - 1 if sch is not None else 0, swin=int(bool(self_attn.get("swin"))),
+                    n_images=self_attn.get("n_images", 0), grid_h=self_attn.get("grid_h", 0),
+                    grid_w=self_attn.get("grid_w", 0), window=self_attn.get("window", 0),
+                    shift=self_attn.get("shift", 0), self_problems=ptr(sp), n_self=sp.shape[0] if sp is not None else 0,
+                    taps=ctypes.addressof(tarr), n_taps=len(taps), gemm_ws=ptr(gws), gemm_ws_bytes=gws.numel(),
+                    attn_ws=ptr(_attn_workspace(x.device)))
+    lib = load()
+    ws = torch.empty(int(lib.rf_decoder_workspace_bytes(ctypes.addressof(d))), dtype=torch.uint8, device=x.device)
+    d.workspace = ptr(ws)
+    d.timer_cross = int(_timer_takes(tag, n_layers))
+    call("rf_decoder_forward", ptr(x), x.stride(0), ctypes.addressof(d), stream())
+    return x
 
 
 def swin_attention(q, k, v, out, n_images: int, grid_h: int, grid_w: int, shift: int, n_heads: int,

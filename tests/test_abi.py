@@ -25,11 +25,13 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load(require_device=False)
     for fn in header_functions():
         assert hasattr(lib, fn), fn
-    assert lib.rf_abi_version() == 12
+    assert lib.rf_abi_version() == 13
     # every int-returning entry point has a ctypes signature in the binding
     assert set(_lib.SIGNATURES) == set(header_functions()) - {"rf_last_error", "rf_abi_version",
                                                                "rf_attn_workspace_bytes", "rf_gemm_workspace_bytes",
-                                                               "rf_scene_pos_partials", "rf_attn_grid"}
+                                                               "rf_scene_pos_partials", "rf_attn_grid",
+                                                               "rf_encoder_workspace_bytes",
+                                                               "rf_decoder_workspace_bytes"}
 
 
 def test_invalid_arguments_raise_value_error_without_device():
@@ -316,3 +318,80 @@ def test_conv_desc_layout_matches_header(tmp_path):
     got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
     want = [ctypes.sizeof(_ConvDesc)] + [getattr(_ConvDesc, n).offset for n in names]
     assert got == want
+
+
+@pytest.mark.parametrize("cls,cname", [("EncoderDesc", "rf_encoder_desc"), ("EncoderLayer", "rf_encoder_layer"),
+                                       ("DecoderDesc", "rf_decoder_desc"), ("DecoderLayer", "rf_decoder_layer"),
+                                       ("DecoderTap", "rf_decoder_tap")])
+def test_stage_desc_layout_matches_header(tmp_path, cls, cname):
+    """_lib.EncoderDesc / EncoderLayer (ctypes) have the size and field offsets of rf.h's rf_encoder_desc /
+    rf_encoder_layer (host C compiler on the header itself)."""
+    import ctypes
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no host C compiler")
+    from renderformer_amd import _lib
+    S = getattr(_lib, cls)
+    names = [f[0] for f in S._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "rf.h"\nint main(void) {\n'
+                   f'  printf("%zu", sizeof({cname}));\n' +
+                   "".join(f'  printf(" %zu", offsetof({cname}, {n}));\n' for n in names) + "  return 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.run([cc, "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert got == [ctypes.sizeof(S)] + [getattr(S, n).offset for n in names]
+
+
+def test_encoder_forward_validates_before_any_launch():
+    """rf_encoder_forward rejects bad descriptors with RF_ERR_INVALID and a message, before touching the device
+    (runs without a GPU); an empty stack is a no-op."""
+    import ctypes
+    from renderformer_amd import _lib
+    lib = _lib.load(require_device=False)
+    fwd = lambda d, x=1: int(lib.rf_encoder_forward(x, 1024, ctypes.addressof(d), None))  # noqa: E731
+    assert lib.rf_encoder_forward(None, 0, None, None) == 1
+    assert fwd(_lib.EncoderDesc(n_layers=0, rows=5)) == 0
+    layers = (_lib.EncoderLayer * 1)()
+    good = dict(n_layers=1, rows=64, dim=1024, n_heads=8, ffn_dim=4096, operand_dtype=1, eps=1e-6,
+                layers=ctypes.addressof(layers), problems=1, n_problems=1, workspace=256, attn_ws=256)
+    for bad, msg in ((dict(dim=1000), b"n_heads"), (dict(operand_dtype=7), b"operand_dtype"),
+                     (dict(ffn_dim=100), b"ffn_dim"), (dict(workspace=0), b"null pointer"),
+                     (dict(pos=16), b"freqs"), (dict(n_problems=0), b"problems")):
+        assert fwd(_lib.EncoderDesc(**{**good, **bad})) == 1, bad
+        assert msg in lib.rf_last_error(), (bad, lib.rf_last_error())
+    assert fwd(_lib.EncoderDesc(**good)) == 1 and b"layer 0" in lib.rf_last_error()  # null weights
+    assert lib.rf_encoder_workspace_bytes(5649, 1024, 4096, 1) >= 5649 * (5 * 1024 + 4096) * 2
+
+
+def test_decoder_forward_validates_before_any_launch():
+    """rf_decoder_forward rejects bad descriptors with RF_ERR_INVALID and a message before touching the device;
+    rf_decoder_workspace_bytes sizes the batched K/V and keys of every layer."""
+    import ctypes
+    from renderformer_amd import _lib
+    lib = _lib.load(require_device=False)
+    fwd = lambda d: int(lib.rf_decoder_forward(1, 1024, ctypes.addressof(d), None))  # noqa: E731
+    assert fwd(_lib.DecoderDesc(n_layers=0, rows=5)) == 0
+    layers = (_lib.DecoderLayer * 2)()
+    for L in layers:
+        L.query_norm = L.w_q = L.w_out = L.ffn_norm = L.w13 = L.w2 = 256
+    taps = (_lib.DecoderTap * 2)()
+    taps[0].layer, taps[0].p_hi, taps[0].p_ld = 1, 256, 1024
+    taps[1].layer, taps[1].p_hi, taps[1].p_ld = 0, 256, 1024  # out of layer order
+    good = dict(n_layers=2, rows=4096, dim=1024, n_heads=8, ffn_dim=4096, operand_dtype=1, eps=1e-6,
+                layers=ctypes.addressof(layers), ctx=256, ld_ctx=1024, ctx_rows=5649, ctx_dim=1024, ctx_norm=256,
+                w_kv_all=256, kv_rows=5649, kv_src_rows=256, k_batch=1, cross_problems=256, n_cross=1,
+                workspace=256, attn_ws=256)
+    for bad, msg in ((dict(dim=1000), b"n_heads"), (dict(ctx_dim=1000), b"ctx_dim"), (dict(n_cross=0), b"problems"),
+                     (dict(w_kv_all=0, k_batch=0), b"K/V weights"), (dict(w_kv_all=0), b"k_batch"),
+                     (dict(kv_pos=16), b"freqs"), (dict(ray_pos=16, freqs=16, n_freqs=6, ld_ray_pos=9), b"ray_pos"),
+                     (dict(taps=ctypes.addressof(taps), n_taps=2), b"tap 1")):
+        assert fwd(_lib.DecoderDesc(**{**good, **bad})) == 1, bad
+        assert msg in lib.rf_last_error(), (bad, lib.rf_last_error())
+    layers[1].self_norm = 256  # self-attention weights for one layer only
+    assert fwd(_lib.DecoderDesc(**good)) == 1 and b"every layer or none" in lib.rf_last_error()
+    d = _lib.DecoderDesc(**good)
+    one = int(lib.rf_decoder_workspace_bytes(ctypes.addressof(d)))
+    assert one >= 2 * (4096 * (3 * 1024 + 4096) + 5649 * 1024 * (1 + 2 * 2 + 2))  # h/q2/att, g, hc, kv_all, kview_all

@@ -452,3 +452,34 @@ def test_plan_hint_matches_read_back():
     fresh = _pipeline(cfg, sd)(d["triangles"], d["texture"].clone(), d["mask"].clone(), d["vn"], d["c2w"], d["fov"],
                                resolution=64).cpu()
     assert torch.equal(edited, fresh)
+
+
+@pytest.mark.parametrize("name,env", [("tiny_swin", {}), ("cbox_base", {}), ("tiny_full", {}),
+                                      ("tiny_swin", {"RF_K_BATCH": "0"}), ("tiny_full", {"RF_KV_BATCH": "0"})])
+def test_native_stacks_bit_identical(name, env, monkeypatch):
+    """rf_encoder_forward / rf_decoder_forward (each stage as one library call) issue the same launches in the same
+    order as the Python-issued per-op sequence, so the frames are bit-identical (Swin and full self-attention,
+    batched and per-layer K/V and keys); the kernel timer still sees every stage-1 / cross-attention launch."""
+    from renderformer_amd import ops
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cfg, sd, inp, res, z = load_case(name)
+    pipe = _pipeline(cfg, sd)
+    d = {k: v.cuda() for k, v in inp.items()}
+    outs = []
+    for native in (False, True, False, True):
+        pipe.model.native_stages = native
+        outs.append(pipe(d["triangles"], d["texture"].clone(), d["mask"], d["vn"], d["c2w"], d["fov"],
+                         resolution=res, torch_dtype=torch.bfloat16))
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+    assert rel_l2(outs[1].cpu(), z["hdr"]) < HDR_TOL
+    for tag, n in (("attn_stage1", cfg.num_layers), ("attn_cross", cfg.view_transformer_n_layers)):
+        timer = ops.KernelTimer(tag)
+        ops.TIMER = timer
+        try:
+            pipe(d["triangles"], d["texture"].clone(), d["mask"], d["vn"], d["c2w"], d["fov"], resolution=res,
+                 torch_dtype=torch.bfloat16)
+        finally:
+            ops.TIMER = None
+        ms = timer.durations_ms()
+        assert len(ms) == n and all(m > 0 for m in ms), (tag, ms)
