@@ -1873,6 +1873,133 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c32_kernel(EngineArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// conv3x3_hk_kernel: the chunk-per-barrier structure of conv3x3_c32_kernel for 3x3 / stride 1 / pad 1 fp16
+// convolutions with any multiple of 64 output channels and the full conv epilogue (bias / border-class bias,
+// residuals, SiLU, fp32 and fp16-plane outputs): DPT output_conv1 (512^2, 256 -> 128) and the 256^2 level's
+// ResidualConvUnits (256 -> 256), which halo2_kernel ran at 0.25-0.31 of peak with two barriers per (chunk,
+// tap) step.  A block is 4 waves (one per SIMD, the whole register file) over a 16 x 32 pixel tile and 64
+// output channels; each wave owns 4 tile rows (8 fragments of 16 pixels) x 64 channels, so one tap is 32 MFMAs
+// per wave and a 32-channel chunk (9 taps, 288 MFMAs) runs between two barriers.  Per chunk the 18 x 34 halo
+// (40 KiB, column-keyed XOR image) and the chunk's 9 W slices (36 KiB) land by LDS-DMA in one of two buffers
+// (152 KiB in all) while the previous chunk computes.  Blocks walk pixel tile-major (the channel tiles of a
+// pixel tile are consecutive ids: same XCD, the halo is read from L2 by the second).
+namespace hk {
+constexpr int TH = 16, TW = 32, HWID = TW + 2, HPIX = (TH + 2) * HWID;  // 612 halo pixels
+constexpr int NCO = 64;                                                  // output channels per block
+constexpr int HPIECES = 40, WPIECES = 9 * NCO / 16;                     // 1-KiB pieces per chunk (40 + 36)
+constexpr int HBYTES = HPIECES * 1024, WBYTES = WPIECES * 1024, BUF = HBYTES + WBYTES;
+constexpr int NWAVE = 4, HPW = HPIECES / NWAVE, WPW = WPIECES / NWAVE;   // 10 + 9 pieces per wave
+constexpr int LDS = 2 * BUF;                                             // 152 KiB: one block per CU
+static_assert(WPIECES % NWAVE == 0 && LDS <= 160 * 1024, "hk: LDS budget");
+}  // namespace hk
+// the epilogue's view of the block: 4 waves stacked over the pixel rows, 128 pixels (4 rows of 32) x 64 channels
+struct HkTile {
+    static constexpr int WGN = 1, WGM = 4, MW = 128, NWD = 64, TI = 8, TJ = 4;
+};
+
+__global__ __launch_bounds__(256, 1) void conv3x3_hk_kernel(EngineArgs p) {
+    using namespace hk;
+    __shared__ __attribute__((aligned(16))) char smem[LDS];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nwg = gridDim.x, hw = blockIdx.x;
+    const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
+    const int tiles_n = p.n / NCO, tx_n = p.wo / TW, ty_n = p.ho / TH;
+    const int tn = wg % tiles_n, pt = wg / tiles_n;
+    const int tx = pt % tx_n, rest = pt / tx_n;
+    const int ty = rest % ty_n, img = rest / ty_n;
+    const int y0 = ty * TH, x0 = tx * TW, n0 = tn * NCO;
+    const int nch = p.cin_pad / 32;
+
+    int hpix[HPW], hch[HPW];
+#pragma unroll
+    for (int t = 0; t < HPW; ++t) {
+        const int hp = (wave + NWAVE * t) * 16 + (lane >> 2);
+        hch[t] = (lane & 3) ^ (((hp % HWID) >> 2) & 3);
+        int pix = -1;
+        if (hp < HPIX) {
+            const int hy = hp / HWID, hx = hp - hy * HWID;
+            const int iy = y0 + hy - 1, ix = x0 + hx - 1;
+            if (iy >= 0 && iy < p.hi && ix >= 0 && ix < p.wi) pix = (img * p.hi + iy) * p.wi + ix;
+        }
+        hpix[t] = pix;
+    }
+    // W piece v (0..35) = tap v / 4, output channels n0 + 16 (v & 3) .. + 15 of the [cout_pad][9][cin_pad] bank
+    const int wr = lane >> 2;
+    const bf16_t* wsrc[WPW];
+#pragma unroll
+    for (int u = 0; u < WPW; ++u) {
+        const int v = wave + NWAVE * u, tap = v >> 2, row = 16 * (v & 3) + wr;
+        wsrc[u] = p.w + (int64_t)(n0 + row) * p.ldw + tap * p.cin_pad + (((lane & 3) ^ ((row >> 1) & 3)) * 8);
+    }
+    auto issue = [&](int chunk, int buf) {
+        char* b = smem + buf * BUF;
+#pragma unroll
+        for (int t = 0; t < HPW; ++t) {
+            const bf16_t* src = hpix[t] >= 0 ? p.a + (int64_t)hpix[t] * p.cin_pad + hch[t] * 8 + chunk * 32 : p.zero;
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, src), LDS_PTR(void, b + (wave + NWAVE * t) * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < WPW; ++u)
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, wsrc[u] + chunk * 32),
+                                             LDS_PTR(void, b + HBYTES + (wave + NWAVE * u) * 1024), 16, 0, 0);
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int frow = lane & 15, fch = lane >> 4;
+    // fragment i = tile row 4 wave + i / 2, columns 16 (i & 1) .. + 15; at tap (ty, tx) its lane's halo pixel is
+    // hadr[i & 1][tx] + (i / 2 + ty) HWID 64 (see conv3x3_c32_kernel)
+    uint32_t hadr[2][3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int hx = 16 * h + frow + t;
+            hadr[h][t] = (uint32_t)(uintptr_t)LDS_PTR(char, smem) + ((4 * wave) * HWID + hx) * 64 +
+                         ((fch ^ ((hx >> 2) & 3)) << 4);
+        }
+    const uint32_t wadr = (uint32_t)(uintptr_t)LDS_PTR(char, smem) + HBYTES + lds_off(frow, fch);
+
+    issue(0, 0);
+    for (int c = 0; c < nch; ++c) {
+        const int buf = c & 1;
+        if (c + 1 < nch) {
+            issue(c + 1, buf ^ 1);   // lands under this chunk's MFMAs
+            wait_vm<HPW + WPW>();    // this wave's pieces of chunk c landed (chunk c + 1's still in flight)
+        } else {
+            wait_vm<0>();
+        }
+        __builtin_amdgcn_s_barrier();  // every wave's pieces of chunk c landed
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t bo = buf * BUF;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            bf16x8 fa[8], fb[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                fb[j] = *LDS_PTR(const bf16x8, (uintptr_t)(wadr + bo + tap * 4096 + j * 1024));
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                fa[i] = *LDS_PTR(const bf16x8, (uintptr_t)(hadr[i & 1][tap % 3] + bo + ((i >> 1) + tap / 3) * HWID * 64));
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[j]),
+                                                                       __builtin_bit_cast(f16x8, fa[i]), acc[i][j], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();  // buffer `buf` is free for chunk c + 2
+    }
+    engine_epilogue<HkTile, E_CONV, TW, false>(p, (img * p.ho + y0) * p.wo + x0, n0, acc);
+}
+
 // Tile configurations.  T128: 128x128, 4 waves of 64x64, 3-stage ring (48 KiB / 96 KiB LDS).
 // T256: 256x256, 8 waves of 128x64, 4-stage ring (128 KiB).  T256x128: 8 waves of 64x64, bf16x3 3-stage (144 KiB).
 using T128 = Tile<128, 128, 2, 2, 3>;
@@ -2780,12 +2907,31 @@ static int launch_c32(EngineArgs a, void* stream, const char* what) {
     return rf::check_launch(what);
 }
 
+// conv3x3_hk_kernel serves non-final 3x3 / stride 1 / pad 1 fp16 convolutions on whole 16 x 32 tiles with a
+// multiple of 64 output channels and at least one block per CU (RF_CONV_HK=0: the halo2 / engine paths; 1: whenever
+// it can)
+static bool hk_ok(const EngineArgs& a) {
+    const char* env = getenv("RF_CONV_HK");
+    if ((env && atoi(env) == 0) || (!env && getenv("RF_CONV_TILE")) || (a.flags & RF_CONV_FINAL) || a.deconv)
+        return false;
+    if (a.kw != 3 || a.k != 9 * a.cin_pad || a.stride != 1 || a.pad != 1 || a.ho != a.hi || a.wo != a.wi) return false;
+    if (a.cin_pad % 32 || a.n % hk::NCO || a.ho % hk::TH || a.wo % hk::TW || a.m <= 0) return false;
+    return (env && atoi(env) == 1) || (int64_t)(a.m / (hk::TH * hk::TW)) * (a.n / hk::NCO) >= 256;
+}
+
+static int launch_hk(EngineArgs a, void* stream, const char* what) {
+    const int nwg = (a.m / (hk::TH * hk::TW)) * (a.n / hk::NCO);
+    RF_LAUNCH(conv3x3_hk_kernel, dim3(nwg), dim3(256), 0, (hipStream_t)stream, a);
+    return rf::check_launch(what);
+}
+
 // fp16 convolutions (one MFMA per product): the 256x256 tile when the filter bank is a multiple of 256
 // wide and there is >= one tile per CU (the im2col gather of A is then read once per pixel tile),
 // 256x64 for <= 64 output channels, else 128x128 (faster than 256x128 on every DPT shape measured)
 template <bool GATHER>
 static int conv_f16_dp(EngineArgs& p, void* stream, const char* what, int tile = 0) {
     if (GATHER && c32_ok(p)) return launch_c32(p, stream, what);
+    if (GATHER && hk_ok(p)) return launch_hk(p, stream, what);
     if (GATHER && halo2_ok(p)) return launch_halo2(p, stream, what);
     const char* env = getenv("RF_CONV_TILE");
     const int t = tile ? tile : env ? atoi(env) : 0;
