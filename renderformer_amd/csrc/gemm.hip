@@ -1192,6 +1192,317 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The 4-wave engine ("quad"): one wave per SIMD with the whole register file, waves 2 x 2 over a BM x BN =
+// 2 WM x 2 WN tile (256 x 256: 128 x 128 outputs, 256 accumulator registers per wave).  This is the shape of the
+// vendor library's kernels on the frame's projection shapes (tools/kbench.py vendor, profiles/r4_vendor_study.txt:
+// 4-wave MT256x256x64 / MT160x256x64 / MT128x192x64 on 16x16x32 MFMAs, 15-26 % faster than the 8-wave phased
+// loop on W13, K/V-all and 8192^3).  A fragment read from LDS feeds WN/16 (A) or WM/16 (B) MFMAs — half the LDS
+// bytes per MFMA of the 8-wave 128 x 64 wave tile — and with no partner wave on the SIMD the wave pipelines
+// itself: one 64-deep K-tile = two phases, one per 32-deep k-half,
+//   A(t): MFMAs of k-half 0 (set 0)  ||  ds_reads of tile t's k-half 1 -> set 1
+//   lgkmcnt(0); vmcnt(0) (tile t+1 landed); barrier (every wave is done with buffer t & 1)
+//   B(t): MFMAs of k-half 1 (set 1)  ||  ds_reads of tile t+1's k-half 0 -> set 0  ||  LDS-DMA of tile t+2
+// with the LDS reads and DMA pieces spread between the MFMAs (sched_group_barrier).  One barrier per K-tile; a
+// DMA lands under one K-tile of MFMAs.  The DMA is buffer_load ... lds: one per-lane VGPR offset per operand and
+// each piece's row offset in an SGPR (no 64-bit address VALU per piece); rows past M read as zeros.
+#ifndef RF_QUAD_EXP
+#define RF_QUAD_EXP 0
+#endif
+#ifndef RF_QUAD_WEAVE
+#define RF_QUAD_WEAVE 1  // (build experiments: 0 leaves the phase interleave to the compiler)
+#endif
+namespace qd {
+template <int WM, int WN>
+struct Cfg {
+    static constexpr int BM = 2 * WM, BN = 2 * WN, TI = WM / 16, TJ = WN / 16;
+    static constexpr int A_IMG = BM * 128, B_IMG = BN * 128, STAGE = A_IMG + B_IMG, LDS = 2 * STAGE;
+    static constexpr int NPA = BM / 8, NPB = BN / 8, PPW = (NPA + NPB) / 4;  // 1-KiB DMA pieces per K-tile
+    static constexpr int WGM = 2, WGN = 2, MW = WM, NWD = WN;               // engine_epilogue's view
+    static_assert(WM % 16 == 0 && WN % 16 == 0 && BM % 32 == 0 && BN % 32 == 0, "quad tile");
+    static_assert(LDS <= 160 * 1024, "quad LDS");
+};
+constexpr uint32_t RSRC_CFG = 0x00020000;  // buffer descriptor word 3 (raw, as the stream-K partial stores)
+}  // namespace qd
+
+// MFMA with the accumulator pinned to AGPRs ("+a"): with 256 accumulator registers per wave hipcc otherwise keeps
+// them in VGPRs and uses the AGPRs as spill space (a v_accvgpr copy pair around every MFMA).  Only MFMAs touch
+// the accumulators until the epilogue, whose reads follow quad_drain().
+template <int NTERM>
+RF_DEV void mfma_agpr(f32x4& c, const bf16x8& b, const bf16x8& a) {
+    if constexpr (NTERM == P_F16)
+        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
+    else
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
+}
+RF_DEV void quad_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
+
+template <int WM, int WN, int NTERM, bool INITC>
+RF_DEV void quad_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int kbeg, int kend,
+                          f32x4 (&acc)[WM / 16][WN / 16], bool pre = false) {
+    using G = qd::Cfg<WM, WN>;
+    constexpr int TI = G::TI, TJ = G::TJ, PPW = G::PPW, BM = G::BM, BN = G::BN, NPA = G::NPA;
+    static_assert(NTERM == 1 || NTERM == P_F16, "quad loop: single-term operands");
+    constexpr int NR = TI + TJ, NM = TI * TJ;
+    static_assert(NM % NR == 0 && PPW <= NR, "quad interleave: whole MFMA groups per read");
+    constexpr int MPG = NM / NR;  // MFMAs per interleave group
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wave >> 1, wc = wave & 1;
+    const int nk = kend - kbeg;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
+
+    if (INITC && kbeg == 0) {  // residual epilogue: start from the C tile
+        load_c_acc<TI, TJ>(p, m0 + wr * WM, n0 + wc * WN, acc);
+    } else {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+    // ---- LDS-DMA: piece q = wave + 4 u; q < NPA: A rows 16 (q >> 1) .. + 15, k-half q & 1 (u < NPA / 4 for
+    // every wave); else B likewise.  Lane l: row l >> 2 of the piece, logical 16-B chunk (l & 3) ^ key(row).
+    const int prow = lane >> 2;
+    const int pch = (lane & 3) ^ ((prow >> 1) & 3);
+    const int64_t a_bytes = (int64_t)(p.m - m0) * p.lda * 2;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.a + (int64_t)m0 * p.lda), 0, (int)(a_bytes < 0x7fffffff ? a_bytes : 0x7fffffff), qd::RSRC_CFG);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.w + (int64_t)n0 * p.ldw), 0, (int)((int64_t)BN * p.ldw * 2), qd::RSRC_CFG);
+    const int va = (prow * (int)p.lda + pch * 8) * 2, vb = (prow * (int)p.ldw + pch * 8) * 2;
+    const int kh_w = wave & 1;  // every piece of this wave is k-half (wave & 1)
+    auto piece = [&](int kt, uint32_t stage, int u) {
+        const int kb = (kbeg + kt) * 128 + kh_w * 64;  // bytes along K
+        if (u < NPA / 4) {
+            const int rg = (wave >> 1) + 2 * u;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, LDS_PTR(void, (uintptr_t)(stage + kh_w * BM * 64 + rg * 1024)),
+                                                     16, va, rg * 16 * (int)p.lda * 2 + kb, 0, 0);
+        } else {
+            const int rg = (wave >> 1) + 2 * u - NPA / 2;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rw, LDS_PTR(void, (uintptr_t)(stage + G::A_IMG + kh_w * BN * 64 + rg * 1024)), 16, vb,
+                rg * 16 * (int)p.ldw * 2 + kb, 0, 0);
+        }
+    };
+    auto issue = [&](int kt, uint32_t stage) {
+#pragma unroll
+        for (int u = 0; u < PPW; ++u) piece(kt, stage, u);
+    };
+
+    // ---- fragments: lane row frow, 16-B chunk fch of a 64-B k-half row (image of ph::img).  Read r of a set:
+    // r < TJ: B fragment r, else A fragment r - TJ
+    const int frow = lane & 15, fch = lane >> 4;
+    const uint32_t sw = (uint32_t)((fch ^ ((frow >> 1) & 3)) << 4);
+    const uint32_t a_rd = (uint32_t)((wr * WM + frow) * 64) + sw;
+    const uint32_t b_rd = (uint32_t)(G::A_IMG + (wc * WN + frow) * 64) + sw;
+    bf16x8 fa[2][TI], fb[2][TJ];
+    auto read1 = [&](uint32_t stage, int kh, int s, int r) {
+        if (r < TJ)
+            fb[s][r] = *LDS_PTR(const bf16x8, (uintptr_t)(stage + b_rd + kh * BN * 64 + r * 1024));
+        else
+            fa[s][r - TJ] = *LDS_PTR(const bf16x8, (uintptr_t)(stage + a_rd + kh * BM * 64 + (r - TJ) * 1024));
+    };
+    // one phase: the TI x TJ MFMAs of set s (i-major) in NR groups of MPG; before group g, read g of set s ^ 1
+    // (k-half rkh of `rstage`, when rd) and DMA piece g of K-tile dkt into `dstage` (when dma and g < PPW)
+    auto phase = [&](int s, bool rd, uint32_t rstage, int rkh, bool dma, int dkt, uint32_t dstage) {
+#pragma unroll
+        for (int g = 0; g < NR; ++g) {
+            if (rd) read1(rstage, rkh, s ^ 1, g);
+            if (dma && g < PPW) piece(dkt, dstage, g);
+#pragma unroll
+            for (int e = 0; e < MPG; ++e) {
+                const int m = g * MPG + e, i = m / TJ, j = m % TJ;
+                mfma_agpr<NTERM>(acc[i][j], fb[s][j], fa[s][i]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+    // the body is branch-free (one register assignment for the whole loop): nk is even (the host guarantees
+    // K % 128 == 0 and even stream-K ranges), the last tile's phase B still reads "tile nk" fragments (unused)
+    // and its DMA pieces are skipped by a uniform branch around SALU / VMEM work only
+    if (!pre) {
+        issue(0, lds0);
+        issue(1, lds0 + G::STAGE);
+    }
+    wait_vm<PPW>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < NR; ++r) read1(lds0, 0, 0, r);
+    auto body = [&](const int t, auto par_c) {
+        constexpr int PAR = decltype(par_c)::value;
+        const uint32_t stage = lds0 + PAR * G::STAGE, nstage = lds0 + (PAR ^ 1) * G::STAGE;
+        __builtin_amdgcn_sched_barrier(0);
+        // phase A: k-half 0 of tile t (set 0) || reads of k-half 1 -> set 1
+        __builtin_amdgcn_s_setprio(1);
+        phase(0, true, stage, 1, false, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of buffer PAR are done
+        wait_vm<0>();                          // this wave's pieces of tile t+1 landed
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        // phase B: k-half 1 of tile t (set 1) || reads of tile t+1's k-half 0 -> set 0 || DMA of tile t+2
+        __builtin_amdgcn_s_setprio(1);
+        phase(1, true, nstage, 0, t + 2 < nk, t + 2, stage);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    for (int t = 0; t < nk; t += 2) {
+        body(t, std::integral_constant<int, 0>{});
+        body(t + 1, std::integral_constant<int, 1>{});
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // (the unused reads of the last phase B)
+    quad_drain();  // the last MFMAs' results are readable by VALU (epilogue, partial stores)
+}
+
+// K-tiles 0 and 1 of a quad tile, issued as quad_mainloop's prologue issues them (a persistent block starts the
+// next tile's operand stream before the current tile's epilogue; the next mainloop call then runs with pre = true)
+template <int WM, int WN>
+RF_DEV void quad_issue01(const EngineArgs& p, char* smem, int m0, int n0, int nk) {
+    using G = qd::Cfg<WM, WN>;
+    constexpr int PPW = G::PPW, BM = G::BM, BN = G::BN, NPA = G::NPA;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
+    const int prow = lane >> 2, pch = (lane & 3) ^ ((prow >> 1) & 3);
+    const int64_t a_bytes = (int64_t)(p.m - m0) * p.lda * 2;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.a + (int64_t)m0 * p.lda), 0, (int)(a_bytes < 0x7fffffff ? a_bytes : 0x7fffffff), qd::RSRC_CFG);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.w + (int64_t)n0 * p.ldw), 0, (int)((int64_t)BN * p.ldw * 2), qd::RSRC_CFG);
+    const int va = (prow * (int)p.lda + pch * 8) * 2, vb = (prow * (int)p.ldw + pch * 8) * 2;
+    const int kh_w = wave & 1;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+        if (kt == 1 && nk < 2) break;
+        const uint32_t stage = lds0 + kt * G::STAGE;
+        const int kb = kt * 128 + kh_w * 64;
+#pragma unroll
+        for (int u = 0; u < PPW; ++u) {
+            const bool is_a = u < NPA / 4;
+            const int rg = is_a ? (wave >> 1) + 2 * u : (wave >> 1) + 2 * u - NPA / 2;
+            if (is_a)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, LDS_PTR(void, (uintptr_t)(stage + kh_w * BM * 64 + rg * 1024)),
+                                                         16, va, rg * 16 * (int)p.lda * 2 + kb, 0, 0);
+            else
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rw, LDS_PTR(void, (uintptr_t)(stage + G::A_IMG + kh_w * BN * 64 + rg * 1024)), 16, vb,
+                    rg * 16 * (int)p.ldw * 2 + kb, 0, 0);
+        }
+    }
+}
+
+// The quad tile as data-parallel (one tile per block), persistent (p.persist: whole tiles strided over the grid,
+// the next tile's first K-tiles prefetched before the epilogue) or stream-K (partial tiles in the SkLayout
+// forward-progress order, as phased_sk_kernel).
+template <int WM, int WN, int EPI, int NTERM>
+__global__ __launch_bounds__(256, 1) void quad_kernel(EngineArgs p) {
+    using G = qd::Cfg<WM, WN>;
+    constexpr int TI = G::TI, TJ = G::TJ, BM = G::BM, BN = G::BN, TS = BM * BN;
+    __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+    if (gated_off(p)) return;
+    const int tiles_m = (p.m + BM - 1) / BM, tiles_n = p.n / BN;
+    const int nwg = gridDim.x, hw = blockIdx.x;
+    const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
+    const int iters = p.k / 64;
+    const int ntiles = tiles_m * tiles_n;
+    f32x4 acc[TI][TJ];
+    if (p.persist >= 0 && !p.sk_flag) {  // data-parallel (grid = tiles) or persistent (grid < tiles)
+        bool pre = false;
+        for (int tile = wg; tile < ntiles; tile += nwg) {
+            int tm, tn;
+            tile_coords(tile, tiles_m, tiles_n, p.group_m, tm, tn);
+            quad_mainloop<WM, WN, NTERM, EPI == E_ADD>(p, smem, tm * BM, tn * BN, 0, iters, acc, pre);
+            pre = tile + nwg < ntiles;
+            if (pre) {
+                int tm2, tn2;
+                tile_coords(tile + nwg, tiles_m, tiles_n, p.group_m, tm2, tn2);
+                __syncthreads();  // every wave's last LDS reads of this tile are done
+                quad_issue01<WM, WN>(p, smem, tm2 * BM, tn2 * BN, iters);
+            }
+#if RF_QUAD_EXP == 2
+            if (threadIdx.x == 1000) { float s = 0; for (int i = 0; i < TI; ++i) for (int j = 0; j < TJ; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3]; ((float*)p.c)[0] = s; }
+#else
+            engine_epilogue<G, EPI>(p, tm * BM, tn * BN, acc);
+#endif
+        }
+        return;
+    }
+#if RF_QUAD_EXP
+    return;
+#endif
+    // stream-K over partial tiles (sk_flag set by the host: sk_setup)
+    const int64_t ntiles64 = ntiles;
+    const SkLayout lay(nwg, ntiles64);
+    int grp = 0;
+    const int L = lay.logical(hw, &grp);
+    const int gend = lay.base(grp) + lay.size(grp);
+    int64_t it, it_end;
+    const int iters2 = iters / 2;  // stream-K units: pairs of K-tiles (the main loop runs whole pairs)
+    lay.equal_range(L, grp, ntiles64, iters2, it, it_end);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    while (it < it_end) {
+        const int tile = (int)(it / iters2), kf = (int)(it % iters2);
+        const int kl = (int)min((int64_t)iters2, kf + (it_end - it));
+        int tm, tn;
+        tile_coords(tile, tiles_m, tiles_n, p.group_m, tm, tn);
+        const int m0 = tm * BM, n0 = tn * BN;
+        wait_vm<0>();
+        __syncthreads();  // the previous segment's LDS readers are done
+        quad_mainloop<WM, WN, NTERM, EPI == E_ADD>(p, smem, m0, n0, 2 * kf, 2 * kl, acc);
+        if (kf != 0) {
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(p.sk_part + (int64_t)L * TS, 0, TS * 4, qd::RSRC_CFG);
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < TJ; ++j) {
+                    const int off = (((wave * TI + i) * TJ + j) * 64 + lane) * 16;
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16);
+                }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) __hip_atomic_store(p.sk_flag + L, p.sk_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (kl < iters2) {
+                const int64_t tile_end = (int64_t)(tile + 1) * iters2;
+                for (int c = L + 1; c < gend; ++c) {  // the tile's later pieces: lower blockIdx (SkLayout)
+                    int64_t cb, ce;
+                    lay.equal_range(c, grp, ntiles64, iters2, cb, ce);
+                    if (cb >= tile_end) break;
+                    if (ce == cb) continue;
+                    if (threadIdx.x == 0) {
+                        int spins = 0;
+                        while (__hip_atomic_load(p.sk_flag + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.sk_epoch &&
+                               ++spins < p.spin)
+                            __builtin_amdgcn_s_sleep(1);
+                        if (spins >= p.spin) report_device_error(p.err, RF_DEVERR_SK_GEMM);
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
+                    __syncthreads();
+                    const float4* src = reinterpret_cast<const float4*>(p.sk_part + (int64_t)c * TS) + wave * TI * TJ * 64 + lane;
+#pragma unroll
+                    for (int i = 0; i < TI; ++i)
+#pragma unroll
+                        for (int j = 0; j < TJ; ++j) {
+                            const float4 v = src[(i * TJ + j) * 64];
+                            acc[i][j][0] += v.x;
+                            acc[i][j][1] += v.y;
+                            acc[i][j][2] += v.z;
+                            acc[i][j][3] += v.w;
+                        }
+                }
+            }
+            engine_epilogue<G, EPI>(p, m0, n0, acc);
+        }
+        it += kl - kf;
+    }
+}
+
 // Data-parallel (one output tile per block) or stream-K (SK): the grid's blocks split the
 // tiles x K-steps iteration space evenly; a block that starts inside a tile stores its partial
 // sum and raises its flag, the block that holds the tile's first K-step (it reaches that tile
@@ -2688,6 +2999,45 @@ bool skph(int m, int n, int k) {
 
 extern "C" int64_t rf_gemm_workspace_bytes(void) { return SK_WS_BYTES; }
 
+// The 4-wave 256x256 engine (quad_kernel, 128 x 128 per wave).  RF_GEMM_QUAD (read per call, for A/B in one
+// process): 0 = off, 1 = data-parallel / persistent over whole tiles, 2 = stream-K over 256 blocks.  Needs
+// N % 256 == 0, K % 128 == 0 and operands addressable by 32-bit buffer offsets.
+static int quad_mode(int m, int n, int k, int64_t lda, int64_t ldw) {
+    const char* env = getenv("RF_GEMM_QUAD");
+    const int mode = env ? atoi(env) : 0;
+    if (mode <= 0 || n % 256 || k % 128 || m <= 0) return 0;  // (the loop runs whole pairs of 64-deep K-tiles)
+    if ((int64_t)m * lda * 2 >= 0x7fffffff || (int64_t)n * ldw * 2 >= 0x7fffffff) return 0;
+    return mode;
+}
+
+template <int EPI, int NT>
+static int launch_quad(EngineArgs a, int mode, void* workspace, int64_t ws_bytes, void* stream, const char* what) {
+    using G = qd::Cfg<128, 128>;
+    const int tiles_m = (a.m + G::BM - 1) / G::BM, tiles_n = a.n / G::BN;
+    const int64_t tiles = (int64_t)tiles_m * tiles_n;
+    const int grid = (int)std::min<int64_t>(tiles, 256);
+    a.group_m = pick_group_m(tiles_m, tiles_n, G::BM, G::BN, (grid + 7) / 8);
+    if (mode == 2 && workspace && ws_bytes >= SK_WS_BYTES) {
+        sk_setup(a, workspace, stream);
+        RF_LAUNCH((quad_kernel<128, 128, EPI, NT>), dim3(256), dim3(256), 0, (hipStream_t)stream, a);
+    } else {
+        a.sk_flag = nullptr;
+        RF_LAUNCH((quad_kernel<128, 128, EPI, NT>), dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+    }
+    return rf::check_launch(what);
+}
+
+template <int NT>
+static int run_quad(const EngineArgs& p, int epilogue, int mode, void* workspace, int64_t ws_bytes, void* stream,
+                    const char* what) {
+    switch (epilogue) {
+        case RF_EPI_BF16: return launch_quad<E_BF16, NT>(p, mode, workspace, ws_bytes, stream, what);
+        case RF_EPI_F32: return launch_quad<E_F32, NT>(p, mode, workspace, ws_bytes, stream, what);
+        case RF_EPI_ADD_F32: return launch_quad<E_ADD, NT>(p, mode, workspace, ws_bytes, stream, what);
+        default: return launch_quad<E_SWIGLU, NT>(p, mode, workspace, ws_bytes, stream, what);
+    }
+}
+
 static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
                      const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
                      void* stream, const int* gate, bool f16 = false) {
@@ -2719,6 +3069,10 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
     p.gate = gate;
     p.out_f16 = out_f16;
     p.range = out_f16 ? rf::range_word() : nullptr;
+    if (const int qm = quad_mode(m, n, k, lda, ldw)) {
+        return f16 ? run_quad<P_F16>(p, epilogue, qm, workspace, ws_bytes, stream, "rf_gemm_f16")
+                   : run_quad<1>(p, epilogue, qm, workspace, ws_bytes, stream, "rf_gemm_bf16");
+    }
     if (workspace && ws_bytes >= SK_WS_BYTES && skph(m, n, k)) {
         sk_setup(p, workspace, stream);
         const int64_t tiles = (int64_t)((m + 255) / 256) * (n / 256);

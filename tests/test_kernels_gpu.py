@@ -131,12 +131,13 @@ def test_gemm_256_tiles(monkeypatch, tile, m, n, k):
 
 
 F16_TILES = {"auto": None, "256ph": "256", "128x256ph": "1282", "96x256ph3": "964", "64x256ph3": "645",
-             "128x256ph3": "1283", "96x256ring": "962", "128ring8wk64": "12884", "128ring": "128", "skph": "skph"}
+             "128x256ph3": "1283", "96x256ring": "962", "128ring8wk64": "12884", "128ring": "128", "skph": "skph",
+             "quad": "quad1", "quadsk": "quad2"}
 
 
 @pytest.mark.parametrize("tile", list(F16_TILES))
 @pytest.mark.parametrize("m,n,k", [(1, 256, 64), (777, 256, 192), (5649, 3072, 1024), (4096, 1024, 4096),
-                                   (5649, 1024, 1024), (4096, 8192, 1024)])
+                                   (5649, 1024, 1024), (4096, 8192, 1024), (300, 512, 256), (1000, 768, 384)])
 def test_gemm_f16_operands(monkeypatch, tile, m, n, k):
     """rf_gemm_f16 (fp16 A and W, fp16 MFMAs) on every loop the cost model can pick, every epilogue incl. the
     fp16 outputs (RF_EPI_F16, RF_EPI_SWIGLU_F16) and the bf16 one, vs fp64 of the same fp16 operands."""
@@ -145,6 +146,10 @@ def test_gemm_f16_operands(monkeypatch, tile, m, n, k):
         if (m + 255) // 256 * (n // 256) < 512:
             pytest.skip("the phased stream-K path needs >= 512 whole 256x256 tiles")
         monkeypatch.setenv("RF_GEMM_SKPH", "1")
+    elif (F16_TILES[tile] or "").startswith("quad"):
+        if n % 256 or k % 128:
+            pytest.skip("the 4-wave 256x256 engine needs N % 256 == 0 and K % 128 == 0")
+        monkeypatch.setenv("RF_GEMM_QUAD", F16_TILES[tile][4:])
     elif F16_TILES[tile]:
         monkeypatch.setenv("RF_GEMM_TILE", F16_TILES[tile])
     g = torch.Generator(device="cpu").manual_seed(m + 5 * n + k)
@@ -169,6 +174,33 @@ def test_gemm_f16_operands(monkeypatch, tile, m, n, k):
         outs = torch.empty(m, n // 2, device=dev, dtype=dt)
         ops.gemm(a, _interleave_swiglu(w[: n // 2].cpu(), w[n // 2:].cpu()).to(dev), outs, None, ops.EPI_SWIGLU)
         assert relerr(outs.float(), refs) < tol, dt
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("m,n,k", [(5649, 8192, 1024), (513, 2048, 640), (8192, 512, 2048)])
+def test_gemm_quad_bf16_and_persistent(monkeypatch, mode, m, n, k):
+    """The 4-wave 256x256 engine (RF_GEMM_QUAD: 1 data-parallel / persistent over whole tiles with the next tile's
+    prefetch, 2 stream-K over pairs of K-tiles) on bf16 operands: more tiles than CUs (persistent), ragged rows,
+    odd K-pair counts split over blocks; fp32, residual and SwiGLU epilogues vs fp64."""
+    monkeypatch.setenv("RF_GEMM_QUAD", mode)
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(m + n + k)
+    a = torch.randn(m, k, generator=g).bfloat16().to(dev)
+    w = (torch.randn(n, k, generator=g) / math.sqrt(k)).bfloat16().to(dev)
+    ref = a.double() @ w.double().t()
+    out = torch.empty(m, n, device=dev)
+    ops.gemm(a, w, out, None, ops.EPI_F32)
+    assert relerr(out, ref) < 1e-5
+    acc = torch.randn(m, n, generator=g).to(dev)
+    ref2 = acc.double() + ref
+    ops.gemm(a, w, acc, None, ops.EPI_ADD_F32)
+    assert relerr(acc, ref2) < 1e-5
+    from renderformer_amd.model import _interleave_swiglu
+    outs = torch.empty(m, n // 2, device=dev, dtype=torch.bfloat16)
+    ops.gemm(a, _interleave_swiglu(w[: n // 2].cpu(), w[n // 2:].cpu()).to(dev), outs, None, ops.EPI_SWIGLU)
+    refs = F.silu(a.double() @ w[: n // 2].double().t()) * (a.double() @ w[n // 2:].double().t())
+    assert relerr(outs.float(), refs) < 5e-3
+    assert ops.load().rf_device_error() == 0
 
 
 def test_rmsnorm_f16_and_attention_f16_out():

@@ -16,6 +16,8 @@
 #   attnab           attention GPU tests, then interleaved ablation timings of the RF_ATTN_DBG variants in $ABL
 #   fold             the DPT fold A/B: kernel-trace of the frame with RF_DPT_FOLD=1 and 0, then the bench A/B
 #   c4               config 4: bench.py --workload c4 (64 example scenes) and batch_infer.py end to end (tools/batch_e2e.py)
+#   new              GPU tests of this round's new kernels / entry points (4-wave GEMM, hk conv, native stages), the
+#                    quad GEMM study leg, then a kernel-trace profile of the default bench
 #   vendor           kernel-trace of the vendor GEMM library vs the engine on the frame's projection shapes
 #                    (tools/kbench.py vendor: study only, nothing of it is linked into librfhip)
 # Every GPU step runs under its own timeout and the steps are chained with && (set -e): the first failure
@@ -92,6 +94,11 @@ fold)
 c4)
     timeout -k 10 400 python bench.py --workload c4 --steps 3 --warmup 1 > $O/c4.json 2> $O/c4.err
     timeout -k 10 500 python -u tools/batch_e2e.py 64 1 > $O/e2e.log 2>&1 ;;
+new)
+    timeout -k 10 600 $T tests/test_kernels_gpu.py -k "quad or hk or border_bias or c32 or f16_operands" > $O/t_new.log 2>&1
+    timeout -k 10 300 $T tests/test_parity_gpu.py -k "native" > $O/t_native.log 2>&1
+    timeout -k 10 400 python -u tools/kbench.py quad > $O/quad.log 2>&1
+    prof_run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --profile --steps 5 --warmup 2 > $O/prof.log 2>&1 ;;
 vendor)
     prof_run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/vend -o run -- python3 $R/tools/kbench.py vendor > $O/vendor.log 2>&1 ;;
 *)

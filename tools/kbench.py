@@ -345,5 +345,45 @@ def vendor():
         torch.cuda.empty_cache()
 
 
+def quad():
+    """The 4-wave 256x256 engine (RF_GEMM_QUAD=1 whole tiles / persistent, 2 stream-K) against the default pick on
+    the 256-divisible frame shapes, fp16 operands, cold rotating operand sets; the SwiGLU shapes with the SwiGLU
+    epilogue (as in the frame), the others with fp16 outputs."""
+    from renderformer_amd.model import _interleave_swiglu
+    shapes = [("s1 qkv", S, 3 * D, D, 0), ("s1 w13", S, 2 * F, D, 1), ("s2 w13", R, 2 * F, D, 1),
+              ("s2 qkv", R, 3 * D, D, 0), ("kvall", S, 20 * D, D, 0), ("sq8k", 8192, 8192, 8192, 0),
+              ("s1 w2", S, D, F, 0), ("s2 w2", R, D, F, 0)]
+    if os.environ.get("KB_SHAPES"):
+        shapes = [x for x in shapes if x[0] in os.environ["KB_SHAPES"].split(",")]
+    modes = os.environ.get("KB_QUAD", "0,1,2").split(",")
+    for name, m, n, k, sw in shapes:
+        per = m * k * 2 + n * k * 2 + m * n * 2
+        nrot = max(2, int((768 << 20) // per) + 1)
+        sets = []
+        for _ in range(nrot):
+            w = (torch.randn(n, k, device=dev) / math.sqrt(k)).half()
+            if sw:
+                w = _interleave_swiglu(w[: n // 2].cpu(), w[n // 2:].cpu()).to(dev)
+            sets.append((torch.randn(m, k, device=dev).half(), w,
+                         torch.empty(m, n // 2 if sw else n, device=dev, dtype=torch.float16)))
+        i = [0]
+
+        def run():
+            a, w, c = sets[i[0] % nrot]
+            i[0] += 1
+            ops.gemm(a, w, c, None, ops.EPI_SWIGLU if sw else ops.EPI_BF16)
+        fl = 2 * m * n * k
+        for md in modes:
+            os.environ["RF_GEMM_QUAD"] = md
+            ms = timeit(run, reps=3 * nrot)
+            print(f"quad-study {name:7s} {m}x{n}x{k} RF_GEMM_QUAD={md}: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF "
+                  f"({nrot} rotating operand sets{', SwiGLU' if sw else ''})", flush=True)
+        os.environ.pop("RF_GEMM_QUAD", None)
+        del sets
+        torch.cuda.empty_cache()
+
+
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "vendor":
     vendor()
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "quad":
+    quad()
