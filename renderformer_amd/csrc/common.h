@@ -77,6 +77,14 @@ RF_DEV float silu(float x) {
 // kernel's register allocation changes and its main loop spills (6 scratch ops per K-step instead of 1:
 // 114 -> 186 us at the 256^2 DPT level), which costs far more than the epilogue saves.
 RF_DEV float silu_precise(float x) { return x / (1.0f + expf(-x)); }
+// The DPT head's output transforms on the hardware exp2 (~1 ulp, v_exp_f32): ELU's negative branch
+// alpha (e^y - 1) and the log decode 10^y - 1 (rendering_pipeline.py:119-123).  The libm expm1f / powf they
+// replace cost ~70 VALU per output value, a third of the fused-head conv's time; the difference is ~1e-7
+// absolute (y near 0) / relative, far inside the frame's 1e-3 bar.
+RF_DEV float elu_fast(float y, float alpha) {
+    return y > 0.f ? y : alpha * (__builtin_amdgcn_exp2f(y * 1.4426950408889634f) - 1.0f);
+}
+RF_DEV float pow10m1_fast(float y) { return __builtin_amdgcn_exp2f(y * 3.3219280948873623f) - 1.0f; }
 
 // Device-side error word (host-pinned, mapped): a stream-K owner whose partial never arrived within the
 // spin bound stores a code here instead of failing silently; every later entry point returns

@@ -471,14 +471,13 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
 #pragma unroll
                     for (int j = 0; j < TJ; ++j)
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) s += silu_precise(acc[i][j][e] + bsum[j][e]) * wf[j][e];
+                        for (int e = 0; e < 4; ++e) s += silu(acc[i][j][e] + bsum[j][e]) * wf[j][e];
                     s += __shfl_xor(s, 16, 64);
                     s += __shfl_xor(s, 32, 64);
                     const int m = frow(i);
                     if (lane < 16 && wn == 0 && m < p.m) {
-                        float y = s + p.b_fin[f];
-                        y = y > 0.f ? y : p.elu_alpha * expm1f(y);
-                        if (p.flags & RF_CONV_LOG_DECODE) y = powf(10.0f, y) - 1.0f;
+                        float y = elu_fast(s + p.b_fin[f], p.elu_alpha);
+                        if (p.flags & RF_CONV_LOG_DECODE) y = pow10m1_fast(y);
                         const int hwp = p.ho * p.wo;
                         const int64_t o = (p.flags & RF_CONV_NCHW_OUT) ? ((int64_t)(m / hwp) * p.n_fin + f) * hwp + (m % hwp)
                                                                       : (int64_t)m * p.n_fin + f;
@@ -541,7 +540,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                 for (int e = 0; e < 4; ++e) {
                     if (brow) v[e] += brow[co + e];
                     v[e] = (v[e] + rr1[e]) + rr2[e];
-                    if (p.flags & RF_CONV_SILU_OUT) v[e] = silu_precise(v[e]);
+                    if (p.flags & RF_CONV_SILU_OUT) v[e] = silu(v[e]);
                 }
                 if (p.c)
                     *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + pix * p.cout + co) =
@@ -550,7 +549,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                     float a[4] = {v[0], v[1], v[2], v[3]};
                     if (p.flags & RF_CONV_PLANE_SILU) {
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) a[e] = silu_precise(a[e]);
+                        for (int e = 0; e < 4; ++e) a[e] = silu(a[e]);
                     }
                     amax = amax3(amax3(amax, a[0], a[1]), a[2], a[3]);
                     *reinterpret_cast<uint2*>(p.p_hi + pix * p.p_ld + co) = make_uint2(pack_f16x2(a[0], a[1]),
@@ -561,8 +560,8 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                     for (int e = 0; e < 2; ++e) {
                         float a0 = v[2 * e], a1 = v[2 * e + 1];
                         if (p.flags & RF_CONV_PLANE_SILU) {
-                            a0 = silu_precise(a0);
-                            a1 = silu_precise(a1);
+                            a0 = silu(a0);
+                            a1 = silu(a1);
                         }
                         const bf16_t h0 = f32_to_bf16(a0), h1 = f32_to_bf16(a1);
                         h[e] = (uint32_t)h0 | ((uint32_t)h1 << 16);
@@ -2153,6 +2152,14 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c32_kernel(EngineArgs p) {
             bsum[j][e] = (p.bias && col < p.cout) ? p.bias[col] : 0.f;
         }
     const int hwp = p.ho * p.wo;
+    // silu(conv + bias) once per value (64 per lane: one wave per SIMD has the registers), then n_fin dot products
+    float sv[8][2][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sv[i][j][e] = silu(acc[i][j][e] + bsum[j][e]);
     for (int f = 0; f < p.n_fin; ++f) {
         float wf[2][4];
 #pragma unroll
@@ -2168,14 +2175,13 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c32_kernel(EngineArgs p) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) s += silu_precise(acc[i][j][e] + bsum[j][e]) * wf[j][e];
+                for (int e = 0; e < 4; ++e) s += sv[i][j][e] * wf[j][e];
             s += __shfl_xor(s, 16, 64);
             s += __shfl_xor(s, 32, 64);
             if (lane < 16) {
                 const int m = (img * p.ho + y0 + 4 * wave + (i >> 1)) * p.wo + x0 + 16 * (i & 1) + lane;
-                float y = s + p.b_fin[f];
-                y = y > 0.f ? y : p.elu_alpha * expm1f(y);
-                if (p.flags & RF_CONV_LOG_DECODE) y = powf(10.0f, y) - 1.0f;
+                float y = elu_fast(s + p.b_fin[f], p.elu_alpha);
+                if (p.flags & RF_CONV_LOG_DECODE) y = pow10m1_fast(y);
                 const int64_t o = (p.flags & RF_CONV_NCHW_OUT) ? ((int64_t)(m / hwp) * p.n_fin + f) * hwp + (m % hwp)
                                                               : (int64_t)m * p.n_fin + f;
                 reinterpret_cast<float*>(p.c)[o] = y;
