@@ -26,6 +26,7 @@
 #include <type_traits>
 #include <cmath>
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -183,7 +184,8 @@ RF_DEV void load_c_acc(const EngineArgs& p, int rbase, int cbase, f32x4 (&acc)[T
         const float* src = c + (int64_t)(ok ? row : 0) * p.ldc + cbase + 4 * (lane >> 4);
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
-            const float4 v = *reinterpret_cast<const float4*>(src + j * 16);
+            const bool okc = cbase + 4 * (lane >> 4) + j * 16 < p.n;
+            const float4 v = okc ? *reinterpret_cast<const float4*>(src + j * 16) : float4{0.f, 0.f, 0.f, 0.f};
             acc[i][j] = ok ? f32x4{v.x, v.y, v.z, v.w} : f32x4{0.f, 0.f, 0.f, 0.f};
         }
     }
@@ -582,6 +584,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
 #pragma unroll
             for (int j = 0; j < TJ; ++j) {
                 const int col = cbase + j * 16 + cq;
+                if (col >= p.n) continue;  // (a ragged last column tile of the 4-wave engine)
                 float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
                 if (p.bias) {
                     const float4 b = *reinterpret_cast<const float4*>(p.bias + col);
@@ -1242,9 +1245,8 @@ RF_DEV void quad_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int k
     using G = qd::Cfg<WM, WN>;
     constexpr int TI = G::TI, TJ = G::TJ, PPW = G::PPW, BM = G::BM, BN = G::BN, NPA = G::NPA;
     static_assert(NTERM == 1 || NTERM == P_F16, "quad loop: single-term operands");
-    constexpr int NR = TI + TJ, NM = TI * TJ;
-    static_assert(NM % NR == 0 && PPW <= NR, "quad interleave: whole MFMA groups per read");
-    constexpr int MPG = NM / NR;  // MFMAs per interleave group
+    constexpr int NR = TI + TJ, NM = TI * TJ;  // reads and MFMAs per phase: group g = read g + MFMAs
+    static_assert(PPW <= NR && NM >= NR, "quad interleave: a read and a DMA piece per MFMA group");  // [NM g / NR, NM (g+1) / NR)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wr = wave >> 1, wc = wave & 1;
@@ -1268,7 +1270,7 @@ RF_DEV void quad_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int k
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(p.a + (int64_t)m0 * p.lda), 0, (int)(a_bytes < 0x7fffffff ? a_bytes : 0x7fffffff), qd::RSRC_CFG);
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.w + (int64_t)n0 * p.ldw), 0, (int)((int64_t)BN * p.ldw * 2), qd::RSRC_CFG);
+        (void*)(p.w + (int64_t)n0 * p.ldw), 0, (int)((int64_t)min(BN, p.n - n0) * p.ldw * 2), qd::RSRC_CFG);
     const int va = (prow * (int)p.lda + pch * 8) * 2, vb = (prow * (int)p.ldw + pch * 8) * 2;
     const int kh_w = wave & 1;  // every piece of this wave is k-half (wave & 1)
     auto piece = [&](int kt, uint32_t stage, int u) {
@@ -1310,10 +1312,7 @@ RF_DEV void quad_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int k
             if (rd) read1(rstage, rkh, s ^ 1, g);
             if (dma && g < PPW) piece(dkt, dstage, g);
 #pragma unroll
-            for (int e = 0; e < MPG; ++e) {
-                const int m = g * MPG + e, i = m / TJ, j = m % TJ;
-                mfma_agpr<NTERM>(acc[i][j], fb[s][j], fa[s][i]);
-            }
+            for (int m = NM * g / NR; m < NM * (g + 1) / NR; ++m) mfma_agpr<NTERM>(acc[m / TJ][m % TJ], fb[s][m % TJ], fa[s][m / TJ]);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -1370,7 +1369,7 @@ RF_DEV void quad_issue01(const EngineArgs& p, char* smem, int m0, int n0, int nk
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(p.a + (int64_t)m0 * p.lda), 0, (int)(a_bytes < 0x7fffffff ? a_bytes : 0x7fffffff), qd::RSRC_CFG);
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.w + (int64_t)n0 * p.ldw), 0, (int)((int64_t)BN * p.ldw * 2), qd::RSRC_CFG);
+        (void*)(p.w + (int64_t)n0 * p.ldw), 0, (int)((int64_t)min(BN, p.n - n0) * p.ldw * 2), qd::RSRC_CFG);
     const int va = (prow * (int)p.lda + pch * 8) * 2, vb = (prow * (int)p.ldw + pch * 8) * 2;
     const int kh_w = wave & 1;
 #pragma unroll
@@ -1402,8 +1401,8 @@ __global__ __launch_bounds__(256, 1) void quad_kernel(EngineArgs p) {
     constexpr int TI = G::TI, TJ = G::TJ, BM = G::BM, BN = G::BN, TS = BM * BN;
     __shared__ __attribute__((aligned(16))) char smem[G::LDS];
     if (gated_off(p)) return;
-    const int tiles_m = (p.m + BM - 1) / BM, tiles_n = p.n / BN;
-    const int nwg = gridDim.x, hw = blockIdx.x;
+    const int tiles_m = (p.m + BM - 1) / BM, tiles_n = (p.n + BN - 1) / BN;  // (a ragged last column tile:
+    const int nwg = gridDim.x, hw = blockIdx.x;                               //  not with the SwiGLU epilogue)
     const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
     const int iters = p.k / 64;
@@ -2120,21 +2119,29 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c32_kernel(EngineArgs p) {
         __builtin_amdgcn_s_barrier();  // every wave's pieces of chunk c landed
         __builtin_amdgcn_sched_barrier(0);
         const uint32_t bo = buf * BUF;
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-            bf16x8 fa[8], fb[2];
+        // one wave per SIMD: tap t + 1's fragments are read under tap t's MFMAs (two register sets)
+        bf16x8 fa[2][8], fb[2][2];
+        auto rd = [&](int tap, int s) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-                fb[j] = *LDS_PTR(const bf16x8, (uintptr_t)(wadr + bo + tap * 2048 + j * 1024));
+                fb[s][j] = *LDS_PTR(const bf16x8, (uintptr_t)(wadr + bo + tap * 2048 + j * 1024));
 #pragma unroll
             for (int i = 0; i < 8; ++i)
-                fa[i] = *LDS_PTR(const bf16x8, (uintptr_t)(hadr[i & 1][tap % 3] + bo + ((i >> 1) + tap / 3) * HWID * 64));
+                fa[s][i] = *LDS_PTR(const bf16x8, (uintptr_t)(hadr[i & 1][tap % 3] + bo + ((i >> 1) + tap / 3) * HWID * 64));
+        };
+        rd(0, 0);
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int s = tap & 1;
+            if (tap + 1 < 9) rd(tap + 1, s ^ 1);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < 8; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[j]),
-                                                                       __builtin_bit_cast(f16x8, fa[i]), acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[s][j]),
+                                                                       __builtin_bit_cast(f16x8, fa[s][i]), acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
         }
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();  // buffer `buf` is free for chunk c + 2
@@ -2295,21 +2302,29 @@ __global__ __launch_bounds__(256, 1) void conv3x3_hk_kernel(EngineArgs p) {
         __builtin_amdgcn_s_barrier();  // every wave's pieces of chunk c landed
         __builtin_amdgcn_sched_barrier(0);
         const uint32_t bo = buf * BUF;
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-            bf16x8 fa[8], fb[4];
+        // one wave per SIMD: tap t + 1's fragments are read under tap t's MFMAs (two register sets)
+        bf16x8 fa[2][8], fb[2][4];
+        auto rd = [&](int tap, int s) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                fb[j] = *LDS_PTR(const bf16x8, (uintptr_t)(wadr + bo + tap * 4096 + j * 1024));
+                fb[s][j] = *LDS_PTR(const bf16x8, (uintptr_t)(wadr + bo + tap * 4096 + j * 1024));
 #pragma unroll
             for (int i = 0; i < 8; ++i)
-                fa[i] = *LDS_PTR(const bf16x8, (uintptr_t)(hadr[i & 1][tap % 3] + bo + ((i >> 1) + tap / 3) * HWID * 64));
+                fa[s][i] = *LDS_PTR(const bf16x8, (uintptr_t)(hadr[i & 1][tap % 3] + bo + ((i >> 1) + tap / 3) * HWID * 64));
+        };
+        rd(0, 0);
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int s = tap & 1;
+            if (tap + 1 < 9) rd(tap + 1, s ^ 1);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < 8; ++i)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[j]),
-                                                                       __builtin_bit_cast(f16x8, fa[i]), acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[s][j]),
+                                                                       __builtin_bit_cast(f16x8, fa[s][i]), acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
         }
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();  // buffer `buf` is free for chunk c + 2
@@ -3005,42 +3020,67 @@ bool skph(int m, int n, int k) {
 
 extern "C" int64_t rf_gemm_workspace_bytes(void) { return SK_WS_BYTES; }
 
-// The 4-wave 256x256 engine (quad_kernel, 128 x 128 per wave).  RF_GEMM_QUAD (read per call, for A/B in one
-// process): 0 = off, 1 = data-parallel / persistent over whole tiles, 2 = stream-K over 256 blocks.  Needs
-// N % 256 == 0, K % 128 == 0 and operands addressable by 32-bit buffer offsets.
-static int quad_mode(int m, int n, int k, int64_t lda, int64_t ldw) {
+// The 4-wave engine (quad_kernel).  RF_GEMM_QUAD (read per call, for A/B in one process): 0 = off, 1 = data-
+// parallel / persistent over whole tiles, 2 = stream-K over 256 blocks in pairs of K-tiles.  RF_GEMM_QUAD_TILE
+// picks the block tile (BM x BN): 256x256 (default; 128 x 128 per wave), 192x256, 160x256, 128x192, 128x128.
+// Needs K % 128 == 0, a column-tile multiple of N for the SwiGLU epilogue, and operands addressable by 32-bit
+// buffer offsets.
+static int quad_tile() {
+    const char* env = getenv("RF_GEMM_QUAD_TILE");
+    if (!env) return 256256;
+    int bm = 0, bn = 0;
+    if (sscanf(env, "%dx%d", &bm, &bn) != 2) return 256256;
+    return bm * 1000 + bn;
+}
+
+static int quad_mode(int m, int n, int k, int64_t lda, int64_t ldw, int epilogue) {
     const char* env = getenv("RF_GEMM_QUAD");
     const int mode = env ? atoi(env) : 0;
-    if (mode <= 0 || n % 256 || k % 128 || m <= 0) return 0;  // (the loop runs whole pairs of 64-deep K-tiles)
+    if (mode <= 0 || k % 128 || m <= 0) return 0;  // (the loop runs whole pairs of 64-deep K-tiles)
+    const int t = quad_tile(), bn = t % 1000;
+    if (bn != 256 && bn != 192 && bn != 128) return 0;
+    if (epilogue == RF_EPI_SWIGLU && n % bn) return 0;
     if ((int64_t)m * lda * 2 >= 0x7fffffff || (int64_t)n * ldw * 2 >= 0x7fffffff) return 0;
     return mode;
 }
 
-template <int EPI, int NT>
+template <int WM, int WN, int EPI, int NT>
 static int launch_quad(EngineArgs a, int mode, void* workspace, int64_t ws_bytes, void* stream, const char* what) {
-    using G = qd::Cfg<128, 128>;
-    const int tiles_m = (a.m + G::BM - 1) / G::BM, tiles_n = a.n / G::BN;
+    using G = qd::Cfg<WM, WN>;
+    const int tiles_m = (a.m + G::BM - 1) / G::BM, tiles_n = (a.n + G::BN - 1) / G::BN;
     const int64_t tiles = (int64_t)tiles_m * tiles_n;
     const int grid = (int)std::min<int64_t>(tiles, 256);
     a.group_m = pick_group_m(tiles_m, tiles_n, G::BM, G::BN, (grid + 7) / 8);
     if (mode == 2 && workspace && ws_bytes >= SK_WS_BYTES) {
         sk_setup(a, workspace, stream);
-        RF_LAUNCH((quad_kernel<128, 128, EPI, NT>), dim3(256), dim3(256), 0, (hipStream_t)stream, a);
+        RF_LAUNCH((quad_kernel<WM, WN, EPI, NT>), dim3(256), dim3(256), 0, (hipStream_t)stream, a);
     } else {
         a.sk_flag = nullptr;
-        RF_LAUNCH((quad_kernel<128, 128, EPI, NT>), dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+        RF_LAUNCH((quad_kernel<WM, WN, EPI, NT>), dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
     }
     return rf::check_launch(what);
+}
+
+template <int WM, int WN, int NT>
+static int run_quad_t(const EngineArgs& p, int epilogue, int mode, void* workspace, int64_t ws_bytes, void* stream,
+                      const char* what) {
+    switch (epilogue) {
+        case RF_EPI_BF16: return launch_quad<WM, WN, E_BF16, NT>(p, mode, workspace, ws_bytes, stream, what);
+        case RF_EPI_F32: return launch_quad<WM, WN, E_F32, NT>(p, mode, workspace, ws_bytes, stream, what);
+        case RF_EPI_ADD_F32: return launch_quad<WM, WN, E_ADD, NT>(p, mode, workspace, ws_bytes, stream, what);
+        default: return launch_quad<WM, WN, E_SWIGLU, NT>(p, mode, workspace, ws_bytes, stream, what);
+    }
 }
 
 template <int NT>
 static int run_quad(const EngineArgs& p, int epilogue, int mode, void* workspace, int64_t ws_bytes, void* stream,
                     const char* what) {
-    switch (epilogue) {
-        case RF_EPI_BF16: return launch_quad<E_BF16, NT>(p, mode, workspace, ws_bytes, stream, what);
-        case RF_EPI_F32: return launch_quad<E_F32, NT>(p, mode, workspace, ws_bytes, stream, what);
-        case RF_EPI_ADD_F32: return launch_quad<E_ADD, NT>(p, mode, workspace, ws_bytes, stream, what);
-        default: return launch_quad<E_SWIGLU, NT>(p, mode, workspace, ws_bytes, stream, what);
+    switch (quad_tile()) {
+        case 192256: return run_quad_t<96, 128, NT>(p, epilogue, mode, workspace, ws_bytes, stream, what);
+        case 160256: return run_quad_t<80, 128, NT>(p, epilogue, mode, workspace, ws_bytes, stream, what);
+        case 128192: return run_quad_t<64, 96, NT>(p, epilogue, mode, workspace, ws_bytes, stream, what);
+        case 128128: return run_quad_t<64, 64, NT>(p, epilogue, mode, workspace, ws_bytes, stream, what);
+        default: return run_quad_t<128, 128, NT>(p, epilogue, mode, workspace, ws_bytes, stream, what);
     }
 }
 
@@ -3075,7 +3115,7 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
     p.gate = gate;
     p.out_f16 = out_f16;
     p.range = out_f16 ? rf::range_word() : nullptr;
-    if (const int qm = quad_mode(m, n, k, lda, ldw)) {
+    if (const int qm = quad_mode(m, n, k, lda, ldw, epilogue)) {
         return f16 ? run_quad<P_F16>(p, epilogue, qm, workspace, ws_bytes, stream, "rf_gemm_f16")
                    : run_quad<1>(p, epilogue, qm, workspace, ws_bytes, stream, "rf_gemm_bf16");
     }
@@ -3272,11 +3312,10 @@ static int launch_c32(EngineArgs a, void* stream, const char* what) {
 // it can)
 static bool hk_ok(const EngineArgs& a) {
     const char* env = getenv("RF_CONV_HK");
-    if ((env && atoi(env) == 0) || (!env && getenv("RF_CONV_TILE")) || (a.flags & RF_CONV_FINAL) || a.deconv)
-        return false;
+    if (!env || atoi(env) == 0 || (a.flags & RF_CONV_FINAL) || a.deconv) return false;  // opt-in: see DESIGN §3.4
     if (a.kw != 3 || a.k != 9 * a.cin_pad || a.stride != 1 || a.pad != 1 || a.ho != a.hi || a.wo != a.wi) return false;
     if (a.cin_pad % 32 || a.n % hk::NCO || a.ho % hk::TH || a.wo % hk::TW || a.m <= 0) return false;
-    return (env && atoi(env) == 1) || (int64_t)(a.m / (hk::TH * hk::TW)) * (a.n / hk::NCO) >= 256;
+    return atoi(env) == 1 || (int64_t)(a.m / (hk::TH * hk::TW)) * (a.n / hk::NCO) >= 256;
 }
 
 static int launch_hk(EngineArgs a, void* stream, const char* what) {

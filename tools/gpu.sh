@@ -18,6 +18,8 @@
 #   c4               config 4: bench.py --workload c4 (64 example scenes) and batch_infer.py end to end (tools/batch_e2e.py)
 #   new              GPU tests of this round's new kernels / entry points (4-wave GEMM, hk conv, native stages), the
 #                    quad GEMM study leg, then a kernel-trace profile of the default bench
+#   vpmc [legs]      kbench legs (default: vendor) under FETCH / WRITE / L2-hit / MFMA-busy counter passes
+#   convab           halo2 vs conv3x3_hk_kernel on the 512^2 / 256^2 DPT convolutions
 #   vendor           kernel-trace of the vendor GEMM library vs the engine on the frame's projection shapes
 #                    (tools/kbench.py vendor: study only, nothing of it is linked into librfhip)
 # Every GPU step runs under its own timeout and the steps are chained with && (set -e): the first failure
@@ -99,6 +101,17 @@ new)
     timeout -k 10 300 $T tests/test_parity_gpu.py -k "native" > $O/t_native.log 2>&1
     timeout -k 10 400 python -u tools/kbench.py quad > $O/quad.log 2>&1
     prof_run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --profile --steps 5 --warmup 2 > $O/prof.log 2>&1 ;;
+vpmc)  # kbench legs ($@, default vendor) under counter passes (FETCH / WRITE / L2 hit / MFMA busy); KB_* passed through
+    for LEG in ${@:-vendor}; do
+        i=0
+        for P in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES"; do
+            i=$((i+1))
+            prof_run timeout -s KILL 180 rocprofv3 --pmc $P --output-format csv -d $O/${LEG}_p$i -o run -- python3 $R/tools/kbench.py $LEG > $O/${LEG}_p$i.log 2>&1
+        done
+        python tools/pmc_kernels.py $(find $O/${LEG}_p1 $O/${LEG}_p2 $O/${LEG}_p3 $O/${LEG}_p4 -name '*counter_collection.csv') > $O/${LEG}_pmc.txt 2>&1
+    done ;;
+convab)  # the 512^2 / 256^2 DPT convolutions on halo2 vs conv3x3_hk_kernel
+    KB_F16_ONLY=1 KB_CONV_HW=512,256 KB_CONV_TILES=h2,hk timeout -k 10 300 python -u tools/kbench.py conv > $O/convab.log 2>&1 ;;
 vendor)
     prof_run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/vend -o run -- python3 $R/tools/kbench.py vendor > $O/vendor.log 2>&1 ;;
 *)

@@ -197,7 +197,8 @@ def conv():
                 os.environ["RF_CONV_HALO2"] = "1" if t.startswith("h2") else "0"
                 os.environ["RF_CONV_H2S"] = t[4:] if t.startswith("h2s") else "4"
                 os.environ["RF_H2_DBG"] = t[4:] if t.startswith("h2db") else "0"  # h2db1/2/3: ablations
-                if not t.startswith("auto") and not t.startswith("h2"):
+                os.environ["RF_CONV_HK"] = "1" if t == "hk" else "0"  # hk: conv3x3_hk_kernel (4 waves, one barrier per chunk)
+                if not t.startswith("auto") and not t.startswith("h2") and t != "hk":
                     os.environ["RF_CONV_TILE"] = t.replace("ph", "")
                 ms = timeit(lambda: conv(x, out_f32=True), reps=10)
                 os.environ.pop("RF_CONV_TILE", None)
