@@ -1355,6 +1355,131 @@ RF_DEV void quad_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int k
     quad_drain();  // the last MFMAs' results are readable by VALU (epilogue, partial stores)
 }
 
+// quad_mainloop with the operands staged through registers instead of LDS-DMA (the library's form, PGR): a
+// wave's 1-KiB pieces of K-tile t+3 are buffer_load_dwordx4 into 16 VGPR quads while K-tile t+2's quads are
+// ds_write_b128 into the free LDS buffer — ~13 issue cycles per piece against 60-180 for an LDS-DMA piece, which
+// one wave per SIMD cannot hide.  Per K-tile:
+//   A(t): MFMAs of k-half 0 (set 0) || reads of tile t's k-half 1 -> set 1;  lgkmcnt(0); barrier
+//   B(t): MFMAs of k-half 1 (set 1) || reads of tile t+1's k-half 0 -> set 0 || ds_write of tile t+2 into the
+//         buffer tile t used || buffer loads of tile t+3
+// (tile t+2's ds_writes are ordered before their readers in B(t+1) by A(t+1)'s lgkmcnt(0) + barrier).
+template <int WM, int WN, int NTERM, bool INITC>
+RF_DEV void quad_mainloop_reg(const EngineArgs& p, char* smem, int m0, int n0, int kbeg, int kend,
+                              f32x4 (&acc)[WM / 16][WN / 16]) {
+    using G = qd::Cfg<WM, WN>;
+    constexpr int TI = G::TI, TJ = G::TJ, PPW = G::PPW, BM = G::BM, BN = G::BN, NPA = G::NPA;
+    static_assert(NTERM == 1 || NTERM == P_F16, "quad loop: single-term operands");
+    constexpr int NR = TI + TJ, NM = TI * TJ;
+    static_assert(PPW <= NR && NM >= NR, "quad interleave: a read and a piece per MFMA group");
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wave >> 1, wc = wave & 1;
+    const int nk = kend - kbeg;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
+
+    if (INITC && kbeg == 0) {
+        load_c_acc<TI, TJ>(p, m0 + wr * WM, n0 + wc * WN, acc);
+    } else {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    // pieces as quad_mainloop's (same LDS image); lane l holds row l >> 2, logical chunk (l & 3) ^ key(row), and
+    // writes it at the piece base + 16 l
+    const int prow = lane >> 2;
+    const int pch = (lane & 3) ^ ((prow >> 1) & 3);
+    const int64_t a_bytes = (int64_t)(p.m - m0) * p.lda * 2;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.a + (int64_t)m0 * p.lda), 0, (int)(a_bytes < 0x7fffffff ? a_bytes : 0x7fffffff), qd::RSRC_CFG);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.w + (int64_t)n0 * p.ldw), 0, (int)((int64_t)min(BN, p.n - n0) * p.ldw * 2), qd::RSRC_CFG);
+    const int va = (prow * (int)p.lda + pch * 8) * 2, vb = (prow * (int)p.ldw + pch * 8) * 2;
+    const int kh_w = wave & 1;
+    u32x4 gq[PPW];
+    auto gload = [&](int kt, int u) {
+        const int kb = (kbeg + kt) * 128 + kh_w * 64;
+        if (u < NPA / 4) {
+            const int rg = (wave >> 1) + 2 * u;
+            gq[u] = __builtin_amdgcn_raw_buffer_load_b128(ra, va, rg * 16 * (int)p.lda * 2 + kb, 0);
+        } else {
+            const int rg = (wave >> 1) + 2 * u - NPA / 2;
+            gq[u] = __builtin_amdgcn_raw_buffer_load_b128(rw, vb, rg * 16 * (int)p.ldw * 2 + kb, 0);
+        }
+    };
+    auto swrite = [&](uint32_t stage, int u) {
+        const uint32_t base = u < NPA / 4 ? kh_w * BM * 64 + ((wave >> 1) + 2 * u) * 1024
+                                          : G::A_IMG + kh_w * BN * 64 + ((wave >> 1) + 2 * u - NPA / 2) * 1024;
+        *LDS_PTR(u32x4, (uintptr_t)(stage + base + lane * 16)) = gq[u];
+    };
+    const int frow = lane & 15, fch = lane >> 4;
+    const uint32_t sw = (uint32_t)((fch ^ ((frow >> 1) & 3)) << 4);
+    const uint32_t a_rd = (uint32_t)((wr * WM + frow) * 64) + sw;
+    const uint32_t b_rd = (uint32_t)(G::A_IMG + (wc * WN + frow) * 64) + sw;
+    bf16x8 fa[2][TI], fb[2][TJ];
+    auto read1 = [&](uint32_t stage, int kh, int s, int r) {
+        if (r < TJ)
+            fb[s][r] = *LDS_PTR(const bf16x8, (uintptr_t)(stage + b_rd + kh * BN * 64 + r * 1024));
+        else
+            fa[s][r - TJ] = *LDS_PTR(const bf16x8, (uintptr_t)(stage + a_rd + kh * BM * 64 + (r - TJ) * 1024));
+    };
+    // one phase: MFMA groups of set s; before group g: read g of the other set (rd), and (st) ds_write of piece g
+    // into wstage then the buffer load of K-tile lkt's piece g (ld)
+    auto phase = [&](int s, uint32_t rstage, int rkh, bool st, uint32_t wstage, bool ld, int lkt) {
+#pragma unroll
+        for (int g = 0; g < NR; ++g) {
+            read1(rstage, rkh, s ^ 1, g);
+            if (g < PPW) {
+                if (st) swrite(wstage, g);
+                if (ld) gload(lkt, g);
+            }
+#pragma unroll
+            for (int m = NM * g / NR; m < NM * (g + 1) / NR; ++m) mfma_agpr<NTERM>(acc[m / TJ][m % TJ], fb[s][m % TJ], fa[s][m / TJ]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+    // prologue: K-tiles 0 and 1 into the two buffers, K-tile 2 in registers
+#pragma unroll
+    for (int u = 0; u < PPW; ++u) gload(0, u);
+#pragma unroll
+    for (int u = 0; u < PPW; ++u) swrite(lds0, u);
+#pragma unroll
+    for (int u = 0; u < PPW; ++u) gload(1, u);
+#pragma unroll
+    for (int u = 0; u < PPW; ++u) swrite(lds0 + G::STAGE, u);
+    if (nk > 2) {
+#pragma unroll
+        for (int u = 0; u < PPW; ++u) gload(2, u);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's ds_writes are done
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < NR; ++r) read1(lds0, 0, 0, r);
+    auto body = [&](const int t, auto par_c) {
+        constexpr int PAR = decltype(par_c)::value;
+        const uint32_t stage = lds0 + PAR * G::STAGE, nstage = lds0 + (PAR ^ 1) * G::STAGE;
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        phase(0, stage, 1, false, 0, false, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's reads of buffer PAR (and B(t-1)'s ds_writes) are done
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        phase(1, nstage, 0, t + 2 < nk, stage, t + 3 < nk, t + 3);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    for (int t = 0; t < nk; t += 2) {
+        body(t, std::integral_constant<int, 0>{});
+        body(t + 1, std::integral_constant<int, 1>{});
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    quad_drain();
+}
+
 // K-tiles 0 and 1 of a quad tile, issued as quad_mainloop's prologue issues them (a persistent block starts the
 // next tile's operand stream before the current tile's epilogue; the next mainloop call then runs with pre = true)
 template <int WM, int WN>
@@ -1395,7 +1520,7 @@ RF_DEV void quad_issue01(const EngineArgs& p, char* smem, int m0, int n0, int nk
 // The quad tile as data-parallel (one tile per block), persistent (p.persist: whole tiles strided over the grid,
 // the next tile's first K-tiles prefetched before the epilogue) or stream-K (partial tiles in the SkLayout
 // forward-progress order, as phased_sk_kernel).
-template <int WM, int WN, int EPI, int NTERM>
+template <int WM, int WN, int EPI, int NTERM, int STG = 0>
 __global__ __launch_bounds__(256, 1) void quad_kernel(EngineArgs p) {
     using G = qd::Cfg<WM, WN>;
     constexpr int TI = G::TI, TJ = G::TJ, BM = G::BM, BN = G::BN, TS = BM * BN;
@@ -1413,6 +1538,12 @@ __global__ __launch_bounds__(256, 1) void quad_kernel(EngineArgs p) {
         for (int tile = wg; tile < ntiles; tile += nwg) {
             int tm, tn;
             tile_coords(tile, tiles_m, tiles_n, p.group_m, tm, tn);
+            if constexpr (STG == 1) {  // register staging: no cross-tile prefetch
+                quad_mainloop_reg<WM, WN, NTERM, EPI == E_ADD>(p, smem, tm * BM, tn * BN, 0, iters, acc);
+                __syncthreads();  // every wave's last LDS reads of this tile are done before the next tile's writes
+                engine_epilogue<G, EPI>(p, tm * BM, tn * BN, acc);
+                continue;
+            }
             quad_mainloop<WM, WN, NTERM, EPI == E_ADD>(p, smem, tm * BM, tn * BN, 0, iters, acc, pre);
             pre = tile + nwg < ntiles;
             if (pre) {
@@ -1450,7 +1581,8 @@ __global__ __launch_bounds__(256, 1) void quad_kernel(EngineArgs p) {
         const int m0 = tm * BM, n0 = tn * BN;
         wait_vm<0>();
         __syncthreads();  // the previous segment's LDS readers are done
-        quad_mainloop<WM, WN, NTERM, EPI == E_ADD>(p, smem, m0, n0, 2 * kf, 2 * kl, acc);
+        if constexpr (STG == 1) quad_mainloop_reg<WM, WN, NTERM, EPI == E_ADD>(p, smem, m0, n0, 2 * kf, 2 * kl, acc);
+        else quad_mainloop<WM, WN, NTERM, EPI == E_ADD>(p, smem, m0, n0, 2 * kf, 2 * kl, acc);
         if (kf != 0) {
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(p.sk_part + (int64_t)L * TS, 0, TS * 4, qd::RSRC_CFG);
@@ -3044,8 +3176,19 @@ static int quad_mode(int m, int n, int k, int64_t lda, int64_t ldw, int epilogue
     return mode;
 }
 
+template <int WM, int WN, int EPI, int NT, int STG>
+static int launch_quad_s(EngineArgs a, int mode, void* workspace, int64_t ws_bytes, void* stream, const char* what);
+
 template <int WM, int WN, int EPI, int NT>
 static int launch_quad(EngineArgs a, int mode, void* workspace, int64_t ws_bytes, void* stream, const char* what) {
+    // RF_GEMM_QUAD_STG: 1 = register staging (default), 0 = LDS-DMA
+    const char* stg_env = getenv("RF_GEMM_QUAD_STG");
+    if (!stg_env || atoi(stg_env) != 0) return launch_quad_s<WM, WN, EPI, NT, 1>(a, mode, workspace, ws_bytes, stream, what);
+    return launch_quad_s<WM, WN, EPI, NT, 0>(a, mode, workspace, ws_bytes, stream, what);
+}
+
+template <int WM, int WN, int EPI, int NT, int STG>
+static int launch_quad_s(EngineArgs a, int mode, void* workspace, int64_t ws_bytes, void* stream, const char* what) {
     using G = qd::Cfg<WM, WN>;
     const int tiles_m = (a.m + G::BM - 1) / G::BM, tiles_n = (a.n + G::BN - 1) / G::BN;
     const int64_t tiles = (int64_t)tiles_m * tiles_n;
@@ -3053,10 +3196,10 @@ static int launch_quad(EngineArgs a, int mode, void* workspace, int64_t ws_bytes
     a.group_m = pick_group_m(tiles_m, tiles_n, G::BM, G::BN, (grid + 7) / 8);
     if (mode == 2 && workspace && ws_bytes >= SK_WS_BYTES) {
         sk_setup(a, workspace, stream);
-        RF_LAUNCH((quad_kernel<WM, WN, EPI, NT>), dim3(256), dim3(256), 0, (hipStream_t)stream, a);
+        RF_LAUNCH((quad_kernel<WM, WN, EPI, NT, STG>), dim3(256), dim3(256), 0, (hipStream_t)stream, a);
     } else {
         a.sk_flag = nullptr;
-        RF_LAUNCH((quad_kernel<WM, WN, EPI, NT>), dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+        RF_LAUNCH((quad_kernel<WM, WN, EPI, NT, STG>), dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
     }
     return rf::check_launch(what);
 }

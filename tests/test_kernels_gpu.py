@@ -132,7 +132,8 @@ def test_gemm_256_tiles(monkeypatch, tile, m, n, k):
 
 F16_TILES = {"auto": None, "256ph": "256", "128x256ph": "1282", "96x256ph3": "964", "64x256ph3": "645",
              "128x256ph3": "1283", "96x256ring": "962", "128ring8wk64": "12884", "128ring": "128", "skph": "skph",
-             "quad": "quad1", "quadsk": "quad2"}
+             "quad": "quad1", "quadsk": "quad2", "quad128x192": "quad1@128x192", "quad160x256sk": "quad2@160x256",
+             "quad128x128": "quad1@128x128"}
 
 
 @pytest.mark.parametrize("tile", list(F16_TILES))
@@ -147,9 +148,13 @@ def test_gemm_f16_operands(monkeypatch, tile, m, n, k):
             pytest.skip("the phased stream-K path needs >= 512 whole 256x256 tiles")
         monkeypatch.setenv("RF_GEMM_SKPH", "1")
     elif (F16_TILES[tile] or "").startswith("quad"):
-        if n % 256 or k % 128:
-            pytest.skip("the 4-wave 256x256 engine needs N % 256 == 0 and K % 128 == 0")
-        monkeypatch.setenv("RF_GEMM_QUAD", F16_TILES[tile][4:])
+        mode, _, qt = F16_TILES[tile][4:].partition("@")
+        bn = int(qt.split("x")[1]) if qt else 256
+        if k % 128 or n % bn:
+            pytest.skip("the 4-wave engine needs K % 128 == 0 (and whole column tiles for the SwiGLU check)")
+        monkeypatch.setenv("RF_GEMM_QUAD", mode)
+        if qt:
+            monkeypatch.setenv("RF_GEMM_QUAD_TILE", qt)
     elif F16_TILES[tile]:
         monkeypatch.setenv("RF_GEMM_TILE", F16_TILES[tile])
     g = torch.Generator(device="cpu").manual_seed(m + 5 * n + k)
@@ -176,13 +181,15 @@ def test_gemm_f16_operands(monkeypatch, tile, m, n, k):
         assert relerr(outs.float(), refs) < tol, dt
 
 
+@pytest.mark.parametrize("stg", ["1", "0"])
 @pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("m,n,k", [(5649, 8192, 1024), (513, 2048, 640), (8192, 512, 2048)])
-def test_gemm_quad_bf16_and_persistent(monkeypatch, mode, m, n, k):
+def test_gemm_quad_bf16_and_persistent(monkeypatch, mode, stg, m, n, k):
     """The 4-wave 256x256 engine (RF_GEMM_QUAD: 1 data-parallel / persistent over whole tiles with the next tile's
     prefetch, 2 stream-K over pairs of K-tiles) on bf16 operands: more tiles than CUs (persistent), ragged rows,
     odd K-pair counts split over blocks; fp32, residual and SwiGLU epilogues vs fp64."""
     monkeypatch.setenv("RF_GEMM_QUAD", mode)
+    monkeypatch.setenv("RF_GEMM_QUAD_STG", stg)  # register staging (default) / LDS-DMA
     ops = _ops()
     g = torch.Generator(device="cpu").manual_seed(m + n + k)
     a = torch.randn(m, k, generator=g).bfloat16().to(dev)

@@ -356,7 +356,9 @@ def quad():
               ("s1 w2", S, D, F, 0), ("s2 w2", R, D, F, 0)]
     if os.environ.get("KB_SHAPES"):
         shapes = [x for x in shapes if x[0] in os.environ["KB_SHAPES"].split(",")]
-    modes = os.environ.get("KB_QUAD", "0,1,2").split(",")
+    # labels: "0" default pick, "1" / "2" quad whole tiles / stream-K with register staging, "1d" / "2d" the same with
+    # LDS-DMA staging; "1@128x192" etc. picks the block tile (RF_GEMM_QUAD_TILE)
+    modes = os.environ.get("KB_QUAD", "0,1,2,1d").split(",")
     for name, m, n, k, sw in shapes:
         per = m * k * 2 + n * k * 2 + m * n * 2
         nrot = max(2, int((768 << 20) // per) + 1)
@@ -375,11 +377,18 @@ def quad():
             ops.gemm(a, w, c, None, ops.EPI_SWIGLU if sw else ops.EPI_BF16)
         fl = 2 * m * n * k
         for md in modes:
-            os.environ["RF_GEMM_QUAD"] = md
+            lab, _, tile = md.partition("@")
+            os.environ["RF_GEMM_QUAD"] = lab.rstrip("d")
+            os.environ["RF_GEMM_QUAD_STG"] = "0" if lab.endswith("d") else "1"
+            if tile:
+                os.environ["RF_GEMM_QUAD_TILE"] = tile
+            else:
+                os.environ.pop("RF_GEMM_QUAD_TILE", None)
             ms = timeit(run, reps=3 * nrot)
             print(f"quad-study {name:7s} {m}x{n}x{k} RF_GEMM_QUAD={md}: {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF "
                   f"({nrot} rotating operand sets{', SwiGLU' if sw else ''})", flush=True)
-        os.environ.pop("RF_GEMM_QUAD", None)
+        for e in ("RF_GEMM_QUAD", "RF_GEMM_QUAD_STG", "RF_GEMM_QUAD_TILE"):
+            os.environ.pop(e, None)
         del sets
         torch.cuda.empty_cache()
 
