@@ -181,15 +181,18 @@ def test_gemm_f16_operands(monkeypatch, tile, m, n, k):
         assert relerr(outs.float(), refs) < tol, dt
 
 
+@pytest.mark.parametrize("tile", ["256x256", "128x192", "160x256"])
 @pytest.mark.parametrize("stg", ["1", "0"])
 @pytest.mark.parametrize("mode", ["1", "2"])
-@pytest.mark.parametrize("m,n,k", [(5649, 8192, 1024), (513, 2048, 640), (8192, 512, 2048)])
-def test_gemm_quad_bf16_and_persistent(monkeypatch, mode, stg, m, n, k):
-    """The 4-wave 256x256 engine (RF_GEMM_QUAD: 1 data-parallel / persistent over whole tiles with the next tile's
-    prefetch, 2 stream-K over pairs of K-tiles) on bf16 operands: more tiles than CUs (persistent), ragged rows,
-    odd K-pair counts split over blocks; fp32, residual and SwiGLU epilogues vs fp64."""
+@pytest.mark.parametrize("m,n,k", [(5649, 8192, 1024), (513, 2048, 640), (8192, 512, 2048), (777, 1024, 384)])
+def test_gemm_quad_bf16_and_persistent(monkeypatch, tile, mode, stg, m, n, k):
+    """The 4-wave engine (RF_GEMM_QUAD: 1 data-parallel / persistent over whole tiles, 2 stream-K over pairs of
+    K-tiles; register or LDS-DMA staging; 256x256 / 128x192 / 160x256 tiles) on bf16 operands: more tiles than CUs
+    (persistent), ragged rows and ragged column tiles, odd K-pair counts split over blocks; fp32, residual and
+    SwiGLU epilogues vs fp64 (SwiGLU with a ragged column tile runs on the default engine)."""
     monkeypatch.setenv("RF_GEMM_QUAD", mode)
     monkeypatch.setenv("RF_GEMM_QUAD_STG", stg)  # register staging (default) / LDS-DMA
+    monkeypatch.setenv("RF_GEMM_QUAD_TILE", tile)  # 128x192: a ragged last column tile when 192 does not divide N
     ops = _ops()
     g = torch.Generator(device="cpu").manual_seed(m + n + k)
     a = torch.randn(m, k, generator=g).bfloat16().to(dev)
