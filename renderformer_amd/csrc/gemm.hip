@@ -1208,12 +1208,6 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
 // with the LDS reads and DMA pieces spread between the MFMAs (sched_group_barrier).  One barrier per K-tile; a
 // DMA lands under one K-tile of MFMAs.  The DMA is buffer_load ... lds: one per-lane VGPR offset per operand and
 // each piece's row offset in an SGPR (no 64-bit address VALU per piece); rows past M read as zeros.
-#ifndef RF_QUAD_EXP
-#define RF_QUAD_EXP 0
-#endif
-#ifndef RF_QUAD_WEAVE
-#define RF_QUAD_WEAVE 1  // (build experiments: 0 leaves the phase interleave to the compiler)
-#endif
 namespace qd {
 template <int WM, int WN>
 struct Cfg {
@@ -1552,17 +1546,10 @@ __global__ __launch_bounds__(256, 1) void quad_kernel(EngineArgs p) {
                 __syncthreads();  // every wave's last LDS reads of this tile are done
                 quad_issue01<WM, WN>(p, smem, tm2 * BM, tn2 * BN, iters);
             }
-#if RF_QUAD_EXP == 2
-            if (threadIdx.x == 1000) { float s = 0; for (int i = 0; i < TI; ++i) for (int j = 0; j < TJ; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3]; ((float*)p.c)[0] = s; }
-#else
             engine_epilogue<G, EPI>(p, tm * BM, tn * BN, acc);
-#endif
         }
         return;
     }
-#if RF_QUAD_EXP
-    return;
-#endif
     // stream-K over partial tiles (sk_flag set by the host: sk_setup)
     const int64_t ntiles64 = ntiles;
     const SkLayout lay(nwg, ntiles64);
