@@ -1925,6 +1925,13 @@ __global__ __launch_bounds__(C::THREADS, C::BM == 256 ? 1 : 2) void halo_kernel(
 // last tap also the next chunk's halo (issued before that W slice).
 namespace h2 {
 constexpr int TH = 16, TW = 32, HWID = TW + 2, HPIX = (TH + 2) * HWID;  // 612 halo pixels
+// The halo's 16-B chunk XOR key, a function of the halo column hx only (one halo row down is then a constant
+// HWID * 64 bytes for every lane).  A fragment read (ds_read_b128: pixel = lane & 15, chunk = lane >> 4) is served
+// in four 16-lane groups, each mixing 8 lanes of one chunk over pixels {0-3, 12-15} with 8 lanes of the next chunk
+// over pixels 4-11; the key must give those 16 lanes 16 distinct bank quads for every tap shift (0-2) of the column.
+// ((hx >> 2) & 3), used through round 4, made every such read 2-way conflicted (SQ_LDS_BANK_CONFLICT = half of
+// SQ_LDS_IDX_ACTIVE, profiles/r4_halo_lds.txt); ((hx >> 1) & 2) is conflict-free for all shifts (tools/halo_key.py).
+RF_DEV constexpr int hkey(int hx) { return (hx >> 1) & 2; }
 constexpr int PIECES = 40, PPW = PIECES / 8;                            // 1-KiB pieces per buffer, per wave
 constexpr int HBYTES = PIECES * 1024;                                   // 640 pixel slots x 64 B
 static_assert(PIECES * 16 >= HPIX, "halo buffer");
@@ -1991,16 +1998,15 @@ RF_DEV void halo2_mainloop(const EngineArgs& p, char* smem, int img, int y0, int
     char* wring = smem + 2 * HBYTES;      // S W stages
 
     // halo staging: piece wave + 8 t of a buffer holds halo pixels 16 (wave + 8 t) .. + 15 (64 B each, 16-B chunk
-    // XOR hkey(column) = ((hp mod HWID) >> 2) & 3: a function of the halo column only, so one halo row down is a
-    // constant HWID * 64 bytes for every lane and a tap's fragment address is a per-(column half, tap column)
-    // register plus an immediate (no per-tap address VALU); any 16 consecutive columns of a row still cover the
-    // 16 (pixel mod 4, chunk) bank groups once, so the fragment reads stay conflict-free).  Pixels past the
+    // XOR h2::hkey(column): a function of the halo column only, so one halo row down is a constant HWID * 64 bytes
+    // for every lane and a tap's fragment address is a per-(column half, tap column) register plus an immediate
+    // (no per-tap address VALU); the fragment reads are conflict-free for every tap shift).  Pixels past the
     // image or past the 612 in use read the zero row
     int hpix[PPW], hch[PPW];
 #pragma unroll
     for (int t = 0; t < PPW; ++t) {
         const int hp = (wave + 8 * t) * 16 + (lane >> 2);
-        hch[t] = (lane & 3) ^ (((hp % HWID) >> 2) & 3);
+        hch[t] = (lane & 3) ^ h2::hkey(hp % HWID);
         int pix = -1;
         if (hp < HPIX) {
             const int hy = hp / HWID, hx = hp - hy * HWID;
@@ -2040,7 +2046,7 @@ RF_DEV void halo2_mainloop(const EngineArgs& p, char* smem, int img, int y0, int
         for (int tx = 0; tx < 3; ++tx) {
             const int hx = 16 * h + frow + tx;
             hadr[h][tx] = (uint32_t)(uintptr_t)LDS_PTR(char, hbuf) + ((G::RW * wm) * HWID + hx) * 64 +
-                          ((fch ^ ((hx >> 2) & 3)) << 4);
+                          ((fch ^ h2::hkey(hx)) << 4);
         }
     bf16x8 fa[TI], fb[4];
     auto read_a = [&](int tap) {
@@ -2144,6 +2150,162 @@ __global__ __launch_bounds__(512, 1) void halo2_kernel(EngineArgs p) {
 }
 
 // ---------------------------------------------------------------------------------------------------
+// halo3: halo2's block (16 x 32 pixels x 128 output channels, 8 waves, the same halo image and double buffer) with
+// the filter bank read straight from L2 into registers instead of through an LDS ring.  halo2 needed two barriers
+// per (chunk, tap) step because the W slice of each step was a shared LDS stage; its ablations showed the
+// load / sync skeleton taking half the kernel (58.5 of 114.6 us).  Here the only shared LDS data is
+// the halo, so a whole 32-channel chunk (9 taps, 288 MFMAs per wave) runs between two barriers, and the two waves
+// of a SIMD interleave freely.  Waves are 2 (rows) x 4 (channels): each owns 8 tile rows (16 pixel fragments) x 32
+// channels (2 W fragments), so per tap a wave reads 16 A fragments from LDS (128 KiB per CU per tap: half the LDS
+// array's rate at the MFMA's) and 2 W fragments (2 KiB) from the L2-resident bank through a 3-deep register ring,
+// two taps ahead.  The bank (9 cin x 128 x 2 B per block, 0.6 MB at cin 256) is read 2x per block from L2.
+namespace h3 {
+constexpr int WGN = 4, WGM = 2, RW = h2::TH / WGM, TI = 2 * RW, TJ = 2;  // 8 rows x 32 pixels x 32 channels per wave
+constexpr int LDS = 2 * h2::HBYTES;                                     // two halo buffers (80 KiB)
+}  // namespace h3
+struct H3Tile {  // the epilogue's view of the block
+    static constexpr int WGN = h3::WGN, WGM = h3::WGM, MW = 512 / h3::WGM, NWD = 128 / h3::WGN, TI = h3::TI,
+                         TJ = h3::TJ;
+};
+
+// DBG (ablation timing only, wrong results): 1 = no MFMAs, 2 = no W loads in the loop, 4 = no halo DMA in the loop,
+// 8 = no chunk-end wait + barrier
+template <int DBG = 0>
+__global__ __launch_bounds__(512, 1) void halo3_kernel(EngineArgs p) {
+    using namespace h2;
+    __shared__ __attribute__((aligned(16))) char smem[h3::LDS];
+    constexpr int TI = h3::TI;
+    // XCD-contiguous tile ids as halo2 (the channel tiles of one pixel tile and neighbouring pixel tiles share an L2)
+    const int nwg = gridDim.x, hw = blockIdx.x;
+    const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
+    const int tiles_n = p.n / 128, tx_n = p.wo / TW, ty_n = p.ho / TH;
+    const int tn = wg % tiles_n, pt = wg / tiles_n;
+    const int tx = pt % tx_n, rest = pt / tx_n;
+    const int ty = rest % ty_n, img = rest / ty_n;
+    const int y0 = ty * TH, x0 = tx * TW, n0 = tn * 128;
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave / h3::WGN, wn = wave % h3::WGN;
+    const int nch = p.cin_pad / 32, nk = 9 * nch;
+    char* hbuf = smem;
+
+    // halo staging exactly as halo2 (piece wave + 8 t of a buffer = halo pixels 16 (wave + 8 t) .. + 15)
+    int hpix[PPW], hch[PPW];
+#pragma unroll
+    for (int t = 0; t < PPW; ++t) {
+        const int hp = (wave + 8 * t) * 16 + (lane >> 2);
+        hch[t] = (lane & 3) ^ h2::hkey(hp % HWID);
+        int pix = -1;
+        if (hp < HPIX) {
+            const int hy = hp / HWID, hx = hp - hy * HWID;
+            const int iy = y0 + hy - 1, ix = x0 + hx - 1;
+            if (iy >= 0 && iy < p.hi && ix >= 0 && ix < p.wi) pix = (img * p.hi + iy) * p.wi + ix;
+        }
+        hpix[t] = pix;
+    }
+    // The halo pieces are issued by inline asm: with the builtin, hipcc counts the LDS-DMA as a second kind of
+    // vector-memory event and, unable to order it against the W loads, waits vmcnt(0) at every third tap (the
+    // W ring's prefetch then never overlaps).  Hidden from it, its vmcnt for a W slot also covers the (older) halo
+    // pieces issued between, which only waits for what landed long ago; the chunk-end wait publishes the halo.
+    // M0 is clobbered: every M0 use in this kernel is one of these statements.
+    const uint32_t hbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(char, hbuf) + wave * 1024);
+    auto issue_halo = [&](int chunk, int buf, int t) {
+        const bf16_t* src = hpix[t] >= 0 ? p.a + (int64_t)hpix[t] * p.cin_pad + hch[t] * 8 + chunk * 32 : p.zero;
+        const uint32_t lds = hbase + buf * HBYTES + t * 8 * 1024;
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds)
+                     : "memory", "m0");
+    };
+
+    const int frow = lane & 15, fch = lane >> 4;
+    // W fragment j of this wave: filter rows n0 + 32 wn + 16 j + frow, K = tap * cin_pad + 32 chunk + 8 fch .. + 7
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.w + (int64_t)n0 * p.ldw), 0, (int)((int64_t)128 * p.ldw * 2), qd::RSRC_CFG);
+    const int wv0 = ((wn * 32 + frow) * (int)p.ldw + fch * 8) * 2, wv1 = wv0 + 16 * (int)p.ldw * 2;
+    u32x4 fb[3][2];  // ring slot kt % 3 (9 taps per chunk: the slot of a tap does not depend on its chunk)
+    auto load_b = [&](int kt, int slot) {
+        const int chunk = kt / 9, tap = kt - 9 * chunk;
+        const int so = (tap * p.cin_pad + chunk * 32) * 2;
+        fb[slot][0] = __builtin_amdgcn_raw_buffer_load_b128(rw, wv0, so, 0);
+        fb[slot][1] = __builtin_amdgcn_raw_buffer_load_b128(rw, wv1, so, 0);
+    };
+
+    f32x4 acc[TI][2];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // LDS byte address of fragment i's lane pixel at tap (ty, tx): tile row RW wm + i / 2 + ty, halo column
+    // 16 (i & 1) + frow + tx (halo2's register + immediate form)
+    uint32_t hadr[2][3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int tx3 = 0; tx3 < 3; ++tx3) {
+            const int hx = 16 * h + frow + tx3;
+            hadr[h][tx3] = (uint32_t)(uintptr_t)LDS_PTR(char, hbuf) + ((h3::RW * wm) * HWID + hx) * 64 +
+                           ((fch ^ h2::hkey(hx)) << 4);
+        }
+
+    // prologue: chunk 0's halo and W(0), W(1)
+#pragma unroll
+    for (int t = 0; t < PPW; ++t) issue_halo(0, 0, t);
+    load_b(0, 0);
+    load_b(min(1, nk - 1), 1);
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+
+    for (int c = 0; c < nch; ++c) {
+        const bool last = c + 1 == nch;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int kt = 9 * c + t;
+            bf16x8 fa[TI];
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+                fa[i] = *LDS_PTR(const bf16x8, (uintptr_t)(hadr[i & 1][t % 3] + ((i >> 1) + t / 3) * HWID * 64));
+            // branch-free issue (a conditional load makes hipcc's vmcnt accounting fall back to vmcnt(0) at the
+            // ring slot's next use): the last chunk re-stages its own halo into the idle buffer and the last two
+            // taps re-load the last W slice
+            if (!(DBG & 4) && t < PPW) issue_halo(last ? c : c + 1, (c + 1) & 1, t);
+            if (!(DBG & 2)) load_b(min(kt + 2, nk - 1), (t + 2) % 3);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if constexpr (DBG & 1) {
+                        acc[i][j][0] += __builtin_bit_cast(float, fb[t % 3][j][0]) * (float)fa[i][0];
+                    } else {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[t % 3][j]),
+                                                                           __builtin_bit_cast(f16x8, fa[i]), acc[i][j], 0, 0, 0);
+                    }
+                }
+            __builtin_amdgcn_s_setprio(0);
+        }
+        if (!(DBG & 8) && !last) {
+            // the next chunk's halo (and the W loads behind it) landed, and every wave is done reading this chunk's
+            // buffer, which the chunk after next overwrites
+            wait_vm<0>();
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t step = (c & 1) ? (uint32_t)-HBYTES : (uint32_t)HBYTES;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int tx3 = 0; tx3 < 3; ++tx3) hadr[h][tx3] += step;
+        }
+    }
+    wait_vm<0>();  // the last chunk's re-staged halo pieces land before the block's LDS is released
+    engine_epilogue<H3Tile, E_CONV, TW, false>(p, (img * p.ho + y0) * p.wo + x0, n0, acc);
+}
+
+// ---------------------------------------------------------------------------------------------------
 // The DPT's last 3x3 convolution (output_conv2, dpt.py:234-240: <= 32 filters, fp16) with its fused head
 // (SiLU -> 1x1 to n_fin -> ELU -> 10^x - 1).  The halo2 kernel pads the 32-filter bank to a 64-wide tile (half
 // its MFMAs multiply zeros) and runs 16 MFMAs per barrier-delimited section, which left it bound by its section
@@ -2181,7 +2343,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c32_kernel(EngineArgs p) {
 #pragma unroll
     for (int t = 0; t < HPW; ++t) {
         const int hp = (wave + NWAVE * t) * 16 + (lane >> 2);
-        hch[t] = (lane & 3) ^ (((hp % HWID) >> 2) & 3);
+        hch[t] = (lane & 3) ^ h2::hkey(hp % HWID);
         int pix = -1;
         if (hp < HPIX) {
             const int hy = hp / HWID, hx = hp - hy * HWID;
@@ -2222,7 +2384,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c32_kernel(EngineArgs p) {
         for (int t = 0; t < 3; ++t) {
             const int hx = 16 * h + frow + t;
             hadr[h][t] = (uint32_t)(uintptr_t)LDS_PTR(char, smem) + ((4 * wave) * HWID + hx) * 64 +
-                         ((fch ^ ((hx >> 2) & 3)) << 4);
+                         ((fch ^ h2::hkey(hx)) << 4);
         }
     const uint32_t wadr = (uint32_t)(uintptr_t)LDS_PTR(char, smem) + HBYTES + lds_off(frow, fch);
 
@@ -2360,7 +2522,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_hk_kernel(EngineArgs p) {
 #pragma unroll
     for (int t = 0; t < HPW; ++t) {
         const int hp = (wave + NWAVE * t) * 16 + (lane >> 2);
-        hch[t] = (lane & 3) ^ (((hp % HWID) >> 2) & 3);
+        hch[t] = (lane & 3) ^ h2::hkey(hp % HWID);
         int pix = -1;
         if (hp < HPIX) {
             const int hy = hp / HWID, hx = hp - hy * HWID;
@@ -2405,7 +2567,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_hk_kernel(EngineArgs p) {
         for (int t = 0; t < 3; ++t) {
             const int hx = 16 * h + frow + t;
             hadr[h][t] = (uint32_t)(uintptr_t)LDS_PTR(char, smem) + ((4 * wave) * HWID + hx) * 64 +
-                         ((fch ^ ((hx >> 2) & 3)) << 4);
+                         ((fch ^ h2::hkey(hx)) << 4);
         }
     const uint32_t wadr = (uint32_t)(uintptr_t)LDS_PTR(char, smem) + HBYTES + lds_off(frow, fch);
 
@@ -3168,9 +3330,11 @@ static int launch_quad_s(EngineArgs a, int mode, void* workspace, int64_t ws_byt
 
 template <int WM, int WN, int EPI, int NT>
 static int launch_quad(EngineArgs a, int mode, void* workspace, int64_t ws_bytes, void* stream, const char* what) {
-    // RF_GEMM_QUAD_STG: 1 = register staging (default), 0 = LDS-DMA
+    // RF_GEMM_QUAD_STG: 0 = LDS-DMA (default), 1 = register staging.  Measured (profiles/r4_quad_reg_study.txt):
+    // staging a 64-deep K-tile through registers costs 64 VGPRs a lane at 256x256, which the 256 accumulator
+    // AGPRs leave no room for; the loop spills and runs 2-3x slower than the DMA form.
     const char* stg_env = getenv("RF_GEMM_QUAD_STG");
-    if (!stg_env || atoi(stg_env) != 0) return launch_quad_s<WM, WN, EPI, NT, 1>(a, mode, workspace, ws_bytes, stream, what);
+    if (stg_env && atoi(stg_env) == 1) return launch_quad_s<WM, WN, EPI, NT, 1>(a, mode, workspace, ws_bytes, stream, what);
     return launch_quad_s<WM, WN, EPI, NT, 0>(a, mode, workspace, ws_bytes, stream, what);
 }
 
@@ -3422,6 +3586,28 @@ static int launch_halo2(EngineArgs a, void* stream, const char* what) {
     return rf::check_launch(what);
 }
 
+// halo3_kernel serves halo2's non-final convolutions with a multiple of 128 output channels (RF_CONV_HALO3=0:
+// halo2 instead); the bank must be addressable by 32-bit buffer offsets
+static bool halo3_ok(const EngineArgs& a) {
+    const char* env = getenv("RF_CONV_HALO3");
+    if ((env && atoi(env) == 0) || (a.flags & RF_CONV_FINAL) || a.n % 128 || a.deconv) return false;
+    if ((int64_t)128 * a.ldw * 2 >= 0x7fffffff) return false;
+    return halo2_ok(a);
+}
+
+static int launch_halo3(EngineArgs a, void* stream, const char* what) {
+    const int nwg = (a.m / 512) * (a.n / 128);
+    const int dbg = getenv("RF_H3_DBG") ? atoi(getenv("RF_H3_DBG")) : 0;  // ablation timing only
+    if (dbg == 1) RF_LAUNCH(halo3_kernel<1>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    else if (dbg == 2) RF_LAUNCH(halo3_kernel<2>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    else if (dbg == 4) RF_LAUNCH(halo3_kernel<4>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    else if (dbg == 6) RF_LAUNCH(halo3_kernel<6>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    else if (dbg == 8) RF_LAUNCH(halo3_kernel<8>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    else if (dbg == 14) RF_LAUNCH(halo3_kernel<14>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    else RF_LAUNCH(halo3_kernel<0>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    return rf::check_launch(what);
+}
+
 // conv3x3_c32_kernel serves the fused-head 3x3 convolution with <= 32 filters (output_conv2) on whole 16 x 32
 // tiles (RF_CONV_C32=0: the halo2 / engine paths instead)
 static bool c32_ok(const EngineArgs& a) {
@@ -3461,6 +3647,7 @@ template <bool GATHER>
 static int conv_f16_dp(EngineArgs& p, void* stream, const char* what, int tile = 0) {
     if (GATHER && c32_ok(p)) return launch_c32(p, stream, what);
     if (GATHER && hk_ok(p)) return launch_hk(p, stream, what);
+    if (GATHER && halo3_ok(p)) return launch_halo3(p, stream, what);
     if (GATHER && halo2_ok(p)) return launch_halo2(p, stream, what);
     const char* env = getenv("RF_CONV_TILE");
     const int t = tile ? tile : env ? atoi(env) : 0;

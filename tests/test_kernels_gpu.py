@@ -973,6 +973,7 @@ def test_conv_halo2(cin, cout, hh, ww, n_img, h2s, monkeypatch):
     128-channel block (1 or 2 channel tiles) and the 64-channel block (32 and 64 output channels), fused
     bias + 2 residuals + SiLU fp16 planes with a padded row stride."""
     monkeypatch.setenv("RF_CONV_HALO2", "1")
+    monkeypatch.setenv("RF_CONV_HALO3", "0")
     monkeypatch.setenv("RF_CONV_HK", "0")
     monkeypatch.setenv("RF_CONV_H2S", h2s)
     from renderformer_amd.dpt import _Conv, split_planes
@@ -995,6 +996,41 @@ def test_conv_halo2(cin, cout, hh, ww, n_img, h2s, monkeypatch):
     out2, _ = conv(split_planes(xn, conv.cin_pad, f16=True), out_f32=True)
     ref2 = F.conv2d(_q(x, "f16"), _q(w, "f16"), b.double(), padding=1).permute(0, 2, 3, 1)
     assert relerr(out2.cpu(), ref2) < 2e-5
+
+
+@pytest.mark.parametrize("cin,cout,hh,ww,n_img", [(256, 128, 32, 64, 2), (128, 256, 48, 32, 1), (32, 128, 16, 32, 3),
+                                                  (96, 128, 16, 96, 1), (256, 256, 64, 64, 1), (64, 384, 16, 32, 1),
+                                                  (512, 128, 16, 32, 1)])
+def test_conv_halo3(cin, cout, hh, ww, n_img, monkeypatch):
+    """halo3_kernel (the default for the 512^2 / 256^2 DPT convs with a multiple of 128 filters: the bank read from L2
+    into a register ring, one barrier per 32-channel chunk): 1 to 16 channel chunks (the last chunk re-stages its own
+    halo and the last taps re-load the last W slice), several images, tiles along both axes, 1 to 3 channel tiles,
+    fused bias + 2 residuals + SiLU fp16 planes with a padded row stride, and the plain fp32 output; against fp64 on
+    the same fp16 operands and against halo2 (same products, fp32 summation order)."""
+    monkeypatch.setenv("RF_CONV_HALO2", "1")
+    monkeypatch.setenv("RF_CONV_HALO3", "1")
+    from renderformer_amd.dpt import _Conv, split_planes
+    g = torch.Generator(device="cpu").manual_seed(cin * hh + cout + ww + 11)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(cin * 9)
+    b = torch.randn(cout, generator=g)
+    x = torch.randn(n_img, cin, hh, ww, generator=g)
+    conv = _Conv(w, b, dev, f16=True)
+    xn = x.permute(0, 2, 3, 1).contiguous().to(dev)
+    r1 = torch.randn(n_img, hh, ww, cout, generator=g)
+    r2 = torch.randn(n_img, hh, ww, cout, generator=g)
+    out, pl = conv(split_planes(xn, conv.cin_pad, silu=True, f16=True), res1=r1.to(dev), res2=r2.to(dev),
+                   out_f32=True, planes_ld=cout + 32, planes_silu=True)
+    sx = _q(F.silu(x.double()).float(), "f16")
+    ref = F.conv2d(sx, _q(w, "f16"), b.double(), padding=1).permute(0, 2, 3, 1) + r1 + r2
+    assert relerr(out.cpu(), ref) < 2e-5
+    assert relerr(_planes_value(pl)[..., :cout].cpu(), F.silu(ref)) < 1e-3
+    assert (pl.hi[..., cout:] == 0).all()
+    out2, _ = conv(split_planes(xn, conv.cin_pad, f16=True), out_f32=True)
+    ref2 = F.conv2d(_q(x, "f16"), _q(w, "f16"), b.double(), padding=1).permute(0, 2, 3, 1)
+    assert relerr(out2.cpu(), ref2) < 2e-5
+    monkeypatch.setenv("RF_CONV_HALO3", "0")  # halo2 on the same operands
+    out3, _ = conv(split_planes(xn, conv.cin_pad, f16=True), out_f32=True)
+    assert relerr(out3.cpu(), out2.cpu().double()) < 1e-6
 
 
 @pytest.mark.parametrize("cin,cout,hh,ww,n_img", [(256, 128, 32, 64, 2), (128, 256, 48, 32, 1), (32, 64, 16, 32, 3),
@@ -1027,6 +1063,7 @@ def test_conv_hk(cin, cout, hh, ww, n_img, monkeypatch):
     if cout % 128 == 0:  # the halo2 kernel on the same operands
         monkeypatch.setenv("RF_CONV_HK", "0")
         monkeypatch.setenv("RF_CONV_HALO2", "1")
+        monkeypatch.setenv("RF_CONV_HALO3", "0")
         out3, _ = conv(split_planes(xn, conv.cin_pad, f16=True), out_f32=True)
         assert relerr(out3.cpu(), out2.cpu().double()) < 1e-6
 
@@ -1144,13 +1181,15 @@ def test_conv_group_matches_single_launches():
         conv_group([dict(conv=c2, x=planes(64, 9))])  # input planes of the wrong width
 
 
-@pytest.mark.parametrize("hw,halo2,hk", [(24, "0", "0"), (64, "1", "0"), (64, "0", "1")])
-def test_conv_border_bias(hw, halo2, hk, monkeypatch):
-    """RF_CONV_BORDER_BIAS: per-pixel bias row by border class (3 ry + rx), on the engine tile, the halo2 kernel and
-    the hk kernel (the folded output_conv1), vs torch conv + the class bias."""
+@pytest.mark.parametrize("hw,halo2,hk,halo3", [(24, "0", "0", "0"), (64, "1", "0", "0"), (64, "0", "1", "0"),
+                                               (64, "1", "0", "1")])
+def test_conv_border_bias(hw, halo2, hk, halo3, monkeypatch):
+    """RF_CONV_BORDER_BIAS: per-pixel bias row by border class (3 ry + rx), on the engine tile, the halo2, hk and
+    halo3 kernels (the folded output_conv1), vs torch conv + the class bias."""
     from renderformer_amd.dpt import _Conv, split_planes
     monkeypatch.setenv("RF_CONV_HALO2", halo2)
     monkeypatch.setenv("RF_CONV_HK", hk)
+    monkeypatch.setenv("RF_CONV_HALO3", halo3)
     g = torch.Generator(device="cpu").manual_seed(hw)
     cin, cout = 64, 128
     w = torch.randn(cout, cin, 3, 3, generator=g) / 24

@@ -194,11 +194,13 @@ def conv():
                 os.environ["RF_CONV_PHASED"] = "1" if t == "256ph" else "0"
                 os.environ["RF_CONV_SKW8"] = "0" if t == "auto4w" else "1"
                 # h2 / h2s3 / h2s5: the 16 x 32-pixel halo kernel (4- / 3- / 5-deep W ring); other labels run without it
-                os.environ["RF_CONV_HALO2"] = "1" if t.startswith("h2") else "0"
+                os.environ["RF_CONV_HALO2"] = "1" if t.startswith("h2") or t.startswith("h3") else "0"
+                os.environ["RF_CONV_HALO3"] = "1" if t.startswith("h3") else "0"  # h3: halo3_kernel (W from L2)
+                os.environ["RF_H3_DBG"] = t[4:] if t.startswith("h3db") else "0"  # h3db1/2/4/8: ablations
                 os.environ["RF_CONV_H2S"] = t[4:] if t.startswith("h2s") else "4"
                 os.environ["RF_H2_DBG"] = t[4:] if t.startswith("h2db") else "0"  # h2db1/2/3: ablations
                 os.environ["RF_CONV_HK"] = "1" if t == "hk" else "0"  # hk: conv3x3_hk_kernel (4 waves, one barrier per chunk)
-                if not t.startswith("auto") and not t.startswith("h2") and t != "hk":
+                if not t.startswith("auto") and not t.startswith("h2") and t != "hk" and not t.startswith("h3"):
                     os.environ["RF_CONV_TILE"] = t.replace("ph", "")
                 ms = timeit(lambda: conv(x, out_f32=True), reps=10)
                 os.environ.pop("RF_CONV_TILE", None)
