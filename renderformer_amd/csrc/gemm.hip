@@ -492,10 +492,30 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
         const int kk = p.deconv;
         const int nreal = kk ? p.cout * kk * kk : p.cout;
         const bool border = (p.flags & RF_CONV_BORDER_BIAS) && !kk;
+        // Every load of this epilogue is issued before the stores it could wait behind: vmcnt counts loads and
+        // stores together in issue order, so a load issued after a fragment's stores (the bias re-read per
+        // fragment, since hipcc could not prove it does not alias the output) made each fragment wait for the
+        // previous fragment's stores to be acknowledged — 34 of a 256^2 conv's 92 us.  The bias of
+        // the plain case is loop-invariant and read once; the per-pixel operands of fragment i + 1 (residuals,
+        // border-class bias row) are read before fragment i is stored.
+        float* __restrict__ outp = reinterpret_cast<float*>(p.c);
+        const float* __restrict__ res1 = p.res1;
+        const float* __restrict__ res2 = p.res2;
+        const float* __restrict__ bias = p.bias;
+        struct PixOp {
+            float4 r1[TJ], r2[TJ], b[TJ];
+            int64_t pix[TJ];
+            int co[TJ];
+        };
+        float4 bconst[TJ];
 #pragma unroll
-        for (int i = 0; i < TI; ++i) {
+        for (int j = 0; j < TJ; ++j) {
+            const int col = cbase + j * 16 + cq;
+            bconst[j] = float4{0.f, 0.f, 0.f, 0.f};
+            if (bias && !border && !kk && col < nreal) bconst[j] = *reinterpret_cast<const float4*>(bias + col);
+        }
+        auto fetch = [&](int i, PixOp& o) {
             const int m = frow(i);
-            if (m >= p.m) continue;
             int img = 0, y = 0, x = 0;
             if (kk || border) {
                 x = m % p.wo;
@@ -504,12 +524,9 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                 img = t / p.ho;
             }
             // RF_CONV_BORDER_BIAS: bias row 3 ry + rx of the pixel's border class (rf.h)
-            const float* brow = p.bias;
+            const float* brow = bias;
             if (border && brow)
                 brow += (3 * (y == 0 ? 0 : y == p.ho - 1 ? 2 : 1) + (x == 0 ? 0 : x == p.wo - 1 ? 2 : 1)) * p.cout;
-            float4 r1[TJ], r2[TJ];
-            int64_t pixv[TJ];
-            int cov[TJ];
 #pragma unroll
             for (int j = 0; j < TJ; ++j) {
                 const int col = cbase + j * 16 + cq;
@@ -520,33 +537,48 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                     co = col - tap * p.cout;
                     pix = ((int64_t)img * p.ho * kk + y * kk + dy) * (p.wo * kk) + x * kk + dx;
                 }
-                pixv[j] = pix;
-                cov[j] = co;
-                r1[j] = float4{0.f, 0.f, 0.f, 0.f};
-                r2[j] = float4{0.f, 0.f, 0.f, 0.f};
-                if (col < nreal) {
-                    if (p.res1) r1[j] = *reinterpret_cast<const float4*>(p.res1 + pix * p.cout + co);
-                    if (p.res2) r2[j] = *reinterpret_cast<const float4*>(p.res2 + pix * p.cout + co);
+                o.pix[j] = pix;
+                o.co[j] = co;
+                o.r1[j] = float4{0.f, 0.f, 0.f, 0.f};
+                o.r2[j] = float4{0.f, 0.f, 0.f, 0.f};
+                o.b[j] = bconst[j];
+                if (m < p.m && col < nreal) {
+                    if (res1) o.r1[j] = *reinterpret_cast<const float4*>(res1 + pix * p.cout + co);
+                    if (res2) o.r2[j] = *reinterpret_cast<const float4*>(res2 + pix * p.cout + co);
+                    if (brow && (border || kk)) o.b[j] = *reinterpret_cast<const float4*>(brow + co);
                 }
             }
+        };
+        // (4-fragment-wide tiles (TJ = 4) fetch a fragment's operands at its own turn: double-buffered they spill)
+        constexpr bool PF = TJ <= 2;
+        PixOp ops[PF ? 2 : 1];
+        if constexpr (PF) fetch(0, ops[0]);
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+            if constexpr (PF) {
+                if (i + 1 < TI) fetch(i + 1, ops[(i + 1) & 1]);
+            } else {
+                fetch(i, ops[0]);
+            }
+            const PixOp& o = ops[PF ? (i & 1) : 0];
+            if (frow(i) >= p.m) continue;
 #pragma unroll
             for (int j = 0; j < TJ; ++j) {
                 const int col = cbase + j * 16 + cq;
                 if (col >= nreal) continue;
-                const int64_t pix = pixv[j];
-                const int co = cov[j];
+                const int64_t pix = o.pix[j];
+                const int co = o.co[j];
+                const float bb[4] = {o.b[j].x, o.b[j].y, o.b[j].z, o.b[j].w};
+                const float rr1[4] = {o.r1[j].x, o.r1[j].y, o.r1[j].z, o.r1[j].w};
+                const float rr2[4] = {o.r2[j].x, o.r2[j].y, o.r2[j].z, o.r2[j].w};
                 float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-                const float rr1[4] = {r1[j].x, r1[j].y, r1[j].z, r1[j].w};
-                const float rr2[4] = {r2[j].x, r2[j].y, r2[j].z, r2[j].w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    if (brow) v[e] += brow[co + e];
-                    v[e] = (v[e] + rr1[e]) + rr2[e];
+                    v[e] = ((v[e] + bb[e]) + rr1[e]) + rr2[e];
                     if (p.flags & RF_CONV_SILU_OUT) v[e] = silu(v[e]);
                 }
-                if (p.c)
-                    *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + pix * p.cout + co) =
-                        make_float4(v[0], v[1], v[2], v[3]);
+                if (outp)
+                    *reinterpret_cast<float4*>(outp + pix * p.cout + co) = make_float4(v[0], v[1], v[2], v[3]);
                 if (p.p_hi && p.plane_f16) {
                     float a[4] = {v[0], v[1], v[2], v[3]};
                     if (p.flags & RF_CONV_PLANE_SILU) {
@@ -2258,15 +2290,20 @@ __global__ __launch_bounds__(512, 1) void halo3_kernel(EngineArgs p) {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
 
-    for (int c = 0; c < nch; ++c) {
+    for (int c = 0; c < ((DBG & 32) ? 0 : nch); ++c) {  // DBG 32 (ablation): prologue + epilogue only
         const bool last = c + 1 == nch;
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const int kt = 9 * c + t;
             bf16x8 fa[TI];
 #pragma unroll
-            for (int i = 0; i < TI; ++i)
-                fa[i] = *LDS_PTR(const bf16x8, (uintptr_t)(hadr[i & 1][t % 3] + ((i >> 1) + t / 3) * HWID * 64));
+            for (int i = 0; i < TI; ++i) {
+                if constexpr (DBG & 16) {  // ablation: no fragment reads (the MFMAs take lane-dependent junk)
+                    fa[i] = __builtin_bit_cast(bf16x8, u32x4{(uint32_t)(lane + i), (uint32_t)t, 0u, (uint32_t)c});
+                } else {
+                    fa[i] = *LDS_PTR(const bf16x8, (uintptr_t)(hadr[i & 1][t % 3] + ((i >> 1) + t / 3) * HWID * 64));
+                }
+            }
             // branch-free issue (a conditional load makes hipcc's vmcnt accounting fall back to vmcnt(0) at the
             // ring slot's next use): the last chunk re-stages its own halo into the idle buffer and the last two
             // taps re-load the last W slice
@@ -2277,8 +2314,8 @@ __global__ __launch_bounds__(512, 1) void halo3_kernel(EngineArgs p) {
             for (int i = 0; i < TI; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    if constexpr (DBG & 1) {
-                        acc[i][j][0] += __builtin_bit_cast(float, fb[t % 3][j][0]) * (float)fa[i][0];
+                    if constexpr (DBG & 1) {  // ablation: no MFMAs (the reads stay live)
+                        if (j == 0) asm volatile("" ::"v"(fa[i]));
                     } else {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[t % 3][j]),
                                                                            __builtin_bit_cast(f16x8, fa[i]), acc[i][j], 0, 0, 0);
@@ -2302,6 +2339,11 @@ __global__ __launch_bounds__(512, 1) void halo3_kernel(EngineArgs p) {
         }
     }
     wait_vm<0>();  // the last chunk's re-staged halo pieces land before the block's LDS is released
+    if constexpr ((DBG & 64) != 0) {  // ablation: no epilogue (the accumulators stay live)
+#pragma unroll
+        for (int i = 0; i < TI; ++i) asm volatile("" ::"v"(acc[i][0]), "v"(acc[i][1]));
+        return;
+    }
     engine_epilogue<H3Tile, E_CONV, TW, false>(p, (img * p.ho + y0) * p.wo + x0, n0, acc);
 }
 
@@ -3604,6 +3646,12 @@ static int launch_halo3(EngineArgs a, void* stream, const char* what) {
     else if (dbg == 6) RF_LAUNCH(halo3_kernel<6>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
     else if (dbg == 8) RF_LAUNCH(halo3_kernel<8>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
     else if (dbg == 14) RF_LAUNCH(halo3_kernel<14>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    else if (dbg == 15) RF_LAUNCH(halo3_kernel<15>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    else if (dbg == 30) RF_LAUNCH(halo3_kernel<30>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    else if (dbg == 16) RF_LAUNCH(halo3_kernel<16>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    else if (dbg == 32) RF_LAUNCH(halo3_kernel<32>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    else if (dbg == 64) RF_LAUNCH(halo3_kernel<64>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+    else if (dbg == 96) RF_LAUNCH(halo3_kernel<96>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
     else RF_LAUNCH(halo3_kernel<0>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
     return rf::check_launch(what);
 }
