@@ -459,6 +459,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                     bsum[j][e] = (p.bias && col < p.cout) ? p.bias[col] : 0.f;
                 }
             for (int f = 0; f < p.n_fin; ++f) {
+                const float bfin = p.b_fin[f];  // (read before this output's stores, not behind them)
                 float wf[TJ][4];
 #pragma unroll
                 for (int j = 0; j < TJ; ++j)
@@ -478,7 +479,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                     s += __shfl_xor(s, 32, 64);
                     const int m = frow(i);
                     if (lane < 16 && wn == 0 && m < p.m) {
-                        float y = elu_fast(s + p.b_fin[f], p.elu_alpha);
+                        float y = elu_fast(s + bfin, p.elu_alpha);
                         if (p.flags & RF_CONV_LOG_DECODE) y = pow10m1_fast(y);
                         const int hwp = p.ho * p.wo;
                         const int64_t o = (p.flags & RF_CONV_NCHW_OUT) ? ((int64_t)(m / hwp) * p.n_fin + f) * hwp + (m % hwp)
@@ -2363,6 +2364,7 @@ constexpr int HPIECES = 40, WPIECES = 18;                               // 1-KiB
 constexpr int HBYTES = HPIECES * 1024, WBYTES = WPIECES * 1024, BUF = HBYTES + WBYTES;
 constexpr int NWAVE = 4, HPW = HPIECES / NWAVE;                         // 10 halo pieces per wave
 constexpr int LDS = 2 * BUF;                                             // 116 KiB: one block per CU
+constexpr int NFIN = 4;                                                  // head outputs (RGB: 3)
 }  // namespace c32
 
 __global__ __launch_bounds__(256, 1) void conv3x3_c32_kernel(EngineArgs p) {
@@ -2490,31 +2492,43 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c32_kernel(EngineArgs p) {
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e) sv[i][j][e] = silu(acc[i][j][e] + bsum[j][e]);
-    for (int f = 0; f < p.n_fin; ++f) {
-        float wf[2][4];
+    // every head weight is read before the first store: a load issued after a store waits for it (vmcnt counts
+    // both in issue order), and b_fin re-read per pixel fragment made each fragment wait for the previous one's
+    // stores (n_fin <= c32::NFIN, c32_ok)
+    const float* __restrict__ w_fin = p.w_fin;
+    const float* __restrict__ b_fin = p.b_fin;
+    float* __restrict__ out = reinterpret_cast<float*>(p.c);
+    float wf[NFIN][2][4], bf[NFIN];
+#pragma unroll
+    for (int f = 0; f < NFIN; ++f) {
+        bf[f] = f < p.n_fin ? b_fin[f] : 0.f;
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int col = j * 16 + 4 * (lane >> 4) + e;
-                wf[j][e] = col < p.cout ? p.w_fin[f * p.cout + col] : 0.f;
+                wf[f][j][e] = (f < p.n_fin && col < p.cout) ? w_fin[f * p.cout + col] : 0.f;
             }
+    }
+#pragma unroll
+    for (int f = 0; f < NFIN; ++f) {
+        if (f >= p.n_fin) break;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             float s = 0.f;
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) s += sv[i][j][e] * wf[j][e];
+                for (int e = 0; e < 4; ++e) s += sv[i][j][e] * wf[f][j][e];
             s += __shfl_xor(s, 16, 64);
             s += __shfl_xor(s, 32, 64);
             if (lane < 16) {
                 const int m = (img * p.ho + y0 + 4 * wave + (i >> 1)) * p.wo + x0 + 16 * (i & 1) + lane;
-                float y = elu_fast(s + p.b_fin[f], p.elu_alpha);
+                float y = elu_fast(s + bf[f], p.elu_alpha);
                 if (p.flags & RF_CONV_LOG_DECODE) y = pow10m1_fast(y);
                 const int64_t o = (p.flags & RF_CONV_NCHW_OUT) ? ((int64_t)(m / hwp) * p.n_fin + f) * hwp + (m % hwp)
                                                               : (int64_t)m * p.n_fin + f;
-                reinterpret_cast<float*>(p.c)[o] = y;
+                out[o] = y;
             }
         }
     }
@@ -3662,7 +3676,7 @@ static bool c32_ok(const EngineArgs& a) {
     const char* env = getenv("RF_CONV_C32");
     if ((env && atoi(env) == 0) || !(a.flags & RF_CONV_FINAL) || a.cout > 32 || a.n < 32) return false;
     if (a.kw != 3 || a.k != 9 * a.cin_pad || a.stride != 1 || a.pad != 1 || a.ho != a.hi || a.wo != a.wi) return false;
-    return a.cin_pad % 32 == 0 && a.ho % c32::TH == 0 && a.wo % c32::TW == 0 && a.m > 0;
+    return a.cin_pad % 32 == 0 && a.ho % c32::TH == 0 && a.wo % c32::TW == 0 && a.m > 0 && a.n_fin <= c32::NFIN;
 }
 
 static int launch_c32(EngineArgs a, void* stream, const char* what) {
