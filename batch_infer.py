@@ -95,6 +95,7 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
     kw = dict(resolution=args.resolution, torch_dtype=PRECISION[args.precision])
 
     model = getattr(pipeline, "model", None)
+    resolve = getattr(pipeline, "resolve", None)
 
     def render(batch, host=None):
         if host is not None and hasattr(model, "plan_hint"):  # a new scene's plan from the host mask: no read-back
@@ -108,7 +109,10 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
     if not pipelined or dev.type != "cuda":
         for idx in batches:
             items, host = _load_batch(files, idx, args.padding_length, False)
-            yield items, render({k: v.to(dev) for k, v in host.items()}, host).cpu()
+            imgs = render({k: v.to(dev) for k, v in host.items()}, host)
+            if resolve is not None:
+                resolve(imgs)
+            yield items, imgs.cpu()
         return
     # HDF5 decode (zlib releases the GIL) runs LOADERS batches ahead on a thread pool, consumed in order
     pool = ThreadPoolExecutor(max_workers=LOADERS)
@@ -156,10 +160,14 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
                 copied = torch.cuda.Event()
                 copied.record(d2h)
             imgs.record_stream(d2h)
-            nxt = (items, out, copied, host)  # `host` (pinned inputs) lives until this batch is yielded
+            nxt = (items, out, copied, host, imgs)  # `host` (pinned inputs) lives until this batch is yielded
         if pending is not None:  # batch i is handed out while batch i+1 renders
-            p_items, p_out, p_copied, _ = pending
+            p_items, p_out, p_copied, _, p_imgs = pending
             p_copied.synchronize()
+            # the frame is complete: its fp16 range check reads a host word (no wait); a frame that overflowed is
+            # rendered again in place, and copied back again
+            if resolve is not None and resolve(p_imgs):
+                p_out.copy_(p_imgs)
             yield p_items, p_out
         if nxt is None:
             return

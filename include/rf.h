@@ -61,7 +61,7 @@ extern "C" {
 #define RF_ERR_UNSUPPORTED 3
 #define RF_ERR_DEVICE 4       /* an earlier launch reported a device-side error (see rf_device_error) */
 
-#define RF_ABI_VERSION 13
+#define RF_ABI_VERSION 14
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -96,6 +96,19 @@ int rf_clear_device_error(void);
  * rf_clear_f16_range_flag().  The model re-renders such a frame with bf16 operands (RenderFormer.range_check). */
 int rf_f16_range_flag(void);
 int rf_clear_f16_range_flag(void);
+/* Per-render fp16 range words (ABI 14): one word per frame, so concurrent renders (other streams, other models,
+ * other threads) never clear or inherit each other's overflow.  rf_range_word_new(&handle) allocates a zeroed
+ * host-mapped word; rf_range_word_bind(handle) makes it the word every fp16 writer launched from the CALLING THREAD
+ * raises, until the next bind (NULL: back to the process-wide word above); rf_range_word_read(handle) returns its
+ * code (>= 0) with a plain host load, no device sync (read it once the frame's launches have completed);
+ * rf_range_word_clear(handle) zeroes it; rf_range_word_free(handle) releases it (no launch that may still write it
+ * can be in flight).  NULL handles address the process-wide word.  The model takes one word per render
+ * (RenderFormer.range_check) and checks it when the frame's end event has completed. */
+int rf_range_word_new(void** handle);
+int rf_range_word_bind(void* handle);
+int rf_range_word_read(void* handle);
+int rf_range_word_clear(void* handle);
+int rf_range_word_free(void* handle);
 int rf_debug_raise_device_error(int code, void* stream);
 
 /* Kernel timer (measurement only; bench.py's roofline).  rf_ktimer_arm() creates a start/stop event pair on the

@@ -79,6 +79,7 @@ def main(argv=None):
     fov = data["fov"].unsqueeze(0).unsqueeze(-1).to(dev)
     imgs = pipeline(triangles=triangles, texture=texture, mask=mask, vn=vn, c2w=c2w, fov=fov,
                     resolution=args.resolution, torch_dtype=PRECISION[args.precision])
+    pipeline.resolve(imgs)  # the frame's fp16 range check (re-rendered in place if it overflowed) before reading it
     print("Inference completed. Rendered images shape:", imgs.shape)
     output_dir = args.output_dir if args.output_dir else os.path.dirname(os.path.abspath(args.h5_file))
     os.makedirs(output_dir, exist_ok=True)

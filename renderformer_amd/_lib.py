@@ -83,6 +83,11 @@ SIGNATURES = {
     "rf_clear_device_error": [],
     "rf_f16_range_flag": [],
     "rf_clear_f16_range_flag": [],
+    "rf_range_word_new": [_P],
+    "rf_range_word_bind": [_P],
+    "rf_range_word_read": [_P],
+    "rf_range_word_clear": [_P],
+    "rf_range_word_free": [_P],
     "rf_debug_raise_device_error": [_I, _P],
     "rf_ktimer_arm": [],
     "rf_ktimer_read": [_P, _I],

@@ -46,6 +46,8 @@
 
 #include "common.h"
 
+#define RF_CONST __attribute__((address_space(4)))  // read-only for the launch: scalar loads
+
 namespace {
 
 constexpr int HD = 128;
@@ -733,7 +735,10 @@ constexpr int NW5 = 8;
 constexpr int QB5 = NW5 * 32;
 constexpr int K5 = 0;                  // K ring: 2 x 16 KiB
 constexpr int V5 = 2 * TILE_BYTES;     // V ring: 2 x 16 KiB
+constexpr int Q5 = 4 * TILE_BYTES;     // Q image of a piece: 8 waves x 8 KiB (attn_sk_kernel)
 constexpr int SK5_MAX_GRID = 512;
+static_assert(KT == rf::ATTN_KT && QB5 == rf::ATTN_QB && SK5_MAX_GRID == rf::ATTN_MAX_GRID,
+              "attn_sched.cpp prices the kernel's geometry");
 constexpr int PIECE_O = QB5 * HD;                // f32, register order
 constexpr int PIECE_FLOATS = PIECE_O + QB5 * 2 * 2;  // + (m, l) per lane
 
@@ -776,6 +781,13 @@ RF_DEV void set_pk(bf16x8& f, int w, uint32_t v) {
     f = __builtin_bit_cast(bf16x8, u);
 }
 
+// x through an empty asm: computations from the result cannot be hoisted out of the enclosing loop (hoisted
+// lane-constant offsets of the piece epilogue were spilled across the tile loop and reloaded behind vmcnt(0))
+RF_DEV int opaque(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 // One 1-KiB LDS-DMA piece: lane l's 16 B land at LDS byte lds + 16 l.  Inline asm so hipcc neither
 // counts it (the loop waits with its own vmcnt) nor guards later ds_read_b64_tr_b16 with vmcnt(0).
 // M0 is declared clobbered (hipcc warns: reserved register); the kernel has no other M0 user (checked
@@ -806,11 +818,12 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     constexpr bool MINIT_EVERY = (DBG & 1024) == 0;
     constexpr auto x_blk = [](int x) { return x >> 4; };
     constexpr auto x_sp = [](int x) { return (x >> 3) & 1; };
-    __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // 64 KiB
+    // K ring, V ring (2 x 16 KiB each), then the Q image of the next piece (8 waves x 8 KiB)
+    __shared__ __attribute__((aligned(16))) char smem[Q5 + QB5 * HD * 2];  // 128 KiB
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR): row windows, flags
     const int half = lane >> 5;
     const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
     const bool late = __builtin_amdgcn_readfirstlane(tid) >= 256;  // waves 4-7 (SIMD partners of 0-3)
@@ -825,14 +838,19 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         if (tid == 0) report_device_error(p.err, RF_DEVERR_SK_SCHED);
         return;
     }
-    int64_t it = p.bounds[wg];
-    const int64_t it_end = p.bounds[wg + 1];
+    // The problem table and the range table are read-only for the launch: constant-address-space (scalar) loads
+    // keep them off the vector memory counter.  (As vector loads, their results sat in VGPRs across pieces and the
+    // compiler's wait for them at the next piece's top was a vmcnt(0) that also drained the previous piece's
+    // partial stores before the next piece issued a single load.)
+    const RF_CONST int32_t* probs = (const RF_CONST int32_t*)p.problems;
+    const RF_CONST int64_t* bnds = (const RF_CONST int64_t*)p.bounds;
+    int64_t it = bnds[wg];
+    const int64_t it_end = bnds[wg + 1];
 
     const float c = UNIT ? 1.f : p.c;
     const float inv_c = UNIT ? 1.f : 1.f / p.c;
     const float sum_thr = exp2f(p.thr);  // half-row sum of one tile's P above which the running max moves
     const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;  // ds_read_b64_tr_b16 lane geometry
-    const int qi = wave * 32 + (lane & 31);
     // LDS image of a K/V tile (guide T10 image (a)): 8-row x 32-column subtiles of 512 B,
     // off(row, ch) = 2048 (row >> 3) + 512 (ch >> 2) + 64 (row & 7) + 16 ((ch & 3) ^ ((row >> 2) & 3)),
     // conflict-free for the K ds_read_b128 and the V ds_read_b64_tr_b16 of the 32x32x16 operands, and
@@ -850,6 +868,10 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     int pi = -1;
     int64_t base = 0, usz = 0;
     int q_start = 0, q_len = 0, k_start = 0, k_len = 0, v_start = 0, nqb = 1, nt = 1;
+    // the current piece: tiles [kt0, kt1) of its unit (n of them), query rows [q0, q1) of head column hoff
+    int kt0 = 0, kt1 = 0, n = 0, q0 = 0, q1 = 0, hoff = 0;
+    int64_t unit_end = 0;
+    bool active = false;  // wave-uniform: this wave owns at least one row
     // DBG & 32: top wait, K DMA issue, mask+max+check, A, seam wait, V DMA issue, B, tiles
     uint64_t stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t t_prev = 0, clk0 = 0, ref0 = 0;
@@ -864,17 +886,11 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             t_prev = now;
         }
     };
-    // publish pending: this workgroup's partial stores were issued at the end of its previous piece and are
-    // covered by the next piece's prologue wait; the flag goes up after that piece's first barrier (all
-    // waves' stores complete), so the store latency hides under the next piece's Q / K / V loads
-    bool pend = false;
-    while (it < it_end) {
-        uint64_t t_piece = 0;  // DBG & 32: piece prologue cycles -> stamp[6]
-        if constexpr (DBG & 32) t_piece = __builtin_amdgcn_s_memtime();
+    auto next_piece = [&]() {  // the piece holding tile `it` (scalar: SGPRs only)
         while (it >= base + usz) {  // advance to the problem holding tile `it`
             base += usz;
             ++pi;
-            const int32_t* d = p.problems + 5 * pi;
+            const RF_CONST int32_t* d = probs + 5 * pi;
             q_start = d[0];
             q_len = d[1];
             k_start = d[2];
@@ -886,45 +902,97 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         }
         const int64_t rel = it - base;
         const int unit = (int)(rel / nt);
-        const int kt0 = (int)(rel - (int64_t)unit * nt);
-        const int kt1 = (int)min((int64_t)nt, kt0 + (it_end - it));
-        const int n = kt1 - kt0;
-        const int64_t unit_end = base + (int64_t)(unit + 1) * nt;
+        kt0 = (int)(rel - (int64_t)unit * nt);
+        kt1 = (int)min((int64_t)nt, kt0 + (it_end - it));
+        n = kt1 - kt0;
+        unit_end = base + (int64_t)(unit + 1) * nt;
         it += n;
         const int h = unit / nqb, qb = unit - (unit / nqb) * nqb;
-        const int q0 = (int)((int64_t)qb * q_len / nqb), q1 = (int)((int64_t)(qb + 1) * q_len / nqb);
-        const int hoff = h * HD;
-        const bool active = q0 + wave * 32 < q1;  // wave-uniform: this wave owns at least one row
+        q0 = (int)((int64_t)qb * q_len / nqb);
+        q1 = (int)((int64_t)(qb + 1) * q_len / nqb);
+        hoff = h * HD;
+        active = q0 + wave * 32 < q1;
+    };
 
-        if (!pend) attn_wait_vm<0>();
-        __syncthreads();  // the previous piece's LDS readers are done
-
-        bf16x8 qf[8];
-        {
-            const int qrow = q_start + min(q0 + qi, q1 - 1);
-            const bf16_t* src = p.q + (int64_t)qrow * p.ldq + hoff + 8 * half;
-#pragma unroll
-            for (int st = 0; st < 8; ++st) qf[st] = *reinterpret_cast<const bf16x8*>(src + 16 * st);
+    const bf16_t* kp = nullptr;
+    const bf16_t* vp = nullptr;
+    int64_t kstep = 0, vstep = 0;
+    // tiles are issued in order; rows past k_len (tail tile) re-read row k_len - 1, masked later
+    auto issue = [&](const bf16_t*& src, int64_t ld, int64_t step, int t, uint32_t dst) {
+        const uint32_t d0 = __builtin_amdgcn_readfirstlane(dst + wave * 2048);
+        if ((t + 1) * KT <= k_len) {
+            dma_piece(src, d0);
+            dma_piece(src + 64, d0 + 1024);
+        } else {
+            const int over = t * KT + opaque(d_row) - (k_len - 1);
+            const bf16_t* a = src - (int64_t)(over > 0 ? over : 0) * ld;
+            dma_piece(a, d0);
+            dma_piece(a + 64, d0 + 1024);
         }
+        src += step;
+    };
+    // A piece's first loads, in vector-memory-counter order: Q (8 LDS-DMA pieces per wave into the wave's 8 KiB
+    // of the Q image: piece st holds lane l's 16 B of qf[st], so the ds_read_b128 back is lane-linear), K(t0),
+    // K(t0+1) when n > 1 (the K ring is free once every wave is past the previous piece's last phase A), then,
+    // after a barrier, V(t0) (its slot may still be read by the partner group's last phase B).  Issued at the end
+    // of the previous piece's tile loop, AHEAD of its partial or O stores: vmcnt counts loads and stores together
+    // in issue order, so the piece's counted waits below leave the younger stores in flight (nst of them).
+    auto issue_qk = [&]() {
+        {
+            const int ql = wave * 32 + (opaque(lane) & 31);
+            const int qrow = q_start + min(q0 + ql, q1 - 1);
+            const bf16_t* src = p.q + (int64_t)qrow * p.ldq + hoff + 8 * half;
+            const uint32_t d0 = __builtin_amdgcn_readfirstlane(lds0 + Q5 + wave * 8192);
+#pragma unroll
+            for (int st = 0; st < 8; ++st) dma_piece(src + 16 * st, d0 + 1024 * st);
+        }
+        kp = p.k + (int64_t)(k_start + kt0 * KT + d_row) * p.ldk + hoff + 8 * d_ch;
+        vp = p.v + (int64_t)(v_start + kt0 * KT + d_row) * p.ldv + hoff + 8 * d_ch;
+        kstep = KT * p.ldk;
+        vstep = KT * p.ldv;
+        issue(kp, p.ldk, kstep, kt0, lds0 + K5);
+        if (n > 1) issue(kp, p.ldk, kstep, kt0 + 1, lds0 + K5 + TILE_BYTES);
+    };
+    auto issue_v0 = [&]() { issue(vp, p.ldv, vstep, kt0, lds0 + V5); };
 
-        const bf16_t* kp = p.k + (int64_t)(k_start + kt0 * KT + d_row) * p.ldk + hoff + 8 * d_ch;
-        const bf16_t* vp = p.v + (int64_t)(v_start + kt0 * KT + d_row) * p.ldv + hoff + 8 * d_ch;
-        const int64_t kstep = KT * p.ldk, vstep = KT * p.ldv;
-        // tiles are issued in order; rows past k_len (tail tile) re-read row k_len - 1, masked later
-        auto issue = [&](const bf16_t*& src, int64_t ld, int64_t step, int t, uint32_t dst) {
-            const uint32_t d0 = __builtin_amdgcn_readfirstlane(dst + wave * 2048);
-            if ((t + 1) * KT <= k_len) {
-                dma_piece(src, d0);
-                dma_piece(src + 64, d0 + 1024);
-            } else {
-                const int over = t * KT + d_row - (k_len - 1);
-                const bf16_t* a = src - (int64_t)(over > 0 ? over : 0) * ld;
-                dma_piece(a, d0);
-                dma_piece(a + 64, d0 + 1024);
-            }
-            src += step;
-        };
-
+    // nst: vector-memory stores this wave issued after the current piece's first loads (0, 8 O stores or 17
+    // partial stores; wave-uniform), the counted waits' allowance for them.  pend: the previous piece's partial
+    // is stored but its flag not raised; the flag goes up once every wave has passed a vmcnt(0) (the second
+    // barrier of this piece's first tile), so the store latency hides under this piece's loads and first tile.
+    int nst = 0;
+    bool pend = false;
+    auto raise_pend = [&]() {
+        if (pend) {
+            if (tid == 0) __hip_atomic_store(p.flag + wg, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pend = false;
+        }
+    };
+    const bool any = it < it_end;
+    if (any) {
+        next_piece();
+        issue_qk();
+        issue_v0();
+    }
+    while (any) {  // one pass per piece; ends after the range's last piece
+        uint64_t t_piece = 0;  // DBG & 32: piece prologue cycles -> stamp[6]
+        if constexpr (DBG & 32) t_piece = __builtin_amdgcn_s_memtime();
+        // Q and K(t0) landed for this wave (K(t0+1), V(t0) and the nst stores may still be in flight) ...
+        const int nw = __builtin_amdgcn_readfirstlane(nst);
+        if (n > 1) {
+            if (nw == 17) attn_wait_vm<4 + 17>();
+            else if (nw == 8) attn_wait_vm<4 + 8>();
+            else attn_wait_vm<4>();
+        } else {
+            if (nw == 17) attn_wait_vm<2 + 17>();
+            else if (nw == 8) attn_wait_vm<2 + 8>();
+            else attn_wait_vm<2>();
+        }
+        __builtin_amdgcn_s_barrier();  // ... and for every wave
+        __builtin_amdgcn_sched_barrier(0);
+        bf16x8 qf[8];
+#pragma unroll
+        for (int st = 0; st < 8; ++st)
+            qf[st] = *reinterpret_cast<const bf16x8*>(smem + Q5 + wave * 8192 + 1024 * st + 16 * lane);
         f32x16 o[4];
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
@@ -936,7 +1004,6 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         f32x16 minit;
 #pragma unroll
         for (int r = 0; r < 16; ++r) minit[r] = 0.f;
-
 
         auto qk = [&](const int koff, f32x16* s) {
 #pragma unroll
@@ -996,22 +1063,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 }
         };
 
-        issue(kp, p.ldk, kstep, kt0, lds0 + K5);
-        issue(vp, p.ldv, vstep, kt0, lds0 + V5);
-        // the first QK^T needs Q and K(t0) only: V(t0) and K(t0+1) (2 DMA pieces each, the youngest
-        // vector-memory ops) keep landing under it (guide T20: wait at the first consumer)
-        if (n > 1) {
-            issue(kp, p.ldk, kstep, kt0 + 1, lds0 + K5 + TILE_BYTES);
-            attn_wait_vm<4>();
-        } else {
-            attn_wait_vm<2>();
-        }
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        if (pend) {  // every wave's older partial stores completed before its counted wait above
-            if (tid == 0) __hip_atomic_store(p.flag + wg, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            pend = false;
-        }
+
         f32x16 sA[2], sB[2];
         qk(K5, sA);  // raw scores of the piece's first tile (base 0)
         mask_tail(sA, kt0);
@@ -1034,10 +1086,20 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (DBG & 32) t_prev = __builtin_amdgcn_s_memtime();
             if constexpr (!(DBG & 2)) {
-                attn_wait_vm<0>();             // K(t+1) and V(t) landed for this wave ...
+                // K(t+1) and V(t) landed for this wave (the first tile: only the nst stores may stay in flight) ...
+                if (i == 0) {
+                    if (nw == 17) attn_wait_vm<17>();
+                    else if (nw == 8) attn_wait_vm<8>();
+                    else attn_wait_vm<0>();
+                } else {
+                    attn_wait_vm<0>();
+                }
                 __builtin_amdgcn_s_barrier();  // ... and for every wave; K(t) and V(t-1) are free
             }
             __builtin_amdgcn_sched_barrier(0);
+            // the second barrier of the piece for waves 0-3 and the third for 4-7: every wave has passed a vmcnt(0)
+            // since its stores (0-3 at tile 0's seam, 4-7 at tile 0's seam = this barrier's partner)
+            if (i == 1) raise_pend();
             stamp_at(0);
 
             const int koff = K5 + (PAR ^ 1) * TILE_BYTES;
@@ -1200,30 +1262,20 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         }
         if (i < n) body(i, std::integral_constant<int, 0>{}, sA, sB);
         if (!late) __builtin_amdgcn_s_barrier();  // re-align the groups' barrier counts
+        raise_pend();  // (a one-tile piece: this barrier is the one tile 1's top would have been)
 
-        // ---- piece epilogue.  Register order: lane owns query (lane & 31), d = dt*32 + 8 gq + 4 half + 0..3
-        float* piece = p.part_o + (int64_t)wg * PIECE_FLOATS;
-        if (kt0 > 0) {
-            // not the unit's first tile: publish the unnormalised partial for the owner (sc1 stores,
-            // every storing wave drains, one lane flags; guide Guideline 16 / MI355X_MICROARCH hand-offs)
-            if (active) {
-                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(piece, 0, PIECE_FLOATS * 4, 0x00020000);
-#pragma unroll
-                for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-                    for (int gq = 0; gq < 4; ++gq) {
-                        const f32x4 v4 = {o[dt][4 * gq], o[dt][4 * gq + 1], o[dt][4 * gq + 2], o[dt][4 * gq + 3]};
-                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v4), rs,
-                                                               (((wave * 16 + dt * 4 + gq) * 64) + lane) * 16, 0, 16);
-                    }
-                const f32x2 ml = {m_run, l_run};
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ml), rs,
-                                                      PIECE_O * 4 + (wave * 64 + lane) * 8, 0, 16);
-            }
-            pend = true;  // flag raised in the next piece's prologue, or after the loop
-            continue;
-        }
-        if (kt1 < nt) {
+        // ---- piece epilogue.  This piece's state first (the next piece's loads go out before its stores).
+        // Register order: lane owns query (lane & 31), d = dt*32 + 8 gq + 4 half + 0..3
+        const bool e_pub = kt0 > 0;     // not the unit's first tile: publish the partial for the owner
+        const bool e_cut = kt1 < nt;    // the unit continues in later workgroups: merge their partials
+        const int64_t e_unit_end = unit_end;
+        const bool e_active = active;
+        // O rows of this wave: a buffer window of its 32 rows (rows >= q1 land out of range and are dropped), so
+        // an active wave always issues exactly 8 O stores (the count the next piece's waits allow for)
+        bf16_t* const e_orow = p.o + (int64_t)(q_start + q0 + wave * 32) * p.ldo + hoff;
+        const int eln = opaque(lane);  // the epilogue's lane offsets are computed here, not hoisted
+        const int e_ovalid = q0 + wave * 32 + (eln & 31) < q1;
+        if (!e_pub && e_cut) {
             // owner of a cut unit: fold in the partials of the logically later workgroups that hold its other
             // tiles (lower blockIdx: SkLayout), the LAST one first: the middle piece of a unit cut three ways (a
             // workgroup whose whole range lies inside the unit) publishes at the end of its range, the tail piece
@@ -1236,8 +1288,8 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 uint32_t mask = 0;
                 int cw = cw0;
                 for (; cw < gend && cw - cw0 < 32; ++cw) {
-                    const int64_t cs = p.bounds[cw], ce = p.bounds[cw + 1];
-                    if (cs >= unit_end) {
+                    const int64_t cs = bnds[cw], ce = bnds[cw + 1];
+                    if (cs >= e_unit_end) {
                         done = true;
                         break;
                     }
@@ -1257,9 +1309,15 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     }
                     __syncthreads();
-                    if (active) {
+                    if (e_active) {
+                        // all 17 loads in flight at once (one round trip), then the fold
                         const float* src = p.part_o + (int64_t)f * PIECE_FLOATS;
                         const f32x2 ml = *reinterpret_cast<const f32x2*>(src + PIECE_O + (wave * 64 + lane) * 2);
+                        f32x4 pv[16];
+#pragma unroll
+                        for (int k = 0; k < 16; ++k)
+                            pv[k] = *reinterpret_cast<const f32x4*>(src + (((wave * 16 + k) * 64) + lane) * 4);
+                        __builtin_amdgcn_sched_barrier(0);
                         const float mx = __builtin_fmaxf(m_run, ml[0]);
                         const float wa = fast_exp2(m_run - mx), wb = fast_exp2(ml[0] - mx);
                         l_run = l_run * wa + ml[1] * wb;
@@ -1267,38 +1325,71 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
 #pragma unroll
                         for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-                            for (int gq = 0; gq < 4; ++gq) {
-                                const f32x4 v4 = *reinterpret_cast<const f32x4*>(
-                                    src + (((wave * 16 + dt * 4 + gq) * 64) + lane) * 4);
+                            for (int gq = 0; gq < 4; ++gq)
 #pragma unroll
-                                for (int e = 0; e < 4; ++e) o[dt][4 * gq + e] = o[dt][4 * gq + e] * wa + v4[e] * wb;
-                            }
+                                for (int e = 0; e < 4; ++e)
+                                    o[dt][4 * gq + e] = o[dt][4 * gq + e] * wa + pv[dt * 4 + gq][e] * wb;
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 if (done) break;
                 cw0 = cw;
             }
-            if (!done && p.bounds[gend] < unit_end && tid == 0) report_device_error(p.err, RF_DEVERR_SK_SCHED);
+            if (!done && bnds[gend] < e_unit_end && tid == 0) report_device_error(p.err, RF_DEVERR_SK_SCHED);
         }
-        if (!active) continue;
-        const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-        const float inv = l_tot > 0.f ? 1.0f / l_tot : 0.f;
-        // row-per-lane store widened to 16 B (guide T21): column group k = 4 dt + gq is split across the halves
-        // (lane l: columns 8k..8k+3, lane l+32: 8k+4..8k+7); one v_permlane32_swap per dword of the pair (k, k+1)
-        // gives the lower half columns 8k..8k+7 and the upper half 8k+8..8k+15.  (Staging the tile through LDS for
-        // whole-line stores measured slower: 137 vs 129 us per stage-1 launch, the extra registers spill.)
-        const int qrow_o = q0 + qi;
-        if (qrow_o < q1) {  // (lanes l and l + 32 hold the same query row: both store or neither)
-            bf16_t* dst = p.o + (int64_t)(q_start + qrow_o) * p.ldo + hoff;
+        const bool more = it < it_end;
+        // the next piece's first loads go out before this piece's stores (after the merge's loads: the owner's
+        // merge is normally its range's last piece, and its partial reads want the registers)
+        if (more) {
+            next_piece();
+            issue_qk();                    // the K ring is free: every wave is past this piece's last phase A
+            __builtin_amdgcn_s_barrier();  // every wave is past its last phase B: V slot 0 is free
+            issue_v0();
+        }
+
+        float* piece = p.part_o + (int64_t)wg * PIECE_FLOATS;
+        if (e_pub) {
+            // publish the unnormalised partial for the owner (sc1 stores; every storing wave drains and one lane
+            // flags after the next piece's drain, or after the loop; guide Guideline 16 / MI355X_MICROARCH hand-offs)
+            if (e_active) {
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(piece, 0, PIECE_FLOATS * 4, 0x00020000);
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int gq = 0; gq < 4; ++gq) {
+                        const f32x4 v4 = {o[dt][4 * gq], o[dt][4 * gq + 1], o[dt][4 * gq + 2], o[dt][4 * gq + 3]};
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v4), rs,
+                                                               (((wave * 16 + dt * 4 + gq) * 64) + eln) * 16, 0, 16);
+                    }
+                const f32x2 ml = {m_run, l_run};
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ml), rs,
+                                                      PIECE_O * 4 + (wave * 64 + eln) * 8, 0, 16);
+            }
+            nst = e_active ? 17 : 0;
+            pend = true;  // flag raised in the next piece's first tile, or after the loop
+            if (!more) break;
+            continue;
+        }
+        nst = e_active ? 8 : 0;
+        if (e_active) {
+            const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+            const float inv = l_tot > 0.f ? 1.0f / l_tot : 0.f;
+            // row-per-lane store widened to 16 B (guide T21): column group k = 4 dt + gq is split across the halves
+            // (lane l: columns 8k..8k+3, lane l+32: 8k+4..8k+7); one v_permlane32_swap per dword of the pair (k, k+1)
+            // gives the lower half columns 8k..8k+7 and the upper half 8k+8..8k+15.  (Staging the tile through LDS
+            // for whole-line stores measured slower: 137 vs 129 us per stage-1 launch, the extra registers spill.)
             if constexpr (OF16) {  // fp16 O: |O| <= max |V| row-wise, but V (bf16) may exceed fp16's range
                 float amax = 0.f;
 #pragma unroll
                 for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
                     for (int r = 0; r < 16; r += 2) amax = amax3(amax, o[dt][r] * inv, o[dt][r + 1] * inv);
-                if (p.range && !f16_in_range(amax)) report_f16_range(p.range, RF_RANGE_ATTN);
+                if (e_ovalid && p.range && !f16_in_range(amax)) report_f16_range(p.range, RF_RANGE_ATTN);
             }
+            const __amdgpu_buffer_rsrc_t ro =
+                __builtin_amdgcn_make_buffer_rsrc(e_orow, 0, (int)(32 * p.ldo * 2), 0x00020000);
+            // (lanes l and l + 32 hold the same query row: both store or neither)
+            const int obase = e_ovalid ? (int)(((eln & 31) * p.ldo + 8 * (eln >> 5)) * 2) : 0x40000000;
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
@@ -1309,9 +1400,11 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                     uint32_t b1 = pack_o<OF16>(o[dt][4 * gq + 6] * inv, o[dt][4 * gq + 7] * inv);
                     const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
                     const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-                    *reinterpret_cast<uint4*>(dst + dt * 32 + 8 * gq + 8 * half) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+                    const u32x4 w4 = {r0[0], r1[0], r0[1], r1[1]};
+                    __builtin_amdgcn_raw_buffer_store_b128(w4, ro, obase + (dt * 32 + 8 * gq) * 2, 0, 0);
                 }
         }
+        if (!more) break;
     }
     if (pend) {  // the range ended with a published piece
         attn_wait_vm<0>();
@@ -1894,6 +1987,7 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
     // a fresh flag value per launch: a publisher's flag from an earlier launch (even one that timed out and left
     // a late flag behind) never equals this launch's, so flags need no re-arm and no memset
     a.epoch = rf::next_epoch(a.flag, SK5_MAX_GRID * sizeof(int), st0);
+    if (a.epoch == 0) return RF_ERR_LAUNCH;  // the flag area could not be re-zeroed at an epoch wrap
     // (the grid may exceed the CUs: the SkLayout waits only go to earlier-dispatched blocks)
     // q pre-scaled by scale*log2(e) upstream (scale = ln 2): scores are already exp2 exponents
     const bool unit = fabsf(a.c - 1.0f) < 1e-6f;
@@ -2003,225 +2097,7 @@ extern "C" int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ld
     return rf::check_launch("rf_attn_fwd");
 }
 
-// ---------------------------------------------------------------------------------------------
-// Cost-balanced stream-K ranges (rf_attn_schedule).  With equal tile counts per workgroup the launch
-// ends with the owners of units cut three ways: a workgroup whose range lies inside one unit ("mid")
-// has one piece (one prologue, one publish) and finishes ~14 % early, while the owner of that unit
-// has two pieces and merges two partials (bench shape, per-role lifetimes from the s_memtime stamps of
-// tools/attn_ablate.py stamps: mid 222k, owners of 3-way units 257k, others 246k cycles).  Here every
-// piece costs a prologue, its tiles, and a publish (non-first piece of its unit) or a finish (first
-// piece: one merge per later piece, each after that piece's publish, then the O store), and the
-// ranges are chosen backwards from the last workgroup (whose successors' publish times are then known)
-// so that every workgroup finishes by a common time T, the smallest T that covers all tiles.
-namespace {
-struct SkCost {
-    double tile = 3170, pro = 8700, pub = 8500, merge = 9800, store = 6000;  // shader cycles
-};
-
-struct SkUnits {
-    std::vector<int64_t> base;  // first tile of problem i
-    std::vector<int64_t> nt;    // tiles per unit of problem i (0: problem holds no tiles)
-    int64_t total = 0;
-    void unit_of(int64_t x, int64_t& us, int64_t& ue) const {  // [start, end) of the unit holding tile x
-        int64_t i = (int64_t)(std::upper_bound(base.begin(), base.end(), x) - base.begin()) - 1;
-        while (nt[i] == 0) --i;
-        const int64_t u = (x - base[i]) / nt[i];
-        us = base[i] + u * nt[i];
-        ue = us + nt[i];
-    }
-};
-
-// finish time of workgroup w with range [a, b), given the later workgroups' bounds and publish times;
-// *pub = the publish time of its first piece when that piece is a unit's later piece
-double sk_simulate(const SkUnits& U, const SkCost& c, int w, int64_t a, int64_t b, const std::vector<int64_t>& bnd,
-                   const std::vector<double>& pubt, int grid, double* pub) {
-    double t = 0;
-    *pub = 0;
-    for (int64_t x = a; x < b;) {
-        int64_t us, ue;
-        U.unit_of(x, us, ue);
-        const int64_t e = std::min(b, ue);
-        t += c.pro + (double)(e - x) * c.tile;
-        if (x > us) {
-            t += c.pub;
-            *pub = t;
-        } else {
-            if (e < ue) {  // merges in the kernel's order: the last later workgroup first
-                int last = w + 1;
-                while (last < grid && bnd[last] < ue) ++last;
-                for (int cw = last - 1; cw > w; --cw)
-                    if (bnd[cw + 1] > bnd[cw]) t = std::max(t, pubt[cw]) + c.merge;
-            }
-            t += c.store;
-        }
-        x = e;
-    }
-    return t;
-}
-
-// backward fill with finish time T; returns bnd[0] (0 = every tile placed).  A range is feasible when the
-// workgroup finishes by T and its published piece (if any) lands early enough for the owner to merge it
-// and store by T; the largest feasible range is found by bisection on its start (the finish time grows
-// with the range except at unit boundaries, where a piece changes role).
-int64_t sk_fill(const SkUnits& U, const SkCost& c, int grid, double T, std::vector<int64_t>& bnd,
-                std::vector<double>& pubt) {
-    bnd.assign(grid + 1, 0);
-    pubt.assign(grid + 1, 0);
-    bnd[grid] = U.total;
-    // a published piece must land in time for the owner's merges from it on and its store: a unit's middle piece
-    // (the range lies strictly inside one unit) is merged last, so one merge follows; a tail piece is merged
-    // first, so one merge follows when the rest of its unit fits one earlier range (a two-way cut, e.g. every
-    // cross-attention unit) and two when it needs two (a three-way cut)
-    const double avg = (double)U.total / grid;
-    auto ok = [&](int w, int64_t a, int64_t b, double* pub) {
-        if (sk_simulate(U, c, w, a, b, bnd, pubt, grid, pub) > T) return false;
-        int64_t us, ue;
-        U.unit_of(a, us, ue);
-        const bool mid = a > us && b < ue;
-        const int after = (mid || (double)(a - us) <= 1.3 * avg) ? 1 : 2;
-        return *pub <= T - after * c.merge - c.store;
-    };
-    for (int w = grid - 1; w >= 0; --w) {
-        const int64_t b = bnd[w + 1];
-        double pub = 0;
-        // no range holds more than T / tile tiles: search starts in [b - that - 1, b) only
-        const int64_t reach = (int64_t)(T / c.tile) + 1;
-        int64_t lo = b, hi = 0;  // lo: feasible start (empty range), search [hi, lo)
-        if (b > 0 && b <= reach && ok(w, 0, b, &pub)) {
-            lo = 0;
-        } else if (b > 0) {
-            hi = std::max<int64_t>(1, b - reach);
-            while (hi < lo) {  // smallest feasible a in [hi, lo]
-                const int64_t mid = (hi + lo) / 2;
-                if (ok(w, mid, b, &pub)) lo = mid;
-                else hi = mid + 1;
-            }
-            // feasibility is not monotone where the first piece changes role: a start just inside a unit makes a
-            // published piece, the unit's first tile an owned one; prefer the owned start when it also fits
-            if (lo < b) {
-                int64_t us, ue;
-                U.unit_of(lo, us, ue);
-                if (us < lo && ok(w, us, b, &pub)) lo = us;
-            }
-        }
-        bnd[w] = lo;
-        ok(w, lo, b, &pub);
-        pubt[w] = lo < b ? pub : 0;
-    }
-    return bnd[0];
-}
-// the model's finish time of a given table (every workgroup, successors first so publish times are known)
-double sk_span(const SkUnits& U, const SkCost& c, int grid, const std::vector<int64_t>& bnd) {
-    std::vector<double> pubt(grid + 1, 0.0);
-    double span = 0;
-    for (int w = grid - 1; w >= 0; --w) {
-        double pub = 0;
-        const double t = bnd[w + 1] > bnd[w] ? sk_simulate(U, c, w, bnd[w], bnd[w + 1], bnd, pubt, grid, &pub) : 0.0;
-        pubt[w] = pub;
-        span = std::max(span, t);
-    }
-    return span;
-}
-}  // namespace
-
 extern "C" int rf_attn_grid(void) { return cu_count(); }
-
-namespace {
-// One XCD group's ranges (sk_fill + bisection on the common finish time; equal tile counts kept when the model
-// prices them no worse), bounds relative to the group's first tile: out[0..grid].
-void sk_schedule_group(const SkUnits& U, const SkCost& c, int grid, int64_t* out) {
-    if (U.total <= grid) {
-        // fewer tiles than workgroups: one whole unit per workgroup, nothing cut, so a unit's result does not
-        // depend on the rest of the launch (a view rendered alone equals the same view in a batch)
-        int w = 0;
-        for (size_t i = 0; i < U.base.size(); ++i)
-            if (U.nt[i])
-                for (int64_t x = U.base[i]; x < (i + 1 < U.base.size() ? U.base[i + 1] : U.total); x += U.nt[i])
-                    out[w++] = x;
-        for (; w <= grid; ++w) out[w] = U.total;
-        return;
-    }
-    std::vector<int64_t> bnd;
-    std::vector<double> pubt;
-    // lo is infeasible (less than the average tile work); hi doubled until feasible
-    double lo = (double)U.total * c.tile / grid;
-    double hi = 2 * lo + 4 * (c.pro + c.pub + c.merge + c.store);
-    while (sk_fill(U, c, grid, hi, bnd, pubt) != 0) {
-        lo = hi;
-        hi *= 2;
-    }
-    for (int iter = 0; iter < 60 && hi - lo > 0.25 * c.tile; ++iter) {
-        const double mid = 0.5 * (lo + hi);
-        (sk_fill(U, c, grid, mid, bnd, pubt) == 0 ? hi : lo) = mid;
-    }
-    sk_fill(U, c, grid, hi, bnd, pubt);
-    std::vector<int64_t> eq(grid + 1);
-    for (int w = 0; w <= grid; ++w) eq[w] = U.total * w / grid;
-    const std::vector<int64_t>& best = sk_span(U, c, grid, eq) <= sk_span(U, c, grid, bnd) ? eq : bnd;
-    for (int w = 0; w <= grid; ++w) out[w] = best[w];
-}
-}  // namespace
-
-// Cost-balanced stream-K ranges in the forward-progress layout (common.h SkLayout): the units (head x q-block
-// of each problem with keys, in problem order) are cut into one contiguous chunk per XCD group, balanced by
-// tiles, so a unit never spans two groups (its pieces' blocks share an XCD's L2 when there are 8 groups, and
-// an owner only waits on lower-numbered blocks); each chunk is scheduled over its group's blocks by the cost
-// model above.  bounds[L] is the first tile of LOGICAL block L (bounds[grid] = total), as the kernel reads it.
-extern "C" int rf_attn_schedule(const int32_t* problems, int n_problems, int n_heads, int grid, int64_t* bounds) {
-    RF_REQUIRE(problems && bounds && n_problems > 0 && n_heads > 0, "rf_attn_schedule: bad arguments");
-    RF_REQUIRE(grid >= 1 && grid <= SK5_MAX_GRID, "rf_attn_schedule: grid %d out of range", grid);
-    // every unit as (first tile, tiles): the problems' units in order
-    std::vector<int64_t> ustart, unt;
-    int64_t total = 0;
-    for (int i = 0; i < n_problems; ++i) {
-        const int32_t* d = problems + 5 * i;
-        RF_REQUIRE(d[1] >= 0 && d[3] >= 0, "rf_attn_schedule: negative length in problem %d", i);
-        const int64_t nt = (d[3] + KT - 1) / KT;
-        const int64_t nu = nt > 0 ? (int64_t)n_heads * ((d[1] + QB5 - 1) / QB5) : 0;
-        for (int64_t u = 0; u < nu; ++u) {
-            ustart.push_back(total);
-            unt.push_back(nt);
-            total += nt;
-        }
-    }
-    const int64_t NU = (int64_t)ustart.size();
-    if (total == 0) {
-        for (int w = 0; w <= grid; ++w) bounds[w] = 0;
-        return RF_OK;
-    }
-    SkCost c;
-    if (const char* env = getenv("RF_ATTN_COST"))  // tile,pro,pub,merge,store (tuning)
-        sscanf(env, "%lf,%lf,%lf,%lf,%lf", &c.tile, &c.pro, &c.pub, &c.merge, &c.store);
-    const SkLayout lay(grid, NU);
-    int64_t u0 = 0;
-    for (int g = 0; g < lay.G; ++g) {
-        // this group's units: up to the unit boundary nearest its share of the tiles (>= 1 unit per group)
-        int64_t u1 = NU;
-        if (g + 1 < lay.G) {
-            const int64_t target = total * lay.base(g + 1) / grid;
-            u1 = (int64_t)(std::lower_bound(ustart.begin(), ustart.end(), target) - ustart.begin());
-            if (u1 > 0 && u1 < NU && target - ustart[u1 - 1] < ustart[u1] - target) --u1;  // nearer boundary
-            u1 = std::max(u1, u0 + 1);
-            u1 = std::min(u1, NU - (lay.G - g - 1));
-        }
-        SkUnits U;  // the chunk as runs of equal-size units, relative tiles
-        const int64_t t0 = ustart[u0];
-        for (int64_t u = u0; u < u1; ++u) {
-            if (u == u0 || unt[u] != unt[u - 1] || U.nt.back() == 0) {
-                U.base.push_back(ustart[u] - t0);
-                U.nt.push_back(unt[u]);
-            }
-            U.total += unt[u];
-        }
-        const int nb = lay.size(g), b0 = lay.base(g);
-        std::vector<int64_t> rel(nb + 1);
-        sk_schedule_group(U, c, nb, rel.data());
-        for (int i = 0; i < nb; ++i) bounds[b0 + i] = t0 + rel[i];
-        u0 = u1;
-    }
-    bounds[grid] = total;
-    return RF_OK;
-}
 
 extern "C" int rf_attn_fwd_sched(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                                  void* o, int64_t ldo, const int32_t* problems, int n_problems, int n_heads,

@@ -42,11 +42,22 @@ int* device_error_word() {
     return g_dev_err_dev;
 }
 
-// word 1 of the same mapped allocation: the fp16 range flag (rf_f16_range_flag)
+// The fp16 range word the calling thread's launches raise: the word bound by rf_range_word_bind (one per frame,
+// the model's), else word 1 of the error allocation (the process-wide rf_f16_range_flag).  Thread-local: a render
+// issues all its launches from one thread, so two renders on two threads (or one after the other on one thread,
+// each binding its own word) never share a word.
+static thread_local int* g_bound_range = nullptr;
+
 int* range_word() {
+    if (g_bound_range) return g_bound_range;
     int* w = device_error_word();
     return w ? w + 1 : nullptr;
 }
+
+struct RangeWord {
+    volatile int* host;  // mapped, coherent: kernels store, the host reads with a plain load
+    int* dev;
+};
 
 // Hand-off flag epochs of the stream-K kernels (attention and GEMM/conv): every launch gets a fresh flag value,
 // so flags need no re-arm and no memset between launches.  Values are 1 + (counter mod 2^B) (B = 30, or
@@ -67,7 +78,12 @@ int next_epoch(void* flags, size_t bytes, hipStream_t st) {
     if (it == gen_of.end()) {
         gen_of.emplace(flags, gen);  // a new area is zero-filled by its owner (rf.h workspace contract)
     } else if (it->second != gen) {
-        (void)hipMemsetAsync(flags, 0, bytes, st);
+        // a failed re-zero would leave last generation's flags in place, where one can equal a new epoch: the
+        // generation stays unchanged and the launch is refused (0 is never an epoch; callers return the error)
+        if (hipMemsetAsync(flags, 0, bytes, st) != hipSuccess) {
+            set_error("stream-K flag area re-zero (hipMemsetAsync) failed at an epoch generation wrap");
+            return 0;
+        }
         it->second = gen;
     }
     return 1 + (int)(c & ((1ull << bits) - 1));
@@ -137,6 +153,50 @@ extern "C" int rf_f16_range_flag(void) {
 extern "C" int rf_clear_f16_range_flag(void) {
     rf::device_error_word();
     if (rf::g_dev_err_host) rf::g_dev_err_host[1] = 0;
+    return RF_OK;
+}
+
+extern "C" int rf_range_word_new(void** handle) {
+    RF_REQUIRE(handle, "rf_range_word_new: null handle pointer");
+    *handle = nullptr;
+    void* h = nullptr;
+    void* d = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess) {
+        rf::set_error("rf_range_word_new: hipHostMalloc failed");
+        return RF_ERR_LAUNCH;
+    }
+    memset(h, 0, 64);
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        (void)hipHostFree(h);
+        rf::set_error("rf_range_word_new: hipHostGetDevicePointer failed");
+        return RF_ERR_LAUNCH;
+    }
+    *handle = new rf::RangeWord{(volatile int*)h, (int*)d};
+    return RF_OK;
+}
+
+extern "C" int rf_range_word_bind(void* handle) {
+    rf::g_bound_range = handle ? ((rf::RangeWord*)handle)->dev : nullptr;
+    return RF_OK;
+}
+
+extern "C" int rf_range_word_read(void* handle) {
+    if (!handle) return rf_f16_range_flag();
+    return *((rf::RangeWord*)handle)->host;
+}
+
+extern "C" int rf_range_word_clear(void* handle) {
+    if (!handle) return rf_clear_f16_range_flag();
+    *((rf::RangeWord*)handle)->host = 0;
+    return RF_OK;
+}
+
+extern "C" int rf_range_word_free(void* handle) {
+    if (!handle) return RF_OK;
+    rf::RangeWord* r = (rf::RangeWord*)handle;
+    if (rf::g_bound_range == r->dev) rf::g_bound_range = nullptr;
+    (void)hipHostFree((void*)r->host);
+    delete r;
     return RF_OK;
 }
 

@@ -73,10 +73,9 @@ RF_DEV void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 RF_DEV float silu(float x) {
     return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
 }
-// libm expf + IEEE division.  Kept for the convolution epilogue: with the short form the 256x256 conv
-// kernel's register allocation changes and its main loop spills (6 scratch ops per K-step instead of 1:
-// 114 -> 186 us at the 256^2 DPT level), which costs far more than the epilogue saves.
-RF_DEV float silu_precise(float x) { return x / (1.0f + expf(-x)); }
+// (The conv epilogues use silu() too since round 4: the halo / c32 conv kernels that replaced the 256x256 engine
+// tile at the large DPT levels do not spill with it — scratch 0 in their resource usage — so the libm form that
+// once kept the 256x256 conv main loop from spilling is gone.)
 // The DPT head's output transforms on the hardware exp2 (~1 ulp, v_exp_f32): ELU's negative branch
 // alpha (e^y - 1) and the log decode 10^y - 1 (rendering_pipeline.py:119-123).  The libm expm1f / powf they
 // replace cost ~70 VALU per output value, a third of the fused-head conv's time; the difference is ~1e-7
@@ -172,6 +171,10 @@ struct SkLayout {
 
 // ------------------------------------------------------------------------- host side
 namespace rf {
+// stream-K attention geometry shared by the kernel (attention.hip) and its host schedule (attn_sched.cpp)
+constexpr int ATTN_KT = 64;         // keys per tile
+constexpr int ATTN_QB = 256;        // query rows per unit (8 waves x 32)
+constexpr int ATTN_MAX_GRID = 512;  // workgroups per launch (partial slots / flags in the workspace)
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 int* device_error_word();  // device pointer of the mapped error word (nullptr if it could not be allocated)

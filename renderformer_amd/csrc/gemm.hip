@@ -2768,16 +2768,19 @@ int launch_sk(EngineArgs a, int grid, void* stream, const char* what) {
     return rf::check_launch(what);
 }
 
-void sk_setup(EngineArgs& p, void* workspace, void* stream) {
+// RF_OK, or RF_ERR_LAUNCH when the flag area could not be re-zeroed at an epoch wrap (the launch must not run)
+int sk_setup(EngineArgs& p, void* workspace, void* stream) {
     p.sk_part = (float*)workspace;
     p.sk_flag = (int*)(p.sk_part + SK_PART_FLOATS);
     // flags from earlier launches never equal the current epoch (rf::next_epoch re-zeroes the area on a wrap)
     p.sk_epoch = rf::next_epoch(p.sk_flag, SK_MAX_GRID * sizeof(int), (hipStream_t)stream);
+    if (p.sk_epoch == 0) return RF_ERR_LAUNCH;
     p.err = rf::device_error_word();
     p.spin = rf::spin_limit();
     // diagnostics: stamps in the last 256 KiB of the partial area (tools/kbench.py skstamps)
     static const bool stamps = getenv("RF_GEMM_STAMPS") && atoi(getenv("RF_GEMM_STAMPS")) != 0;
     p.stamps = stamps ? (uint64_t*)(p.sk_part + SK_PART_FLOATS - 65536) : nullptr;
+    return RF_OK;
 }
 
 
@@ -3402,7 +3405,7 @@ static int launch_quad_s(EngineArgs a, int mode, void* workspace, int64_t ws_byt
     const int grid = (int)std::min<int64_t>(tiles, 256);
     a.group_m = pick_group_m(tiles_m, tiles_n, G::BM, G::BN, (grid + 7) / 8);
     if (mode == 2 && workspace && ws_bytes >= SK_WS_BYTES) {
-        sk_setup(a, workspace, stream);
+        if (const int rc = sk_setup(a, workspace, stream)) return rc;
         RF_LAUNCH((quad_kernel<WM, WN, EPI, NT, STG>), dim3(256), dim3(256), 0, (hipStream_t)stream, a);
     } else {
         a.sk_flag = nullptr;
@@ -3470,7 +3473,7 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
                    : run_quad<1>(p, epilogue, qm, workspace, ws_bytes, stream, "rf_gemm_bf16");
     }
     if (workspace && ws_bytes >= SK_WS_BYTES && skph(m, n, k)) {
-        sk_setup(p, workspace, stream);
+        if (const int rc = sk_setup(p, workspace, stream)) return rc;
         const int64_t tiles = (int64_t)((m + 255) / 256) * (n / 256);
         p.persist = tiles % 256 == 0 && persist_on();  // whole tiles per block either way: prefetching form
         if (f16) {
@@ -3493,7 +3496,7 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
     const bool big = cfg != 128;
     const int grid = (!big && workspace && ws_bytes >= SK_WS_BYTES) ? sk_grid(m, n, k) : 0;
     if (grid) {
-        sk_setup(p, workspace, stream);
+        if (const int rc = sk_setup(p, workspace, stream)) return rc;
         switch (epilogue) {
             case RF_EPI_BF16: return launch_sk<T128, E_BF16>(p, grid, stream, "rf_gemm_bf16");
             case RF_EPI_F32: return launch_sk<T128, E_F32>(p, grid, stream, "rf_gemm_bf16");
@@ -3504,7 +3507,7 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
     // 256x256 tiles at one 512-thread block per CU reach ~1.2 PF/s when every CU has work; when the tile count
     // would leave a ragged last round, stream-K the K loop over exactly 256 blocks instead.
     if (workspace && ws_bytes >= SK_WS_BYTES && n % 256 == 0 && sk256(m, n, k)) {
-        sk_setup(p, workspace, stream);
+        if (const int rc = sk_setup(p, workspace, stream)) return rc;
         switch (epilogue) {
             case RF_EPI_BF16: return launch_sk<T256, E_BF16>(p, 256, stream, "rf_gemm_bf16");
             case RF_EPI_F32: return launch_sk<T256, E_F32>(p, 256, stream, "rf_gemm_bf16");
@@ -3740,7 +3743,7 @@ static int conv_dispatch(EngineArgs& p, bool gather, bool big, int64_t sk_grid_n
             return gather ? conv_f16_dp<true>(p, stream, what, tile) : conv_f16_dp<false>(p, stream, what, tile);
     }
     if (sk_grid_n) {
-        sk_setup(p, workspace, stream);
+        if (const int rc = sk_setup(p, workspace, stream)) return rc;
         // fp16 convolutions stream-K over the 8-wave 128x128 tile (64^2 / 32^2 DPT levels: 1.6x / 2.1x)
         if (NT == P_F16 && !(getenv("RF_CONV_SKW8") && atoi(getenv("RF_CONV_SKW8")) == 0))
             return gather ? launch_sk<T128w8, E_CONV, NT, true>(p, (int)sk_grid_n, stream, what)
@@ -3817,7 +3820,7 @@ static int conv_common(EngineArgs& p, int nterm, bool gather, const void* w_hi, 
         const int64_t tiles = (int64_t)((p.m + 63) / 64) * (p.n / 64);
         const int64_t grid = std::min<int64_t>(512, tiles * (p.k / BK) / 12);
         if (grid > tiles) {
-            sk_setup(p, workspace, stream);
+            if (const int rc = sk_setup(p, workspace, stream)) return rc;
             return gather ? launch_sk<T64c, E_CONV, P_F16, true>(p, (int)grid, stream, what)
                           : launch_sk<T64c, E_CONV, P_F16, false>(p, (int)grid, stream, what);
         }

@@ -14,12 +14,15 @@ kernels receive per-problem row ranges.  The residual streams are fp32; the
 projection GEMMs take fp16 operands (RMSNorm / SwiGLU / attention outputs and
 weights; ``operands="bf16"`` selects bf16), attention q/k/v are bf16 with an fp32
 softmax, and the DPT convolutions take fp16 operands with fp32 accumulation.
-fp16 operands are range-checked on the device (every fp16 writer raises a flag on
-|x| > 65504; ``range_check``): a frame that overflowed is rendered again
-with bf16 operands, or reported as a DeviceError in the deferred mode.
+fp16 operands are range-checked on the device (every fp16 writer raises a word of the
+frame's own on |x| > 65504; ``range_check``): a frame that overflowed is rendered again
+with bf16 operands (bf16x3 DPT planes), or reported as a DeviceError in the deferred mode.
+The check never blocks ``render``: the default ("lazy") reads a frame's word once its end
+event has completed (at a later render, ``resolve(out)`` or ``check_range()``).
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 from dataclasses import dataclass
@@ -265,7 +268,20 @@ class PrecisionWarning(UserWarning):
     pass
 
 
-RANGE_CHECKS = ("sync", "deferred", "off")
+RANGE_CHECKS = ("lazy", "sync", "deferred", "off")
+RANGE_WORDS_MAX = 8  # frames with an unresolved range word per model; the oldest is resolved (waited for) beyond
+
+
+class _Frame:
+    """A rendered frame whose fp16 range word is not yet read: the word, the frame's end event and stream, the
+    output tensor, a replay closure (the same render with the texture already log-encoded) and the inputs'
+    version counters (an input edited in place since the render cannot be replayed)."""
+    __slots__ = ("word", "event", "stream", "out", "replay", "inputs", "versions")
+
+    def __init__(self, word, event, stream, out, replay, inputs):
+        self.word, self.event, self.stream, self.out, self.replay = word, event, stream, out, replay
+        self.inputs = inputs
+        self.versions = [t._version for t in inputs]
 
 
 def _hf_cache_snapshot(model_id: str) -> Optional[str]:
@@ -296,16 +312,21 @@ class RenderFormer:
                  view_chunk: Optional[int] = None, operands: Optional[str] = None,
                  range_check: Optional[str] = None):
         self.config = config
-        # fp16 range check (RF_RANGE_CHECK): the fp16-writing kernels raise a host-mapped flag on |x| > 65504 (inf included)
-        # (a checkpoint whose activations exceed fp16's range).  "sync" (default): after each frame the host waits for
-        # THAT frame's end event (no device sync) and reads the flag; an overflowed frame is rendered again with bf16
-        # operands, which the model then keeps (PrecisionWarning).  "deferred": no wait per frame (bench.py's timed
-        # loop); check_range() — called after a synchronize, and at the start of the next render — raises DeviceError
-        # for an overflowed frame.  "off": no check.
-        self.range_check = range_check or os.environ.get("RF_RANGE_CHECK", "sync")
+        # fp16 range check (RF_RANGE_CHECK).  Every render binds a host-mapped word of its own (rf_range_word_bind)
+        # that the fp16-writing kernels raise on |x| > 65504 (inf included): a checkpoint whose activations exceed
+        # fp16's range.  Concurrent renders (streams, models, threads) never share a word.
+        #   "lazy" (default): render returns without waiting; the word is read once the frame's end event has
+        #     completed — at the start of a later render (non-blocking), in resolve(out) or check_range() (waiting).
+        #     An overflowed frame is rendered again IN PLACE (same output tensor, same stream) with bf16 projection
+        #     operands (code 1/2/4) and/or bf16x3 DPT planes (code 8), which the model keeps (PrecisionWarning).
+        #   "sync": render waits for its own frame's end event (no device sync) and re-renders before returning.
+        #   "deferred": like lazy, but an overflow raises DeviceError (bench.py's timed loop).   "off": no check.
+        self.range_check = range_check or os.environ.get("RF_RANGE_CHECK", "lazy")
         if self.range_check not in RANGE_CHECKS:
             raise ValueError(f"range_check must be one of {RANGE_CHECKS}")
         self.range_fallbacks = 0  # frames rendered again with bf16 operands after an fp16 overflow
+        self._range_free: List[int] = []  # range-word handles not in use
+        self._range_pending: List[_Frame] = []  # frames whose word is unread, oldest first
         # render_views: stage 2 + DPT over at most view_chunk views per pass (stage 1 once per scene); None = all
         # views of the batch in one pass.  A fixed chunk makes each view's image independent of the batching.
         self.view_chunk = view_chunk if view_chunk is not None else (int(os.environ.get("RF_VIEW_CHUNK", "0")) or None)
@@ -686,57 +707,141 @@ class RenderFormer:
         caller (the reference's own infer.py places the model on cuda:1, infer.py:43)."""
         self._require()
         with torch.cuda.device(self._device):
-            self._range_enter()
-            out = self._render_views(triangles, texture, mask, vn, c2w, fov, resolution, log_encode)
-            if self._range_overflowed():
-                # the texture was log-encoded in place by the first render: the second one must not encode again
-                out = self._render_views(triangles, texture, mask, vn, c2w, fov, resolution, False)
-            return out
+            # the replay (an fp16 overflow's re-render) must not log-encode the texture a second time
+            return self._guarded(
+                lambda: self._render_views(triangles, texture, mask, vn, c2w, fov, resolution, log_encode),
+                lambda: self._render_views(triangles, texture, mask, vn, c2w, fov, resolution, False),
+                (triangles, texture, mask, vn, c2w, fov))
 
     # ------------------------------------------------------------------ fp16 range check
     def _range_active(self) -> bool:
-        return self.operands == "f16" and self.range_check != "off"
+        return (self.operands == "f16" or self.dpt_precision == "f16") and self.range_check != "off"
 
-    def _range_enter(self):
+    def _guarded(self, run, replay, inputs):
+        """Run one render under a range word of its own; resolve it now (sync) or later (lazy / deferred)."""
         if not self._range_active():
-            return
-        if self.range_check == "deferred":
-            self.check_range()  # an earlier deferred frame (its completion already observed) overflowed: raise
-        else:
-            ops.clear_f16_range_flag()
-
-    def check_range(self):
-        """Deferred mode: raise DeviceError if a frame rendered with fp16 operands overflowed fp16's range.  Reads
-        the host-mapped flag without a device sync, so call it after the frames in question have completed (e.g.
-        after torch.cuda.synchronize())."""
-        if self._range_active() and ops.f16_range_flag():
-            code = ops.f16_range_flag()
-            ops.clear_f16_range_flag()
-            from ._lib import DeviceError
-            raise DeviceError(f"fp16 operand overflow (range flag {code}: |x| > 65504 in an fp16 operand) -- "
-                              "this checkpoint's activations exceed fp16's range: render with operands='bf16' "
-                              "(RF_OPERANDS=bf16) or range_check='sync' (re-renders such frames in bf16)")
-
-    def _range_overflowed(self) -> bool:
-        """sync mode: wait for this frame's end event (host-side, no device sync), read the flag; on overflow switch
-        the projections to bf16 operands for good and return True (the caller renders the frame again)."""
-        if not self._range_active() or self.range_check != "sync":
-            return False
+            return run()
+        self._range_poll()
+        lib = _load_lib()
+        word = self._range_free.pop() if self._range_free else None
+        if word is None:
+            h = ctypes.c_void_p()
+            if lib.rf_range_word_new(ctypes.byref(h)) != 0:
+                raise RuntimeError(f"rf_range_word_new: {lib.rf_last_error().decode(errors='replace')}")
+            word = h.value
+        lib.rf_range_word_clear(word)
+        lib.rf_range_word_bind(word)
+        try:
+            out = run()
+        finally:
+            lib.rf_range_word_bind(None)
+        stream = torch.cuda.current_stream()
         ev = torch.cuda.Event()
-        ev.record()
-        ev.synchronize()
-        code = ops.f16_range_flag()
+        ev.record(stream)
+        fr = _Frame(word, ev, stream, out, replay, inputs)
+        if self.range_check == "sync":
+            self._range_resolve(fr, wait=True)
+        else:
+            self._range_pending.append(fr)
+            if len(self._range_pending) > RANGE_WORDS_MAX:
+                self._range_resolve(self._range_pending.pop(0), wait=True)
+        return out
+
+    def _range_poll(self):
+        """Resolve (oldest first) the pending frames whose end event has completed: no host wait."""
+        while self._range_pending and self._range_pending[0].event.query():
+            self._range_resolve(self._range_pending.pop(0), wait=False)
+
+    def _range_resolve(self, fr: _Frame, wait: bool) -> bool:
+        """Read a frame's word (after its end event); on an overflow fall back and re-render it in place (lazy /
+        sync) or raise DeviceError (deferred).  Returns True if the frame was rendered again."""
+        from ._lib import DeviceError
+        if wait:
+            fr.event.synchronize()
+        lib = _load_lib()
+        code = int(lib.rf_range_word_read(fr.word))
+        self._range_free.append(fr.word)
         if not code:
             return False
         import warnings
-        warnings.warn(f"fp16 operand overflow (range flag {code}): this checkpoint's activations exceed fp16's range; "
-                      "the frame is rendered again and the model keeps bf16 projection operands from now on",
-                      PrecisionWarning, stacklevel=3)
-        ops.clear_f16_range_flag()
-        self.operands = "bf16"
+        what = [n for n, bit in (("GEMM", 1), ("RMSNorm", 2), ("attention", 4), ("DPT plane", 8)) if code & bit]
+        if self.range_check == "deferred":
+            raise DeviceError(f"fp16 operand overflow (range code {code}: |x| > 65504 in an fp16 {'/'.join(what)} "
+                              "output) -- this checkpoint's activations exceed fp16's range: render with "
+                              "operands='bf16' (RF_OPERANDS=bf16) and dpt_precision='bf16x3', or range_check='lazy' "
+                              "/ 'sync' (re-renders such frames)")
+        if any(t._version != v for t, v in zip(fr.inputs, fr.versions)):
+            raise DeviceError(f"fp16 operand overflow (range code {code}) in a frame whose inputs were modified in "
+                              "place before it could be rendered again: call resolve(out) / check_range() before "
+                              "reusing input buffers, or use range_check='sync'")
+        # projections and attention (codes 1/2/4) -> bf16 operands; the DPT planes (code 8) -> bf16x3, and a stage-1
+        # or stage-2 overflow reaches the DPT as inf too, so it sets 8 as well
+        if code & 7:
+            self.operands = "bf16"
+        if code & 8 and self.dpt_precision == "f16":
+            self.dpt_precision = "bf16x3"
         self._w = _DeviceWeights(self.config, self._sd, self._device, self.dpt_precision, self.operands)
         self.range_fallbacks += 1
+        warnings.warn(f"fp16 operand overflow (range code {code}: {'/'.join(what)}): this checkpoint's activations "
+                      f"exceed fp16's range; the frame is rendered again and the model keeps "
+                      f"{self.operands} projection operands and {self.dpt_precision} DPT planes from now on",
+                      PrecisionWarning, stacklevel=4)
+        with torch.cuda.device(self._device), torch.cuda.stream(fr.stream):
+            new = self._guarded_replay(fr.replay)
+            fr.out.copy_(new.view_as(fr.out))
+        fr.out._rf_rerendered = True  # resolve(out) reports it even when a later render's poll did the re-render
         return True
+
+    def _guarded_replay(self, replay):
+        """The re-render after a fallback, checked at once: an overflow that survives it is an error."""
+        from ._lib import DeviceError
+        if not self._range_active():
+            return replay()
+        lib = _load_lib()
+        h = ctypes.c_void_p()
+        if lib.rf_range_word_new(ctypes.byref(h)) != 0:
+            raise RuntimeError(f"rf_range_word_new: {lib.rf_last_error().decode(errors='replace')}")
+        lib.rf_range_word_bind(h.value)
+        try:
+            out = replay()
+        finally:
+            lib.rf_range_word_bind(None)
+        torch.cuda.current_stream().synchronize()
+        code = int(lib.rf_range_word_read(h.value))
+        lib.rf_range_word_free(h.value)
+        if code:
+            raise DeviceError(f"fp16 overflow (range code {code}) persists after the bf16 fallback")
+        return out
+
+    def resolve(self, out: Optional[torch.Tensor] = None) -> bool:
+        """Finish the range check of the frame whose output is ``out`` (every pending frame if None), waiting for
+        it: afterwards ``out`` holds the final frame (rendered again if it overflowed fp16).  Returns True if a
+        frame was rendered again.  batch_infer.py calls it where it already waits for the frame's copy."""
+        keep, done = [], []
+        for fr in self._range_pending:
+            (done if out is None or fr.out is out else keep).append(fr)
+        self._range_pending = keep
+        for fr in done:
+            self._range_resolve(fr, wait=True)
+        redo = False
+        for t in ([fr.out for fr in done] if out is None else [out]):
+            if getattr(t, "_rf_rerendered", False):
+                t._rf_rerendered = False
+                redo = True
+        return redo
+
+    def check_range(self):
+        """Resolve every pending frame (waiting for each): deferred mode raises DeviceError for an overflowed frame,
+        lazy mode re-renders it in place.  Call before reading frames whose range check is pending."""
+        pending, self._range_pending = self._range_pending, []
+        for i, fr in enumerate(pending):
+            try:
+                self._range_resolve(fr, wait=True)
+            except BaseException:
+                for rest in pending[i + 1:]:  # the others' words stay usable
+                    rest.event.synchronize()
+                    self._range_free.append(rest.word)
+                raise
 
     @property
     def precision(self) -> str:
@@ -803,12 +908,8 @@ class RenderFormer:
         """Reference signature (renderformer.py:171-206).  Returns ELU'd log-space images [B, V, C, H, W]."""
         self._require()
         with torch.cuda.device(self._device):
-            self._range_enter()
-            out = self._forward(tri_vpos_list, texture_patch_list, valid_mask, vns, rays_o, rays_d, tri_vpos_view_tf)
-            if self._range_overflowed():
-                out = self._forward(tri_vpos_list, texture_patch_list, valid_mask, vns, rays_o, rays_d,
-                                    tri_vpos_view_tf)
-            return out
+            args = (tri_vpos_list, texture_patch_list, valid_mask, vns, rays_o, rays_d, tri_vpos_view_tf)
+            return self._guarded(lambda: self._forward(*args), lambda: self._forward(*args), args)
 
     def _forward(self, tri_vpos_list, texture_patch_list, valid_mask, vns, rays_o, rays_d, tri_vpos_view_tf):
         cfg, dev = self.config, self._device

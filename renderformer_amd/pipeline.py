@@ -17,8 +17,9 @@ within the 1e-3 relative-L2 parity budget of the reference CPU fp32 output at ev
 BASELINE configuration (tests/test_parity_gpu.py).  The argument is validated
 exactly like the reference; ``torch.float32`` (which in the reference selects
 fp32 stage-1 arithmetic) emits a one-time ``PrecisionWarning`` saying so, and
-``last_precision`` records what ran (``RenderFormer.precision``, read after the
-frame, so an fp16-overflow fallback to bf16 shows).
+``last_precision`` records what ran (``RenderFormer.precision``; refreshed by
+``resolve`` / ``check_range``, so an fp16-overflow fallback to bf16 shows once the
+frame's range check has run — ``render`` returns before the frame completes).
 """
 from __future__ import annotations
 
@@ -71,9 +72,24 @@ class RenderFormerRenderingPipeline:
         self.last_precision = {"requested": str(torch_dtype), "computed": self.model.precision}
         return out
 
+    def resolve(self, out=None) -> bool:
+        """RenderFormer.resolve: finish the fp16 range check of the frame ``out`` (every pending frame if None),
+        waiting for it; an overflowed frame is rendered again in place.  ``render`` itself never waits (like the
+        reference's, rendering_pipeline.py:105-125): call this (or ``check_range``) before reading frames when the
+        model's range_check is "lazy" and the checkpoint may exceed fp16's range."""
+        redo = self.model.resolve(out)
+        if self.last_precision is not None:
+            self.last_precision["computed"] = self.model.precision
+        return redo
+
     def check_range(self):
-        """RenderFormer.check_range (deferred fp16 range check): raise DeviceError if a completed frame overflowed."""
-        self.model.check_range()
+        """RenderFormer.check_range: resolve every pending frame (deferred mode: raise DeviceError if one
+        overflowed; lazy: re-render it in place)."""
+        try:
+            self.model.check_range()
+        finally:
+            if self.last_precision is not None:
+                self.last_precision["computed"] = self.model.precision
 
     def __call__(self, *args, **kwargs):
         return self.render(*args, **kwargs)

@@ -309,6 +309,53 @@ def test_f16_range_flag_writers():
     assert flag_after(lambda: split(xs * 1e6)) != 0
 
 
+def test_range_words_are_per_render():
+    """rf_range_word_* (ABI 14): a bound word collects exactly the overflows of the launches issued while it is
+    bound on this thread; another word and the process-wide word stay clear; unbinding returns to the process
+    word; a word bound on another thread does not capture this thread's launches."""
+    import ctypes
+    import threading
+    from renderformer_amd import _lib, ops
+    lib = _lib.load()
+    ops.clear_f16_range_flag()
+    words = []
+    for _ in range(2):
+        h = ctypes.c_void_p()
+        assert lib.rf_range_word_new(ctypes.byref(h)) == 0 and h.value
+        words.append(h.value)
+    wa, wb = words
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randn(64, 1024, generator=g).to(dev)
+    h16 = torch.empty(64, 1024, device=dev, dtype=torch.float16)
+    big = torch.full((1024,), 1e5, device=dev)
+    lib.rf_range_word_bind(wa)
+    ops.rmsnorm(x, big, 1e-6, h16)                               # overflows: raises word A
+    lib.rf_range_word_bind(wb)
+    ops.rmsnorm(x, torch.ones(1024, device=dev), 1e-6, h16)      # in range: word B stays 0
+    seen = {}
+
+    def other_thread():  # this thread's binding is B; a launch from a thread with nothing bound -> process word
+        ops.rmsnorm(x, big, 1e-6, h16)
+        torch.cuda.synchronize()
+        seen["global"] = ops.f16_range_flag()
+    t = threading.Thread(target=other_thread)
+    t.start()
+    t.join()
+    lib.rf_range_word_bind(None)
+    torch.cuda.synchronize()
+    assert lib.rf_range_word_read(wa) == 2 and lib.rf_range_word_read(wb) == 0
+    assert seen["global"] == 2
+    ops.clear_f16_range_flag()
+    ops.rmsnorm(x, big, 1e-6, h16)                               # unbound again: the process word
+    torch.cuda.synchronize()
+    assert ops.f16_range_flag() == 2 and lib.rf_range_word_read(wa) == 2
+    lib.rf_range_word_clear(wa)
+    assert lib.rf_range_word_read(wa) == 0
+    ops.clear_f16_range_flag()
+    for w in words:
+        assert lib.rf_range_word_free(w) == 0
+
+
 def test_gemm_asymmetric_identity():
     """A = I with an asymmetric W catches a transposed C write (guide §3)."""
     ops = _ops()

@@ -20,6 +20,9 @@
 #                    quad GEMM study leg, then a kernel-trace profile of the default bench
 #   vpmc [legs]      kbench legs (default: vendor) under FETCH / WRITE / L2-hit / MFMA-busy counter passes
 #   convab           halo2 vs conv3x3_hk_kernel on the 512^2 / 256^2 DPT convolutions
+#   libab            the current library vs $BASE (default renderformer_amd/lib/librfhip_base.so, a build of another
+#                    tree): GPU tests on the current one, then interleaved stage-1 attention timings, per-role stamps
+#                    and bench runs of both (RF_LIB selects the library)
 #   vendor           kernel-trace of the vendor GEMM library vs the engine on the frame's projection shapes
 #                    (tools/kbench.py vendor: study only, nothing of it is linked into librfhip)
 # Every GPU step runs under its own timeout and the steps are chained with && (set -e): the first failure
@@ -112,6 +115,19 @@ vpmc)  # kbench legs ($@, default vendor) under counter passes (FETCH / WRITE / 
     done ;;
 convab)  # the 512^2 / 256^2 DPT convolutions on halo2 vs conv3x3_hk_kernel
     KB_F16_ONLY=1 KB_CONV_HW=512,256 KB_CONV_TILES=h2,hk timeout -k 10 300 python -u tools/kbench.py conv > $O/convab.log 2>&1 ;;
+libab)
+    BASE=${BASE:-$R/renderformer_amd/lib/librfhip_base.so}
+    timeout -k 10 900 $T tests -m gpu > $O/tests.log 2>&1
+    for i in 1 2; do
+        ABL=0 timeout -k 10 200 python -u tools/attn_ablate.py > $O/attn_new$i.log 2>&1
+        ABL=0 RF_LIB=$BASE timeout -k 10 200 python -u tools/attn_ablate.py > $O/attn_base$i.log 2>&1
+    done
+    timeout -k 10 120 python tools/attn_ablate.py stamps > $O/stamps_new.log 2>&1
+    RF_LIB=$BASE timeout -k 10 120 python tools/attn_ablate.py stamps > $O/stamps_base.log 2>&1
+    for i in 1 2; do
+        timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_new$i.json 2>> $O/bench.err
+        RF_LIB=$BASE timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_base$i.json 2>> $O/bench.err
+    done ;;
 vendor)
     prof_run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/vend -o run -- python3 $R/tools/kbench.py vendor > $O/vendor.log 2>&1 ;;
 *)
