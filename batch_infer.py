@@ -25,6 +25,7 @@ import glob
 import os
 import re
 import sys
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -79,11 +80,97 @@ LOADERS = 3  # batches decoded ahead (threads)
 WRITERS = 4  # image encode/write threads
 
 
+class StageTimes:
+    """Per-stage host time of the data path (RF_BATCH_PROFILE=1; tools/batch_e2e.py): seconds summed over the
+    threads that ran each stage, plus the main thread's wall time blocked in each wait."""
+
+    def __init__(self):
+        import threading
+        self.on = os.environ.get("RF_BATCH_PROFILE", "0") != "0"
+        self.t = {}
+        self.n = {}
+        self._lock = threading.Lock()
+
+    def add(self, name, dt):
+        if self.on:
+            with self._lock:
+                self.t[name] = self.t.get(name, 0.0) + dt
+                self.n[name] = self.n.get(name, 0) + 1
+
+    def timed(self, name, fn, *a, **k):
+        if not self.on:
+            return fn(*a, **k)
+        t0 = time.perf_counter()
+        try:
+            return fn(*a, **k)
+        finally:
+            self.add(name, time.perf_counter() - t0)
+
+    def summary(self):
+        return {k: {"s": round(v, 4), "calls": self.n[k]} for k, v in sorted(self.t.items())}
+
+
+STAGES = StageTimes()
+
+
 def _load_batch(files, idx, padding_length, pin):
-    items = [load_scene(files[i], padding_length, None if pin else torch.float32) for i in idx]
-    host = collate(items)
     if pin:
-        host = {k: v.pin_memory() for k, v in host.items()}
+        return _load_batch_pinned(files, idx, padding_length)
+    items = [STAGES.timed("load: HDF5 read + inflate", load_scene, files[i], padding_length, torch.float32)
+             for i in idx]
+    host = STAGES.timed("load: collate", collate, items)
+    return items, host
+
+
+def _load_batch_pinned(files, idx, padding_length, pinned: bool = True):
+    """The batch's tensors allocated once in pinned host memory (torch's caching host allocator) with every scene
+    decoded straight into its slot (h5io read(out=)): no per-scene array, no collate stack and no pin_memory()
+    copy -- those two full copies of the ~150-300 MB texture were a third of a scene's host time.  Same result as
+    collate(load_scene(...)) + pin_memory(): the file's texture dtype, zero padding rows, padded mask False."""
+    t0 = time.perf_counter()
+    fs = [File(files[i]) for i in idx]
+    try:
+        ns = [f["triangles"].shape[0] for f in fs]
+        if padding_length is not None:
+            for i, n in zip(idx, ns):
+                if padding_length < n:
+                    raise ValueError(f"{files[i]}: {n} triangles exceed --padding_length {padding_length}")
+            N = padding_length
+        else:
+            if len(set(ns)) > 1:
+                raise ValueError("scenes in one batch differ in shape: pass --padding_length (as the reference requires)")
+            N = ns[0]
+        views = {f["c2w"].shape[0] for f in fs}
+        if len(views) > 1:
+            raise ValueError("scenes in one batch differ in shape: pass --padding_length (as the reference requires)")
+        B, V = len(fs), views.pop()
+        tex_ds = [f["texture"] for f in fs]
+        tdt = {torch.from_numpy(np.empty(0, dtype=d.dtype)).dtype for d in tex_ds}
+        if len(tdt) > 1:
+            raise ValueError("scenes in one batch store textures of different dtypes")
+        pin = dict(pin_memory=pinned)  # (pinned=False: the same decode into pageable memory, for CPU tests)
+        host = {"triangles": torch.zeros(B, N, 3, 3, dtype=torch.float32, **pin),
+                "texture": torch.empty(B, N, *tex_ds[0].shape[1:], dtype=tdt.pop(), **pin),
+                "mask": torch.zeros(B, N, dtype=torch.bool, **pin),
+                "c2w": torch.empty(B, V, 4, 4, dtype=torch.float32, **pin),
+                "fov": torch.empty(B, V, dtype=torch.float32, **pin),
+                "vn": torch.zeros(B, N, 3, 3, dtype=torch.float32, **pin)}
+        items = []
+        for b, (f, n) in enumerate(zip(fs, ns)):
+            tex = host["texture"][b]
+            tex_ds[b].read(out=tex[:n].numpy())
+            if n < N:
+                tex[n:].zero_()
+            host["triangles"][b, :n] = torch.from_numpy(np.array(f["triangles"])).float()
+            host["vn"][b, :n] = torch.from_numpy(np.array(f["vn"])).float()
+            host["c2w"][b] = torch.from_numpy(np.array(f["c2w"]).astype(np.float32))
+            host["fov"][b] = torch.from_numpy(np.array(f["fov"]).astype(np.float32).reshape(V))
+            host["mask"][b, :n] = True
+            items.append({"file_path": files[idx[b]]})
+    finally:
+        for f in fs:
+            f.close()
+    STAGES.add("load: HDF5 read + inflate into pinned", time.perf_counter() - t0)
     return items, host
 
 
@@ -130,7 +217,7 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
                 ahead.append(pool.submit(_load_batch, files, batches[nxt_batch], args.padding_length, True))
                 nxt_batch += 1
             try:
-                return fut.result()
+                return STAGES.timed("main: wait for loader", fut.result)
             except BaseException as e:  # surfaced on the main thread
                 return e
 
@@ -151,7 +238,7 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
             compute.wait_stream(h2d)
             for v in batch.values():  # allocated on the copy stream, used on the compute stream
                 v.record_stream(compute)
-            imgs = render(batch, host)
+            imgs = STAGES.timed("main: render issue (plan + launches)", render, batch, host)
             # the result goes back on its own stream right behind this batch, not behind the next one
             d2h.wait_stream(compute)
             with torch.cuda.stream(d2h):
@@ -163,10 +250,10 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
             nxt = (items, out, copied, host, imgs)  # `host` (pinned inputs) lives until this batch is yielded
         if pending is not None:  # batch i is handed out while batch i+1 renders
             p_items, p_out, p_copied, _, p_imgs = pending
-            p_copied.synchronize()
+            STAGES.timed("main: wait for frame + D2H", p_copied.synchronize)
             # the frame is complete: its fp16 range check reads a host word (no wait); a frame that overflowed is
             # rendered again in place, and copied back again
-            if resolve is not None and resolve(p_imgs):
+            if resolve is not None and STAGES.timed("main: range check", resolve, p_imgs):
                 p_out.copy_(p_imgs)
             yield p_items, p_out
         if nxt is None:
@@ -214,15 +301,18 @@ def main(argv=None):
         for i, it in enumerate(items):
             base = os.path.splitext(os.path.basename(it["file_path"]))[0]
             if writers is None:
-                save_views(imgs[i], output_dir, base)
+                save_views(imgs[i], output_dir, base, STAGES)
             else:  # EXR/PNG encode + write off the render loop (zlib releases the GIL)
-                pending.append(writers.submit(save_views, imgs[i], output_dir, base))
+                pending.append(writers.submit(save_views, imgs[i], output_dir, base, STAGES))
             n_frames += imgs.shape[1]
     if writers is not None:
         for f in pending:
-            f.result()  # re-raises a writer's error
+            STAGES.timed("main: wait for writers", f.result)  # re-raises a writer's error
         writers.shutdown()
     print(f"Output saved to: {output_dir} ({n_frames} frames on rank {rank}/{world})")
+    if STAGES.on:
+        import json
+        print("stage times:", json.dumps(STAGES.summary()), flush=True)
     if args.save_video:
         print("video.mp4 not written: no mp4 encoder in this environment (frames are saved as PNG)")
     return 0

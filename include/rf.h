@@ -78,6 +78,11 @@ extern "C" {
 
 const char* rf_last_error(void);
 int rf_abi_version(void);
+/* Build flags: RF_BUILD_STUDY set in the study build (librfhip_study.so: the measured-slower alternatives and
+ * ablation variants -- legacy split-KV attention, the one-wave-per-SIMD attention, the 4-wave GEMM, the 4-wave
+ * conv -- kept for A/B studies); the production librfhip.so refuses them with RF_ERR_UNSUPPORTED. */
+#define RF_BUILD_STUDY 1
+int rf_build_flags(void);
 
 /* Device-side error word.  A stream-K owner (GEMM or attention) whose partner's partial does not arrive within
  * the spin bound (env RF_SPIN_LIMIT polls, default 2^24; code 1 GEMM, 2 attention), a stream-K launch handed a

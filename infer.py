@@ -48,15 +48,19 @@ def load_pipeline(args) -> RenderFormerRenderingPipeline:
     return pipe.to("cuda")
 
 
-def save_views(hdr: torch.Tensor, output_dir: str, base_name: str) -> list:
-    """hdr [nv, H, W, 3] -> {base}_view_{i}.exr / .png (infer.py:89-103)."""
+def save_views(hdr: torch.Tensor, output_dir: str, base_name: str, stages=None) -> list:
+    """hdr [nv, H, W, 3] -> {base}_view_{i}.exr / .png (infer.py:89-103).  `stages`: batch_infer.StageTimes."""
     paths = []
     for i in range(hdr.shape[0]):
         img = hdr[i].cpu().numpy().astype("float32")
         hdr_path = os.path.join(output_dir, f"{base_name}_view_{i}.exr")
         ldr_path = os.path.join(output_dir, f"{base_name}_view_{i}.png")
-        write_exr(hdr_path, img)
-        write_png(ldr_path, hdr_to_ldr(img))
+        if stages is None:
+            write_exr(hdr_path, img)
+            write_png(ldr_path, hdr_to_ldr(img))
+        else:
+            stages.timed("write: EXR", write_exr, hdr_path, img)
+            stages.timed("write: PNG", lambda: write_png(ldr_path, hdr_to_ldr(img)))
         paths += [hdr_path, ldr_path]
     return paths
 

@@ -166,6 +166,8 @@ def load(require_device: bool = True):
             lib.rf_last_error.restype = ctypes.c_char_p
             lib.rf_last_error.argtypes = []
             lib.rf_abi_version.restype = ctypes.c_int
+            lib.rf_build_flags.restype = ctypes.c_int
+            lib.rf_build_flags.argtypes = []
             lib.rf_attn_workspace_bytes.restype = ctypes.c_int64
             lib.rf_gemm_workspace_bytes.restype = ctypes.c_int64
             lib.rf_gemm_workspace_bytes.argtypes = []
@@ -181,6 +183,12 @@ def load(require_device: bool = True):
     if require_device and not torch.cuda.is_available():
         raise HipLibraryError("renderformer_amd needs a HIP device (MI355X); none is visible")
     return _lib
+
+
+def study_build() -> bool:
+    """True for the study build of the library (rf_build_flags(): RF_BUILD_STUDY): the measured-slower kernels and
+    ablation variants are compiled only there; the production build refuses them (RF_ERR_UNSUPPORTED)."""
+    return bool(load(require_device=False).rf_build_flags() & 1)
 
 
 def call(name: str, *args) -> None:

@@ -478,6 +478,7 @@ RF_DEV void attn_wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+#ifdef RF_STUDY  // the legacy per-unit split-KV kernel: study build only (make study)
 __global__ __launch_bounds__(NW3 * 64, 1) void attn_v3_kernel(AttnArgs p) {
     __shared__ __attribute__((aligned(16))) char smem[NST3 * 2 * TILE_BYTES];  // 96 KiB
 
@@ -705,6 +706,8 @@ __global__ __launch_bounds__(NW3 * 64, 1) void attn_v3_kernel(AttnArgs p) {
         }
 }
 
+#endif  // RF_STUDY
+
 // ---------------------------------------------------------------------------------------------
 // Stream-K varlen kernel (rf_attn_fwd with n_split == 0, the default).
 //
@@ -731,6 +734,7 @@ __global__ __launch_bounds__(NW3 * 64, 1) void attn_v3_kernel(AttnArgs p) {
 //     max: the running max (exact on a piece's first tile) is only re-based (deferred rescale, guide
 //     T13) when a half-row sum of P(t) exceeds 2^12 (which bounds every P by 2^12), checked at the seam
 //     after A(t); that tile's P is then recomputed on the new base.
+
 constexpr int NW5 = 8;
 constexpr int QB5 = NW5 * 32;
 constexpr int K5 = 0;                  // K ring: 2 x 16 KiB
@@ -955,11 +959,8 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     };
     auto issue_v0 = [&]() { issue(vp, p.ldv, vstep, kt0, lds0 + V5); };
 
-    // nst: vector-memory stores this wave issued after the current piece's first loads (0, 8 O stores or 17
-    // partial stores; wave-uniform), the counted waits' allowance for them.  pend: the previous piece's partial
-    // is stored but its flag not raised; the flag goes up once every wave has passed a vmcnt(0) (the second
-    // barrier of this piece's first tile), so the store latency hides under this piece's loads and first tile.
-    int nst = 0;
+    // pend: the previous piece's partial is stored but its flag not raised; it goes up after this piece's first
+    // barrier, which every wave passes after a vmcnt(0) that covers both the piece's loads and those stores
     bool pend = false;
     auto raise_pend = [&]() {
         if (pend) {
@@ -976,19 +977,12 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     while (any) {  // one pass per piece; ends after the range's last piece
         uint64_t t_piece = 0;  // DBG & 32: piece prologue cycles -> stamp[6]
         if constexpr (DBG & 32) t_piece = __builtin_amdgcn_s_memtime();
-        // Q and K(t0) landed for this wave (K(t0+1), V(t0) and the nst stores may still be in flight) ...
-        const int nw = __builtin_amdgcn_readfirstlane(nst);
-        if (n > 1) {
-            if (nw == 17) attn_wait_vm<4 + 17>();
-            else if (nw == 8) attn_wait_vm<4 + 8>();
-            else attn_wait_vm<4>();
-        } else {
-            if (nw == 17) attn_wait_vm<2 + 17>();
-            else if (nw == 8) attn_wait_vm<2 + 8>();
-            else attn_wait_vm<2>();
-        }
+        // the piece's loads (Q, K(t0), K(t0+1), V(t0)) and the previous piece's stores, issued after them, completed
+        // for this wave: the wait is the longer of the two flights, not their sum ...
+        attn_wait_vm<0>();
         __builtin_amdgcn_s_barrier();  // ... and for every wave
         __builtin_amdgcn_sched_barrier(0);
+        raise_pend();  // every storing wave drained its partial stores before this barrier
         bf16x8 qf[8];
 #pragma unroll
         for (int st = 0; st < 8; ++st)
@@ -1086,20 +1080,10 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (DBG & 32) t_prev = __builtin_amdgcn_s_memtime();
             if constexpr (!(DBG & 2)) {
-                // K(t+1) and V(t) landed for this wave (the first tile: only the nst stores may stay in flight) ...
-                if (i == 0) {
-                    if (nw == 17) attn_wait_vm<17>();
-                    else if (nw == 8) attn_wait_vm<8>();
-                    else attn_wait_vm<0>();
-                } else {
-                    attn_wait_vm<0>();
-                }
+                attn_wait_vm<0>();             // K(t+1) and V(t) landed for this wave ...
                 __builtin_amdgcn_s_barrier();  // ... and for every wave; K(t) and V(t-1) are free
             }
             __builtin_amdgcn_sched_barrier(0);
-            // the second barrier of the piece for waves 0-3 and the third for 4-7: every wave has passed a vmcnt(0)
-            // since its stores (0-3 at tile 0's seam, 4-7 at tile 0's seam = this barrier's partner)
-            if (i == 1) raise_pend();
             stamp_at(0);
 
             const int koff = K5 + (PAR ^ 1) * TILE_BYTES;
@@ -1262,7 +1246,6 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         }
         if (i < n) body(i, std::integral_constant<int, 0>{}, sA, sB);
         if (!late) __builtin_amdgcn_s_barrier();  // re-align the groups' barrier counts
-        raise_pend();  // (a one-tile piece: this barrier is the one tile 1's top would have been)
 
         // ---- piece epilogue.  This piece's state first (the next piece's loads go out before its stores).
         // Register order: lane owns query (lane & 31), d = dt*32 + 8 gq + 4 half + 0..3
@@ -1270,8 +1253,8 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
         const bool e_cut = kt1 < nt;    // the unit continues in later workgroups: merge their partials
         const int64_t e_unit_end = unit_end;
         const bool e_active = active;
-        // O rows of this wave: a buffer window of its 32 rows (rows >= q1 land out of range and are dropped), so
-        // an active wave always issues exactly 8 O stores (the count the next piece's waits allow for)
+        // O rows of this wave: a buffer window of its 32 rows (rows >= q1 land out of range and are dropped: no
+        // per-lane branch around the stores)
         bf16_t* const e_orow = p.o + (int64_t)(q_start + q0 + wave * 32) * p.ldo + hoff;
         const int eln = opaque(lane);  // the epilogue's lane offsets are computed here, not hoisted
         const int e_ovalid = q0 + wave * 32 + (eln & 31) < q1;
@@ -1365,12 +1348,10 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ml), rs,
                                                       PIECE_O * 4 + (wave * 64 + eln) * 8, 0, 16);
             }
-            nst = e_active ? 17 : 0;
             pend = true;  // flag raised in the next piece's first tile, or after the loop
             if (!more) break;
             continue;
         }
-        nst = e_active ? 8 : 0;
         if (e_active) {
             const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
             const float inv = l_tot > 0.f ? 1.0f / l_tot : 0.f;
@@ -1423,6 +1404,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     }
 }
 
+#ifdef RF_STUDY  // the one-wave-per-SIMD stream-K kernel (10 % slower than attn_sk_kernel): study build only
 // ---------------------------------------------------------------------------------------------
 // One-wave-per-SIMD stream-K kernel (attn_p4_kernel): the unit decomposition, partial format and owner merge
 // of attn_sk_kernel, but 4 waves per workgroup, each owning 64 query rows (two 32-row sub-blocks qs = 0, 1)
@@ -1904,7 +1886,9 @@ __global__ __launch_bounds__(NW4 * 64, 1) void attn_p4_kernel(AttnArgs p) {
         }
     }
 }
+#endif  // RF_STUDY
 
+#ifdef RF_STUDY
 // merge split partials: out = sum_s 2^(m_s - M) O_s / sum_s 2^(m_s - M) l_s   (one wave per (row, head))
 __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restrict__ part_o,
                                                            const float* __restrict__ part_ml, int64_t part_rows,
@@ -1931,6 +1915,7 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
     dst[lane] = f32_to_bf16(a0 * inv);
     dst[lane + 64] = f32_to_bf16(a1 * inv);
 }
+#endif  // RF_STUDY
 
 constexpr float LOG2E = 1.4426950408889634f;
 
@@ -2006,14 +1991,22 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
         return rf::check_launch("rf_attn_fwd_dt");
     }
     if (getenv("RF_ATTN_P4") && atoi(getenv("RF_ATTN_P4")) == 1) {  // one-wave-per-SIMD kernel
+#ifdef RF_STUDY
         a.thr = getenv("RF_ATTN_THR") ? (float)atof(getenv("RF_ATTN_THR")) : P4_SUM_THR_LOG2;
         if (unit)
             RF_LAUNCH((attn_p4_kernel<true>), g, dim3(NW4 * 64), 0, st, a);
         else
             RF_LAUNCH((attn_p4_kernel<false>), g, dim3(NW4 * 64), 0, st, a);
         return rf::check_launch("rf_attn_fwd");
+#else
+        return rf::study_only("rf_attn_fwd: RF_ATTN_P4=1 (the one-wave-per-SIMD kernel)");
+#endif
     }
+#ifndef RF_STUDY
+    if (unit && dbg) return rf::study_only("rf_attn_fwd: RF_ATTN_DBG (ablation builds)");
+#endif
     switch (unit ? dbg : 0) {  // diagnostic variants (garbage results): ablation timing only
+#ifdef RF_STUDY
         case 1: RF_LAUNCH((attn_sk_kernel<true, 1>), g, b, 0, st, a); break;
         case 2: RF_LAUNCH((attn_sk_kernel<true, 2>), g, b, 0, st, a); break;
         case 3: RF_LAUNCH((attn_sk_kernel<true, 3>), g, b, 0, st, a); break;
@@ -2035,6 +2028,7 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
             if (o_f16) RF_LAUNCH((attn_sk_kernel<true, 1024, true>), g, b, 0, st, a);
             else RF_LAUNCH((attn_sk_kernel<true, 1024>), g, b, 0, st, a);
             break;
+#endif
         default:
             if (unit && o_f16)
                 RF_LAUNCH((attn_sk_kernel<true, 0, true>), g, b, 0, st, a);
@@ -2062,6 +2056,9 @@ extern "C" int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ld
     if (n_problems <= 0 || max_q_len <= 0) return RF_OK;
     if (n_split == 0) return attn_sk_launch(q, ldq, k, ldk, v, ldv, o, ldo, problems, n_problems, n_heads, scale,
                                             workspace, stream);
+#ifndef RF_STUDY
+    return rf::study_only("rf_attn_fwd: n_split >= 1 (the legacy split-KV kernels)");
+#else
     const int kv = getenv("RF_ATTN_KERNEL") ? atoi(getenv("RF_ATTN_KERNEL")) : 3;
     const int qrows = kv == 2 ? 128 : 256;  // v2: 128 rows per workgroup; v3 (8 x 32): 256
     const int n_qblk = (max_q_len + qrows - 1) / qrows;
@@ -2095,6 +2092,7 @@ extern "C" int rf_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ld
     else
         RF_LAUNCH((attn_fwd_kernel<false, 4>), dim3((unsigned)total), dim3(256), 0, (hipStream_t)stream, a);
     return rf::check_launch("rf_attn_fwd");
+#endif
 }
 
 extern "C" int rf_attn_grid(void) { return cu_count(); }
@@ -2150,12 +2148,17 @@ extern "C" int rf_attn_combine(const void* workspace, int64_t ws_rows, int n_spl
                                int n_rows, void* o, int64_t ldo, void* stream) {
     RF_REQUIRE(workspace && o, "rf_attn_combine: null pointer");
     if (n_rows <= 0) return RF_OK;
+#ifndef RF_STUDY
+    (void)ws_rows, (void)n_split, (void)n_heads, (void)rows, (void)ldo, (void)stream;
+    return rf::study_only("rf_attn_combine (the legacy split-KV merge)");
+#else
     const float* po = (const float*)workspace;
     const float* pml = po + (int64_t)n_split * ws_rows * n_heads * HD;
     const int64_t items = (int64_t)n_rows * n_heads;
     RF_LAUNCH(attn_combine_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, (hipStream_t)stream, po,
                        pml, ws_rows, n_split, n_heads, rows, n_rows, (bf16_t*)o, ldo);
     return rf::check_launch("rf_attn_combine");
+#endif
 }
 
 extern "C" int rf_swin_attn_fwd_dt(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,

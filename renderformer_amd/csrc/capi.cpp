@@ -89,6 +89,12 @@ int next_epoch(void* flags, size_t bytes, hipStream_t st) {
     return 1 + (int)(c & ((1ull << bits) - 1));
 }
 
+int study_only(const char* what) {
+    set_error("%s is a study kernel: this librfhip is the production build; use the study build "
+              "(make -C renderformer_amd/csrc study -> lib/librfhip_study.so, selected with RF_LIB)", what);
+    return RF_ERR_UNSUPPORTED;
+}
+
 int spin_limit() {
     static const int lim = [] {
         const char* e = getenv("RF_SPIN_LIMIT");
@@ -251,3 +257,10 @@ extern "C" int rf_ktimer_read(float* ms, int max_n) {
 
 extern "C" const char* rf_last_error(void) { return rf::g_err; }
 extern "C" int rf_abi_version(void) { return RF_ABI_VERSION; }
+extern "C" int rf_build_flags(void) {
+#ifdef RF_STUDY
+    return RF_BUILD_STUDY;
+#else
+    return 0;
+#endif
+}

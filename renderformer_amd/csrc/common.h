@@ -73,9 +73,9 @@ RF_DEV void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 RF_DEV float silu(float x) {
     return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
 }
-// (The conv epilogues use silu() too since round 4: the halo / c32 conv kernels that replaced the 256x256 engine
-// tile at the large DPT levels do not spill with it — scratch 0 in their resource usage — so the libm form that
-// once kept the 256x256 conv main loop from spilling is gone.)
+// (The conv epilogues use silu() too since round 4.  The libm form was once kept for the 256x256 engine conv tile,
+// whose main loop spilled with the short one; the large DPT levels now run halo3_kernel<0> / conv3x3_c32_kernel,
+// whose resource usage with silu() shows no scratch (hipcc -Rpass-analysis=kernel-resource-usage, round 5).)
 // The DPT head's output transforms on the hardware exp2 (~1 ulp, v_exp_f32): ELU's negative branch
 // alpha (e^y - 1) and the log decode 10^y - 1 (rendering_pipeline.py:119-123).  The libm expm1f / powf they
 // replace cost ~70 VALU per output value, a third of the fused-head conv's time; the difference is ~1e-7
@@ -179,6 +179,10 @@ void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 int* device_error_word();  // device pointer of the mapped error word (nullptr if it could not be allocated)
 int* range_word();         // device pointer of the mapped fp16 range flag (rf_f16_range_flag)
+// Study-only kernels (measured slower than the defaults, or ablation builds whose results are garbage) are compiled
+// only with -DRF_STUDY (make study -> librfhip_study.so); a production build asked for one refuses: sets the error
+// and returns RF_ERR_UNSUPPORTED (capi.cpp)
+int study_only(const char* what);
 int spin_limit();          // stream-K hand-off spin bound (RF_SPIN_LIMIT, default 2^24 polls)
 // fresh hand-off flag value (>= 1) for a stream-K launch on the flag area [flags, flags + bytes); re-zeroes the
 // area on the stream when the epoch sequence wraps (capi.cpp)

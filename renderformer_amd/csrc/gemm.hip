@@ -2534,6 +2534,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c32_kernel(EngineArgs p) {
     }
 }
 
+#ifdef RF_STUDY  // conv3x3_hk_kernel (measured slower than halo3): study build only
 // ---------------------------------------------------------------------------------------------------
 // conv3x3_hk_kernel: the chunk-per-barrier structure of conv3x3_c32_kernel for 3x3 / stride 1 / pad 1 fp16
 // convolutions with any multiple of 64 output channels and the full conv epilogue (bias / border-class bias,
@@ -2668,6 +2669,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_hk_kernel(EngineArgs p) {
     }
     engine_epilogue<HkTile, E_CONV, TW, false>(p, (img * p.ho + y0) * p.wo + x0, n0, acc);
 }
+#endif  // RF_STUDY
 
 // Tile configurations.  T128: 128x128, 4 waves of 64x64, 3-stage ring (48 KiB / 96 KiB LDS).
 // T256: 256x256, 8 waves of 128x64, 4-stage ring (128 KiB).  T256x128: 8 waves of 64x64, bf16x3 3-stage (144 KiB).
@@ -3360,6 +3362,7 @@ bool skph(int m, int n, int k) {
 
 extern "C" int64_t rf_gemm_workspace_bytes(void) { return SK_WS_BYTES; }
 
+#ifdef RF_STUDY  // the 4-wave GEMM (measured slower than the 8-wave engine): study build only
 // The 4-wave engine (quad_kernel).  RF_GEMM_QUAD (read per call, for A/B in one process): 0 = off, 1 = data-
 // parallel / persistent over whole tiles, 2 = stream-K over 256 blocks in pairs of K-tiles.  RF_GEMM_QUAD_TILE
 // picks the block tile (BM x BN): 256x256 (default; 128 x 128 per wave), 192x256, 160x256, 128x192, 128x128.
@@ -3436,6 +3439,7 @@ static int run_quad(const EngineArgs& p, int epilogue, int mode, void* workspace
         default: return run_quad_t<128, 128, NT>(p, epilogue, mode, workspace, ws_bytes, stream, what);
     }
 }
+#endif  // RF_STUDY
 
 static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
                      const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
@@ -3468,10 +3472,14 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
     p.gate = gate;
     p.out_f16 = out_f16;
     p.range = out_f16 ? rf::range_word() : nullptr;
+#ifdef RF_STUDY
     if (const int qm = quad_mode(m, n, k, lda, ldw, epilogue)) {
         return f16 ? run_quad<P_F16>(p, epilogue, qm, workspace, ws_bytes, stream, "rf_gemm_f16")
                    : run_quad<1>(p, epilogue, qm, workspace, ws_bytes, stream, "rf_gemm_bf16");
     }
+#else
+    if (getenv("RF_GEMM_QUAD") && atoi(getenv("RF_GEMM_QUAD")) > 0) return rf::study_only("rf_gemm: RF_GEMM_QUAD");
+#endif
     if (workspace && ws_bytes >= SK_WS_BYTES && skph(m, n, k)) {
         if (const int rc = sk_setup(p, workspace, stream)) return rc;
         const int64_t tiles = (int64_t)((m + 255) / 256) * (n / 256);
@@ -3625,6 +3633,9 @@ static int launch_halo2(EngineArgs a, void* stream, const char* what) {
     const int ring = env ? atoi(env) : 4;
     const hipStream_t st = (hipStream_t)stream;
     const int dbg = getenv("RF_H2_DBG") ? atoi(getenv("RF_H2_DBG")) : 0;  // ablation timing only
+#ifndef RF_STUDY
+    if (dbg) return rf::study_only("rf_conv: RF_H2_DBG (halo2 ablation builds)");
+#else
     if (!n64 && ring == 4 && dbg >= 1 && dbg <= 8) {
         if (dbg == 1) RF_LAUNCH((halo2_kernel<4, 128, 1>), dim3(nwg), dim3(512), 0, st, a);
         if (dbg == 2) RF_LAUNCH((halo2_kernel<4, 128, 2>), dim3(nwg), dim3(512), 0, st, a);
@@ -3633,6 +3644,7 @@ static int launch_halo2(EngineArgs a, void* stream, const char* what) {
         if (dbg == 8) RF_LAUNCH((halo2_kernel<4, 128, 8>), dim3(nwg), dim3(512), 0, st, a);
         return rf::check_launch(what);
     }
+#endif
     if (n64) {
         if (ring == 3) RF_LAUNCH((halo2_kernel<3, 64>), dim3(nwg), dim3(512), 0, st, a);
         else if (ring == 5) RF_LAUNCH((halo2_kernel<5, 64>), dim3(nwg), dim3(512), 0, st, a);
@@ -3657,6 +3669,10 @@ static bool halo3_ok(const EngineArgs& a) {
 static int launch_halo3(EngineArgs a, void* stream, const char* what) {
     const int nwg = (a.m / 512) * (a.n / 128);
     const int dbg = getenv("RF_H3_DBG") ? atoi(getenv("RF_H3_DBG")) : 0;  // ablation timing only
+#ifndef RF_STUDY
+    if (dbg) return rf::study_only("rf_conv: RF_H3_DBG (halo3 ablation builds, garbage results)");
+    RF_LAUNCH(halo3_kernel<0>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+#else
     if (dbg == 1) RF_LAUNCH(halo3_kernel<1>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
     else if (dbg == 2) RF_LAUNCH(halo3_kernel<2>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
     else if (dbg == 4) RF_LAUNCH(halo3_kernel<4>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
@@ -3670,6 +3686,7 @@ static int launch_halo3(EngineArgs a, void* stream, const char* what) {
     else if (dbg == 64) RF_LAUNCH(halo3_kernel<64>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
     else if (dbg == 96) RF_LAUNCH(halo3_kernel<96>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
     else RF_LAUNCH(halo3_kernel<0>, dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
+#endif
     return rf::check_launch(what);
 }
 
@@ -3694,15 +3711,24 @@ static int launch_c32(EngineArgs a, void* stream, const char* what) {
 static bool hk_ok(const EngineArgs& a) {
     const char* env = getenv("RF_CONV_HK");
     if (!env || atoi(env) == 0 || (a.flags & RF_CONV_FINAL) || a.deconv) return false;  // opt-in: see DESIGN §3.4
+#ifndef RF_STUDY
+    return true;  // (the production build refuses it in launch_hk)
+#else
     if (a.kw != 3 || a.k != 9 * a.cin_pad || a.stride != 1 || a.pad != 1 || a.ho != a.hi || a.wo != a.wi) return false;
     if (a.cin_pad % 32 || a.n % hk::NCO || a.ho % hk::TH || a.wo % hk::TW || a.m <= 0) return false;
     return atoi(env) == 1 || (int64_t)(a.m / (hk::TH * hk::TW)) * (a.n / hk::NCO) >= 256;
+#endif
 }
 
 static int launch_hk(EngineArgs a, void* stream, const char* what) {
+#ifdef RF_STUDY
     const int nwg = (a.m / (hk::TH * hk::TW)) * (a.n / hk::NCO);
     RF_LAUNCH(conv3x3_hk_kernel, dim3(nwg), dim3(256), 0, (hipStream_t)stream, a);
     return rf::check_launch(what);
+#else
+    (void)a, (void)stream, (void)what;
+    return rf::study_only("rf_conv: RF_CONV_HK=1 (conv3x3_hk_kernel)");
+#endif
 }
 
 // fp16 convolutions (one MFMA per product): the 256x256 tile when the filter bank is a multiple of 256

@@ -87,24 +87,35 @@ class _Dataset:
         a = self.read()
         return a.astype(dtype) if dtype is not None else a
 
-    def read(self) -> np.ndarray:
+    def read(self, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """The dataset as an array; with `out` (this shape and dtype, e.g. a view of a pinned host tensor) the data
+        is decoded straight into it (batch_infer.py: no intermediate array, no copy into the pinned batch)."""
         kind = self._layout[0]
         n = int(np.prod(self.shape, dtype=np.int64)) if self.shape else 1
         nbytes = n * self.dtype.itemsize
-        if kind == "compact":
-            raw = self._layout[1][:nbytes]
-            return np.frombuffer(raw, dtype=self.dtype, count=n).reshape(self.shape).copy()
-        if kind == "contiguous":
-            addr, size = self._layout[1], self._layout[2]
-            if addr == UNDEF:
-                return np.zeros(self.shape, dtype=self.dtype)
-            raw = self._f._read(addr, nbytes)
-            return np.frombuffer(raw, dtype=self.dtype, count=n).reshape(self.shape).copy()
+        if out is not None and (tuple(out.shape) != tuple(self.shape) or out.dtype != self.dtype):
+            raise ValueError(f"read(out=): expected {self.shape} {self.dtype}, got {tuple(out.shape)} {out.dtype}")
+        if kind == "compact" or kind == "contiguous":
+            if kind == "compact":
+                raw = self._layout[1][:nbytes]
+            elif self._layout[1] == UNDEF:
+                raw = None
+            else:
+                raw = self._f._read(self._layout[1], nbytes)
+            a = np.zeros(self.shape, dtype=self.dtype) if raw is None else \
+                np.frombuffer(raw, dtype=self.dtype, count=n).reshape(self.shape)
+            if out is None:
+                return a.copy() if raw is not None else a
+            out[...] = a
+            return out
         # chunked: the file is read in order, the chunks are inflated in parallel (zlib releases the GIL; the
         # scene texture is ~90 % of a scene's decode time, SURVEY 8f row 4)
         btree, cdims = self._layout[1], self._layout[2]
         if btree == UNDEF:
-            return np.zeros(self.shape, dtype=self.dtype)
+            if out is None:
+                return np.zeros(self.shape, dtype=self.dtype)
+            out[...] = 0
+            return out
         rank = len(self.shape)
         cshape = tuple(cdims[:rank])
         jobs, covered = [], 0
@@ -118,7 +129,10 @@ class _Dataset:
                 vol *= max(0, hi - lo)
             covered += vol
             jobs.append((self._f._read(caddr, size), fmask, tuple(sl_out), tuple(sl_in)))
-        out = (np.empty if covered == n else np.zeros)(self.shape, dtype=self.dtype)
+        if out is None:
+            out = (np.empty if covered == n else np.zeros)(self.shape, dtype=self.dtype)
+        elif covered != n:
+            out[...] = 0
         cn = int(np.prod(cshape))
 
         def place(job):

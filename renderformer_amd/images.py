@@ -44,14 +44,18 @@ def write_exr(path: str, img: np.ndarray) -> None:
     header += b"\0"
     line_bytes = w * c * 4
     start = len(header) + 8 * h
-    offsets = struct.pack(f"<{h}Q", *[start + y * (8 + line_bytes) for y in range(h)])
-    planes = np.ascontiguousarray(a[:, :, order].transpose(0, 2, 1)).astype("<f4")  # [H, C, W]
+    offsets = (start + np.arange(h, dtype="<u8") * (8 + line_bytes)).astype("<u8")
+    # every scanline as one record: int32 y, int32 byte count, then the [C, W] float32 planes of that line, so the
+    # whole pixel block is one array and one write (per-line struct.pack + write was most of the file's time)
+    lines = np.empty((h, 2 + c * w), dtype="<f4")
+    lines_i = lines.view("<i4")
+    lines_i[:, 0] = np.arange(h, dtype="<i4")
+    lines_i[:, 1] = line_bytes
+    lines[:, 2:] = a[:, :, order].transpose(0, 2, 1).reshape(h, c * w)  # [H, C, W]
     with open(path, "wb") as f:
         f.write(header)
-        f.write(offsets)
-        for y in range(h):
-            f.write(struct.pack("<ii", y, line_bytes))
-            f.write(planes[y].tobytes())
+        f.write(offsets.tobytes())
+        f.write(lines.tobytes())
 
 
 def read_exr(path: str) -> np.ndarray:

@@ -25,3 +25,12 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+def needs_study(what: str) -> None:
+    """Skip unless librfhip is the study build (rf_build_flags() & RF_BUILD_STUDY): the measured-slower kernels
+    and ablation variants (4-wave GEMM / conv, one-wave-per-SIMD and legacy split-KV attention) are compiled only
+    there (make -C renderformer_amd/csrc study; RF_LIB=renderformer_amd/lib/librfhip_study.so)."""
+    from renderformer_amd import _lib
+    if not _lib.study_build():
+        pytest.skip(f"{what}: a study kernel, not in the production librfhip (RF_LIB=<librfhip_study.so> to test)")

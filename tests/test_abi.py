@@ -27,11 +27,13 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, fn), fn
     assert lib.rf_abi_version() == 14
     # every int-returning entry point has a ctypes signature in the binding
-    assert set(_lib.SIGNATURES) == set(header_functions()) - {"rf_last_error", "rf_abi_version",
+    assert set(_lib.SIGNATURES) == set(header_functions()) - {"rf_last_error", "rf_abi_version", "rf_build_flags",
                                                                "rf_attn_workspace_bytes", "rf_gemm_workspace_bytes",
                                                                "rf_scene_pos_partials", "rf_attn_grid",
                                                                "rf_encoder_workspace_bytes",
                                                                "rf_decoder_workspace_bytes"}
+    # the production build (what the product path loads) carries no study kernels; the study build says so
+    assert lib.rf_build_flags() in (0, 1)
 
 
 def test_invalid_arguments_raise_value_error_without_device():
@@ -395,3 +397,25 @@ def test_decoder_forward_validates_before_any_launch():
     d = _lib.DecoderDesc(**good)
     one = int(lib.rf_decoder_workspace_bytes(ctypes.addressof(d)))
     assert one >= 2 * (4096 * (3 * 1024 + 4096) + 5649 * 1024 * (1 + 2 * 2 + 2))  # h/q2/att, g, hc, kv_all, kview_all
+
+
+def test_production_build_refuses_study_kernels():
+    """the measured-slower alternatives and ablation variants live in the study build only; the
+    production librfhip refuses a request for one with RF_ERR_UNSUPPORTED (before any launch, so no device is
+    needed) instead of running something else or garbage."""
+    import ctypes
+
+    import torch  # noqa: F401
+    from renderformer_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("librfhip.so not built")
+    lib = _lib.load(require_device=False)
+    if _lib.study_build():
+        pytest.skip("RF_LIB points at the study build")
+    # the legacy split-KV path (n_split >= 1) and its merge
+    rc = lib.rf_attn_fwd(ctypes.c_void_p(16), 256, ctypes.c_void_p(16), 256, ctypes.c_void_p(16), 256,
+                         ctypes.c_void_p(16), 256, ctypes.c_void_p(16), 1, 10, 2, 128, 1.0, 2, ctypes.c_void_p(16),
+                         10, None)
+    assert rc == 3 and b"study" in lib.rf_last_error()
+    rc = lib.rf_attn_combine(ctypes.c_void_p(16), 10, 2, 2, None, 10, ctypes.c_void_p(16), 256, None)
+    assert rc == 3 and b"study" in lib.rf_last_error()

@@ -141,3 +141,29 @@ def test_batch_infer_pipelined_matches_inline(tmp_path, monkeypatch, tex_dtype):
         b = read_exr(str(outs["0"] / f"{name}_view_0.exr"))
         assert rel_l2(a, b) < 1e-4  # (fp32 sum-order differences only, as in test_batch_infer_cli)
         assert rel_l2(a, z["hdr"][0, 0]) < 1e-3
+
+
+def test_batch_loader_decodes_into_pinned_slots_like_collate(tmp_path):
+    """batch_infer's pipelined loader decodes each scene straight into its slot of the batch tensors (h5io
+    read(out=), no collate / pin copies): same tensors as collate(load_scene(...)) for equal-N batches and with
+    --padding_length (zero padding rows, mask False), in the file's texture dtype."""
+    import numpy as np
+    import batch_infer
+    from renderformer_amd.h5io import write_scene
+    rng = np.random.default_rng(3)
+    paths = []
+    for i, n in enumerate((37, 37, 20)):
+        p = str(tmp_path / f"s{i}.h5")
+        tex = rng.random((n, 13, 32, 32), dtype=np.float32)
+        write_scene(p, rng.random((n, 3, 3)), rng.random((n, 3, 3)), tex, rng.random((2, 4, 4)),
+                    rng.random(2) * 40 + 20)
+        paths.append(p)
+    for idx, pad in (([0, 1], None), ([0, 2], 64), ([2], None)):
+        _, got = batch_infer._load_batch_pinned(paths, idx, pad, pinned=False)
+        ref = batch_infer.collate([batch_infer.load_scene(paths[i], pad, None) for i in idx])
+        assert set(got) == set(ref)
+        for k in ref:
+            assert got[k].dtype == ref[k].dtype and got[k].shape == ref[k].shape, k
+            assert torch.equal(got[k], ref[k]), k
+    with pytest.raises(ValueError, match="padding_length"):
+        batch_infer._load_batch_pinned(paths, [0, 2], None, pinned=False)

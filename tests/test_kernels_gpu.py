@@ -8,6 +8,7 @@ import math
 import pytest
 import torch
 import torch.nn.functional as F
+from conftest import needs_study
 
 from oracle import rf_ref
 
@@ -148,6 +149,7 @@ def test_gemm_f16_operands(monkeypatch, tile, m, n, k):
             pytest.skip("the phased stream-K path needs >= 512 whole 256x256 tiles")
         monkeypatch.setenv("RF_GEMM_SKPH", "1")
     elif (F16_TILES[tile] or "").startswith("quad"):
+        needs_study("the 4-wave GEMM")
         mode, _, qt = F16_TILES[tile][4:].partition("@")
         bn = int(qt.split("x")[1]) if qt else 256
         if k % 128 or n % bn:
@@ -190,6 +192,7 @@ def test_gemm_quad_bf16_and_persistent(monkeypatch, tile, mode, stg, m, n, k):
     K-tiles; register or LDS-DMA staging; 256x256 / 128x192 / 160x256 tiles) on bf16 operands: more tiles than CUs
     (persistent), ragged rows and ragged column tiles, odd K-pair counts split over blocks; fp32, residual and
     SwiGLU epilogues vs fp64 (SwiGLU with a ragged column tile runs on the default engine)."""
+    needs_study("the 4-wave GEMM")
     monkeypatch.setenv("RF_GEMM_QUAD", mode)
     monkeypatch.setenv("RF_GEMM_QUAD_STG", stg)  # register staging (default) / LDS-DMA
     monkeypatch.setenv("RF_GEMM_QUAD_TILE", tile)  # 128x192: a ragged last column tile when 192 does not divide N
@@ -479,6 +482,8 @@ def attn_mode(request, monkeypatch):
     """Varlen attention modes: the stream-K kernel on the full grid, on small grids that cut most units
     into 2-3 pieces merged by their owner (RF_ATTN_GRID), the same for the one-wave-per-SIMD stream-K kernel
     (RF_ATTN_P4=1), and the legacy per-unit kernel (n_split=1).  Returns the n_split to pass."""
+    if request.param.startswith("p4") or request.param == "legacy":
+        needs_study("the one-wave-per-SIMD / legacy split-KV attention")
     if request.param.startswith("p4"):
         monkeypatch.setenv("RF_ATTN_P4", "1")
     if "_grid" in request.param:
@@ -489,6 +494,8 @@ def attn_mode(request, monkeypatch):
 @pytest.fixture(params=["sk", "p4"])
 def sk_kernel(request, monkeypatch):
     """The two stream-K kernels: 8 waves x 32 rows (default) and 4 waves x 64 rows (RF_ATTN_P4=1)."""
+    if request.param == "p4":
+        needs_study("the one-wave-per-SIMD attention")
     monkeypatch.setenv("RF_ATTN_P4", "1" if request.param == "p4" else "0")
     return request.param
 
@@ -523,6 +530,7 @@ def test_attention_split_kv(n_split):
     """Split-KV partials + merge: ragged problems (incl. one shorter than a key tile, so some splits see no
     keys), repeated calls on the reused workspace, and a spiked key that forces the deferred-rescale branch
     inside one split."""
+    needs_study("the legacy split-KV attention")
     ops = _ops()
     H = 2
     D = H * 128
@@ -721,6 +729,8 @@ def test_attention_longest_example_sequence(sk_kernel_name, monkeypatch):
     """S = 11,819 (cbox-lucy: 11,803 triangles + 16 register tokens, the longest example scene; SURVEY §5 needs
     S ~ 12k in one pass) at the model's 8 heads, pre-scaled q, with the cost-balanced schedule: 376 units of
     185 key tiles cut over 256 workgroups.  Checked against fp64 on 768 sampled query rows of every head."""
+    if sk_kernel_name == "p4":
+        needs_study("the one-wave-per-SIMD attention")
     monkeypatch.setenv("RF_ATTN_P4", "1" if sk_kernel_name == "p4" else "0")
     ops = _ops()
     H, S = 8, 11819
@@ -1087,6 +1097,7 @@ def test_conv_hk(cin, cout, hh, ww, n_img, monkeypatch):
     1 to 8 channel chunks, several images, tiles along both axes, 1 to 4 channel tiles of 64, fused bias + 2
     residuals + SiLU fp16 planes with a padded row stride, and the plain fp32 output; against fp64 on the same fp16
     operands and against the halo2 kernel (same products, fp32 summation order)."""
+    needs_study("conv3x3_hk_kernel")
     monkeypatch.setenv("RF_CONV_HK", "1")
     from renderformer_amd.dpt import _Conv, split_planes
     g = torch.Generator(device="cpu").manual_seed(cin * hh + cout + ww + 7)
@@ -1234,6 +1245,8 @@ def test_conv_border_bias(hw, halo2, hk, halo3, monkeypatch):
     """RF_CONV_BORDER_BIAS: per-pixel bias row by border class (3 ry + rx), on the engine tile, the halo2, hk and
     halo3 kernels (the folded output_conv1), vs torch conv + the class bias."""
     from renderformer_amd.dpt import _Conv, split_planes
+    if hk == "1":
+        needs_study("conv3x3_hk_kernel")
     monkeypatch.setenv("RF_CONV_HALO2", halo2)
     monkeypatch.setenv("RF_CONV_HK", hk)
     monkeypatch.setenv("RF_CONV_HALO3", halo3)

@@ -1,7 +1,8 @@
 """Stage-1 stream-K attention at the bench shape under the RF_ATTN_DBG ablation builds (timing only).
 
 python tools/attn_ablate.py            -> one line per variant
-python tools/attn_ablate.py pmc [reps] -> just the shipped kernel, `reps` launches (for rocprofv3 --pmc)"""
+python tools/attn_ablate.py pmc [reps] -> just the shipped kernel, `reps` launches (for rocprofv3 --pmc)
+The RF_ATTN_DBG variants (stamps, ablations) exist only in the study build: RF_LIB=renderformer_amd/lib/librfhip_study.so."""
 import os
 import sys
 
@@ -16,7 +17,9 @@ S, D, H = 5649, 1024, 8
 g = torch.Generator(device="cuda").manual_seed(0)
 qkv = torch.randn(S, 3 * D, device="cuda", generator=g).bfloat16()
 qs = (qkv[:, :D].float() * ops.Q_LOG2_SCALE).bfloat16()
-out = torch.empty(S, D, device="cuda", dtype=torch.bfloat16)
+# O as fp16 (the frame's instantiation, attn_sk_kernel<true, 0, true, false>: the out-projection's fp16 operand);
+# ABL_O=bf16 for the bf16-output kernel
+out = torch.empty(S, D, device="cuda", dtype=torch.bfloat16 if os.environ.get("ABL_O") == "bf16" else torch.float16)
 prob = torch.tensor([[0, S, 0, S, 0]], dtype=torch.int32, device="cuda")
 
 

@@ -29,7 +29,11 @@ args = ["--h5_folder", scenes, "--model_id", "renderformer-v1.1-swin-large", "--
         "--resolution", "512", "--batch_size", bs, "--precision", "fp16"]
 batch_infer.main(args + ["--output_dir", os.path.join(root, "warm")])  # model build + first-touch allocations
 res = {}
+os.environ["RF_BATCH_PROFILE"] = "1"  # batch_infer.StageTimes: per-stage host time, printed by each run
 for mode in ("0", "1", "0"):
+    batch_infer.STAGES.t.clear()
+    batch_infer.STAGES.n.clear()
+    batch_infer.STAGES.on = True
     os.environ["RF_BATCH_INLINE"] = mode
     out = os.path.join(root, "out" + mode)
     t0 = time.perf_counter()

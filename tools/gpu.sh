@@ -23,6 +23,8 @@
 #   libab            the current library vs $BASE (default renderformer_amd/lib/librfhip_base.so, a build of another
 #                    tree): GPU tests on the current one, then interleaved stage-1 attention timings, per-role stamps
 #                    and bench runs of both (RF_LIB selects the library)
+#   quadstudy        tools/kbench.py quad on the study build: the 4-wave GEMM at MT128x192 / MT160x256 (register or
+#                    LDS-DMA staging, whole tiles or stream-K) vs the default engine on the projection shapes
 #   vendor           kernel-trace of the vendor GEMM library vs the engine on the frame's projection shapes
 #                    (tools/kbench.py vendor: study only, nothing of it is linked into librfhip)
 # Every GPU step runs under its own timeout and the steps are chained with && (set -e): the first failure
@@ -51,7 +53,8 @@ round)
     prof_run timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --profile --steps 2 --warmup 1 > $O/pmc_fetch.log 2>&1
     prof_run timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 $R/bench.py --profile --steps 2 --warmup 1 > $O/pmc_write.log 2>&1
     RF_TRAFFIC_OUT=$O/attn_stage1_traffic.json python tools/pmc_traffic.py $(find $O/pmc_fetch -name '*counter_collection.csv' -print -quit) $(find $O/pmc_write -name '*counter_collection.csv' -print -quit) $O/pmc_traffic.json > $O/pmc_traffic.txt 2>&1
-    timeout -k 10 300 python tools/attn_ablate.py stamps > $O/attn_clock.log 2>&1
+    STUDY=$R/renderformer_amd/lib/librfhip_study.so  # the stamp build (RF_ATTN_DBG=32) is a study variant
+    if [ -f $STUDY ]; then RF_LIB=$STUDY timeout -k 10 300 python tools/attn_ablate.py stamps > $O/attn_clock.log 2>&1; fi
     prof_run timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_mfma -o run -- python3 $R/tools/attn_ablate.py pmc 5 > $O/pmc_mfma.log 2>&1 ;;
 prof)
     prof_run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --profile --steps 5 --warmup 2 "$@" > $O/prof.log 2>&1 ;;
@@ -122,12 +125,16 @@ libab)
         ABL=0 timeout -k 10 200 python -u tools/attn_ablate.py > $O/attn_new$i.log 2>&1
         ABL=0 RF_LIB=$BASE timeout -k 10 200 python -u tools/attn_ablate.py > $O/attn_base$i.log 2>&1
     done
-    timeout -k 10 120 python tools/attn_ablate.py stamps > $O/stamps_new.log 2>&1
+    STUDY=$R/renderformer_amd/lib/librfhip_study.so  # the stamp build (RF_ATTN_DBG=32) of the current tree
+    if [ -f $STUDY ]; then RF_LIB=$STUDY timeout -k 10 120 python tools/attn_ablate.py stamps > $O/stamps_new.log 2>&1; fi
     RF_LIB=$BASE timeout -k 10 120 python tools/attn_ablate.py stamps > $O/stamps_base.log 2>&1
     for i in 1 2; do
         timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_new$i.json 2>> $O/bench.err
         RF_LIB=$BASE timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_base$i.json 2>> $O/bench.err
     done ;;
+quadstudy)  # the 4-wave GEMM (study build) at the library's tiles vs the default engine on the projection shapes
+    KB_SHAPES=${KB_SHAPES:-"s1 qkv,s1 out,s1 w2,s2 out,s2 w2"} KB_QUAD=${KB_QUAD:-"0,1@128x192,2@128x192,1d@128x192,1@160x256,2@160x256,1d@160x256"} \
+        RF_LIB=$R/renderformer_amd/lib/librfhip_study.so timeout -k 10 600 python -u tools/kbench.py quad > $O/quad.log 2>&1 ;;
 vendor)
     prof_run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/vend -o run -- python3 $R/tools/kbench.py vendor > $O/vendor.log 2>&1 ;;
 *)

@@ -355,7 +355,7 @@ def quad():
     from renderformer_amd.model import _interleave_swiglu
     shapes = [("s1 qkv", S, 3 * D, D, 0), ("s1 w13", S, 2 * F, D, 1), ("s2 w13", R, 2 * F, D, 1),
               ("s2 qkv", R, 3 * D, D, 0), ("kvall", S, 20 * D, D, 0), ("sq8k", 8192, 8192, 8192, 0),
-              ("s1 w2", S, D, F, 0), ("s2 w2", R, D, F, 0)]
+              ("s1 w2", S, D, F, 0), ("s2 w2", R, D, F, 0), ("s1 out", S, D, D, 0), ("s2 out", R, D, D, 0)]
     if os.environ.get("KB_SHAPES"):
         shapes = [x for x in shapes if x[0] in os.environ["KB_SHAPES"].split(",")]
     # labels: "0" default pick, "1" / "2" quad whole tiles / stream-K with register staging, "1d" / "2d" the same with
