@@ -233,8 +233,10 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
         nxt = None
         if got is not None:
             items, host = got
+            t_h = time.perf_counter()
             with torch.cuda.stream(h2d):
                 batch = {k: v.to(dev, non_blocking=True) for k, v in host.items()}
+            STAGES.add("main: H2D issue", time.perf_counter() - t_h)
             compute.wait_stream(h2d)
             for v in batch.values():  # allocated on the copy stream, used on the compute stream
                 v.record_stream(compute)
@@ -255,13 +257,17 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
             # rendered again in place, and copied back again
             if resolve is not None and STAGES.timed("main: range check", resolve, p_imgs):
                 p_out.copy_(p_imgs)
+            t_y = time.perf_counter()
             yield p_items, p_out
+            STAGES.add("main: consumer (writer submission)", time.perf_counter() - t_y)
         if nxt is None:
             return
         pending = nxt
 
 
-def main(argv=None):
+def main(argv=None, pipeline=None):
+    """The CLI.  `pipeline`: an already-built RenderFormerRenderingPipeline for the same model flags (tools/batch_e2e.py
+    times the data path apart from the model build)."""
     parser = argparse.ArgumentParser(description="Batch inference using triangle radiosity transformer model (MI355X)")
     parser.add_argument("--h5_folder", type=str, required=True)
     parser.add_argument("--batch_size", type=int, default=8)
@@ -279,7 +285,11 @@ def main(argv=None):
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     files = sorted(glob.glob(os.path.join(args.h5_folder, "*.h5")), key=natural_key)
     print(f"Found {len(files)} h5 files in {args.h5_folder}")
-    pipeline = load_pipeline(args)
+    t_build = time.perf_counter()
+    if pipeline is None:
+        pipeline = load_pipeline(args)
+    STAGES.add("main: model build (load_pipeline)", time.perf_counter() - t_build)
+    t_loop = time.perf_counter()
     cfg = pipeline.config
     if world > 1:
         costs = []
@@ -309,6 +319,7 @@ def main(argv=None):
         for f in pending:
             STAGES.timed("main: wait for writers", f.result)  # re-raises a writer's error
         writers.shutdown()
+    STAGES.add("main: data path wall (first load -> last file)", time.perf_counter() - t_loop)
     print(f"Output saved to: {output_dir} ({n_frames} frames on rank {rank}/{world})")
     if STAGES.on:
         import json

@@ -28,7 +28,11 @@ constexpr int SK5_MAX_GRID = rf::ATTN_MAX_GRID;
 // so that every workgroup finishes by a common time T, the smallest T that covers all tiles.
 namespace {
 struct SkCost {
-    double tile = 3170, pro = 8700, pub = 8500, merge = 9800, store = 6000;  // shader cycles
+    // shader cycles, refit in round 5 on the kernel whose next piece's loads go out ahead of the previous piece's
+    // stores (prologues 17.6k -> 7.2k per two-piece workgroup; profiles/r5b_attn_prefetch_ab.txt): the A/B of
+    // tools/gpu.sh costab measured 130.8 us per stage-1 launch against 131.3 us on the round-4 constants
+    // (3170, 8700, 8500, 9800, 6000) and 131.7 us on (3080, 6000, 6500, 8800, 3000) (profiles/r5c_attn_cost_ab.txt)
+    double tile = 3080, pro = 5000, pub = 5000, merge = 8800, store = 2500;
 };
 
 struct SkUnits {

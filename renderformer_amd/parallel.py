@@ -12,7 +12,7 @@ host sync), overlapping the next step (FrameGather; gloo in the CPU tests).
 from __future__ import annotations
 
 import heapq
-from typing import List, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -77,7 +77,10 @@ class FrameGather:
     caller launches next (the next step's render) until ``result()``.  Under gloo (CPU-side tests) the frames go
     through the host synchronously.  The gathered order is global: slot (rank r, j) holds frame rank_ids[r][j]."""
 
-    def __init__(self, rank_ids: Sequence[Sequence[int]], frame_shape, device, dtype=torch.float32):
+    def __init__(self, rank_ids: Sequence[Sequence[int]], frame_shape, device, dtype=torch.float32,
+                 collective: Optional[bool] = None):
+        """collective: run the all-gather through torch.distributed (default: when a process group of more than one
+        rank is initialised; True also for a one-rank group, which is how the RCCL path is tested on one GPU)."""
         self.rank_ids = [list(r) for r in rank_ids]
         self.world = len(self.rank_ids)
         self.n_total = sum(len(r) for r in self.rank_ids)
@@ -88,7 +91,8 @@ class FrameGather:
         self.frame_shape = tuple(frame_shape)
         self.device = torch.device(device)
         self.dtype = dtype
-        self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        inited = dist.is_available() and dist.is_initialized()
+        self.distributed = inited and (dist.get_world_size() > 1 if collective is None else bool(collective))
         if self.distributed and dist.get_world_size() != self.world:
             raise ValueError(f"rank_ids for {self.world} ranks, world size {dist.get_world_size()}")
         self.rank = dist.get_rank() if self.distributed else 0

@@ -132,6 +132,18 @@ libab)
         timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_new$i.json 2>> $O/bench.err
         RF_LIB=$BASE timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_base$i.json 2>> $O/bench.err
     done ;;
+costab)  # stage-1 attention timing + per-role stamps under the stream-K cost-model constants in $COSTS (';'-separated
+         # RF_ATTN_COST values "tile,pro,pub,merge,store"; "-" = the built-in constants)
+    STUDY=$R/renderformer_amd/lib/librfhip_study.so
+    IFS=';' read -ra CS <<< "${COSTS:--}"
+    for i in 1 2; do
+        for c in "${CS[@]}"; do
+            if [ "$c" = "-" ]; then unset RF_ATTN_COST; else export RF_ATTN_COST=$c; fi
+            ABL=0 timeout -k 10 200 python -u tools/attn_ablate.py > $O/attn_${c//,/_}_$i.log 2>&1
+            if [ $i = 1 ] && [ -f $STUDY ]; then RF_LIB=$STUDY timeout -k 10 120 python tools/attn_ablate.py stamps > $O/stamps_${c//,/_}.log 2>&1; fi
+        done
+    done
+    unset RF_ATTN_COST ;;
 quadstudy)  # the 4-wave GEMM (study build) at the library's tiles vs the default engine on the projection shapes
     KB_SHAPES=${KB_SHAPES:-"s1 qkv,s1 out,s1 w2,s2 out,s2 w2"} KB_QUAD=${KB_QUAD:-"0,1@128x192,2@128x192,1d@128x192,1@160x256,2@160x256,1d@160x256"} \
         RF_LIB=$R/renderformer_amd/lib/librfhip_study.so timeout -k 10 600 python -u tools/kbench.py quad > $O/quad.log 2>&1 ;;
