@@ -12,6 +12,9 @@
  *   rf_gemm_bf16       nn.Linear / aten mm+addmm in attention.py:51-57,95-100,121-125,202,342,361;
  *                      renderformer.py:49,63 (encoders); view_transformer.py:45 (ray encoder)
  *   rf_rmsnorm         nn.RMSNorm pre-norms attention.py:436-439,463,482 (+ kv_norm :508)
+ *   rf_prenorm / rf_gemm_add_prenorm / rf_gemm_rownorm  the same pre-norms deferred into the GEMMs around them
+ *                      (the residual GEMM's epilogue writes x * g and row sums of squares, the projection after
+ *                      the norm scales its rows by 1 / rms): what rf_encoder_forward / rf_decoder_forward issue
  *   rf_qk_norm_rope    q/k RMSNorm over full width (attention.py:127-133) fused with the
  *                      triangle RoPE (rope.py:106-149 apply_rotary_emb_*cossin, :78-103, :315-333)
  *   rf_attn_fwd        flash_attn_varlen_qkvpacked_func / flash_attn_varlen_kvpacked_func
@@ -61,7 +64,7 @@ extern "C" {
 #define RF_ERR_UNSUPPORTED 3
 #define RF_ERR_DEVICE 4       /* an earlier launch reported a device-side error (see rf_device_error) */
 
-#define RF_ABI_VERSION 14
+#define RF_ABI_VERSION 15
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -146,6 +149,34 @@ int64_t rf_gemm_workspace_bytes(void);
 int rf_gemm_f16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
                 const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
                 void* stream);
+/* Deferred RMSNorm (ABI 15): the pre-norm of a transformer layer folded into the GEMMs on either side of it, with
+ * no row kernel in between.  rmsnorm(x) W^T = ((x * g) W^T) / rms(x) row by row, rms(x) = sqrt(mean(x^2) + eps), so
+ *   - the producer, rf_gemm_add_prenorm, runs rf_gemm_*(RF_EPI_ADD_F32) (x += A W^T, x fp32 [M, N]) and from the
+ *     same epilogue also writes xg = x * g (16-bit: fp16 when operand_dtype is RF_DT_F16, else bf16; [M, N],
+ *     row stride ldxg) and per row up to RF_PRENORM_SLOTS partial sums of x^2 (ss: [M][RF_PRENORM_SLOTS] floats,
+ *     16-B aligned; one slot per output-column tile, unused slots 0);
+ *   - the consumer, rf_gemm_rownorm, is rf_gemm_*(epilogue) of A = xg whose output rows are scaled by
+ *     1 / sqrt(sum of the row's slots / norm_dim + eps) before the bias and the SwiGLU (epilogue RF_EPI_BF16 /
+ *     RF_EPI_F16 / RF_EPI_SWIGLU / RF_EPI_SWIGLU_F16).
+ * rf_prenorm writes xg and ss (slot 0 = the whole row's sum) from x directly: the first layer's norm, whose x comes
+ * from a kernel that is not a GEMM.  N <= RF_PRENORM_SLOTS * 128 for the fused producer; above it
+ * rf_gemm_add_prenorm runs the GEMM and then rf_prenorm.  Replaces the pair rf_rmsnorm* + GEMM of
+ * AttentionLayer.forward's pre-norms (renderformer/layers/attention.py:509, 520) and the decoder's (:634-661):
+ * same values up to rounding (xg rounds x * g where rf_rmsnorm rounds x * g / rms(x); the same relative error),
+ * the sums of squares in a fixed order (bit-reproducible).  An fp16 xg beyond 65504 raises range code 2. */
+#define RF_PRENORM_SLOTS 8
+int rf_prenorm(const float* x, int64_t ldx, const float* norm_w, void* xg, int64_t ldxg, float* ss, int rows,
+               int dim, int operand_dtype, void* stream);
+int rf_gemm_add_prenorm(const void* a, int64_t lda, const void* w, int64_t ldw, float* x, int64_t ldx, int m, int n,
+                        int k, const float* norm_w, void* xg, int64_t ldxg, float* ss, int operand_dtype,
+                        void* workspace, int64_t ws_bytes, void* stream);
+/* seg_ss (optional, NULL = none; RF_EPI_BF16 / RF_EPI_F16 only): also the partial sums of the squares of the
+ * written (rounded) outputs per row for each of the first n_seg segments of seg_w columns (seg_w % 256 == 0,
+ * <= RF_PRENORM_SLOTS * 128), [M][n_seg][RF_PRENORM_SLOTS] floats — the row sums a following full-width RMSNorm
+ * of those segments needs (the Swin q/k norm folded into rf_swin_attn_fwd_qkn). */
+int rf_gemm_rownorm(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int m, int n,
+                    int k, int epilogue, const float* ss, int norm_dim, float eps, float* seg_ss, int seg_w,
+                    int n_seg, int operand_dtype, void* workspace, int64_t ws_bytes, void* stream);
 /* rf_gemm_bf16 on the HIP engine that does nothing unless *flag != 0 (read on the device when the launch
  * runs); stream-ordered after whatever wrote the flag. */
 int rf_gemm_bf16_if(const int* flag, const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
@@ -258,6 +289,15 @@ int rf_swin_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, con
 int rf_swin_attn_fwd_dt(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                         void* o, int64_t ldo, int o_dtype, int n_images, int grid_h, int grid_w, int window, int shift,
                         int n_heads, int head_dim, float scale, void* stream);
+/* rf_swin_attn_fwd_dt with the full-width q/k RMSNorm folded into its loads (ABI 15): q, k as the projection wrote
+ * them (rf_gemm_rownorm with seg_ss = qk_ss, seg_w = n_heads * 128, n_seg = 2), each q row scaled by
+ * q_scale / rms(q row) * qk_norm_w[c] and each k row by 1 / rms(k row) * qk_norm_w[n_heads * 128 + c] before the
+ * scores -- rf_qk_norm_rope(n_seg = 2, no RoPE, seg0_scale = q_scale)'s arithmetic without its pass over q and k
+ * (reference SwinSelfAttention q/k norm, attention.py:345-359).  qk_norm_w NULL: only the q scale. */
+int rf_swin_attn_fwd_qkn(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv, void* o,
+                         int64_t ldo, int o_dtype, int n_images, int grid_h, int grid_w, int window, int shift,
+                         int n_heads, int head_dim, float scale, const float* qk_ss, const float* qk_norm_w, float eps,
+                         float q_scale, void* stream);
 
 /* texture: f32 [n_rows, channels, patch_elems]; channels >= channels-log_channels are log10(x+1)
  * encoded IN PLACE for every row; rows with dst_row[r] >= 0 are written as bf16 to out[dst_row[r]]. */

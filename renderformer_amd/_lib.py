@@ -42,7 +42,11 @@ SIGNATURES = {
     "rf_attn_fwd_sk": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _P, _I, _I, _I, _F, _P, _P, _I, _P],
     "rf_attn_fwd_dt": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _P, _I, _I, _I, _F, _P, _P, _I, _P],
     "rf_swin_attn_fwd_dt": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P],
+    "rf_swin_attn_fwd_qkn": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P, _P, _F, _F, _P],
     "rf_rmsnorm": [_P, _L, _P, _F, _P, _L, _I, _I, _P],
+    "rf_prenorm": [_P, _L, _P, _P, _L, _P, _I, _I, _I, _P],
+    "rf_gemm_add_prenorm": [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _P, _L, _P, _I, _P, _L, _P],
+    "rf_gemm_rownorm": [_P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _I, _F, _P, _I, _I, _I, _P, _L, _P],
     "rf_qk_norm_rope": [_P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _F, _F, _P, _L, _I, _P, _I, _P],
     "rf_qk_norm_rope_groups": [_P, _L, _L, _P, _L, _L, _P, _I, _I, _I, _I, _I, _P, _L, _F, _F, _P, _L, _I, _P, _I,
                                _P],
@@ -160,7 +164,9 @@ def load(require_device: bool = True):
                     f"librfhip.so not found at {LIB_PATH}; build it with `python -c 'import __graft_entry__ as g; g.build()'`")
             lib = ctypes.CDLL(LIB_PATH)
             for name, args in SIGNATURES.items():
-                fn = getattr(lib, name)
+                fn = getattr(lib, name, None)
+                if fn is None:  # (an older build selected with RF_LIB for an A/B: calling it raises AttributeError)
+                    continue
                 fn.argtypes = args
                 fn.restype = ctypes.c_int
             lib.rf_last_error.restype = ctypes.c_char_p

@@ -87,6 +87,14 @@ struct AttnArgs {
     int o_f16;  // output O as fp16 (the A operand of an fp16 out-projection) instead of bf16
     int* range; // o_f16: the mapped fp16 range flag (|O| > 65504), else null
     int ascend; // diagnostic (RF_SK_ASCEND=1): ascending blockIdx order inside a group (the round-2 layout), A/B only
+    // Swin with the q/k norm folded in (rf_swin_attn_fwd_qkn): q and k arrive as the projection wrote them and are
+    // normalised on load over the full width (qk_dim columns per segment) from the projection's per-row partial sums
+    // of squares (qk_ss [row][2][PRENORM_SLOTS]: q, k), weighted by qk_w [2 * qk_dim] (null: no norm) and, for q,
+    // scaled by qk_scale (softmax scale * log2 e) -- rf_qk_norm_rope's arithmetic, without its HBM round trip
+    const float* qk_ss;
+    const float* qk_w;
+    float qk_eps, qk_scale;
+    int qk_dim;
 };
 
 // two f32 -> the 16-bit output pair: fp16 (OF16) or bf16, RNE
@@ -154,7 +162,29 @@ RF_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 RF_DEV float max3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
 
-template <bool SWIN, int NW, bool OF16 = false>
+// 1 / rms of row `row`'s segment `seg` from its RF_PRENORM_SLOTS partial sums, in slot order (as rf_gemm_rownorm)
+RF_DEV float qk_inv_rms(const AttnArgs& p, int64_t row, int seg) {
+    const float4* q = reinterpret_cast<const float4*>(p.qk_ss + (row * 2 + seg) * RF_PRENORM_SLOTS);
+    const float4 a = q[0], b = q[1];
+    const float sum = ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
+    return 1.0f / sqrtf(sum / (float)p.qk_dim + p.qk_eps);
+}
+
+// 8 bf16 values x -> bf16(x * s * w[e]) (rf_qk_norm_rope's order: row scale first, then the weight)
+RF_DEV u32x4 qk_scale8(u32x4 x, float s, const float* w) {
+    const float4 w0 = *reinterpret_cast<const float4*>(w), w1 = *reinterpret_cast<const float4*>(w + 4);
+    const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    u32x4 r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float a = __uint_as_float(x[e] << 16) * s * wv[2 * e];
+        const float b = __uint_as_float(x[e] & 0xffff0000u) * s * wv[2 * e + 1];
+        r[e] = pack_bf16x2(a, b);
+    }
+    return r;
+}
+
+template <bool SWIN, int NW, bool OF16 = false, bool QKN = false>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_fwd_kernel(AttnArgs p) {
     constexpr int T = NW * 64;
     constexpr int CPT = (KT * HD / 8) / T;  // 16-B chunks per thread per tile (per operand)
@@ -232,6 +262,19 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_fwd_kernel(Attn
         const bf16_t* src = p.q + (int64_t)qrow * p.ldq + hoff + 8 * half;
 #pragma unroll
         for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(src + 16 * s);
+        if constexpr (QKN) {  // q = bf16(q * (inv_rms * scale) * w): the fused rf_qk_norm_rope of segment 0
+            const float sq = (p.qk_w ? qk_inv_rms(p, qrow, 0) : 1.f) * p.qk_scale;
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const u32x4 x = __builtin_bit_cast(u32x4, qf[s]);
+                if (p.qk_w) {
+                    qf[s] = __builtin_bit_cast(bf16x8, qk_scale8(x, sq, p.qk_w + hoff + 16 * s + 8 * half));
+                } else {
+                    const float one[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+                    qf[s] = __builtin_bit_cast(bf16x8, qk_scale8(x, sq, one));
+                }
+            }
+        }
     }
     int qlabel = 0;
     if constexpr (SWIN) qlabel = p.shift > 0 ? swin_label(qi) : 0;
@@ -258,6 +301,10 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_fwd_kernel(Attn
                 const int r = swin_row(srow + i * (T / 16));
                 kreg[i] = *reinterpret_cast<const u32x4*>(kbase + (int64_t)r * p.ldk);
                 vreg[i] = *reinterpret_cast<const u32x4*>(vbase + (int64_t)r * p.ldv);
+                if constexpr (QKN) {  // k = bf16(k * inv_rms * w): segment 1 of the fused q/k norm
+                    if (p.qk_w)
+                        kreg[i] = qk_scale8(kreg[i], qk_inv_rms(p, r, 1), p.qk_w + p.qk_dim + hoff + sch * 8);
+                }
             }
         } else if ((kt + 1) * KT <= k_len) {
 #pragma unroll
@@ -2161,9 +2208,10 @@ extern "C" int rf_attn_combine(const void* workspace, int64_t ws_rows, int n_spl
 #endif
 }
 
-extern "C" int rf_swin_attn_fwd_dt(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
-                                   void* o, int64_t ldo, int o_dtype, int n_images, int grid_h, int grid_w, int window, int shift,
-                                int n_heads, int head_dim, float scale, void* stream) {
+static int swin_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv, void* o,
+                       int64_t ldo, int o_dtype, int n_images, int grid_h, int grid_w, int window, int shift,
+                       int n_heads, int head_dim, float scale, bool qkn, const float* qk_ss, const float* qk_w,
+                       float eps, float q_scale, void* stream) {
     RF_REQUIRE(q && k && v && o, "rf_swin_attn_fwd: null pointer");
     RF_REQUIRE(head_dim == HD, "rf_swin_attn_fwd: head_dim must be 128");
     RF_REQUIRE(window == 8, "rf_swin_attn_fwd: window must be 8 (64-token tiles)");
@@ -2171,6 +2219,8 @@ extern "C" int rf_swin_attn_fwd_dt(const void* q, int64_t ldq, const void* k, in
                grid_h, grid_w);
     RF_REQUIRE(shift >= 0 && shift < window, "rf_swin_attn_fwd: bad shift");
     RF_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0, "rf_swin_attn_fwd: strides must be 16-B aligned");
+    RF_REQUIRE(!qkn || !qk_w || (qk_ss && ((uintptr_t)qk_ss & 15) == 0 && ((uintptr_t)qk_w & 15) == 0),
+               "rf_swin_attn_fwd_qkn: qk_norm_w needs qk_ss (both 16-B aligned)");
     if (n_images <= 0) return RF_OK;
     AttnArgs a{};
     a.q = (const bf16_t*)q;
@@ -2187,14 +2237,41 @@ extern "C" int rf_swin_attn_fwd_dt(const void* q, int64_t ldq, const void* k, in
     a.shift = shift;
     a.window = window;
     a.n_split = 1;
+    a.qk_ss = qk_ss;
+    a.qk_w = qk_w;
+    a.qk_eps = eps;
+    a.qk_scale = q_scale;
+    a.qk_dim = n_heads * HD;
     dim3 grid((grid_h / window) * (grid_w / window), n_heads, n_images);
     RF_REQUIRE(o_dtype == RF_DT_BF16 || o_dtype == RF_DT_F16, "rf_swin_attn_fwd: o_dtype must be RF_DT_BF16/F16");
     a.range = o_dtype == RF_DT_F16 ? rf::range_word() : nullptr;
-    if (o_dtype == RF_DT_F16)
-        RF_LAUNCH((attn_fwd_kernel<true, 2, true>), grid, dim3(128), 0, (hipStream_t)stream, a);
-    else
-        RF_LAUNCH((attn_fwd_kernel<true, 2>), grid, dim3(128), 0, (hipStream_t)stream, a);
+    if (qkn) {
+        if (o_dtype == RF_DT_F16)
+            RF_LAUNCH((attn_fwd_kernel<true, 2, true, true>), grid, dim3(128), 0, (hipStream_t)stream, a);
+        else
+            RF_LAUNCH((attn_fwd_kernel<true, 2, false, true>), grid, dim3(128), 0, (hipStream_t)stream, a);
+    } else {
+        if (o_dtype == RF_DT_F16)
+            RF_LAUNCH((attn_fwd_kernel<true, 2, true>), grid, dim3(128), 0, (hipStream_t)stream, a);
+        else
+            RF_LAUNCH((attn_fwd_kernel<true, 2>), grid, dim3(128), 0, (hipStream_t)stream, a);
+    }
     return rf::check_launch("rf_swin_attn_fwd");
+}
+
+extern "C" int rf_swin_attn_fwd_dt(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                                   void* o, int64_t ldo, int o_dtype, int n_images, int grid_h, int grid_w, int window,
+                                   int shift, int n_heads, int head_dim, float scale, void* stream) {
+    return swin_launch(q, ldq, k, ldk, v, ldv, o, ldo, o_dtype, n_images, grid_h, grid_w, window, shift, n_heads,
+                       head_dim, scale, false, nullptr, nullptr, 0.f, 1.f, stream);
+}
+
+extern "C" int rf_swin_attn_fwd_qkn(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                                    void* o, int64_t ldo, int o_dtype, int n_images, int grid_h, int grid_w, int window,
+                                    int shift, int n_heads, int head_dim, float scale, const float* qk_ss,
+                                    const float* qk_norm_w, float eps, float q_scale, void* stream) {
+    return swin_launch(q, ldq, k, ldk, v, ldv, o, ldo, o_dtype, n_images, grid_h, grid_w, window, shift, n_heads,
+                       head_dim, scale, true, qk_ss, qk_norm_w, eps, q_scale, stream);
 }
 
 extern "C" int rf_swin_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,

@@ -100,11 +100,43 @@ struct EngineArgs {
     int persist;  // phased_sk_kernel: whole tiles strided over the grid, next tile's first K-tiles prefetched
     int out_f16;  // E_BF16 / E_SWIGLU: 16-bit output as fp16 instead of bf16 (rf_gemm_f16's RF_EPI_*_F16)
     int* range;   // fp16 outputs (out_f16, fp16 conv planes): the mapped range flag, raised on |x| > 65504
+    // Deferred RMSNorm (rf_gemm_add_prenorm / rf_gemm_rownorm, rf.h).  Producer (E_ADD, xg set): besides the
+    // fp32 residual, xg = 16-bit(x * g) and, per row, one partial sum of x^2 per BN-column tile into slot n0 / BN
+    // of that row's RF_PRENORM_SLOTS floats in ss_out (tile 0 zeroes the unused slots).  Consumer (E_BF16 /
+    // E_SWIGLU, rs_part set): every output row scaled by 1 / sqrt(sum of its slots / rs_n + rs_eps) before the
+    // bias / SwiGLU, i.e. rmsnorm(x) W^T = (x * g) W^T / rms(x) with the row scale after the dot products.
+    bf16_t* xg;
+    int64_t ldxg;
+    const float* norm_g;
+    float* ss_out;
+    int xg_f16;
+    const float* rs_part;
+    float rs_n, rs_eps;
+    // E_BF16 with seg_ss (rf_gemm_rownorm's q/k sums for a following full-width q/k RMSNorm): per row and per
+    // segment s < seg_n of seg_w output columns, PN_SLOTS partial sums of the squares of the written (rounded)
+    // values, seg_ss[row][s][slot], slot = (n0 % seg_w) / BN (the segment's first tile zeroes the unused slots)
+    float* seg_ss;
+    int seg_w, seg_n;
 };
+
+constexpr int PN_SLOTS = RF_PRENORM_SLOTS;  // partial sums per row (N <= PN_SLOTS x the narrowest BN, 128)
+
+// Deferred-RMSNorm operands of a tile live in an LDS area after the main loop's buffers (PN_AREA bytes), filled by
+// LDS-DMA (pn_issue) before the tile's main loop, so the epilogue reads them from LDS: a global load there would
+// wait (vmcnt counts in issue order) behind the epilogue's own stores or the next tile's prefetched operands.
+//   consumer (E_BF16 / E_SWIGLU, rs_part): the tile's BM rows x PN_SLOTS partial sums (32 B a row);
+//   producer (E_ADD, xg): g of the tile's BN columns, then BM x WGN floats of row-sum scratch.
+// Every issuing wave has passed its main loop's last operand wait (newer than these loads) before the epilogue,
+// whose first barrier then makes the area visible to all waves.
 
 // two f32 -> the kernel's 16-bit output pair (RNE): fp16 when the launch asks for it, else bf16
 RF_DEV uint32_t pack16(const EngineArgs& p, float lo, float hi) {
     return p.out_f16 ? pack_f16x2(lo, hi) : pack_bf16x2(lo, hi);
+}
+
+// the value of one 16-bit output as written (fp16 when the launch writes fp16, else bf16)
+RF_DEV float unpack16(const EngineArgs& p, uint32_t h) {
+    return p.out_f16 ? f16_bits_to_f32((uint16_t)h) : __uint_as_float(h << 16);
 }
 
 // uniform early exit of a gated launch (every block reads the same flag, so a stream-K grid exits whole)
@@ -399,8 +431,58 @@ RF_DEV void engine_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
 // wave's MW pixels are MW / TW2D whole rows of it and fragment i covers 16 consecutive pixels of one row.
 // FINAL = false compiles out the fused-head path (RF_CONV_FINAL) for blocks that never take it: its silu
 // values are loop-invariant across the head's outputs, get hoisted, and double the accumulators' registers.
+// LDS accesses of the deferred-RMSNorm area as inline asm, and a barrier that waits for LDS only: hipcc guards a
+// ds_read it can see with vmcnt(0) while a builtin LDS-DMA may be in flight (the persistent loop's next-tile
+// prefetch), and __syncthreads() waits vmcnt(0) too; either would drain that prefetch and this tile's stores
+RF_DEV uint32_t lds_addr(const char* p) { return (uint32_t)(uintptr_t)LDS_PTR(const char, p); }
+RF_DEV float lds_ld_f32(const char* p) {
+    float v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+    return v;
+}
+RF_DEV f32x4 lds_ld_f4(const char* p) {
+    f32x4 v;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+    return v;
+}
+RF_DEV void lds_st_f32(char* p, float v) { asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory"); }
+RF_DEV void lds_sync() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <class C, int EPI>
+constexpr int PN_AREA = EPI == E_ADD      ? C::BN * 4 + C::BM * C::WGN * 4
+                        : EPI == E_BF16   ? C::BM * PN_SLOTS * 4 + C::BM * C::WGN * 4
+                        : EPI == E_SWIGLU ? C::BM * PN_SLOTS * 4
+                                          : 0;
+
+// LDS-DMA of tile (m0, n0)'s deferred-RMSNorm operands into `area` (a no-op unless the launch has them)
+template <class C, int EPI>
+RF_DEV void pn_issue(const EngineArgs& p, char* area, int m0, int n0) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if constexpr (EPI == E_ADD) {
+        if (p.xg && wave == 0 && n0 + 4 * lane < p.n && 4 * lane < C::BN)  // 16 B (4 columns of g) a lane
+            __builtin_amdgcn_global_load_lds(GLB_PTR(void, p.norm_g + n0 + 4 * lane), LDS_PTR(void, area), 16, 0, 0);
+    } else if constexpr (EPI == E_BF16 || EPI == E_SWIGLU) {
+        if (p.rs_part) {
+            static_assert(C::BM % 32 == 0, "1-KiB pieces of 32 rows");
+            for (int c = wave; c < C::BM / 32; c += C::NWAVE) {  // piece c: rows 32 c .. 32 c + 31, 2 lanes a row
+                const int row = min(m0 + 32 * c + (lane >> 1), p.m - 1);
+                __builtin_amdgcn_global_load_lds(GLB_PTR(void, p.rs_part + (int64_t)row * PN_SLOTS + 4 * (lane & 1)),
+                                                 LDS_PTR(void, area + c * 1024), 16, 0, 0);
+            }
+        }
+    }
+}
+
+// area: the tile's deferred-RMSNorm LDS area (PN_AREA<C, EPI> bytes, staged by pn_issue; null for kernels without)
 template <class C, int EPI, int TW2D = 0, bool FINAL = true>
-RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&acc)[C::TI][C::TJ]) {
+RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&acc)[C::TI][C::TJ],
+                            char* area = nullptr) {
     constexpr int TI = C::TI, TJ = C::TJ;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -417,20 +499,40 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
         else return m0 + (wm * (C::MW / TW2D) + (i * 16) / TW2D) * p.wo + (i * 16) % TW2D + rl;
     };
     float amax = 0.f;  // fp16 outputs: running max |value| (NaN-propagating) for the range flag
+    // deferred RMSNorm consumer: 1 / rms of each row, one thread per row from its slot sums in slot order (unused
+    // slots hold +0, so any producer tiling gives its partials' exact sum), kept in slot 0 of the row's LDS entry;
+    // the stores below read it per row (no per-lane array across the epilogue: the 256-row tiles are at 256 VGPRs)
+    const bool rsc = (EPI == E_SWIGLU || EPI == E_BF16) && p.rs_part && area;
+    if constexpr (EPI == E_SWIGLU || EPI == E_BF16) {
+        if (rsc) {
+            lds_sync();  // the staged rows are visible (their DMA was waited for inside the main loop)
+            for (int t = threadIdx.x; t < C::BM; t += C::THREADS) {
+                char* q = area + t * (PN_SLOTS * 4);
+                const f32x4 a = lds_ld_f4(q), b = lds_ld_f4(q + 16);
+                const float sum = ((a[0] + a[1]) + (a[2] + a[3])) + ((b[0] + b[1]) + (b[2] + b[3]));
+                lds_st_f32(q, 1.0f / sqrtf(sum / p.rs_n + p.rs_eps));
+            }
+            lds_sync();
+        }
+    }
+    auto row_scale = [&](int i) -> float {
+        return rsc ? lds_ld_f32(area + (wm * C::MW + i * 16 + rl) * (PN_SLOTS * 4)) : 1.f;
+    };
     if constexpr (EPI == E_SWIGLU) {
         bf16_t* c = reinterpret_cast<bf16_t*>(p.c);
 #pragma unroll
-        for (int pair = 0; pair < TJ / 2; ++pair) {
-            const int gcol = cbase + pair * 32;  // 32-row interleave group: [w1 x16 | w3 x16]
-            const int ocol = (gcol >> 5) * 16 + cq;
+        for (int i = 0; i < TI; ++i) {
+            const float rsi = row_scale(i);
 #pragma unroll
-            for (int i = 0; i < TI; ++i) {
+            for (int pair = 0; pair < TJ / 2; ++pair) {
+                const int gcol = cbase + pair * 32;  // 32-row interleave group: [w1 x16 | w3 x16]
+                const int ocol = (gcol >> 5) * 16 + cq;
                 const int row = rbase + i * 16 + rl;
                 if (row < p.m) {
                     float o[4];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        float g = acc[i][2 * pair][e], u = acc[i][2 * pair + 1][e];
+                        float g = acc[i][2 * pair][e] * rsi, u = acc[i][2 * pair + 1][e] * rsi;
                         if (p.bias) {
                             g += p.bias[gcol + cq + e];
                             u += p.bias[gcol + 16 + cq + e];
@@ -610,15 +712,26 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
         if (p.range && !f16_in_range(amax)) report_f16_range(p.range, RF_RANGE_CONV);
         return;
     } else {
+        // deferred-RMSNorm producer (E_ADD with p.xg): per-lane partial sums of x^2 of the lane's rows
+        const bool pre = EPI == E_ADD && p.xg && area;
+        // q/k segment sums of the written values (E_BF16 with seg_ss): this tile's segment, if it is one of them
+        const bool segq = EPI == E_BF16 && p.seg_ss && area && n0 / p.seg_w < p.seg_n;
+        // row-sum scratch: after g of the tile's columns (producer) / after the staged ss rows (consumer)
+        char* const red = area + (EPI == E_ADD ? C::BN * 4 : C::BM * PN_SLOTS * 4);
+        if (pre) lds_sync();  // g staged (pn_issue) and visible
+        float ssr[TI];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) ssr[i] = 0.f;
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
             const int row = rbase + i * 16 + rl;
             if (row >= p.m) continue;
+            const float rsi = row_scale(i);
 #pragma unroll
             for (int j = 0; j < TJ; ++j) {
                 const int col = cbase + j * 16 + cq;
                 if (col >= p.n) continue;  // (a ragged last column tile of the 4-wave engine)
-                float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                float v[4] = {acc[i][j][0] * rsi, acc[i][j][1] * rsi, acc[i][j][2] * rsi, acc[i][j][3] * rsi};
                 if (p.bias) {
                     const float4 b = *reinterpret_cast<const float4*>(p.bias + col);
                     v[0] += b.x;
@@ -629,17 +742,77 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                 const int64_t o = (int64_t)row * p.ldc + col;
                 if constexpr (EPI == E_BF16) {
                     amax = amax3(amax3(amax, v[0], v[1]), v[2], v[3]);
-                    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.c) + o) =
-                        make_uint2(pack16(p, v[0], v[1]), pack16(p, v[2], v[3]));
+                    const uint32_t lo = pack16(p, v[0], v[1]), hi = pack16(p, v[2], v[3]);
+                    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.c) + o) = make_uint2(lo, hi);
+                    if (segq) {  // squares of the rounded values, as a row kernel reading them back would sum
+                        const float r0 = unpack16(p, lo & 0xffffu), r1 = unpack16(p, lo >> 16);
+                        const float r2 = unpack16(p, hi & 0xffffu), r3 = unpack16(p, hi >> 16);
+                        ssr[i] += r0 * r0 + r1 * r1 + r2 * r2 + r3 * r3;
+                    }
                 } else {  // E_F32, or E_ADD whose accumulators started from the C tile (load_c_acc)
                     *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + o) = make_float4(v[0], v[1], v[2], v[3]);
+                    if (pre) {
+                        const f32x4 g = lds_ld_f4(area + (col - n0) * 4);
+                        const float y0 = v[0] * g[0], y1 = v[1] * g[1], y2 = v[2] * g[2], y3 = v[3] * g[3];
+                        amax = amax3(amax3(amax, y0, y1), y2, y3);
+                        const uint32_t lo = p.xg_f16 ? pack_f16x2(y0, y1) : pack_bf16x2(y0, y1);
+                        const uint32_t hi = p.xg_f16 ? pack_f16x2(y2, y3) : pack_bf16x2(y2, y3);
+                        *reinterpret_cast<uint2*>(p.xg + (int64_t)row * p.ldxg + col) = make_uint2(lo, hi);
+                        ssr[i] += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+                    }
                 }
             }
         }
         if constexpr (EPI == E_BF16)
             if (p.range && !f16_in_range(amax)) report_f16_range(p.range, RF_RANGE_GEMM);
+        if constexpr (EPI == E_ADD || EPI == E_BF16) {
+            if (pre && p.xg_f16 && p.range && !f16_in_range(amax)) report_f16_range(p.range, RF_RANGE_RMSNORM);
+            if (pre || segq) {
+                // row sums: the 4 lane groups of a row (lanes l, l ^ 16, l ^ 32, l ^ 48), then the WGN waves of
+                // its row band through LDS, in a fixed order (bit-reproducible)
+#pragma unroll
+                for (int i = 0; i < TI; ++i) {
+                    ssr[i] += __shfl_xor(ssr[i], 16, 64);
+                    ssr[i] += __shfl_xor(ssr[i], 32, 64);
+                }
+                if (lane < 16) {
+#pragma unroll
+                    for (int i = 0; i < TI; ++i) lds_st_f32(red + (wn * C::BM + wm * C::MW + i * 16 + rl) * 4, ssr[i]);
+                }
+                lds_sync();
+                // destination row block and slot: the producer's [row][PN_SLOTS] (slot = column tile), or the
+                // segment's [row][seg_n][PN_SLOTS] (slot = column tile inside the segment)
+                int slot, nslots, ld;
+                float* base;
+                if (pre) {
+                    slot = n0 / C::BN;
+                    nslots = (p.n + C::BN - 1) / C::BN;
+                    ld = PN_SLOTS;
+                    base = p.ss_out;
+                } else {
+                    slot = (n0 % p.seg_w) / C::BN;
+                    nslots = p.seg_w / C::BN;
+                    ld = p.seg_n * PN_SLOTS;
+                    base = p.seg_ss + (n0 / p.seg_w) * PN_SLOTS;
+                }
+                for (int t = threadIdx.x; t < C::BM; t += C::THREADS) {
+                    const int row = m0 + t;
+                    if (row < p.m) {
+                        float s = 0.f;
+#pragma unroll
+                        for (int w = 0; w < C::WGN; ++w) s += lds_ld_f32(red + (w * C::BM + t) * 4);
+                        float* dst = base + (int64_t)row * ld;
+                        dst[slot] = s;
+                        if (slot == 0)
+                            for (int z = nslots; z < PN_SLOTS; ++z) dst[z] = 0.f;
+                    }
+                }
+            }
+        }
     }
 }
+
+
 
 // ---------------------------------------------------------------------------------------------
 // 256x256 tile, BK = 64, 8 waves (2 x 4, each 128 x 64): the phased main loop.
@@ -1049,7 +1222,8 @@ RF_DEV void phased3_mainloop(const EngineArgs& p, char* smem, int m0, int n0, in
 
 template <int BM, int EPI, int NTERM = 1>
 __global__ __launch_bounds__(512, 1) void phased3_kernel(EngineArgs p) {
-    __shared__ __attribute__((aligned(16))) char smem[3 * ph::Cfg<BM>::TILE];
+    using TE = Tile<BM, 256, 2, 4, 4>;  // the epilogue's view of the block
+    __shared__ __attribute__((aligned(16))) char smem[3 * ph::Cfg<BM>::TILE + PN_AREA<TE, EPI>];
     if (gated_off(p)) return;
     const int tiles_m = (p.m + BM - 1) / BM;
     const int nwg = gridDim.x;
@@ -1059,13 +1233,16 @@ __global__ __launch_bounds__(512, 1) void phased3_kernel(EngineArgs p) {
     int tm, tn;
     tile_coords(wg, tiles_m, p.n / ph::BN, p.group_m, tm, tn);
     f32x4 acc[BM / 32][4];
+    char* const area = smem + 3 * ph::Cfg<BM>::TILE;
+    pn_issue<TE, EPI>(p, area, tm * BM, tn * ph::BN);
     phased3_mainloop<BM, NTERM, EPI == E_ADD>(p, smem, tm * BM, tn * ph::BN, 0, p.k / ph::BK2, acc);
-    engine_epilogue<Tile<BM, 256, 2, 4, 4>, EPI>(p, tm * BM, tn * ph::BN, acc);
+    engine_epilogue<TE, EPI>(p, tm * BM, tn * ph::BN, acc, area);
 }
 
 template <int BM, int EPI, int NTERM, bool GATHER>
 __global__ __launch_bounds__(512, 1) void phased_kernel(EngineArgs p) {
-    __shared__ __attribute__((aligned(16))) char smem[ph::Cfg<BM>::LDS];
+    using TE = Tile<BM, 256, 2, 4, 4>;
+    __shared__ __attribute__((aligned(16))) char smem[ph::Cfg<BM>::LDS + PN_AREA<TE, EPI>];
     if (gated_off(p)) return;
     const int tiles_m = (p.m + BM - 1) / BM;
     const int nwg = gridDim.x;
@@ -1075,8 +1252,10 @@ __global__ __launch_bounds__(512, 1) void phased_kernel(EngineArgs p) {
     int tm, tn;
     tile_coords(wg, tiles_m, p.n / ph::BN, p.group_m, tm, tn);
     f32x4 acc[BM / 32][4];
+    char* const area = smem + ph::Cfg<BM>::LDS;
+    pn_issue<TE, EPI>(p, area, tm * BM, tn * ph::BN);
     phased_mainloop<BM, NTERM, GATHER, EPI == E_ADD>(p, smem, tm * BM, tn * ph::BN, 0, p.k / ph::BK2, acc);
-    engine_epilogue<Tile<BM, 256, 2, 4, 4>, EPI>(p, tm * BM, tn * ph::BN, acc);
+    engine_epilogue<TE, EPI>(p, tm * BM, tn * ph::BN, acc, area);
 }
 
 // K-tiles 0 and 1 of a 256x256 phased tile, issued exactly as phased_mainloop's prologue issues them (same
@@ -1119,7 +1298,10 @@ RF_DEV void phased_issue01(const EngineArgs& p, char* smem, int m0, int n0, int 
 template <int EPI, int NTERM>
 __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
     constexpr int TI = 8, TJ = 4, BM = 256, TS = BM * ph::BN;
-    __shared__ __attribute__((aligned(16))) char smem[ph::Cfg<BM>::LDS];
+    using TE = Tile<256, 256, 2, 4, 4>;  // the epilogue's view of the block
+    __shared__ __attribute__((aligned(16))) char smem[ph::Cfg<BM>::LDS + PN_AREA<TE, EPI>];
+    char* const area = smem + ph::Cfg<BM>::LDS;
+    const bool pn = p.xg || p.rs_part;  // deferred-RMSNorm operands staged per tile (pn_issue)
     if (gated_off(p)) return;
     const int tiles_m = (p.m + BM - 1) / BM, tiles_n = p.n / ph::BN;
     const int nwg = gridDim.x;
@@ -1146,6 +1328,10 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
         for (int tile = wg; tile < ntiles; tile += nwg) {
             int tm, tn;
             tile_coords(tile, tiles_m, tiles_n, p.group_m, tm, tn);
+            if (pn) {
+                if (tile != wg) lds_sync();  // the previous tile's epilogue is done with the area
+                pn_issue<TE, EPI>(p, area, tm * BM, tn * ph::BN);
+            }
             phased_mainloop<BM, NTERM, false, EPI == E_ADD>(p, smem, tm * BM, tn * ph::BN, 0, iters, acc, pre);
             pre = tile + nwg < ntiles;
             if (pre) {
@@ -1154,7 +1340,7 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
                 __syncthreads();  // every wave's last LDS reads of this tile are done (lgkmcnt drained per phase)
                 phased_issue01(p, smem, tm2 * BM, tn2 * ph::BN, iters);
             }
-            engine_epilogue<Tile<256, 256, 2, 4, 4>, EPI>(p, tm * BM, tn * ph::BN, acc);
+            engine_epilogue<TE, EPI>(p, tm * BM, tn * ph::BN, acc, area);
         }
         return;
     }
@@ -1170,6 +1356,7 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
         const int m0 = tm * BM, n0 = tn * ph::BN;
         wait_vm<0>();
         __syncthreads();  // the previous segment's LDS readers are done
+        if (pn && kf == 0) pn_issue<TE, EPI>(p, area, m0, n0);  // (only the tile's owner runs its epilogue)
         phased_mainloop<BM, NTERM, false, EPI == E_ADD>(p, smem, m0, n0, kf, kl, acc);
         if (stamp && ns < 14) st[ns++] = __builtin_amdgcn_s_memtime();
         if (kf != 0) {
@@ -1217,7 +1404,7 @@ __global__ __launch_bounds__(512, 1) void phased_sk_kernel(EngineArgs p) {
                 }
             }
             if (stamp && ns < 14) st[ns++] = __builtin_amdgcn_s_memtime();
-            engine_epilogue<Tile<256, 256, 2, 4, 4>, EPI>(p, m0, n0, acc);
+            engine_epilogue<TE, EPI>(p, m0, n0, acc, area);
         }
         if (stamp && ns < 14) st[ns++] = __builtin_amdgcn_s_memtime();
         it += kl - kf;
@@ -1661,7 +1848,9 @@ __global__ __launch_bounds__(256, 1) void quad_kernel(EngineArgs p) {
 template <class C, int EPI, int NTERM, bool GATHER, bool SK>
 __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
     constexpr int BM = C::BM, BN = C::BN, TI = C::TI, TJ = C::TJ;
-    __shared__ __attribute__((aligned(16))) char smem[C::STAGES * stage_bytes<C, NTERM>()];
+    constexpr int MAIN = C::STAGES * stage_bytes<C, NTERM>();
+    __shared__ __attribute__((aligned(16))) char smem[MAIN + PN_AREA<C, EPI>];
+    char* const area = smem + MAIN;
     if (gated_off(p)) return;
 
     const int tiles_m = (p.m + BM - 1) / BM;
@@ -1674,8 +1863,9 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
         int tm, tn;
         tile_coords(wg, tiles_m, p.n / BN, p.group_m, tm, tn);
         const int m0 = tm * BM, n0 = tn * BN;
+        pn_issue<C, EPI>(p, area, m0, n0);
         engine_mainloop<C, NTERM, GATHER, EPI == E_ADD>(p, smem, m0, n0, 0, p.k / (BK * C::KH), acc);
-        engine_epilogue<C, EPI>(p, m0, n0, acc);
+        engine_epilogue<C, EPI>(p, m0, n0, acc, area);
     } else {
         const int iters = p.k / (BK * C::KH);
         const int64_t ntiles64 = (int64_t)tiles_m * (p.n / BN);
@@ -1694,6 +1884,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
             const int m0 = tm * BM, n0 = tn * BN;
             wait_vm<0>();
             __syncthreads();  // the previous segment's LDS readers are done with the ring
+            if (kf == 0) pn_issue<C, EPI>(p, area, m0, n0);  // (only the tile's owner runs its epilogue)
             engine_mainloop<C, NTERM, GATHER, EPI == E_ADD>(p, smem, m0, n0, kf, kl, acc);
             if (kf != 0) {
                 // partial tile in accumulator order (1 KiB per wave-instruction), stored write-through
@@ -1743,7 +1934,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void engine_kernel(EngineArgs p) {
                             }
                     }
                 }
-                engine_epilogue<C, EPI>(p, m0, n0, acc);
+                engine_epilogue<C, EPI>(p, m0, n0, acc, area);
             }
             it += kl - kf;
         }
@@ -3441,9 +3632,22 @@ static int run_quad(const EngineArgs& p, int epilogue, int mode, void* workspace
 }
 #endif  // RF_STUDY
 
+// the deferred-RMSNorm operands of one GEMM (rf_gemm_add_prenorm: xg / norm_g / ss_out; rf_gemm_rownorm: rs_*)
+struct NormIO {
+    void* xg = nullptr;
+    int64_t ldxg = 0;
+    const float* norm_g = nullptr;
+    float* ss_out = nullptr;
+    int xg_f16 = 0;
+    const float* rs_part = nullptr;
+    float rs_n = 0.f, rs_eps = 0.f;
+    float* seg_ss = nullptr;
+    int seg_w = 0, seg_n = 0;
+};
+
 static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
                      const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
-                     void* stream, const int* gate, bool f16 = false) {
+                     void* stream, const int* gate, bool f16 = false, const NormIO* nio = nullptr) {
     RF_REQUIRE(a && w && c, "rf_gemm_bf16: null pointer");
     int out_f16 = 0;
     if (epilogue == RF_EPI_F16 || epilogue == RF_EPI_SWIGLU_F16) {  // fp16 16-bit outputs
@@ -3472,8 +3676,22 @@ static int gemm_bf16(const void* a, int64_t lda, const void* w, int64_t ldw, voi
     p.gate = gate;
     p.out_f16 = out_f16;
     p.range = out_f16 ? rf::range_word() : nullptr;
+    if (nio) {
+        p.xg = (bf16_t*)nio->xg;
+        p.ldxg = nio->ldxg;
+        p.norm_g = nio->norm_g;
+        p.ss_out = nio->ss_out;
+        p.xg_f16 = nio->xg_f16;
+        p.rs_part = nio->rs_part;
+        p.rs_n = nio->rs_n;
+        p.rs_eps = nio->rs_eps;
+        p.seg_ss = nio->seg_ss;
+        p.seg_w = nio->seg_w;
+        p.seg_n = nio->seg_n;
+        if (nio->xg && nio->xg_f16) p.range = rf::range_word();
+    }
 #ifdef RF_STUDY
-    if (const int qm = quad_mode(m, n, k, lda, ldw, epilogue)) {
+    if (const int qm = nio ? 0 : quad_mode(m, n, k, lda, ldw, epilogue)) {  // (the 4-wave epilogue has no norm I/O)
         return f16 ? run_quad<P_F16>(p, epilogue, qm, workspace, ws_bytes, stream, "rf_gemm_f16")
                    : run_quad<1>(p, epilogue, qm, workspace, ws_bytes, stream, "rf_gemm_bf16");
     }
@@ -3536,6 +3754,60 @@ extern "C" int rf_gemm_f16(const void* a, int64_t lda, const void* w, int64_t ld
                            const float* bias, int m, int n, int k, int epilogue, void* workspace, int64_t ws_bytes,
                            void* stream) {
     return gemm_bf16(a, lda, w, ldw, c, ldc, bias, m, n, k, epilogue, workspace, ws_bytes, stream, nullptr, true);
+}
+
+// Deferred RMSNorm (rf.h): the producer.  Every kernel the dispatch below can pick for RF_EPI_ADD_F32 (phased3,
+// phased, phased stream-K, ring engine data-parallel / stream-K) runs the engine epilogue with the LDS row-sum
+// area; N > RF_PRENORM_SLOTS x 128 (more column tiles than slots) takes the GEMM + rf_prenorm.
+extern "C" int rf_gemm_add_prenorm(const void* a, int64_t lda, const void* w, int64_t ldw, float* x, int64_t ldx,
+                                   int m, int n, int k, const float* norm_w, void* xg, int64_t ldxg, float* ss,
+                                   int operand_dtype, void* workspace, int64_t ws_bytes, void* stream) {
+    RF_REQUIRE(x && norm_w && xg && ss, "rf_gemm_add_prenorm: null pointer");
+    RF_REQUIRE(operand_dtype == RF_DT_F16 || operand_dtype == RF_DT_BF16, "rf_gemm_add_prenorm: operand_dtype");
+    RF_REQUIRE(ldxg >= n && ldxg % 4 == 0 && ((uintptr_t)xg & 7) == 0, "rf_gemm_add_prenorm: xg rows (ldxg >= N, 8-B)");
+    RF_REQUIRE(((uintptr_t)ss & 15) == 0 && ((uintptr_t)norm_w & 15) == 0, "rf_gemm_add_prenorm: ss / norm_w 16-B aligned");
+    const bool f16 = operand_dtype == RF_DT_F16;
+    if (n > PN_SLOTS * 128) {
+        const int rc = gemm_bf16(a, lda, w, ldw, x, ldx, nullptr, m, n, k, RF_EPI_ADD_F32, workspace, ws_bytes, stream,
+                                 nullptr, f16);
+        if (rc != RF_OK) return rc;
+        return rf_prenorm(x, ldx, norm_w, xg, ldxg, ss, m, n, operand_dtype, stream);
+    }
+    NormIO nio;
+    nio.xg = xg;
+    nio.ldxg = ldxg;
+    nio.norm_g = norm_w;
+    nio.ss_out = ss;
+    nio.xg_f16 = f16;
+    return gemm_bf16(a, lda, w, ldw, x, ldx, nullptr, m, n, k, RF_EPI_ADD_F32, workspace, ws_bytes, stream, nullptr,
+                     f16, &nio);
+}
+
+// Deferred RMSNorm: the consumer (A = the producer's xg, rows scaled by 1 / rms in the epilogue)
+extern "C" int rf_gemm_rownorm(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int m,
+                               int n, int k, int epilogue, const float* ss, int norm_dim, float eps, float* seg_ss,
+                               int seg_w, int n_seg, int operand_dtype, void* workspace, int64_t ws_bytes,
+                               void* stream) {
+    RF_REQUIRE(ss && ((uintptr_t)ss & 15) == 0, "rf_gemm_rownorm: ss must be 16-B aligned");
+    RF_REQUIRE(norm_dim > 0, "rf_gemm_rownorm: norm_dim must be positive");
+    RF_REQUIRE(epilogue == RF_EPI_BF16 || epilogue == RF_EPI_F16 || epilogue == RF_EPI_SWIGLU ||
+                   epilogue == RF_EPI_SWIGLU_F16,
+               "rf_gemm_rownorm: epilogue must be RF_EPI_BF16 / F16 / SWIGLU / SWIGLU_F16 (got %d)", epilogue);
+    RF_REQUIRE(operand_dtype == RF_DT_F16 || operand_dtype == RF_DT_BF16, "rf_gemm_rownorm: operand_dtype");
+    RF_REQUIRE(!seg_ss || ((epilogue == RF_EPI_BF16 || epilogue == RF_EPI_F16) && ((uintptr_t)seg_ss & 15) == 0 &&
+                           seg_w > 0 && seg_w % 256 == 0 && seg_w <= PN_SLOTS * 128 && n_seg >= 1 &&
+                           (int64_t)seg_w * n_seg <= n),
+               "rf_gemm_rownorm: seg_ss needs a 16-bit (non-SwiGLU) epilogue, 16-B alignment, seg_w %% 256 == 0 and "
+               "<= %d, n_seg >= 1 segments inside N", PN_SLOTS * 128);
+    NormIO nio;
+    nio.rs_part = ss;
+    nio.rs_n = (float)norm_dim;
+    nio.rs_eps = eps;
+    nio.seg_ss = seg_ss;
+    nio.seg_w = seg_w;
+    nio.seg_n = seg_ss ? n_seg : 0;
+    return gemm_bf16(a, lda, w, ldw, c, ldc, nullptr, m, n, k, epilogue, workspace, ws_bytes, stream, nullptr,
+                     operand_dtype == RF_DT_F16, &nio);
 }
 
 extern "C" int rf_gemm_bf16_if(const int* flag, const void* a, int64_t lda, const void* w, int64_t ldw, void* c,

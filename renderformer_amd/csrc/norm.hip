@@ -84,6 +84,39 @@ __global__ __launch_bounds__(256) void rmsnorm_v_kernel(const float* __restrict_
     if (F16 && range && !f16_in_range(amax)) report_f16_range(range, RF_RANGE_RMSNORM);
 }
 
+// Deferred RMSNorm, row form (rf_prenorm): xg = 16-bit(x * g) and the row's sum of x^2 into slot 0 of its
+// RF_PRENORM_SLOTS floats (slots 1.. zero), one pass over the row; the consumer GEMM (rf_gemm_rownorm) applies
+// 1 / rms.  The first layer's pre-norm (x from the embedding, not from a GEMM) and the fallback of
+// rf_gemm_add_prenorm above RF_PRENORM_SLOTS column tiles.
+template <bool F16>
+__global__ __launch_bounds__(256) void prenorm_kernel(const float* __restrict__ x, int64_t ldx,
+                                                      const float* __restrict__ w, bf16_t* __restrict__ xg,
+                                                      int64_t ldg, float* __restrict__ ss, int rows, int dim,
+                                                      int* range) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float* xr = x + (int64_t)row * ldx;
+    bf16_t* orow = xg + (int64_t)row * ldg;
+    float s = 0.f, amax = 0.f;
+    for (int c = lane * 4; c < dim; c += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(xr + c);
+        const float4 g = *reinterpret_cast<const float4*>(w + c);
+        s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        const float y0 = v.x * g.x, y1 = v.y * g.y, y2 = v.z * g.z, y3 = v.w * g.w;
+        if constexpr (F16) amax = amax3(amax3(amax, y0, y1), y2, y3);
+        uint2 pk;
+        pk.x = pack_out<F16>(y0, y1);
+        pk.y = pack_out<F16>(y2, y3);
+        *reinterpret_cast<uint2*>(orow + c) = pk;
+    }
+    s = wave_sum(s);
+    if (lane < RF_PRENORM_SLOTS / 4)
+        reinterpret_cast<float4*>(ss + (int64_t)row * RF_PRENORM_SLOTS)[lane] =
+            lane == 0 ? make_float4(s, 0.f, 0.f, 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (F16 && range && !f16_in_range(amax)) report_f16_range(range, RF_RANGE_RMSNORM);
+}
+
 // ----------------------------------------------------------------------------- q/k norm + RoPE
 // Work unit = (segment, head h, 8-element chunk j of the first half): it owns chunks j and
 // j+8 of that head, i.e. the rotation pairs (8j+e, 8j+e+64), so the half-split rotation is
@@ -466,6 +499,27 @@ extern "C" int rf_rmsnorm(const float* x, int64_t ldx, const float* weight, floa
 extern "C" int rf_rmsnorm_f16(const float* x, int64_t ldx, const float* weight, float eps, void* out, int64_t ldo,
                               int rows, int dim, void* stream) {
     return rmsnorm_launch<true>(x, ldx, weight, eps, out, ldo, rows, dim, stream, "rf_rmsnorm_f16");
+}
+
+extern "C" int rf_prenorm(const float* x, int64_t ldx, const float* norm_w, void* xg, int64_t ldxg, float* ss,
+                          int rows, int dim, int operand_dtype, void* stream) {
+    RF_REQUIRE(x && norm_w && xg && ss, "rf_prenorm: null pointer");
+    RF_REQUIRE(operand_dtype == RF_DT_F16 || operand_dtype == RF_DT_BF16, "rf_prenorm: operand_dtype");
+    RF_REQUIRE(dim > 0 && dim % 4 == 0 && ldx % 4 == 0 && ldxg % 4 == 0 && ldx >= dim && ldxg >= dim,
+               "rf_prenorm: dim / ld must be multiples of 4 (ld >= dim)");
+    RF_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)norm_w & 15) == 0 && ((uintptr_t)xg & 7) == 0 &&
+                   ((uintptr_t)ss & 15) == 0,
+               "rf_prenorm: x / norm_w / ss 16-B and xg 8-B aligned");
+    if (rows <= 0) return RF_OK;
+    const dim3 grid((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK);
+    hipStream_t st = (hipStream_t)stream;
+    if (operand_dtype == RF_DT_F16)
+        RF_LAUNCH(prenorm_kernel<true>, grid, dim3(256), 0, st, x, ldx, norm_w, (bf16_t*)xg, ldxg, ss, rows, dim,
+                  rf::range_word());
+    else
+        RF_LAUNCH(prenorm_kernel<false>, grid, dim3(256), 0, st, x, ldx, norm_w, (bf16_t*)xg, ldxg, ss, rows, dim,
+                  nullptr);
+    return rf::check_launch("rf_prenorm");
 }
 
 extern "C" int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t src_gstride, void* dst, int64_t ld_dst,

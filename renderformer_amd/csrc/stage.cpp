@@ -3,9 +3,10 @@
 // rf_encoder_forward replaces TransformerEncoder.forward (renderformer/layers/attention.py:579-590), i.e. per layer
 // AttentionLayer.forward (:484-527): pre-norm multi-head self-attention with full-width q/k RMSNorm and the
 // triangle RoPE (MultiHeadAttention :115-202, rope.py:106-149) and the SwiGLU FFN (:51-57), both residual.  It is
-// host code only: it issues the library's own unit entry points (rf_rmsnorm*, rf_gemm_*, rf_qk_norm_rope,
-// rf_attn_fwd_dt) on the caller's stream in exactly the order model.py::_stage1 does, so a stack run through
-// here is bit-identical to the Python-orchestrated one, with one C call instead of 8 per layer from Python.
+// host code only: it issues the library's own unit entry points (rf_prenorm, rf_gemm_add_prenorm, rf_gemm_rownorm,
+// rf_gemm_*, rf_qk_norm_rope, rf_attn_fwd_dt) on the caller's stream in exactly the order model.py::_stage1 does,
+// so a stack run through here is bit-identical to the Python-orchestrated one, with one C call instead of 7 per
+// layer from Python.  The pre-norms are deferred (rf.h): no RMSNorm row kernel after layer 0's first one.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -18,7 +19,9 @@ int64_t align_up(int64_t b) { return (b + kAlign - 1) / kAlign * kAlign; }
 
 // activation buffers of the encoder stack, carved from one caller-owned workspace
 struct EncBufs {
-    int64_t h, qkv, att, g, total;  // byte offsets: h [T, D] half, qkv [T, 3D] bf16, att [T, D] half, g [T, F] half
+    // byte offsets: h [T, D] half (x * g of the deferred RMSNorm), qkv [T, 3D] bf16, att [T, D] half, g [T, F] half,
+    // ss [T, RF_PRENORM_SLOTS] f32 (the norm's partial sums of squares)
+    int64_t h, qkv, att, g, ss, total;
 };
 EncBufs enc_layout(int rows, int dim, int ffn) {
     EncBufs b;
@@ -27,7 +30,8 @@ EncBufs enc_layout(int rows, int dim, int ffn) {
     b.qkv = b.h + align_up(r * dim * 2);
     b.att = b.qkv + align_up(r * 3 * dim * 2);
     b.g = b.att + align_up(r * dim * 2);
-    b.total = b.g + align_up(r * (int64_t)ffn * 2);
+    b.ss = b.g + align_up(r * (int64_t)ffn * 2);
+    b.total = b.ss + align_up(r * RF_PRENORM_SLOTS * 4);
     return b;
 }
 
@@ -72,28 +76,36 @@ extern "C" int rf_encoder_forward(float* x, int64_t ldx, const rf_encoder_desc* 
     const bool f16 = d->operand_dtype == RF_DT_F16;
     const EncBufs b = enc_layout(T, D, F);
     char* ws = static_cast<char*>(d->workspace);
-    void* h = ws + b.h;                               // rmsnorm output: the next GEMM's A operand
+    void* h = ws + b.h;                               // x * g (deferred RMSNorm): the next GEMM's A operand
     uint16_t* qkv = reinterpret_cast<uint16_t*>(ws + b.qkv);  // bf16 q | k | v (attention operands)
     void* att = ws + b.att;                           // attention O: the out-projection's A operand
     void* g = ws + b.g;                               // SwiGLU output: W2's A operand
-    auto rmsnorm = f16 ? rf_rmsnorm_f16 : rf_rmsnorm;
+    float* ss = reinterpret_cast<float*>(ws + b.ss);  // the pre-norm's partial sums of squares
     auto gemm = f16 ? rf_gemm_f16 : rf_gemm_bf16;
     const int epi_swiglu = f16 ? RF_EPI_SWIGLU_F16 : RF_EPI_SWIGLU;
     const int o_dt = f16 ? RF_DT_F16 : RF_DT_BF16;
+    const int dt = d->operand_dtype;
+    void* gws = d->gemm_ws;
+    const int64_t gwb = d->gemm_ws_bytes;
+    // each pre-norm is deferred (rf.h): the residual GEMM before it writes x * g and the row sums of squares, the
+    // projection after it scales its rows by 1 / rms; only layer 0's attention norm reads x in a row kernel
+    RF_CALL(rf_prenorm(x, ldx, d->layers[0].attn_norm, h, D, ss, T, D, dt, stream));
     for (int i = 0; i < d->n_layers; ++i) {
         const rf_encoder_layer& L = d->layers[i];
-        RF_CALL(rmsnorm(x, ldx, L.attn_norm, d->eps, h, D, T, D, stream));
-        RF_CALL(gemm(h, D, L.w_qkv, D, qkv, 3 * D, nullptr, T, 3 * D, D, RF_EPI_BF16, d->gemm_ws, d->gemm_ws_bytes,
-                     stream));
+        RF_CALL(rf_gemm_rownorm(h, D, L.w_qkv, D, qkv, 3 * D, T, 3 * D, D, RF_EPI_BF16, ss, D, d->eps, nullptr, 0, 0, dt, gws, gwb,
+                                stream));
         RF_CALL(rf_qk_norm_rope(qkv, 3 * D, qkv, 3 * D, nullptr, T, D, H, 2, L.qk_norm, d->eps, kQLog2Scale, d->pos,
                                 d->ld_pos, 1, d->freqs, d->pos ? d->n_freqs : 0, stream));
         if (d->timer_attn) RF_CALL(rf_ktimer_arm());
         RF_CALL(rf_attn_fwd_dt(qkv, 3 * D, qkv + D, 3 * D, qkv + 2 * D, 3 * D, att, D, RF_DT_BF16, o_dt, d->problems,
                                d->n_problems, H, 128, kLn2, d->attn_ws, d->bounds, d->bounds ? d->grid : 0, stream));
-        RF_CALL(gemm(att, D, L.w_out, D, x, ldx, nullptr, T, D, D, RF_EPI_ADD_F32, d->gemm_ws, d->gemm_ws_bytes, stream));
-        RF_CALL(rmsnorm(x, ldx, L.ffn_norm, d->eps, h, D, T, D, stream));
-        RF_CALL(gemm(h, D, L.w13, D, g, F, nullptr, T, 2 * F, D, epi_swiglu, d->gemm_ws, d->gemm_ws_bytes, stream));
-        RF_CALL(gemm(g, F, L.w2, F, x, ldx, nullptr, T, D, F, RF_EPI_ADD_F32, d->gemm_ws, d->gemm_ws_bytes, stream));
+        RF_CALL(rf_gemm_add_prenorm(att, D, L.w_out, D, x, ldx, T, D, D, L.ffn_norm, h, D, ss, dt, gws, gwb, stream));
+        RF_CALL(rf_gemm_rownorm(h, D, L.w13, D, g, F, T, 2 * F, D, epi_swiglu, ss, D, d->eps, nullptr, 0, 0, dt, gws, gwb, stream));
+        if (i + 1 < d->n_layers)
+            RF_CALL(rf_gemm_add_prenorm(g, F, L.w2, F, x, ldx, T, D, F, d->layers[i + 1].attn_norm, h, D, ss, dt, gws,
+                                        gwb, stream));
+        else
+            RF_CALL(gemm(g, F, L.w2, F, x, ldx, nullptr, T, D, F, RF_EPI_ADD_F32, gws, gwb, stream));
     }
     return RF_OK;
 }
@@ -106,7 +118,7 @@ extern "C" int rf_encoder_forward(float* x, int64_t ldx, const rf_encoder_desc* 
 // launches in the same order as model.py::_stage2 (bit-identical), one C call for the whole stack.
 namespace {
 struct DecBufs {
-    int64_t h, q2, att, g, hc, kv, kview, qkv, total;
+    int64_t h, q2, att, g, hc, kv, kview, qkv, ss, qkss, total;
 };
 DecBufs dec_layout(const rf_decoder_desc* d) {
     const int64_t T2 = d->rows, D = d->dim, F = d->ffn_dim, T1 = d->ctx_rows, L = d->n_layers;
@@ -120,7 +132,9 @@ DecBufs dec_layout(const rf_decoder_desc* d) {
     b.kv = b.hc + align_up(T1 * d->ctx_dim * 2);
     b.kview = b.kv + align_up(T1 * (kv_batch ? L : 1) * 2 * D * 2);
     b.qkv = b.kview + align_up((int64_t)d->kv_rows * (k_batch ? L : 1) * D * 2);
-    b.total = b.qkv + (d->layers && d->n_layers > 0 && d->layers[0].self_norm ? align_up(T2 * 3 * D * 2) : 0);
+    b.ss = b.qkv + (d->layers && d->n_layers > 0 && d->layers[0].self_norm ? align_up(T2 * 3 * D * 2) : 0);
+    b.qkss = b.ss + align_up(T2 * RF_PRENORM_SLOTS * 4);
+    b.total = b.qkss + (d->swin ? align_up(T2 * 2 * RF_PRENORM_SLOTS * 4) : 0);
     return b;
 }
 }  // namespace
@@ -186,6 +200,9 @@ extern "C" int rf_decoder_forward(float* x, int64_t ldx, const rf_decoder_desc* 
     uint16_t* kv = reinterpret_cast<uint16_t*>(ws + b.kv);
     uint16_t* kview = reinterpret_cast<uint16_t*>(ws + b.kview);
     uint16_t* qkv = reinterpret_cast<uint16_t*>(ws + b.qkv);
+    float* ss = reinterpret_cast<float*>(ws + b.ss);
+    float* qkss = reinterpret_cast<float*>(ws + b.qkss);  // Swin q/k row sums (rf_swin_attn_fwd_qkn)
+    const int dt = d->operand_dtype;
     const int64_t ld_kv = (kv_batch ? (int64_t)NL : 1) * 2 * D, ld_kview = (k_batch ? (int64_t)NL : 1) * D;
     auto rmsnorm = f16 ? rf_rmsnorm_f16 : rf_rmsnorm;
     auto gemm = f16 ? rf_gemm_f16 : rf_gemm_bf16;
@@ -204,11 +221,12 @@ extern "C" int rf_decoder_forward(float* x, int64_t ldx, const rf_decoder_desc* 
                                        d->k_norm_all, D, d->eps, 1.0f, d->kv_pos, d->ld_kv_pos, 1, d->freqs,
                                        d->kv_pos ? nf : 0, stream));
     int tap = 0;
+    // the ray tokens' pre-norms are deferred as in the encoder (rf.h): only layer 0's query norm is a row kernel
+    RF_CALL(rf_prenorm(x, ldx, d->layers[0].query_norm, h, D, ss, T2, D, dt, stream));
     for (int i = 0; i < NL; ++i) {
         const rf_decoder_layer& L = d->layers[i];
         // (i) cross-attention
-        RF_CALL(rmsnorm(x, ldx, L.query_norm, d->eps, h, D, T2, D, stream));
-        RF_CALL(gemm(h, D, L.w_q, D, q2, D, nullptr, T2, D, D, RF_EPI_BF16, gws, gwb, stream));
+        RF_CALL(rf_gemm_rownorm(h, D, L.w_q, D, q2, D, T2, D, D, RF_EPI_BF16, ss, D, d->eps, nullptr, 0, 0, dt, gws, gwb, stream));
         const uint16_t* kvi = kv_batch ? kv + (int64_t)2 * D * i : kv;
         if (!kv_batch) {
             RF_CALL(rmsnorm(d->ctx, d->ld_ctx, L.kv_norm, d->eps, hc, d->ctx_dim, T1, d->ctx_dim, stream));
@@ -225,12 +243,20 @@ extern "C" int rf_decoder_forward(float* x, int64_t ldx, const rf_decoder_desc* 
         RF_CALL(rf_attn_fwd_dt(q2, D, ki, ld_kview, kvi + D, ld_kv, att, D, RF_DT_BF16, o_dt, d->cross_problems,
                                d->n_cross, H, 128, kLn2, d->attn_ws, d->cross_bounds,
                                d->cross_bounds ? d->cross_grid : 0, stream));
-        RF_CALL(gemm(att, D, L.w_out, D, x, ldx, nullptr, T2, D, D, RF_EPI_ADD_F32, gws, gwb, stream));
+        RF_CALL(rf_gemm_add_prenorm(att, D, L.w_out, D, x, ldx, T2, D, D, self_attn ? L.self_norm : L.ffn_norm, h, D,
+                                    ss, dt, gws, gwb, stream));
         // (ii) self-attention between ray tokens
         if (self_attn) {
-            RF_CALL(rmsnorm(x, ldx, L.self_norm, d->eps, h, D, T2, D, stream));
-            RF_CALL(gemm(h, D, L.w_self_in, D, qkv, 3 * D, nullptr, T2, 3 * D, D, RF_EPI_BF16, gws, gwb, stream));
-            if (d->swin) {
+            // Swin: the full-width q/k norm folds into the attention's loads, fed by the projection's row sums
+            // (rf_swin_attn_fwd_qkn); the per-op q/k norm pass remains for widths the segment sums do not cover
+            const bool qkn = d->swin && D % 256 == 0 && D <= RF_PRENORM_SLOTS * 128;
+            RF_CALL(rf_gemm_rownorm(h, D, L.w_self_in, D, qkv, 3 * D, T2, 3 * D, D, RF_EPI_BF16, ss, D, d->eps,
+                                    qkn && L.self_qk_norm ? qkss : nullptr, D, 2, dt, gws, gwb, stream));
+            if (qkn) {
+                RF_CALL(rf_swin_attn_fwd_qkn(qkv, 3 * D, qkv + D, 3 * D, qkv + 2 * D, 3 * D, att, D, o_dt, d->n_images,
+                                             d->grid_h, d->grid_w, d->window, i % 2 == 0 ? 0 : d->shift, H, 128, kLn2,
+                                             qkss, L.self_qk_norm, d->eps, kQLog2Scale, stream));
+            } else if (d->swin) {
                 RF_CALL(rf_qk_norm_rope(qkv, 3 * D, qkv, 3 * D, nullptr, T2, D, H, 2, L.self_qk_norm, d->eps,
                                         kQLog2Scale, nullptr, 0, 1, nullptr, 0, stream));
                 RF_CALL(rf_swin_attn_fwd_dt(qkv, 3 * D, qkv + D, 3 * D, qkv + 2 * D, 3 * D, att, D, o_dt, d->n_images,
@@ -243,12 +269,16 @@ extern "C" int rf_decoder_forward(float* x, int64_t ldx, const rf_decoder_desc* 
                 RF_CALL(rf_attn_fwd_dt(qkv, 3 * D, qkv + D, 3 * D, qkv + 2 * D, 3 * D, att, D, RF_DT_BF16, o_dt,
                                        d->self_problems, d->n_self, H, 128, kLn2, d->attn_ws, nullptr, 0, stream));
             }
-            RF_CALL(gemm(att, D, L.w_self_out, D, x, ldx, nullptr, T2, D, D, RF_EPI_ADD_F32, gws, gwb, stream));
+            RF_CALL(rf_gemm_add_prenorm(att, D, L.w_self_out, D, x, ldx, T2, D, D, L.ffn_norm, h, D, ss, dt, gws, gwb,
+                                        stream));
         }
         // (iii) FFN
-        RF_CALL(rmsnorm(x, ldx, L.ffn_norm, d->eps, h, D, T2, D, stream));
-        RF_CALL(gemm(h, D, L.w13, D, g, F, nullptr, T2, 2 * F, D, epi_swiglu, gws, gwb, stream));
-        RF_CALL(gemm(g, F, L.w2, F, x, ldx, nullptr, T2, D, F, RF_EPI_ADD_F32, gws, gwb, stream));
+        RF_CALL(rf_gemm_rownorm(h, D, L.w13, D, g, F, T2, 2 * F, D, epi_swiglu, ss, D, d->eps, nullptr, 0, 0, dt, gws, gwb, stream));
+        if (i + 1 < NL)
+            RF_CALL(rf_gemm_add_prenorm(g, F, L.w2, F, x, ldx, T2, D, F, d->layers[i + 1].query_norm, h, D, ss, dt, gws,
+                                        gwb, stream));
+        else
+            RF_CALL(gemm(g, F, L.w2, F, x, ldx, nullptr, T2, D, F, RF_EPI_ADD_F32, gws, gwb, stream));
         if (tap < d->n_taps && d->taps[tap].layer == i) {  // straight into the DPT projection's operand planes
             const rf_decoder_tap& t = d->taps[tap++];
             RF_CALL(rf_split_planes(x, T2, D, ldx, t.p_hi, t.p_lo, t.p_ld, 0, stream));

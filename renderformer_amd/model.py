@@ -536,19 +536,24 @@ class RenderFormer:
         qkv = torch.empty(T, 3 * D, dtype=torch.bfloat16, device=dev)  # attention operands: bf16
         att = torch.empty(T, D, dtype=W.half, device=dev)
         g = torch.empty(T, F, dtype=W.half, device=dev)
+        ss = torch.empty(T, ops.PRENORM_SLOTS, dtype=torch.float32, device=dev)
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
         qk_pair = qkv[:, :2 * D]
-        for L in W.enc:
-            ops.rmsnorm(x, L.query_norm, EPS, h)
-            ops.gemm(h, L.w_in, qkv)
+        # every pre-norm deferred (rf.h rf_gemm_add_prenorm / rf_gemm_rownorm), as rf_encoder_forward issues them:
+        # h holds x * g, ss the row sums of squares, and the projection after the norm applies 1 / rms
+        ops.prenorm(x, W.enc[0].query_norm, h, ss)
+        for li, L in enumerate(W.enc):
+            ops.gemm_rownorm(h, L.w_in, qkv, ss, EPS)
             ops.qk_norm_rope(qk_pair, qk_pair, H, L.qk_norm if cfg.view_indep_qk_norm else None, EPS, pos1, W.enc_freqs,
                              n_seg=2, q_scale=ops.Q_LOG2_SCALE)
             ops.attention(q, k, v, att, plan.prob1, plan.max_s, H, tag="attn_stage1", max_k_len=plan.max_s,
                           q_prescaled=True, schedule=plan.sched1)
-            ops.gemm(att, L.w_out, x, None, ops.EPI_ADD_F32)
-            ops.rmsnorm(x, L.ffn_norm, EPS, h)
-            ops.gemm(h, L.w13, g, None, ops.EPI_SWIGLU, tag="gemm_w13_stage1")
-            ops.gemm(g, L.w2, x, None, ops.EPI_ADD_F32)
+            ops.gemm_add_prenorm(att, L.w_out, x, L.ffn_norm, h, ss)
+            ops.gemm_rownorm(h, L.w13, g, ss, EPS, ops.EPI_SWIGLU, tag="gemm_w13_stage1")
+            if li + 1 < len(W.enc):
+                ops.gemm_add_prenorm(g, L.w2, x, W.enc[li + 1].query_norm, h, ss)
+            else:
+                ops.gemm(g, L.w2, x, None, ops.EPI_ADD_F32)
         self._capture_stage1(plan, x)
         return x
 
@@ -630,10 +635,32 @@ class RenderFormer:
                 ops.gemm(inp, w_bf16, out, None, epi, tag=tag)
         taps = []
         outl = set(cfg.out_layers)
+        # pre-norms deferred into the GEMMs around them as rf_decoder_forward issues them (the fp8 mode keeps the
+        # row kernel: its projections quantise the normalised operand)
+        defer = not fp8
+        ss = torch.empty(T2, ops.PRENORM_SLOTS, dtype=torch.float32, device=dev) if defer else None
+        qkss = torch.empty(T2, 2, ops.PRENORM_SLOTS, dtype=torch.float32, device=dev) if defer and swin else None
+
+        def norm_proj(norm_w, w_half, w_fp8, out, epi=ops.EPI_BF16, tag=None, name=""):
+            """out (epi)= rmsnorm(x) @ w.T: from the deferred operands, or row kernel + proj in the fp8 mode"""
+            if defer:
+                ops.gemm_rownorm(h, w_half, out, ss, EPS, epi, tag=tag)
+            else:
+                ops.rmsnorm(x, norm_w, EPS, h)
+                proj(h, w_half, w_fp8, out, epi, tag=tag, name=name)
+
+        def add_proj(inp, w_half, w_fp8, next_norm, tag=None, name=""):
+            """x += inp @ w.T, and the next pre-norm's deferred operands when there is one"""
+            if defer and next_norm is not None:
+                ops.gemm_add_prenorm(inp, w_half, x, next_norm, h, ss, tag=tag)
+            else:
+                proj(inp, w_half, w_fp8, x, ops.EPI_ADD_F32, tag=tag, name=name)
+
+        if defer:
+            ops.prenorm(x, W.dec[0].query_norm, h, ss)
         for i, L in enumerate(W.dec):
             # (i) cross-attention: K/V projections once per scene, K rotated per view
-            ops.rmsnorm(x, L.query_norm, EPS, h)
-            proj(h, L.wq, getattr(L, "wq8", None), q2, name="q")
+            norm_proj(L.query_norm, L.wq, getattr(L, "wq8", None), q2, name="q")
             if kv_batch:
                 kv = kv_all[:, 2 * D * i:2 * D * (i + 1)]
             else:
@@ -648,14 +675,22 @@ class RenderFormer:
                                  src_rows=plan.kv_src_rows)
             ops.attention(q2, kview, kv[:, D:], att, plan.prob2, R, H, tag="attn_cross", max_k_len=plan.max_s,
                           q_prescaled=True, schedule=plan.sched2)
-            proj(att, L.wo, getattr(L, "wo8", None), x, ops.EPI_ADD_F32, name="out")
+            add_proj(att, L.wo, getattr(L, "wo8", None), L.self_norm if qkv is not None else L.ffn_norm, name="out")
             # (ii) self-attention between ray tokens
             if qkv is not None:
-                ops.rmsnorm(x, L.self_norm, EPS, h)
-                proj(h, L.ws_in, getattr(L, "ws_in8", None), qkv, name="self_in")
                 qs, ks, vs = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
                 qks = qkv[:, :2 * D]
-                if swin:
+                # Swin: q/k norm folded into the attention's loads from the projection's row sums, as
+                # rf_decoder_forward issues it (rf_swin_attn_fwd_qkn)
+                qkn = swin and defer and D % 256 == 0 and D <= ops.PRENORM_SLOTS * 128
+                if qkn:
+                    ops.gemm_rownorm(h, L.ws_in, qkv, ss, EPS, seg_ss=qkss if qk else None, seg_w=D)
+                else:
+                    norm_proj(L.self_norm, L.ws_in, getattr(L, "ws_in8", None), qkv, name="self_in")
+                if qkn:
+                    ops.swin_attention(qs, ks, vs, att, P, plan.hp, plan.wp, 0 if i % 2 == 0 else SWIN_SHIFT, H,
+                                       SWIN_WINDOW, qk_norm=(qkss, L.sqk_norm if qk else None, EPS))
+                elif swin:
                     ops.qk_norm_rope(qks, qks, H, L.sqk_norm if qk else None, EPS, n_seg=2, q_scale=ops.Q_LOG2_SCALE)
                     ops.swin_attention(qs, ks, vs, att, P, plan.hp, plan.wp, 0 if i % 2 == 0 else SWIN_SHIFT, H,
                                        SWIN_WINDOW, q_prescaled=True)
@@ -663,11 +698,11 @@ class RenderFormer:
                     ops.qk_norm_rope(qks, qks, H, L.sqk_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R,
                                      n_seg=2, q_scale=ops.Q_LOG2_SCALE)
                     ops.attention(qs, ks, vs, att, plan.prob_self, R, H, max_k_len=R, q_prescaled=True)
-                proj(att, L.ws_out, getattr(L, "ws_out8", None), x, ops.EPI_ADD_F32, name="self_out")
+                add_proj(att, L.ws_out, getattr(L, "ws_out8", None), L.ffn_norm, name="self_out")
             # (iii) FFN
-            ops.rmsnorm(x, L.ffn_norm, EPS, h)
-            proj(h, L.w13, getattr(L, "w13_8", None), g, ops.EPI_SWIGLU, tag="gemm_w13_stage2", name="w13")
-            proj(g, L.w2, getattr(L, "w2_8", None), x, ops.EPI_ADD_F32, tag="gemm_w2_stage2", name="w2")
+            norm_proj(L.ffn_norm, L.w13, getattr(L, "w13_8", None), g, ops.EPI_SWIGLU, tag="gemm_w13_stage2", name="w13")
+            add_proj(g, L.w2, getattr(L, "w2_8", None), W.dec[i + 1].query_norm if i + 1 < n_dec else None,
+                     tag="gemm_w2_stage2", name="w2")
             if i in outl:  # straight into the DPT projection's operand planes (no fp32 copy of x)
                 taps.append(W.dpt.tap_planes(len(taps), x, P, plan.hp, plan.wp))
             cap = self._capture

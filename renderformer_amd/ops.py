@@ -228,6 +228,85 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor) -> 
     return out
 
 
+PRENORM_SLOTS = 8  # rf.h RF_PRENORM_SLOTS: partial sums of squares per row of a deferred RMSNorm
+
+
+def _dt(t: torch.Tensor) -> int:
+    return 1 if t.dtype == torch.float16 else 0  # RF_DT_F16 / RF_DT_BF16
+
+
+def prenorm(x: torch.Tensor, w: torch.Tensor, xg: torch.Tensor, ss: torch.Tensor) -> torch.Tensor:
+    """Deferred RMSNorm, row form (rf_prenorm): xg = x * w in xg's dtype (bf16 / fp16) and the row sums of x^2 in
+    ss [rows, PRENORM_SLOTS] (slot 0); gemm_rownorm(xg, ...) then equals gemm(rmsnorm(x, w), ...)."""
+    _dev(x, torch.float32, "x")
+    _check(xg.dtype in HALF, "prenorm: xg must be bf16 or fp16")
+    _dev(xg, xg.dtype, "xg")
+    _dev(ss, torch.float32, "ss")
+    _check(xg.shape == x.shape and w.numel() == x.shape[1], "prenorm: shape mismatch")
+    _check(ss.shape[0] >= x.shape[0] and ss.shape[1] == PRENORM_SLOTS and ss.is_contiguous(), "prenorm: ss shape")
+    call("rf_prenorm", ptr(x), x.stride(0), ptr(w), ptr(xg), xg.stride(0), ptr(ss), x.shape[0], x.shape[1], _dt(xg),
+         stream())
+    return xg
+
+
+def gemm_add_prenorm(a: torch.Tensor, w: torch.Tensor, x: torch.Tensor, norm_w: torch.Tensor, xg: torch.Tensor,
+                     ss: torch.Tensor, tag: Optional[str] = None) -> torch.Tensor:
+    """x += a @ w.T (fp32 residual) and, from the same epilogue, the next pre-norm's operands: xg = x * norm_w and
+    the row sums of squares ss (rf_gemm_add_prenorm; a / w / xg all bf16 or all fp16)."""
+    _check(a.dtype in HALF and w.dtype == a.dtype and xg.dtype == a.dtype,
+           f"gemm_add_prenorm: a / w / xg must share bf16 or fp16 ({a.dtype}, {w.dtype}, {xg.dtype})")
+    for t, n in ((a, "a"), (w, "w"), (xg, "xg")):
+        _dev(t, t.dtype, n)
+    _dev(x, torch.float32, "x")
+    _dev(ss, torch.float32, "ss")
+    m, k = a.shape
+    n, k2 = w.shape
+    _check(k == k2 and x.shape == (m, n) and xg.shape == (m, n) and norm_w.numel() == n,
+           "gemm_add_prenorm: shape mismatch")
+    _check(ss.shape[0] >= m and ss.shape[1] == PRENORM_SLOTS and ss.is_contiguous(), "gemm_add_prenorm: ss shape")
+    ws = _gemm_workspace(a.device)
+    _t0(tag)
+    call("rf_gemm_add_prenorm", ptr(a), a.stride(0), ptr(w), w.stride(0), ptr(x), x.stride(0), m, n, k, ptr(norm_w),
+         ptr(xg), xg.stride(0), ptr(ss), _dt(a), ptr(ws), ws.numel(), stream())
+    return x
+
+
+def gemm_rownorm(xg: torch.Tensor, w: torch.Tensor, out: torch.Tensor, ss: torch.Tensor, eps: float,
+                 epilogue: int = EPI_BF16, tag: Optional[str] = None, seg_ss: Optional[torch.Tensor] = None,
+                 seg_w: int = 0) -> torch.Tensor:
+    """out (epilogue)= rmsnorm(x) @ w.T from the deferred form (rf_gemm_rownorm): xg = x * g and ss from prenorm /
+    gemm_add_prenorm; the rows are scaled by 1 / rms(x) in the epilogue (EPI_BF16 or EPI_SWIGLU; out bf16 / fp16).
+    With ``seg_ss`` [M, n_seg, PRENORM_SLOTS] (EPI_BF16 only) also the partial sums of the squares of the written
+    values per segment of ``seg_w`` columns: the row sums of a following full-width q/k RMSNorm (swin_attention's
+    ``qk_norm``)."""
+    _check(xg.dtype in HALF and w.dtype == xg.dtype, "gemm_rownorm: xg / w must both be bf16 or both fp16")
+    _check(epilogue in (EPI_BF16, EPI_SWIGLU), "gemm_rownorm: epilogue must be EPI_BF16 or EPI_SWIGLU")
+    _dev(xg, xg.dtype, "xg")
+    _dev(w, w.dtype, "w")
+    _dev(ss, torch.float32, "ss")
+    _check(out.dtype in HALF, "gemm_rownorm: out must be bf16 or fp16")
+    _dev(out, out.dtype, "out")
+    m, k = xg.shape
+    n, k2 = w.shape
+    ncols = n // 2 if epilogue == EPI_SWIGLU else n
+    _check(k == k2 and out.shape == (m, ncols), "gemm_rownorm: shape mismatch")
+    _check(ss.shape[0] >= m and ss.shape[1] == PRENORM_SLOTS and ss.is_contiguous(), "gemm_rownorm: ss shape")
+    epi = epilogue
+    if out.dtype == torch.float16:
+        epi = _EPI_F16 if epilogue == EPI_BF16 else _EPI_SWIGLU_F16
+    ws = _gemm_workspace(xg.device)
+    _t0(tag)
+    n_seg = 0
+    if seg_ss is not None:
+        _dev(seg_ss, torch.float32, "seg_ss")
+        _check(epilogue == EPI_BF16 and seg_ss.is_contiguous() and seg_ss.dim() == 3 and seg_ss.shape[0] >= m
+               and seg_ss.shape[2] == PRENORM_SLOTS and seg_w > 0, "gemm_rownorm: seg_ss [M, n_seg, 8] with EPI_BF16")
+        n_seg = seg_ss.shape[1]
+    call("rf_gemm_rownorm", ptr(xg), xg.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), m, n, k, epi, ptr(ss),
+         k, eps, ptr(seg_ss), seg_w, n_seg, _dt(xg), ptr(ws), ws.numel(), stream())
+    return out
+
+
 def qk_norm_rope(src: torch.Tensor, dst: torch.Tensor, n_heads: int, norm_w: Optional[torch.Tensor], eps: float,
                  pos: Optional[torch.Tensor] = None, freqs: Optional[torch.Tensor] = None, pos_div: int = 1,
                  src_rows: Optional[torch.Tensor] = None, n_seg: int = 1, q_scale: float = 1.0) -> torch.Tensor:
@@ -504,15 +583,27 @@ def decoder_forward(x: torch.Tensor, layers, n_layers: int, n_heads: int, ffn_di
 
 
 def swin_attention(q, k, v, out, n_images: int, grid_h: int, grid_w: int, shift: int, n_heads: int,
-                   window: int = 8, q_prescaled: bool = False) -> torch.Tensor:
+                   window: int = 8, q_prescaled: bool = False, qk_norm=None) -> torch.Tensor:
+    """Shifted-window self-attention (rf_swin_attn_fwd_dt).  ``qk_norm = (qk_ss, norm_w, eps)`` folds the full-width
+    q/k RMSNorm (and the softmax scale on q) into the kernel's loads (rf_swin_attn_fwd_qkn): q, k as the projection
+    wrote them, qk_ss [rows, 2, PRENORM_SLOTS] from gemm_rownorm(seg_ss=..., seg_w=D), norm_w [2D] or None."""
     for t, nme in ((q, "q"), (k, "k"), (v, "v")):
         _dev(t, torch.bfloat16, nme)
     _check(out.dtype in HALF, "swin_attention: out must be bf16 or fp16")
     _dev(out, out.dtype, "out")
     hd = q.shape[1] // n_heads
-    call("rf_swin_attn_fwd_dt", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
-         out.stride(0), DT_F16 if out.dtype == torch.float16 else DT_BF16, n_images, grid_h, grid_w, window, shift,
-         n_heads, hd, LN2 if q_prescaled else 1.0 / math.sqrt(hd), stream())
+    odt = DT_F16 if out.dtype == torch.float16 else DT_BF16
+    if qk_norm is None:
+        call("rf_swin_attn_fwd_dt", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+             out.stride(0), odt, n_images, grid_h, grid_w, window, shift, n_heads, hd,
+             LN2 if q_prescaled else 1.0 / math.sqrt(hd), stream())
+        return out
+    qk_ss, norm_w, eps = qk_norm
+    _dev(qk_ss, torch.float32, "qk_ss")
+    _check(qk_ss.is_contiguous() and qk_ss.shape[1:] == (2, PRENORM_SLOTS), "swin_attention: qk_ss [rows, 2, 8]")
+    call("rf_swin_attn_fwd_qkn", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+         out.stride(0), odt, n_images, grid_h, grid_w, window, shift, n_heads, hd, LN2, ptr(qk_ss), ptr(norm_w), eps,
+         Q_LOG2_SCALE, stream())
     return out
 
 

@@ -23,6 +23,7 @@
 #   libab            the current library vs $BASE (default renderformer_amd/lib/librfhip_base.so, a build of another
 #                    tree): GPU tests on the current one, then interleaved stage-1 attention timings, per-role stamps
 #                    and bench runs of both (RF_LIB selects the library)
+#   pnab             the deferred RMSNorm: GPU tests, kbench prenorm A/B vs $BASE, interleaved bench runs of both
 #   quadstudy        tools/kbench.py quad on the study build: the 4-wave GEMM at MT128x192 / MT160x256 (register or
 #                    LDS-DMA staging, whole tiles or stream-K) vs the default engine on the projection shapes
 #   vendor           kernel-trace of the vendor GEMM library vs the engine on the frame's projection shapes
@@ -128,6 +129,16 @@ libab)
     STUDY=$R/renderformer_amd/lib/librfhip_study.so  # the stamp build (RF_ATTN_DBG=32) of the current tree
     if [ -f $STUDY ]; then RF_LIB=$STUDY timeout -k 10 120 python tools/attn_ablate.py stamps > $O/stamps_new.log 2>&1; fi
     RF_LIB=$BASE timeout -k 10 120 python tools/attn_ablate.py stamps > $O/stamps_base.log 2>&1
+    for i in 1 2; do
+        timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_new$i.json 2>> $O/bench.err
+        RF_LIB=$BASE timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_base$i.json 2>> $O/bench.err
+    done ;;
+pnab)  # deferred RMSNorm: its GPU tests, the kbench prenorm A/B on this library and the plain GEMMs on $BASE, then
+       # interleaved bench runs of both libraries
+    BASE=${BASE:-$R/renderformer_amd/lib/librfhip_base.so}
+    timeout -k 10 900 $T tests/test_prenorm_gpu.py tests/test_parity_gpu.py -m gpu > $O/tests.log 2>&1
+    timeout -k 10 300 python -u tools/kbench.py prenorm > $O/kb_new.log 2>&1
+    KB_PLAIN_ONLY=1 RF_LIB=$BASE timeout -k 10 300 python -u tools/kbench.py prenorm > $O/kb_base.log 2>&1
     for i in 1 2; do
         timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_new$i.json 2>> $O/bench.err
         RF_LIB=$BASE timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_base$i.json 2>> $O/bench.err

@@ -348,6 +348,98 @@ def vendor():
         torch.cuda.empty_cache()
 
 
+def prenorm():
+    """Deferred RMSNorm A/B (rf.h rf_gemm_add_prenorm / rf_gemm_rownorm) on the frame's shapes, fp16 operands, cold
+    rotating operand sets: producer = residual GEMM + rf_rmsnorm (the row-kernel pair) vs the residual GEMM that also
+    writes x * g and the row sums (and the residual GEMM alone); consumer = the projection from rf_rmsnorm's output
+    vs the projection with the 1 / rms row scale in its epilogue.  Two interleaved rounds."""
+    from renderformer_amd.model import _interleave_swiglu
+    prod = [("s1 out", S, D, D), ("s1 w2", S, D, F), ("s2 out", R, D, D), ("s2 w2", R, D, F)]
+    cons = [("s1 qkv", S, 3 * D, D, 0), ("s1 w13", S, 2 * F, D, 1), ("s2 q", R, D, D, 0), ("s2 qkv", R, 3 * D, D, 0),
+            ("s2 w13", R, 2 * F, D, 1)]
+    sel = os.environ.get("KB_SHAPES")
+    eps = 1e-6
+    for rnd in range(1):
+        for name, m, n, k in prod:
+            if sel and name not in sel.split(","):
+                continue
+            per = m * k * 2 + n * k * 2 + m * n * 6
+            nrot = max(2, int((768 << 20) // per) + 1)
+            sets = [(torch.randn(m, k, device=dev).half(), (torch.randn(n, k, device=dev) / math.sqrt(k)).half(),
+                     torch.randn(m, n, device=dev), torch.empty(m, n, device=dev, dtype=torch.float16),
+                     torch.empty(m, ops.PRENORM_SLOTS, device=dev)) for _ in range(nrot)]
+            g = torch.rand(n, device=dev) + 0.5
+            i = [0]
+
+            def nxt():
+                i[0] += 1
+                return sets[i[0] % nrot]
+
+            def plain():
+                a, w, x, h, ss = nxt()
+                ops.gemm(a, w, x, None, ops.EPI_ADD_F32)
+
+            def pair():
+                a, w, x, h, ss = nxt()
+                ops.gemm(a, w, x, None, ops.EPI_ADD_F32)
+                ops.rmsnorm(x, g, eps, h)
+
+            def fused():
+                a, w, x, h, ss = nxt()
+                ops.gemm_add_prenorm(a, w, x, g, h, ss)
+            plain_only = os.environ.get("KB_PLAIN_ONLY") == "1"  # (a library without the deferred-norm entry points)
+            fns = [("gemm ADD alone", plain), ("gemm ADD + rmsnorm", pair)] + ([] if plain_only else
+                                                                              [("gemm_add_prenorm", fused)])
+            best = {lab: 1e9 for lab, _ in fns}
+            for rep in range(4):
+                for lab, fn in (fns if rep % 2 == 0 else fns[::-1]):
+                    best[lab] = min(best[lab], timeit(fn, reps=2 * nrot))
+            for lab, _ in fns:
+                print(f"prenorm r{rnd} producer {name:7s} {m}x{n}x{k} {lab:20s}: {best[lab]*1e3:8.1f} us ({nrot} sets, "
+                      f"best of 4 interleaved)", flush=True)
+            del sets
+            torch.cuda.empty_cache()
+        for name, m, n, k, sw in cons:
+            if sel and name not in sel.split(","):
+                continue
+            per = m * k * 2 + n * k * 2 + m * n * 2
+            nrot = max(2, int((768 << 20) // per) + 1)
+            odt = torch.float16 if sw else torch.bfloat16
+            ncol = n // 2 if sw else n
+            epi = ops.EPI_SWIGLU if sw else ops.EPI_BF16
+
+            def mkw():
+                w = (torch.randn(n, k, device=dev) / math.sqrt(k)).half()
+                return _interleave_swiglu(w[: n // 2], w[n // 2:]) if sw else w
+            sets = [(torch.randn(m, k, device=dev).half(), mkw(), torch.empty(m, ncol, device=dev, dtype=odt),
+                     torch.rand(m, ops.PRENORM_SLOTS, device=dev) + 1.0) for _ in range(nrot)]
+            i = [0]
+
+            def nxt():
+                i[0] += 1
+                return sets[i[0] % nrot]
+
+            def plain():
+                h, w, o, ss = nxt()
+                ops.gemm(h, w, o, None, epi)
+
+            def rown():
+                h, w, o, ss = nxt()
+                ops.gemm_rownorm(h, w, o, ss, eps, epi)
+            # interleaved A/B/A/B..., best of 4 each: the W13 shapes run at the chip's power limit, so whichever
+            # variant is timed second in a block runs at a lower clock
+            fns = [("gemm", plain)] + ([] if os.environ.get("KB_PLAIN_ONLY") == "1" else [("gemm_rownorm", rown)])
+            best = {lab: 1e9 for lab, _ in fns}
+            for rep in range(4):
+                for lab, fn in (fns if rep % 2 == 0 else fns[::-1]):
+                    best[lab] = min(best[lab], timeit(fn, reps=2 * nrot))
+            for lab, _ in fns:
+                print(f"prenorm r{rnd} consumer {name:7s} {m}x{n}x{k} {lab:20s}: {best[lab]*1e3:8.1f} us ({nrot} sets, "
+                      f"best of 4 interleaved)", flush=True)
+            del sets
+            torch.cuda.empty_cache()
+
+
 def quad():
     """The 4-wave 256x256 engine (RF_GEMM_QUAD=1 whole tiles / persistent, 2 stream-K) against the default pick on
     the 256-divisible frame shapes, fp16 operands, cold rotating operand sets; the SwiGLU shapes with the SwiGLU
@@ -399,3 +491,5 @@ if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "vendor":
     vendor()
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "quad":
     quad()
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "prenorm":
+    prenorm()
