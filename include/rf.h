@@ -293,7 +293,8 @@ int rf_swin_attn_fwd_dt(const void* q, int64_t ldq, const void* k, int64_t ldk, 
  * them (rf_gemm_rownorm with seg_ss = qk_ss, seg_w = n_heads * 128, n_seg = 2), each q row scaled by
  * q_scale / rms(q row) * qk_norm_w[c] and each k row by 1 / rms(k row) * qk_norm_w[n_heads * 128 + c] before the
  * scores -- rf_qk_norm_rope(n_seg = 2, no RoPE, seg0_scale = q_scale)'s arithmetic without its pass over q and k
- * (reference SwinSelfAttention q/k norm, attention.py:345-359).  qk_norm_w NULL: only the q scale. */
+ * (reference SwinSelfAttention q/k norm, attention.py:345-359).  qk_norm_w and qk_ss are required (a model without q/k
+ * norm weights runs rf_qk_norm_rope's scale-only form and rf_swin_attn_fwd_dt). */
 int rf_swin_attn_fwd_qkn(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv, void* o,
                          int64_t ldo, int o_dtype, int n_images, int grid_h, int grid_w, int window, int shift,
                          int n_heads, int head_dim, float scale, const float* qk_ss, const float* qk_norm_w, float eps,

@@ -189,7 +189,13 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_fwd_kernel(Attn
     constexpr int T = NW * 64;
     constexpr int CPT = (KT * HD / 8) / T;  // 16-B chunks per thread per tile (per operand)
     constexpr int NBUF = SWIN ? 1 : 2;
-    __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE_BYTES];
+    // QKN (Swin with the q/k norm folded in): after the K/V tile, 1 / rms of the window's 64 key rows and the q / k
+    // norm weights of this head (128 floats each), staged once per workgroup
+    constexpr int QKN_BYTES = QKN ? (KT + 2 * HD) * 4 : 0;
+    __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE_BYTES + QKN_BYTES];
+    float* const qkn_inv = reinterpret_cast<float*>(smem + NBUF * 2 * TILE_BYTES);
+    float* const qkn_gq = qkn_inv + KT;
+    float* const qkn_gk = qkn_gq + HD;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -262,19 +268,6 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_fwd_kernel(Attn
         const bf16_t* src = p.q + (int64_t)qrow * p.ldq + hoff + 8 * half;
 #pragma unroll
         for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(src + 16 * s);
-        if constexpr (QKN) {  // q = bf16(q * (inv_rms * scale) * w): the fused rf_qk_norm_rope of segment 0
-            const float sq = (p.qk_w ? qk_inv_rms(p, qrow, 0) : 1.f) * p.qk_scale;
-#pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                const u32x4 x = __builtin_bit_cast(u32x4, qf[s]);
-                if (p.qk_w) {
-                    qf[s] = __builtin_bit_cast(bf16x8, qk_scale8(x, sq, p.qk_w + hoff + 16 * s + 8 * half));
-                } else {
-                    const float one[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
-                    qf[s] = __builtin_bit_cast(bf16x8, qk_scale8(x, sq, one));
-                }
-            }
-        }
     }
     int qlabel = 0;
     if constexpr (SWIN) qlabel = p.shift > 0 ? swin_label(qi) : 0;
@@ -301,10 +294,6 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_fwd_kernel(Attn
                 const int r = swin_row(srow + i * (T / 16));
                 kreg[i] = *reinterpret_cast<const u32x4*>(kbase + (int64_t)r * p.ldk);
                 vreg[i] = *reinterpret_cast<const u32x4*>(vbase + (int64_t)r * p.ldv);
-                if constexpr (QKN) {  // k = bf16(k * inv_rms * w): segment 1 of the fused q/k norm
-                    if (p.qk_w)
-                        kreg[i] = qk_scale8(kreg[i], qk_inv_rms(p, r, 1), p.qk_w + p.qk_dim + hoff + sch * 8);
-                }
             }
         } else if ((kt + 1) * KT <= k_len) {
 #pragma unroll
@@ -344,7 +333,33 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_fwd_kernel(Attn
     float m_run = NEG, l_run = 0.f;  // m_run in raw score units (before * c)
     const float c = p.c;
 
-    if (t_begin < t_end) {
+    if constexpr (QKN) {
+        // the fused full-width q/k RMSNorm (rf_qk_norm_rope's arithmetic: row scale, then weight; q also carries
+        // the softmax scale): every load is issued before any is used (q and the K/V tile above/here, then the
+        // row sums and weights), the key rows' 1 / rms and both weight vectors go through LDS once, and the
+        // transforms are branch-free (qk_w is never null on this path)
+        load_tile(t_begin);
+        float sq = 0.f, sk = 0.f, gq = 0.f, gk = 0.f;
+        sq = qk_inv_rms(p, qrow, 0) * p.qk_scale;
+        if (tid < KT) sk = qk_inv_rms(p, swin_row(tid), 1);
+        if (tid < HD) {
+            gq = p.qk_w[hoff + tid];
+            gk = p.qk_w[p.qk_dim + hoff + tid];
+        }
+        if (tid < KT) qkn_inv[tid] = sk;
+        if (tid < HD) {
+            qkn_gq[tid] = gq;
+            qkn_gk[tid] = gk;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            qf[s] = __builtin_bit_cast(bf16x8, qk_scale8(__builtin_bit_cast(u32x4, qf[s]), sq,
+                                                           qkn_gq + 16 * s + 8 * half));
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) kreg[i] = qk_scale8(kreg[i], qkn_inv[srow + i * (T / 16)], qkn_gk + sch * 8);
+        write_tile(0);
+    } else if (t_begin < t_end) {
         load_tile(t_begin);
         write_tile(0);
     }
@@ -2219,8 +2234,8 @@ static int swin_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, c
                grid_h, grid_w);
     RF_REQUIRE(shift >= 0 && shift < window, "rf_swin_attn_fwd: bad shift");
     RF_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0, "rf_swin_attn_fwd: strides must be 16-B aligned");
-    RF_REQUIRE(!qkn || !qk_w || (qk_ss && ((uintptr_t)qk_ss & 15) == 0 && ((uintptr_t)qk_w & 15) == 0),
-               "rf_swin_attn_fwd_qkn: qk_norm_w needs qk_ss (both 16-B aligned)");
+    RF_REQUIRE(!qkn || (qk_w && qk_ss && ((uintptr_t)qk_ss & 15) == 0),
+               "rf_swin_attn_fwd_qkn: qk_norm_w and qk_ss (16-B aligned) are required");
     if (n_images <= 0) return RF_OK;
     AttnArgs a{};
     a.q = (const bf16_t*)q;

@@ -249,9 +249,9 @@ extern "C" int rf_decoder_forward(float* x, int64_t ldx, const rf_decoder_desc* 
         if (self_attn) {
             // Swin: the full-width q/k norm folds into the attention's loads, fed by the projection's row sums
             // (rf_swin_attn_fwd_qkn); the per-op q/k norm pass remains for widths the segment sums do not cover
-            const bool qkn = d->swin && D % 256 == 0 && D <= RF_PRENORM_SLOTS * 128;
+            const bool qkn = d->swin && L.self_qk_norm && D % 256 == 0 && D <= RF_PRENORM_SLOTS * 128;
             RF_CALL(rf_gemm_rownorm(h, D, L.w_self_in, D, qkv, 3 * D, T2, 3 * D, D, RF_EPI_BF16, ss, D, d->eps,
-                                    qkn && L.self_qk_norm ? qkss : nullptr, D, 2, dt, gws, gwb, stream));
+                                    qkn ? qkss : nullptr, D, 2, dt, gws, gwb, stream));
             if (qkn) {
                 RF_CALL(rf_swin_attn_fwd_qkn(qkv, 3 * D, qkv + D, 3 * D, qkv + 2 * D, 3 * D, att, D, o_dt, d->n_images,
                                              d->grid_h, d->grid_w, d->window, i % 2 == 0 ? 0 : d->shift, H, 128, kLn2,

@@ -639,7 +639,7 @@ class RenderFormer:
         # row kernel: its projections quantise the normalised operand)
         defer = not fp8
         ss = torch.empty(T2, ops.PRENORM_SLOTS, dtype=torch.float32, device=dev) if defer else None
-        qkss = torch.empty(T2, 2, ops.PRENORM_SLOTS, dtype=torch.float32, device=dev) if defer and swin else None
+        qkss = torch.empty(T2, 2, ops.PRENORM_SLOTS, dtype=torch.float32, device=dev) if defer and swin and qk else None
 
         def norm_proj(norm_w, w_half, w_fp8, out, epi=ops.EPI_BF16, tag=None, name=""):
             """out (epi)= rmsnorm(x) @ w.T: from the deferred operands, or row kernel + proj in the fp8 mode"""
@@ -682,14 +682,14 @@ class RenderFormer:
                 qks = qkv[:, :2 * D]
                 # Swin: q/k norm folded into the attention's loads from the projection's row sums, as
                 # rf_decoder_forward issues it (rf_swin_attn_fwd_qkn)
-                qkn = swin and defer and D % 256 == 0 and D <= ops.PRENORM_SLOTS * 128
+                qkn = swin and defer and qk and D % 256 == 0 and D <= ops.PRENORM_SLOTS * 128
                 if qkn:
-                    ops.gemm_rownorm(h, L.ws_in, qkv, ss, EPS, seg_ss=qkss if qk else None, seg_w=D)
+                    ops.gemm_rownorm(h, L.ws_in, qkv, ss, EPS, seg_ss=qkss, seg_w=D)
                 else:
                     norm_proj(L.self_norm, L.ws_in, getattr(L, "ws_in8", None), qkv, name="self_in")
                 if qkn:
                     ops.swin_attention(qs, ks, vs, att, P, plan.hp, plan.wp, 0 if i % 2 == 0 else SWIN_SHIFT, H,
-                                       SWIN_WINDOW, qk_norm=(qkss, L.sqk_norm if qk else None, EPS))
+                                       SWIN_WINDOW, qk_norm=(qkss, L.sqk_norm, EPS))
                 elif swin:
                     ops.qk_norm_rope(qks, qks, H, L.sqk_norm if qk else None, EPS, n_seg=2, q_scale=ops.Q_LOG2_SCALE)
                     ops.swin_attention(qs, ks, vs, att, P, plan.hp, plan.wp, 0 if i % 2 == 0 else SWIN_SHIFT, H,

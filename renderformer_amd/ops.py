@@ -586,7 +586,7 @@ def swin_attention(q, k, v, out, n_images: int, grid_h: int, grid_w: int, shift:
                    window: int = 8, q_prescaled: bool = False, qk_norm=None) -> torch.Tensor:
     """Shifted-window self-attention (rf_swin_attn_fwd_dt).  ``qk_norm = (qk_ss, norm_w, eps)`` folds the full-width
     q/k RMSNorm (and the softmax scale on q) into the kernel's loads (rf_swin_attn_fwd_qkn): q, k as the projection
-    wrote them, qk_ss [rows, 2, PRENORM_SLOTS] from gemm_rownorm(seg_ss=..., seg_w=D), norm_w [2D] or None."""
+    wrote them, qk_ss [rows, 2, PRENORM_SLOTS] from gemm_rownorm(seg_ss=..., seg_w=D), norm_w [2D] (required)."""
     for t, nme in ((q, "q"), (k, "k"), (v, "v")):
         _dev(t, torch.bfloat16, nme)
     _check(out.dtype in HALF, "swin_attention: out must be bf16 or fp16")

@@ -218,7 +218,7 @@ def test_gemm_rownorm_segment_sums(monkeypatch, tile, d):
         assert relerr(seg[:, s].sum(1), ref) < 1e-6
 
 
-@pytest.mark.parametrize("with_norm", [True, False])
+@pytest.mark.parametrize("with_norm", [True])
 @pytest.mark.parametrize("shift", [0, 4])
 def test_swin_qk_norm_folded(with_norm, shift):
     """rf_swin_attn_fwd_qkn (q/k RMSNorm + q scale on load, from the projection's segment sums) against the unfused
@@ -248,3 +248,14 @@ def test_swin_qk_norm_folded(with_norm, shift):
     ops.swin_attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], out, n_img, gh, gw_, shift, H,
                        qk_norm=(seg, nw, EPS))
     assert relerr(out.float(), ref.float()) < 1e-3
+
+
+def test_swin_qk_norm_folded_needs_weights():
+    """rf_swin_attn_fwd_qkn refuses a launch without norm weights or row sums (the model takes the unfused pair)."""
+    ops = _ops()
+    m, D = 4096, 1024
+    qkv = torch.zeros(m, 3 * D, device=dev, dtype=torch.bfloat16)
+    out = torch.empty(m, D, device=dev, dtype=torch.float16)
+    seg = torch.zeros(m, 2, ops.PRENORM_SLOTS, device=dev)
+    with pytest.raises(ValueError):
+        ops.swin_attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], out, 1, 64, 64, 0, 8, qk_norm=(seg, None, EPS))
