@@ -1435,6 +1435,7 @@ struct Cfg {
     static constexpr int A_IMG = BM * 128, B_IMG = BN * 128, STAGE = A_IMG + B_IMG, LDS = 2 * STAGE;
     static constexpr int NPA = BM / 8, NPB = BN / 8, PPW = (NPA + NPB) / 4;  // 1-KiB DMA pieces per K-tile
     static constexpr int WGM = 2, WGN = 2, MW = WM, NWD = WN;               // engine_epilogue's view
+    static constexpr int NWAVE = 4, THREADS = 256;
     static_assert(WM % 16 == 0 && WN % 16 == 0 && BM % 32 == 0 && BN % 32 == 0, "quad tile");
     static_assert(LDS <= 160 * 1024, "quad LDS");
 };
