@@ -333,10 +333,12 @@ __global__ __launch_bounds__(256) void qk_norm_rope_row_kernel(const bf16_t* src
                 if ((lane + 64 * u) / upsg == sg) inv[u] = iv;
         }
     }
-    // segment 0 (q) carries seg0_scale (RoPE is linear): folded into the row scale
+    // segment 0 (q) of group 0 carries seg0_scale (RoPE is linear): folded into the row scale
+    if (blockIdx.y == 0) {
 #pragma unroll
-    for (int u = 0; u < UPL; ++u)
-        if (lane + 64 * u < upsg) inv[u] *= seg0_scale;
+        for (int u = 0; u < UPL; ++u)
+            if (lane + 64 * u < upsg) inv[u] *= seg0_scale;
+    }
     float my_c = 1.f, my_s = 0.f;
     if (pos && lane < 9 * n_freqs) __sincosf(ang, &my_s, &my_c);
     float cs[8], sn[8];
@@ -540,7 +542,7 @@ extern "C" int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t s
     RF_REQUIRE(!norm_w || ((uintptr_t)norm_w & 15) == 0, "rf_qk_norm_rope: norm weights must be 16-B aligned");
     const int blocks = (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
     static const bool loop = getenv("RF_QKN_LOOP") && atoi(getenv("RF_QKN_LOOP"));  // A/B only
-    const int units = n_seg * n_heads * 8;
+    int units = n_seg * n_heads * 8;
     hipStream_t st = (hipStream_t)stream;
     if (loop) {  // the grid-stride kernel, one launch per group
         const dim3 grid(blocks > 2048 ? 2048 : blocks);
@@ -558,11 +560,23 @@ extern "C" int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t s
         }
         return rf::check_launch("rf_qk_norm_rope");
     }
+    // q and k of one row as two groups of one segment (grid.y = 2, the one-unit-per-lane kernel: 57 VGPRs, 8 waves per
+    // SIMD) instead of one wave with both (95 VGPRs, 5 waves per SIMD: the stage-1 grid of 5,649 rows then needs a
+    // second round); the per-segment sums and the arithmetic are the same, so the results are bit-identical.
+    // RF_QKN_SPLIT=0 keeps the two-segment wave (A/B)
+    const char* split_env = getenv("RF_QKN_SPLIT");
+    if (n_seg == 2 && n_groups == 1 && (!split_env || atoi(split_env) != 0)) {
+        n_seg = 1;
+        n_groups = 2;
+        src_gstride = dst_gstride = dim;
+        w_gstride = dim;
+    }
     const dim3 grid(blocks, n_groups);
 #define RF_QKN(U)                                                                                                 \
     RF_LAUNCH(qk_norm_rope_row_kernel<U>, grid, dim3(256), 0, st, (const bf16_t*)src, ld_src, (bf16_t*)dst, \
                        ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, seg0_scale, pos, ld_pos, pos_div, freqs, \
                        n_freqs, src_gstride, dst_gstride, (int)w_gstride)
+    units = n_seg * n_heads * 8;
     if (units <= 64) RF_QKN(1);
     else if (units <= 128) RF_QKN(2);
     else RF_QKN(4);

@@ -441,6 +441,26 @@ def test_qk_norm_rope_two_segments():
     assert torch.equal(s[:, 2 * D:].cpu(), src[:, 2 * D:])
 
 
+@pytest.mark.parametrize("rows,H", [(5649, 8), (77, 2)])
+def test_qk_norm_rope_split_segments_bit_identical(monkeypatch, rows, H):
+    """The q/k pair run as two one-segment groups (default) equals the two-segment wave (RF_QKN_SPLIT=0) bit for bit,
+    q scale on q only."""
+    ops = _ops()
+    D = H * 128
+    g = torch.Generator(device="cpu").manual_seed(rows)
+    src = torch.randn(rows, 3 * D, generator=g).bfloat16().to(dev)
+    w = (torch.rand(2 * D, generator=g) + 0.5).to(dev)
+    pos = (torch.rand(rows, 9, generator=g) * 2 - 1).to(dev)
+    freqs = (2 ** torch.linspace(0, math.log2(5), 6)).to(dev)
+    outs = []
+    for split in ("1", "0"):
+        monkeypatch.setenv("RF_QKN_SPLIT", split)
+        s = src.clone()
+        ops.qk_norm_rope(s[:, :2 * D], s[:, :2 * D], H, w, 1e-6, pos, freqs, n_seg=2, q_scale=ops.Q_LOG2_SCALE)
+        outs.append(s)
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("with_norm", [True, False])
 def test_qk_norm_rope_groups_equals_per_group(with_norm):
     """One launch over the keys of every decoder layer (the K columns at stride 2D of the batched K/V

@@ -24,6 +24,7 @@
 #                    tree): GPU tests on the current one, then interleaved stage-1 attention timings, per-role stamps
 #                    and bench runs of both (RF_LIB selects the library)
 #   pnab             the deferred RMSNorm: GPU tests, kbench prenorm A/B vs $BASE, interleaved bench runs of both
+#   libkb            kbench prenorm + bench of this library and $BASE, interleaved
 #   quadstudy        tools/kbench.py quad on the study build: the 4-wave GEMM at MT128x192 / MT160x256 (register or
 #                    LDS-DMA staging, whole tiles or stream-K) vs the default engine on the projection shapes
 #   vendor           kernel-trace of the vendor GEMM library vs the engine on the frame's projection shapes
@@ -143,6 +144,20 @@ pnab)  # deferred RMSNorm: its GPU tests, the kbench prenorm A/B on this library
         timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_new$i.json 2>> $O/bench.err
         RF_LIB=$BASE timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_base$i.json 2>> $O/bench.err
     done ;;
+libkb)  # the kbench prenorm A/B and bench runs of this library and $BASE, interleaved (two rounds each)
+    BASE=${BASE:-$R/renderformer_amd/lib/librfhip_base.so}
+    for i in 1 2; do
+        timeout -k 10 300 python -u tools/kbench.py prenorm > $O/kb_new$i.log 2>&1
+        RF_LIB=$BASE timeout -k 10 300 python -u tools/kbench.py prenorm > $O/kb_base$i.log 2>&1
+    done
+    for i in 1 2; do
+        timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_new$i.json 2>> $O/bench.err
+        RF_LIB=$BASE timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_base$i.json 2>> $O/bench.err
+    done ;;
+qkn)  # q/k norm: its GPU tests, kbench norms (split A/B), bench
+    timeout -k 10 600 $T tests/test_kernels_gpu.py -k "qk_norm or rmsnorm" -m gpu > $O/tests.log 2>&1
+    timeout -k 10 300 python -u tools/kbench.py norms > $O/norms.log 2>&1
+    timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err ;;
 costab)  # stage-1 attention timing + per-role stamps under the stream-K cost-model constants in $COSTS (';'-separated
          # RF_ATTN_COST values "tile,pro,pub,merge,store"; "-" = the built-in constants)
     STUDY=$R/renderformer_amd/lib/librfhip_study.so

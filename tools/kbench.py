@@ -172,8 +172,14 @@ def norms():
         pair = qkv[:, :seg * D]
         nw = torch.rand(seg * D, device=dev)
         pos = torch.randn(rows, 9, device=dev)
-        ms = timeit(lambda: ops.qk_norm_rope(pair, pair, H, nw, 1e-6, pos, freqs, n_seg=seg), reps=50)
-        print(f"qk_norm_rope {name} {rows}x{seg*D}: {ms*1e3:6.1f} us  {rows*seg*D*4/ms/1e9:6.0f} GB/s", flush=True)
+        # the q/k pair as two one-segment groups (default) vs one two-segment wave (RF_QKN_SPLIT=0), interleaved
+        for rep in range(2):
+            for split in (("1", "0") if seg == 2 else ("1",)):
+                os.environ["RF_QKN_SPLIT"] = split
+                ms = timeit(lambda: ops.qk_norm_rope(pair, pair, H, nw, 1e-6, pos, freqs, n_seg=seg), reps=50)
+                print(f"qk_norm_rope {name} {rows}x{seg*D} split={split}: {ms*1e3:6.1f} us  "
+                      f"{rows*seg*D*4/ms/1e9:6.0f} GB/s", flush=True)
+        os.environ.pop("RF_QKN_SPLIT", None)
 
 
 def conv():
