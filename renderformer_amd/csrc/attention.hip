@@ -1355,25 +1355,50 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                     }
                     __syncthreads();
                     if (e_active) {
-                        // all 17 loads in flight at once (one round trip), then the fold
+                        // all the partial's loads in flight at once (one round trip), then the fold
                         const float* src = p.part_o + (int64_t)f * PIECE_FLOATS;
                         const f32x2 ml = *reinterpret_cast<const f32x2*>(src + PIECE_O + (wave * 64 + lane) * 2);
-                        f32x4 pv[16];
+                        if constexpr (OF16) {
+                            // fp16 partial, normalised by the publisher's row sum: O += 2^(m' - m) l' * O'/l'
+                            u32x4 ph[8];
 #pragma unroll
-                        for (int k = 0; k < 16; ++k)
-                            pv[k] = *reinterpret_cast<const f32x4*>(src + (((wave * 16 + k) * 64) + lane) * 4);
-                        __builtin_amdgcn_sched_barrier(0);
-                        const float mx = __builtin_fmaxf(m_run, ml[0]);
-                        const float wa = fast_exp2(m_run - mx), wb = fast_exp2(ml[0] - mx);
-                        l_run = l_run * wa + ml[1] * wb;
-                        m_run = mx;
+                            for (int k = 0; k < 8; ++k)
+                                ph[k] = *reinterpret_cast<const u32x4*>(src + (((wave * 8 + k) * 64) + lane) * 4);
+                            __builtin_amdgcn_sched_barrier(0);
+                            const float mx = __builtin_fmaxf(m_run, ml[0]);
+                            const float wa = fast_exp2(m_run - mx), wb = fast_exp2(ml[0] - mx);
+                            const float lpub = ml[1] + __shfl_xor(ml[1], 32, 64);  // the publisher's whole-row sum
+                            const float wbo = wb * lpub;
+                            l_run = l_run * wa + ml[1] * wb;
+                            m_run = mx;
 #pragma unroll
-                        for (int dt = 0; dt < 4; ++dt)
+                            for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-                            for (int gq = 0; gq < 4; ++gq)
+                                for (int gq = 0; gq < 4; ++gq)
 #pragma unroll
-                                for (int e = 0; e < 4; ++e)
-                                    o[dt][4 * gq + e] = o[dt][4 * gq + e] * wa + pv[dt * 4 + gq][e] * wb;
+                                    for (int e = 0; e < 4; ++e) {
+                                        const uint32_t wrd = ph[dt * 2 + (gq >> 1)][(gq & 1) * 2 + (e >> 1)];
+                                        const float v = f16_bits_to_f32((uint16_t)(e & 1 ? wrd >> 16 : wrd & 0xffffu));
+                                        o[dt][4 * gq + e] = o[dt][4 * gq + e] * wa + v * wbo;
+                                    }
+                        } else {
+                            f32x4 pv[16];
+#pragma unroll
+                            for (int k = 0; k < 16; ++k)
+                                pv[k] = *reinterpret_cast<const f32x4*>(src + (((wave * 16 + k) * 64) + lane) * 4);
+                            __builtin_amdgcn_sched_barrier(0);
+                            const float mx = __builtin_fmaxf(m_run, ml[0]);
+                            const float wa = fast_exp2(m_run - mx), wb = fast_exp2(ml[0] - mx);
+                            l_run = l_run * wa + ml[1] * wb;
+                            m_run = mx;
+#pragma unroll
+                            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                                for (int gq = 0; gq < 4; ++gq)
+#pragma unroll
+                                    for (int e = 0; e < 4; ++e)
+                                        o[dt][4 * gq + e] = o[dt][4 * gq + e] * wa + pv[dt * 4 + gq][e] * wb;
+                        }
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -1398,14 +1423,40 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             // flags after the next piece's drain, or after the loop; guide Guideline 16 / MI355X_MICROARCH hand-offs)
             if (e_active) {
                 const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(piece, 0, PIECE_FLOATS * 4, 0x00020000);
+                if constexpr (OF16) {
+                    // fp16 O / l (the frame's fp16-output launches): half the bytes of the fp32 partial; O / l is a
+                    // convex combination of V rows like the output itself, so it fits fp16 where the output does
+                    // (checked: a partial beyond fp16's range raises the range word as the output would)
+                    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+                    const float inv = l_tot > 0.f ? 1.0f / l_tot : 0.f;
+                    float amax = 0.f;
 #pragma unroll
-                for (int dt = 0; dt < 4; ++dt)
+                    for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-                    for (int gq = 0; gq < 4; ++gq) {
-                        const f32x4 v4 = {o[dt][4 * gq], o[dt][4 * gq + 1], o[dt][4 * gq + 2], o[dt][4 * gq + 3]};
-                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v4), rs,
-                                                               (((wave * 16 + dt * 4 + gq) * 64) + eln) * 16, 0, 16);
-                    }
+                        for (int gq = 0; gq < 4; gq += 2) {
+                            u32x4 w4;
+#pragma unroll
+                            for (int h2 = 0; h2 < 2; ++h2) {
+                                const float a = o[dt][4 * (gq + h2)] * inv, b = o[dt][4 * (gq + h2) + 1] * inv;
+                                const float c = o[dt][4 * (gq + h2) + 2] * inv, d = o[dt][4 * (gq + h2) + 3] * inv;
+                                amax = amax3(amax3(amax, a, b), c, d);
+                                w4[2 * h2] = pack_f16x2(a, b);
+                                w4[2 * h2 + 1] = pack_f16x2(c, d);
+                            }
+                            __builtin_amdgcn_raw_buffer_store_b128(w4, rs, (((wave * 8 + dt * 2 + (gq >> 1)) * 64) + eln) * 16,
+                                                                   0, 16);
+                        }
+                    if (e_ovalid && p.range && !f16_in_range(amax)) report_f16_range(p.range, RF_RANGE_ATTN);
+                } else {
+#pragma unroll
+                    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                        for (int gq = 0; gq < 4; ++gq) {
+                            const f32x4 v4 = {o[dt][4 * gq], o[dt][4 * gq + 1], o[dt][4 * gq + 2], o[dt][4 * gq + 3]};
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v4), rs,
+                                                                   (((wave * 16 + dt * 4 + gq) * 64) + eln) * 16, 0, 16);
+                        }
+                }
                 const f32x2 ml = {m_run, l_run};
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ml), rs,
                                                       PIECE_O * 4 + (wave * 64 + eln) * 8, 0, 16);

@@ -129,7 +129,7 @@ libab)
     done
     STUDY=$R/renderformer_amd/lib/librfhip_study.so  # the stamp build (RF_ATTN_DBG=32) of the current tree
     if [ -f $STUDY ]; then RF_LIB=$STUDY timeout -k 10 120 python tools/attn_ablate.py stamps > $O/stamps_new.log 2>&1; fi
-    RF_LIB=$BASE timeout -k 10 120 python tools/attn_ablate.py stamps > $O/stamps_base.log 2>&1
+    if [ -n "$BASE_STUDY" ]; then RF_LIB=$BASE_STUDY timeout -k 10 120 python tools/attn_ablate.py stamps > $O/stamps_base.log 2>&1; fi
     for i in 1 2; do
         timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_new$i.json 2>> $O/bench.err
         RF_LIB=$BASE timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_base$i.json 2>> $O/bench.err
