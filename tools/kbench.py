@@ -165,7 +165,7 @@ def norms():
         w = torch.rand(D, device=dev)
         o = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
         ms = timeit(lambda: ops.rmsnorm(x, w, 1e-6, o), reps=50)
-        print(f"rmsnorm {rows}x{D}: {ms*1e3:6.1f} us  {rows*D*6/ms/1e9:6.0f} GB/s", flush=True)
+        print(f"rmsnorm {rows}x{D}: {ms*1e3:6.1f} us  {rows*D*6/ms/1e6:6.0f} GB/s", flush=True)
     freqs = torch.rand(6, device=dev)
     for name, rows, seg in (("s1 qk", S, 2), ("s2 q", R, 1)):
         qkv = torch.randn(rows, 3 * D, device=dev).bfloat16()
@@ -178,7 +178,7 @@ def norms():
                 os.environ["RF_QKN_SPLIT"] = split
                 ms = timeit(lambda: ops.qk_norm_rope(pair, pair, H, nw, 1e-6, pos, freqs, n_seg=seg), reps=50)
                 print(f"qk_norm_rope {name} {rows}x{seg*D} split={split}: {ms*1e3:6.1f} us  "
-                      f"{rows*seg*D*4/ms/1e9:6.0f} GB/s", flush=True)
+                      f"{rows*seg*D*4/ms/1e6:6.0f} GB/s", flush=True)
         os.environ.pop("RF_QKN_SPLIT", None)
 
 
