@@ -206,7 +206,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_fwd_kernel(Attn
     int split = 0, t_begin = 0, t_end = 0;
     int img_row0 = 0, wy = 0, wx = 0;
     if constexpr (SWIN) {
-        const int nwx = p.gw / p.window;
+        const int nwx = p.gw >> 3;  // window == 8 (host-checked)
         h = blockIdx.y;
         wy = blockIdx.x / nwx;
         wx = blockIdx.x % nwx;
@@ -240,18 +240,22 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_fwd_kernel(Attn
     }
     const int hoff = h * HD;
 
+    // Swin windows are 8 x 8 tokens (the host requires window == 8: one 64-key tile), so the row / label math is
+    // shifts and compile-time constants instead of run-time divisions (the shifted layers' mask computes a label
+    // for each of a lane's 32 keys)
+    constexpr int SW = 8;
     auto swin_row = [&](int i) {
-        const int hs = wy * p.window + i / p.window;
-        const int ws = wx * p.window + i % p.window;
+        const int hs = wy * SW + (i >> 3);  // i >= 0
+        const int ws = wx * SW + (i & 7);
         int hy = hs + p.shift, wxx = ws + p.shift;
         hy -= hy >= p.gh ? p.gh : 0;
         wxx -= wxx >= p.gw ? p.gw : 0;
         return img_row0 + hy * p.gw + wxx;
     };
     auto swin_label = [&](int i) {
-        const int hs = wy * p.window + i / p.window;
-        const int ws = wx * p.window + i % p.window;
-        return region(hs, p.gh, p.window, p.shift) * 3 + region(ws, p.gw, p.window, p.shift);
+        const int hs = wy * SW + (i >> 3);  // i >= 0
+        const int ws = wx * SW + (i & 7);
+        return region(hs, p.gh, SW, p.shift) * 3 + region(ws, p.gw, SW, p.shift);
     };
 
     // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[q][16 s + 8 half + 0..7]

@@ -98,6 +98,9 @@ class _DeviceWeights:
         # texture fast-path flags by frame parity: frame i raises tex_flags[i % 2] and its scan clears the other
         # one for frame i + 1 (no reset launch in the frame; rf_texture_scan2)
         self.tex_flags = torch.zeros(2, dtype=torch.int32, device=device)
+        # identity camera transforms per view count (read-only; built on the host and copied synchronously, so a
+        # render on another stream never sees it half-written): no fill kernels between stage 1 and stage 2
+        self.eyes: Dict[int, torch.Tensor] = {}
         self.tex_parity = 0
         self.tex_norm = _f32(sd["texture_encoder_norm.weight"], device)
         self.enc_freqs = _f32(sd["transformer.rope_emb.freqs"], device)
@@ -925,7 +928,9 @@ class RenderFormer:
         B, V = plan.B, plan.V
         P = B * V
         c2w_v = c2w.reshape(P, 4, 4).float().contiguous()
-        eye = torch.eye(4, dtype=torch.float32, device=dev).expand(P, 4, 4).contiguous()
+        eye = self._w.eyes.get(P)
+        if eye is None:
+            eye = self._w.eyes[P] = torch.eye(4, dtype=torch.float32).expand(P, 4, 4).contiguous().to(dev)
         rays_c2w, pos_c2w = (eye, c2w_v) if cfg.turn_to_cam_coord else (c2w_v, eye)
         ray_in = torch.empty(P * plan.R, 3 * cfg.patch_size ** 2, dtype=self._w.half, device=dev)
         ray_pos = torch.empty(P, 9, dtype=torch.float32, device=dev)

@@ -27,6 +27,7 @@
 #   libkb            kbench prenorm + bench of this library and $BASE, interleaved
 #   quadstudy        tools/kbench.py quad on the study build: the 4-wave GEMM at MT128x192 / MT160x256 (register or
 #                    LDS-DMA staging, whole tiles or stream-K) vs the default engine on the projection shapes
+#   swin             Swin / q/k-norm-fold GPU tests, kernel-trace profile and one run of the default bench
 #   vendor           kernel-trace of the vendor GEMM library vs the engine on the frame's projection shapes
 #                    (tools/kbench.py vendor: study only, nothing of it is linked into librfhip)
 # Every GPU step runs under its own timeout and the steps are chained with && (set -e): the first failure
@@ -173,6 +174,10 @@ costab)  # stage-1 attention timing + per-role stamps under the stream-K cost-mo
 quadstudy)  # the 4-wave GEMM (study build) at the library's tiles vs the default engine on the projection shapes
     KB_SHAPES=${KB_SHAPES:-"s1 qkv,s1 out,s1 w2,s2 out,s2 w2"} KB_QUAD=${KB_QUAD:-"0,1@128x192,2@128x192,1d@128x192,1@160x256,2@160x256,1d@160x256"} \
         RF_LIB=$R/renderformer_amd/lib/librfhip_study.so timeout -k 10 600 python -u tools/kbench.py quad > $O/quad.log 2>&1 ;;
+swin)  # Swin / q/k-norm-fold GPU tests, then a kernel-trace profile of the default bench and one bench run
+    timeout -k 10 600 $T tests/test_kernels_gpu.py tests/test_prenorm_gpu.py -k "swin or qkn" -m gpu > $O/tests.log 2>&1
+    prof_run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --profile --steps 5 --warmup 2 --no-cpu-baseline > $O/prof.log 2>&1
+    timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err ;;
 vendor)
     prof_run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/vend -o run -- python3 $R/tools/kbench.py vendor > $O/vendor.log 2>&1 ;;
 *)
