@@ -499,3 +499,27 @@ if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "quad":
     quad()
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "prenorm":
     prenorm()
+
+
+def c32():
+    """output_conv2 at 512^2 (128 -> 32 filters, 3x3, fp16 planes) with its fused head (SiLU -> 1x1 to 3 -> ELU ->
+    10^x - 1, NHWC as in the frame): conv3x3_c32_kernel (RF_CONV_C32=1, default) vs the engine path (0), interleaved."""
+    from renderformer_amd.dpt import _Conv, split_planes, LOG_DECODE
+    conv = _Conv(torch.randn(32, 128, 3, 3) / 48, torch.randn(32), dev, f16=True)
+    x = split_planes(torch.randn(1, 512, 512, 128, device=dev), conv.cin_pad, f16=True)
+    wf, bf = torch.randn(3, 32, device=dev) / 8, torch.zeros(3, device=dev)
+    fl = 2 * 512 * 512 * 128 * 32 * 9
+    # RF_C32_GRID=512: one tile per workgroup (the pre-persistent launch shape)
+    for rep in range(2):
+        for env, grid in (("1", "256"), ("1", "512"), ("0", "256")):
+            os.environ["RF_CONV_C32"] = env
+            os.environ["RF_C32_GRID"] = grid
+            ms = timeit(lambda: conv(x, final=(wf, bf, 1.0), final_flags=LOG_DECODE), reps=20)
+            print(f"output_conv2 512^2 128->32 + head RF_CONV_C32={env} RF_C32_GRID={grid}: {ms*1e3:7.1f} us  "
+                  f"{fl/ms/1e9:7.1f} TF", flush=True)
+    os.environ.pop("RF_CONV_C32", None)
+    os.environ.pop("RF_C32_GRID", None)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "c32":
+    c32()
