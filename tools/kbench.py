@@ -519,6 +519,15 @@ def c32():
                   f"{fl/ms/1e9:7.1f} TF", flush=True)
     os.environ.pop("RF_CONV_C32", None)
     os.environ.pop("RF_C32_GRID", None)
+    # per-chunk cost vs the input's channel count: cin = 32 makes each LDS-DMA instruction one contiguous 1-KiB run
+    # (16 whole pixels), cin = 64 / 128 / 256 reads 64-B slices of 128 / 256 / 512-B pixels
+    if os.environ.get("KB_C32_CIN"):
+        for cin in (32, 64, 128, 256):
+            cv = _Conv(torch.randn(32, cin, 3, 3) / 48, torch.randn(32), dev, f16=True)
+            xc = split_planes(torch.randn(1, 512, 512, cin, device=dev), cv.cin_pad, f16=True)
+            ms = timeit(lambda: cv(xc, final=(wf, bf, 1.0), final_flags=LOG_DECODE), reps=20)
+            print(f"output_conv2-shape 512^2 {cin}->32 + head: {ms*1e3:7.1f} us  {ms*1e3/(cin//32):6.1f} us per "
+                  f"32-channel chunk  {2*512*512*cin*32*9/ms/1e9:7.1f} TF", flush=True)
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "c32":
