@@ -2564,63 +2564,30 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c32_kernel(EngineArgs p) {
     __shared__ __attribute__((aligned(16))) char smem[LDS];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // persistent over a contiguous run of tiles (XCD-contiguous workgroup ids: neighbouring tiles, whose halos
-    // overlap, share an XCD's L2): the next tile's first chunk is issued before this tile's head epilogue, so
-    // its load latency and the epilogue overlap instead of adding up per tile
+    // XCD-contiguous tile ids (neighbouring tiles, whose halos overlap, share an XCD's L2)
     const int nwg = gridDim.x, hw = blockIdx.x;
     const int xcd = hw & 7, q = nwg >> 3, r = nwg & 7;
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (hw >> 3);
     const int tx_n = p.wo / TW, ty_n = p.ho / TH;
-    const int ntile = p.m / (TH * TW);
-    const int per = (ntile + nwg - 1) / nwg;
-    const int t0 = wg * per, t1 = min(ntile, t0 + per);
-    if (t0 >= t1) return;  // (a grid with more workgroups than tiles / per: nothing issued)
+    const int tx = wg % tx_n, rest = wg / tx_n;
+    const int ty = rest % ty_n, img = rest / ty_n;
+    const int y0 = ty * TH, x0 = tx * TW;
     const int nch = p.cin_pad / 32;
-
-    // head parameters, loaded once (a load issued after the next tile's LDS-DMA would wait for it: vmcnt counts in
-    // issue order): acc[i][j][e] is conv channel 16 j + 4 (lane >> 4) + e
-    float bsum[2][4], wf[NFIN][2][4], bf[NFIN];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int col = j * 16 + 4 * (lane >> 4) + e;
-            bsum[j][e] = (p.bias && col < p.cout) ? p.bias[col] : 0.f;
-        }
-#pragma unroll
-    for (int f = 0; f < NFIN; ++f) {
-        bf[f] = f < p.n_fin ? p.b_fin[f] : 0.f;
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int col = j * 16 + 4 * (lane >> 4) + e;
-                wf[f][j][e] = (f < p.n_fin && col < p.cout) ? p.w_fin[f * p.cout + col] : 0.f;
-            }
-    }
 
     // halo piece t of this wave = halo pixels 16 (wave + 4 t) .. + 15, 64 B each (16-B chunk ^ column key)
     int hpix[HPW], hch[HPW];
-    int img = 0, y0 = 0, x0 = 0;
-    auto setup = [&](int tile) {
-        const int tx = tile % tx_n, rest = tile / tx_n;
-        const int ty = rest % ty_n;
-        img = rest / ty_n;
-        y0 = ty * TH;
-        x0 = tx * TW;
 #pragma unroll
-        for (int t = 0; t < HPW; ++t) {
-            const int hp = (wave + NWAVE * t) * 16 + (lane >> 2);
-            hch[t] = (lane & 3) ^ h2::hkey(hp % HWID);
-            int pix = -1;
-            if (hp < HPIX) {
-                const int hy = hp / HWID, hx = hp - hy * HWID;
-                const int iy = y0 + hy - 1, ix = x0 + hx - 1;
-                if (iy >= 0 && iy < p.hi && ix >= 0 && ix < p.wi) pix = (img * p.hi + iy) * p.wi + ix;
-            }
-            hpix[t] = pix;
+    for (int t = 0; t < HPW; ++t) {
+        const int hp = (wave + NWAVE * t) * 16 + (lane >> 2);
+        hch[t] = (lane & 3) ^ h2::hkey(hp % HWID);
+        int pix = -1;
+        if (hp < HPIX) {
+            const int hy = hp / HWID, hx = hp - hy * HWID;
+            const int iy = y0 + hy - 1, ix = x0 + hx - 1;
+            if (iy >= 0 && iy < p.hi && ix >= 0 && ix < p.wi) pix = (img * p.hi + iy) * p.wi + ix;
         }
-    };
+        hpix[t] = pix;
+    }
     // W piece v (0..17) = tap v / 2, output channels 16 (v & 1) .. + 15 (rows of the [cout_pad][9][cin_pad] bank)
     const int wr = lane >> 2;
     auto issue = [&](int chunk, int buf) {
@@ -2638,6 +2605,11 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c32_kernel(EngineArgs p) {
     };
     const int n_issue = HPW + (WPIECES - wave + NWAVE - 1) / NWAVE;  // LDS-DMA per wave per chunk (14 or 15)
 
+    f32x4 acc[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int frow = lane & 15, fch = lane >> 4;
     // fragment i = tile row 4 wave + i / 2, columns 16 (i & 1) .. + 15; at tap (ty, tx) its lane's halo pixel is
     // row 4 wave + i / 2 + ty, column hx = 16 (i & 1) + frow + tx: hadr[i & 1][tx] + (i / 2 + ty) HWID 64
@@ -2651,101 +2623,104 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c32_kernel(EngineArgs p) {
                          ((fch ^ h2::hkey(hx)) << 4);
         }
     const uint32_t wadr = (uint32_t)(uintptr_t)LDS_PTR(char, smem) + HBYTES + lds_off(frow, fch);
-    const int hwp = p.ho * p.wo;
-    float* __restrict__ out = reinterpret_cast<float*>(p.c);
 
-    setup(t0);
     issue(0, 0);
-    int g = 0;  // chunks run so far (buffer parity)
-    for (int tile = t0; tile < t1; ++tile) {
-        const int cimg = img, cy0 = y0, cx0 = x0;  // this tile's (setup() moves on to the next during its last chunk)
-        f32x4 acc[8][2];
+    for (int c = 0; c < nch; ++c) {
+        const int buf = c & 1;
+        if (c + 1 < nch) {
+            issue(c + 1, buf ^ 1);  // lands under this chunk's MFMAs
+            wait_vm_rt<16>(n_issue);  // this wave's pieces of chunk c landed (chunk c + 1's still in flight)
+        } else {
+            wait_vm<0>();
+        }
+        __builtin_amdgcn_s_barrier();  // every wave's pieces of chunk c landed
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t bo = buf * BUF;
+        // one wave per SIMD: tap t + 1's fragments are read under tap t's MFMAs (two register sets)
+        bf16x8 fa[2][8], fb[2][2];
+        auto rd = [&](int tap, int s) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+            for (int j = 0; j < 2; ++j)
+                fb[s][j] = *LDS_PTR(const bf16x8, (uintptr_t)(wadr + bo + tap * 2048 + j * 1024));
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int c = 0; c < nch; ++c, ++g) {
-            const int buf = g & 1;
-            if (c + 1 < nch) {
-                if (c == 0 && tile != t0) {
-                    // chunk 0 was issued before the previous tile's head stores: wait for both, then chunk 1
-                    wait_vm<0>();
-                    issue(c + 1, buf ^ 1);
-                } else {
-                    issue(c + 1, buf ^ 1);    // lands under this chunk's MFMAs
-                    wait_vm_rt<16>(n_issue);  // this wave's pieces of chunk c landed (chunk c + 1's still in flight)
-                }
-            } else if (tile + 1 < t1) {
-                if (c == 0 && tile != t0) wait_vm<0>();  // (one-chunk inputs)
-                setup(tile + 1);
-                issue(0, buf ^ 1);  // the next tile's chunk 0 lands under this chunk and the head epilogue
-                wait_vm_rt<16>(n_issue);
-            } else {
-                wait_vm<0>();
-            }
-            __builtin_amdgcn_s_barrier();  // every wave's pieces of chunk c landed
+            for (int i = 0; i < 8; ++i)
+                fa[s][i] = *LDS_PTR(const bf16x8, (uintptr_t)(hadr[i & 1][tap % 3] + bo + ((i >> 1) + tap / 3) * HWID * 64));
+        };
+        rd(0, 0);
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int s = tap & 1;
+            if (tap + 1 < 9) rd(tap + 1, s ^ 1);
             __builtin_amdgcn_sched_barrier(0);
-            const uint32_t bo = buf * BUF;
-            // one wave per SIMD: tap t + 1's fragments are read under tap t's MFMAs (two register sets)
-            bf16x8 fa[2][8], fb[2][2];
-            auto rd = [&](int tap, int s) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    fb[s][j] = *LDS_PTR(const bf16x8, (uintptr_t)(wadr + bo + tap * 2048 + j * 1024));
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-                    fa[s][i] = *LDS_PTR(const bf16x8, (uintptr_t)(hadr[i & 1][tap % 3] + bo + ((i >> 1) + tap / 3) * HWID * 64));
-            };
-            rd(0, 0);
-#pragma unroll
-            for (int tap = 0; tap < 9; ++tap) {
-                const int s = tap & 1;
-                if (tap + 1 < 9) rd(tap + 1, s ^ 1);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[s][j]),
-                                                                           __builtin_bit_cast(f16x8, fa[s][i]), acc[i][j], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-            }
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fb[s][j]),
+                                                                       __builtin_bit_cast(f16x8, fa[s][i]), acc[i][j], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_barrier();  // buffer `buf` is free for chunk g + 2
         }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();  // buffer `buf` is free for chunk c + 2
+    }
 
-        // fused head: acc[i][j][e] = conv channel 16 j + 4 (lane >> 4) + e of pixel (tile row 4 wave + i / 2, column
-        // 16 (i & 1) + (lane & 15)); s_f = sum_c silu(conv_c + b_c) w_fin[f, c], the 32 channels of a pixel summed
-        // over the lane's 8 and the four lane groups.  silu(conv + bias) once per value (64 per lane: one wave per
-        // SIMD has the registers), then n_fin dot products
-        float sv[8][2][4];
+    // fused head: acc[i][j][e] = conv channel 16 j + 4 (lane >> 4) + e of pixel (tile row 4 wave + i / 2, column
+    // 16 (i & 1) + (lane & 15)); s_f = sum_c silu(conv_c + b_c) w_fin[f, c], the 32 channels of a pixel summed over
+    // the lane's 8 and the four lane groups
+    float bsum[2][4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int col = j * 16 + 4 * (lane >> 4) + e;
+            bsum[j][e] = (p.bias && col < p.cout) ? p.bias[col] : 0.f;
+        }
+    const int hwp = p.ho * p.wo;
+    // silu(conv + bias) once per value (64 per lane: one wave per SIMD has the registers), then n_fin dot products
+    float sv[8][2][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sv[i][j][e] = silu(acc[i][j][e] + bsum[j][e]);
+    // every head weight is read before the first store: a load issued after a store waits for it (vmcnt counts
+    // both in issue order), and b_fin re-read per pixel fragment made each fragment wait for the previous one's
+    // stores (n_fin <= c32::NFIN, c32_ok)
+    const float* __restrict__ w_fin = p.w_fin;
+    const float* __restrict__ b_fin = p.b_fin;
+    float* __restrict__ out = reinterpret_cast<float*>(p.c);
+    float wf[NFIN][2][4], bf[NFIN];
+#pragma unroll
+    for (int f = 0; f < NFIN; ++f) {
+        bf[f] = f < p.n_fin ? b_fin[f] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int col = j * 16 + 4 * (lane >> 4) + e;
+                wf[f][j][e] = (f < p.n_fin && col < p.cout) ? w_fin[f * p.cout + col] : 0.f;
+            }
+    }
+#pragma unroll
+    for (int f = 0; f < NFIN; ++f) {
+        if (f >= p.n_fin) break;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float s = 0.f;
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) sv[i][j][e] = silu(acc[i][j][e] + bsum[j][e]);
-#pragma unroll
-        for (int f = 0; f < NFIN; ++f) {
-            if (f >= p.n_fin) break;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                float sm = 0.f;
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) sm += sv[i][j][e] * wf[f][j][e];
-                sm += __shfl_xor(sm, 16, 64);
-                sm += __shfl_xor(sm, 32, 64);
-                if (lane < 16) {
-                    // a tile lies inside one image: the NCHW plane offset needs no division
-                    const int pix = (cy0 + 4 * wave + (i >> 1)) * p.wo + cx0 + 16 * (i & 1) + lane;
-                    float y = elu_fast(sm + bf[f], p.elu_alpha);
-                    if (p.flags & RF_CONV_LOG_DECODE) y = pow10m1_fast(y);
-                    const int64_t o = (p.flags & RF_CONV_NCHW_OUT) ? ((int64_t)cimg * p.n_fin + f) * hwp + pix
-                                                                  : ((int64_t)cimg * hwp + pix) * p.n_fin + f;
-                    out[o] = y;
-                }
+                for (int e = 0; e < 4; ++e) s += sv[i][j][e] * wf[f][j][e];
+            s += __shfl_xor(s, 16, 64);
+            s += __shfl_xor(s, 32, 64);
+            if (lane < 16) {
+                const int m = (img * p.ho + y0 + 4 * wave + (i >> 1)) * p.wo + x0 + 16 * (i & 1) + lane;
+                float y = elu_fast(s + bf[f], p.elu_alpha);
+                if (p.flags & RF_CONV_LOG_DECODE) y = pow10m1_fast(y);
+                const int64_t o = (p.flags & RF_CONV_NCHW_OUT) ? ((int64_t)(m / hwp) * p.n_fin + f) * hwp + (m % hwp)
+                                                              : (int64_t)m * p.n_fin + f;
+                out[o] = y;
             }
         }
     }
@@ -3998,10 +3973,7 @@ static bool c32_ok(const EngineArgs& a) {
 }
 
 static int launch_c32(EngineArgs a, void* stream, const char* what) {
-    // persistent: one workgroup per CU (116 KiB of LDS each) over contiguous runs of tiles (RF_C32_GRID: A/B, tests)
-    const int ntile = a.m / (c32::TH * c32::TW);
-    const char* env = getenv("RF_C32_GRID");
-    const int nwg = std::max(1, std::min(ntile, env ? atoi(env) : 256));
+    const int nwg = a.m / (c32::TH * c32::TW);
     RF_LAUNCH(conv3x3_c32_kernel, dim3(nwg), dim3(256), 0, (hipStream_t)stream, a);
     return rf::check_launch(what);
 }

@@ -1527,14 +1527,10 @@ def test_stream_k_epoch_wrap(monkeypatch):
 @pytest.mark.parametrize("cin,cout,hh,ww,n_img,n_fin", [(128, 32, 32, 64, 1, 3), (128, 32, 48, 32, 2, 3),
                                                         (64, 16, 16, 32, 1, 4), (256, 24, 32, 32, 1, 3)])
 @pytest.mark.parametrize("flags", ["log", "nchw"])
-@pytest.mark.parametrize("grid", [None, "1", "4"])
-def test_conv_c32_final_head(cin, cout, hh, ww, n_img, n_fin, flags, grid, monkeypatch):
+def test_conv_c32_final_head(cin, cout, hh, ww, n_img, n_fin, flags, monkeypatch):
     """output_conv2's kernel (conv3x3_c32_kernel: <= 32 filters, 16 x 32 tiles, fused SiLU -> 1x1 -> ELU -> 10^x - 1
     head) against fp64 on the same fp16 operands, and equal (to fp32 summation order) to the halo2 / engine path it
-    replaces (RF_CONV_C32=0).  The kernel is persistent over runs of tiles: RF_C32_GRID=1 / 4 give a workgroup several
-    tiles (the next tile's first chunk issued under the previous tile's head), with uneven splits and idle groups."""
-    if grid:
-        monkeypatch.setenv("RF_C32_GRID", grid)
+    replaces (RF_CONV_C32=0)."""
     from renderformer_amd.dpt import FINAL, LOG_DECODE, NCHW_OUT, _Conv, split_planes
     g = torch.Generator(device="cpu").manual_seed(cin + cout + hh)
     w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)

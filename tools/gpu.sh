@@ -28,6 +28,7 @@
 #   quadstudy        tools/kbench.py quad on the study build: the 4-wave GEMM at MT128x192 / MT160x256 (register or
 #                    LDS-DMA staging, whole tiles or stream-K) vs the default engine on the projection shapes
 #   swin             Swin / q/k-norm-fold GPU tests, kernel-trace profile and one run of the default bench
+#   profab           kernel-trace profiles of the default bench under each env setting in $ENVS (';'-separated)
 #   vendor           kernel-trace of the vendor GEMM library vs the engine on the frame's projection shapes
 #                    (tools/kbench.py vendor: study only, nothing of it is linked into librfhip)
 # Every GPU step runs under its own timeout and the steps are chained with && (set -e): the first failure
@@ -178,6 +179,14 @@ swin)  # Swin / q/k-norm-fold GPU tests, then a kernel-trace profile of the defa
     timeout -k 10 600 $T tests/test_kernels_gpu.py tests/test_prenorm_gpu.py -k "swin or qkn" -m gpu > $O/tests.log 2>&1
     prof_run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --profile --steps 5 --warmup 2 --no-cpu-baseline > $O/prof.log 2>&1
     timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err ;;
+profab)  # kernel-trace profiles of the default bench under each ';'-separated env setting in $ENVS ("-" = none)
+    IFS=';' read -ra ES <<< "${ENVS:--}"
+    i=0
+    for e in "${ES[@]}"; do
+        i=$((i+1))
+        if [ "$e" = "-" ]; then e=""; fi
+        (export $e; prof_run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof$i -o run -- python3 $R/bench.py --profile --steps 5 --warmup 2 --no-cpu-baseline > $O/prof$i.log 2>&1)
+    done ;;
 vendor)
     prof_run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/vend -o run -- python3 $R/tools/kbench.py vendor > $O/vendor.log 2>&1 ;;
 *)

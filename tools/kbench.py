@@ -509,16 +509,13 @@ def c32():
     x = split_planes(torch.randn(1, 512, 512, 128, device=dev), conv.cin_pad, f16=True)
     wf, bf = torch.randn(3, 32, device=dev) / 8, torch.zeros(3, device=dev)
     fl = 2 * 512 * 512 * 128 * 32 * 9
-    # RF_C32_GRID=512: one tile per workgroup (the pre-persistent launch shape)
     for rep in range(2):
-        for env, grid in (("1", "256"), ("1", "512"), ("0", "256")):
+        for env in ("1", "0"):
             os.environ["RF_CONV_C32"] = env
-            os.environ["RF_C32_GRID"] = grid
             ms = timeit(lambda: conv(x, final=(wf, bf, 1.0), final_flags=LOG_DECODE), reps=20)
-            print(f"output_conv2 512^2 128->32 + head RF_CONV_C32={env} RF_C32_GRID={grid}: {ms*1e3:7.1f} us  "
-                  f"{fl/ms/1e9:7.1f} TF", flush=True)
+            print(f"output_conv2 512^2 128->32 + head RF_CONV_C32={env}: {ms*1e3:7.1f} us  {fl/ms/1e9:7.1f} TF",
+                  flush=True)
     os.environ.pop("RF_CONV_C32", None)
-    os.environ.pop("RF_C32_GRID", None)
     # per-chunk cost vs the input's channel count: cin = 32 makes each LDS-DMA instruction one contiguous 1-KiB run
     # (16 whole pixels), cin = 64 / 128 / 256 reads 64-B slices of 128 / 256 / 512-B pixels
     if os.environ.get("KB_C32_CIN"):
