@@ -44,7 +44,10 @@ def load_pipeline(args) -> RenderFormerRenderingPipeline:
     model_id = args.model_id
     if args.synthetic_seed is not None and model_id.startswith("microsoft/"):
         model_id = model_id.split("/", 1)[1]
-    pipe = RenderFormerRenderingPipeline.from_pretrained(model_id, synthetic_seed=args.synthetic_seed)
+    # "lazy" fp16 range check: the CLIs resolve each frame where they wait for its copy anyway (infer.py: before
+    # reading it; batch_infer.py: before the D2H of the next batch), so render never blocks their pipelining
+    pipe = RenderFormerRenderingPipeline.from_pretrained(model_id, synthetic_seed=args.synthetic_seed,
+                                                         range_check="lazy")
     return pipe.to("cuda")
 
 

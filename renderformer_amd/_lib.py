@@ -169,22 +169,22 @@ def load(require_device: bool = True):
                     continue
                 fn.argtypes = args
                 fn.restype = ctypes.c_int
-            lib.rf_last_error.restype = ctypes.c_char_p
-            lib.rf_last_error.argtypes = []
-            lib.rf_abi_version.restype = ctypes.c_int
-            lib.rf_build_flags.restype = ctypes.c_int
-            lib.rf_build_flags.argtypes = []
-            lib.rf_attn_workspace_bytes.restype = ctypes.c_int64
-            lib.rf_gemm_workspace_bytes.restype = ctypes.c_int64
-            lib.rf_gemm_workspace_bytes.argtypes = []
-            lib.rf_scene_pos_partials.restype = ctypes.c_int64
-            lib.rf_scene_pos_partials.argtypes = [_I, _I]
-            lib.rf_attn_workspace_bytes.argtypes = [_L, _I, _I]
-            lib.rf_attn_grid.argtypes = []
-            lib.rf_encoder_workspace_bytes.restype = ctypes.c_int64
-            lib.rf_encoder_workspace_bytes.argtypes = [_I, _I, _I, _I]
-            lib.rf_decoder_workspace_bytes.restype = ctypes.c_int64
-            lib.rf_decoder_workspace_bytes.argtypes = [_P]
+            # return types of the non-int entry points; each guarded like the signature loop above, so an older
+            # library selected with RF_LIB loads and only a call to a symbol it lacks fails
+            for name, res, args in (("rf_last_error", ctypes.c_char_p, []), ("rf_abi_version", ctypes.c_int, None),
+                                    ("rf_build_flags", ctypes.c_int, []),
+                                    ("rf_attn_workspace_bytes", ctypes.c_int64, [_L, _I, _I]),
+                                    ("rf_gemm_workspace_bytes", ctypes.c_int64, []),
+                                    ("rf_scene_pos_partials", ctypes.c_int64, [_I, _I]), ("rf_attn_grid", None, []),
+                                    ("rf_encoder_workspace_bytes", ctypes.c_int64, [_I, _I, _I, _I]),
+                                    ("rf_decoder_workspace_bytes", ctypes.c_int64, [_P])):
+                fn = getattr(lib, name, None)
+                if fn is None:
+                    continue
+                if res is not None:
+                    fn.restype = res
+                if args is not None:
+                    fn.argtypes = args
             _lib = lib
     if require_device and not torch.cuda.is_available():
         raise HipLibraryError("renderformer_amd needs a HIP device (MI355X); none is visible")
@@ -194,7 +194,10 @@ def load(require_device: bool = True):
 def study_build() -> bool:
     """True for the study build of the library (rf_build_flags(): RF_BUILD_STUDY): the measured-slower kernels and
     ablation variants are compiled only there; the production build refuses them (RF_ERR_UNSUPPORTED)."""
-    return bool(load(require_device=False).rf_build_flags() & 1)
+    lib = load(require_device=False)
+    if getattr(lib, "rf_build_flags", None) is None:  # a pre-round-5 library (RF_LIB): no study variants
+        return False
+    return bool(lib.rf_build_flags() & 1)
 
 
 def call(name: str, *args) -> None:

@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void qk_norm_rope_row_kernel(const bf16_t* src
                                                                const float* __restrict__ pos, int64_t ld_pos,
                                                                int pos_div, const float* __restrict__ freqs,
                                                                int n_freqs, int64_t src_gstride, int64_t dst_gstride,
-                                                               int w_gstride) {
+                                                               int w_gstride, int split_qk) {
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
     if (row >= rows) return;
@@ -333,8 +333,10 @@ __global__ __launch_bounds__(256) void qk_norm_rope_row_kernel(const bf16_t* src
                 if ((lane + 64 * u) / upsg == sg) inv[u] = iv;
         }
     }
-    // segment 0 (q) of group 0 carries seg0_scale (RoPE is linear): folded into the row scale
-    if (blockIdx.y == 0) {
+    // segment 0 carries seg0_scale (RoPE is linear): folded into the row scale.  Every group's segment 0 (the
+    // documented rf_qk_norm_rope_groups contract), except when the host split one two-segment (q, k) group into two
+    // one-segment groups (split_qk): then group 1's segment 0 is k, which is not scaled
+    if (!split_qk || blockIdx.y == 0) {
 #pragma unroll
         for (int u = 0; u < UPL; ++u)
             if (lane + 64 * u < upsg) inv[u] *= seg0_scale;
@@ -565,7 +567,9 @@ extern "C" int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t s
     // second round); the per-segment sums and the arithmetic are the same, so the results are bit-identical.
     // RF_QKN_SPLIT=0 keeps the two-segment wave (A/B)
     const char* split_env = getenv("RF_QKN_SPLIT");
+    int split_qk = 0;
     if (n_seg == 2 && n_groups == 1 && (!split_env || atoi(split_env) != 0)) {
+        split_qk = 1;
         n_seg = 1;
         n_groups = 2;
         src_gstride = dst_gstride = dim;
@@ -575,7 +579,7 @@ extern "C" int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t s
 #define RF_QKN(U)                                                                                                 \
     RF_LAUNCH(qk_norm_rope_row_kernel<U>, grid, dim3(256), 0, st, (const bf16_t*)src, ld_src, (bf16_t*)dst, \
                        ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, seg0_scale, pos, ld_pos, pos_div, freqs, \
-                       n_freqs, src_gstride, dst_gstride, (int)w_gstride)
+                       n_freqs, src_gstride, dst_gstride, (int)w_gstride, split_qk)
     units = n_seg * n_heads * 8;
     if (units <= 64) RF_QKN(1);
     else if (units <= 128) RF_QKN(2);

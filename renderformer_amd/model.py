@@ -17,14 +17,18 @@ softmax, and the DPT convolutions take fp16 operands with fp32 accumulation.
 fp16 operands are range-checked on the device (every fp16 writer raises a word of the
 frame's own on |x| > 65504; ``range_check``): a frame that overflowed is rendered again
 with bf16 operands (bf16x3 DPT planes), or reported as a DeviceError in the deferred mode.
-The check never blocks ``render``: the default ("lazy") reads a frame's word once its end
-event has completed (at a later render, ``resolve(out)`` or ``check_range()``).
+The default ("sync") resolves a frame before ``render`` returns by waiting on that frame's end
+event only (no device sync, like the caller's own ``.cpu()``), so a caller that never calls
+``resolve`` — the reference README example, its ``infer.py`` — always reads the final frame.
+Callers that pipeline frames opt in to "lazy" (read at a later render, ``resolve(out)`` or
+``check_range()``: ``batch_infer.py``, ``infer.py``) or "deferred" (``bench.py``).
 """
 from __future__ import annotations
 
 import ctypes
 import math
 import os
+import threading
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -318,18 +322,22 @@ class RenderFormer:
         # fp16 range check (RF_RANGE_CHECK).  Every render binds a host-mapped word of its own (rf_range_word_bind)
         # that the fp16-writing kernels raise on |x| > 65504 (inf included): a checkpoint whose activations exceed
         # fp16's range.  Concurrent renders (streams, models, threads) never share a word.
-        #   "lazy" (default): render returns without waiting; the word is read once the frame's end event has
-        #     completed — at the start of a later render (non-blocking), in resolve(out) or check_range() (waiting).
-        #     An overflowed frame is rendered again IN PLACE (same output tensor, same stream) with bf16 projection
-        #     operands (code 1/2/4) and/or bf16x3 DPT planes (code 8), which the model keeps (PrecisionWarning).
-        #   "sync": render waits for its own frame's end event (no device sync) and re-renders before returning.
+        #   "sync" (default): render waits for its own frame's end event (no device sync) and, if the frame
+        #     overflowed, renders it again with bf16 projection operands (code 1/2/4) and/or bf16x3 DPT planes
+        #     (code 8) before returning; the model keeps them (PrecisionWarning).  Safe for callers that never call
+        #     resolve (the reference's README example and infer.py).
+        #   "lazy" (opt-in: batch_infer.py, infer.py): render returns without waiting; the word is read once the
+        #     frame's end event has completed — at the start of a later render (non-blocking), in resolve(out) or
+        #     check_range() (waiting) — and an overflowed frame is rendered again IN PLACE (same tensor and stream).
         #   "deferred": like lazy, but an overflow raises DeviceError (bench.py's timed loop).   "off": no check.
-        self.range_check = range_check or os.environ.get("RF_RANGE_CHECK", "lazy")
+        # The range-word lists are guarded by a lock: renders of one model from several threads never share a word.
+        self.range_check = range_check or os.environ.get("RF_RANGE_CHECK", "sync")
         if self.range_check not in RANGE_CHECKS:
             raise ValueError(f"range_check must be one of {RANGE_CHECKS}")
         self.range_fallbacks = 0  # frames rendered again with bf16 operands after an fp16 overflow
         self._range_free: List[int] = []  # range-word handles not in use
         self._range_pending: List[_Frame] = []  # frames whose word is unread, oldest first
+        self._range_lock = threading.RLock()
         # render_views: stage 2 + DPT over at most view_chunk views per pass (stage 1 once per scene); None = all
         # views of the batch in one pass.  A fixed chunk makes each view's image independent of the batching.
         self.view_chunk = view_chunk if view_chunk is not None else (int(os.environ.get("RF_VIEW_CHUNK", "0")) or None)
@@ -380,21 +388,21 @@ class RenderFormer:
     # ------------------------------------------------------------------ module-like API
     @classmethod
     def from_pretrained(cls, model_id: str, synthetic_seed: Optional[int] = None, dpt_precision: Optional[str] = None,
-                        **_):
+                        range_check: Optional[str] = None, **_):
         """PyTorchModelHubMixin.from_pretrained (renderformer.py:13) without the network: ``model_id`` is a local
         snapshot directory (config.json + model.safetensors), or a hub id ("microsoft/renderformer-v1.1-swin-
         large") found in the local Hugging Face cache; with ``synthetic_seed`` (or env RF_SYNTHETIC_SEED) a hub
         id or architecture name that is not cached gets deterministic random weights of that architecture."""
         snap = model_id if os.path.isdir(model_id) else _hf_cache_snapshot(model_id)
         if snap is not None:
-            return cls(named_config(snap), load_snapshot(snap), dpt_precision=dpt_precision)
+            return cls(named_config(snap), load_snapshot(snap), dpt_precision=dpt_precision, range_check=range_check)
         if synthetic_seed is None and os.environ.get("RF_SYNTHETIC_SEED"):
             synthetic_seed = int(os.environ["RF_SYNTHETIC_SEED"])
         if synthetic_seed is None:
             raise FileNotFoundError(f"{model_id!r} is neither a local snapshot directory nor in the local Hugging Face "
                                     "cache (no network here); pass synthetic_seed= (or set RF_SYNTHETIC_SEED) for "
                                     "random-init weights of the named architecture")
-        return cls(named_config(model_id), seed=synthetic_seed, dpt_precision=dpt_precision)
+        return cls(named_config(model_id), seed=synthetic_seed, dpt_precision=dpt_precision, range_check=range_check)
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
         check_state_dict(self.config, sd, strict=strict)
@@ -761,7 +769,8 @@ class RenderFormer:
             return run()
         self._range_poll()
         lib = _load_lib()
-        word = self._range_free.pop() if self._range_free else None
+        with self._range_lock:
+            word = self._range_free.pop() if self._range_free else None
         if word is None:
             h = ctypes.c_void_p()
             if lib.rf_range_word_new(ctypes.byref(h)) != 0:
@@ -771,34 +780,50 @@ class RenderFormer:
         lib.rf_range_word_bind(word)
         try:
             out = run()
-        finally:
+        except BaseException:
+            # a refused launch (validation / DeviceError): whatever did run reads the word only on this stream
             lib.rf_range_word_bind(None)
+            torch.cuda.current_stream().synchronize()
+            with self._range_lock:
+                self._range_free.append(word)
+            raise
+        lib.rf_range_word_bind(None)
         stream = torch.cuda.current_stream()
         ev = torch.cuda.Event()
         ev.record(stream)
         fr = _Frame(word, ev, stream, out, replay, inputs)
         if self.range_check == "sync":
             self._range_resolve(fr, wait=True)
-        else:
+            return out
+        oldest = None
+        with self._range_lock:
             self._range_pending.append(fr)
             if len(self._range_pending) > RANGE_WORDS_MAX:
-                self._range_resolve(self._range_pending.pop(0), wait=True)
+                oldest = self._range_pending.pop(0)
+        if oldest is not None:
+            self._range_resolve(oldest, wait=True)
         return out
 
     def _range_poll(self):
         """Resolve (oldest first) the pending frames whose end event has completed: no host wait."""
-        while self._range_pending and self._range_pending[0].event.query():
-            self._range_resolve(self._range_pending.pop(0), wait=False)
+        while True:
+            with self._range_lock:
+                if not (self._range_pending and self._range_pending[0].event.query()):
+                    return
+                fr = self._range_pending.pop(0)
+            self._range_resolve(fr, wait=False)
 
     def _range_resolve(self, fr: _Frame, wait: bool) -> bool:
         """Read a frame's word (after its end event); on an overflow fall back and re-render it in place (lazy /
-        sync) or raise DeviceError (deferred).  Returns True if the frame was rendered again."""
+        sync) or raise DeviceError (deferred).  Returns True if the frame was rendered again.  The caller has taken
+        ``fr`` off the pending list, so no other thread resolves it."""
         from ._lib import DeviceError
         if wait:
             fr.event.synchronize()
         lib = _load_lib()
         code = int(lib.rf_range_word_read(fr.word))
-        self._range_free.append(fr.word)
+        with self._range_lock:
+            self._range_free.append(fr.word)
         if not code:
             return False
         import warnings
@@ -806,20 +831,26 @@ class RenderFormer:
         if self.range_check == "deferred":
             raise DeviceError(f"fp16 operand overflow (range code {code}: |x| > 65504 in an fp16 {'/'.join(what)} "
                               "output) -- this checkpoint's activations exceed fp16's range: render with "
-                              "operands='bf16' (RF_OPERANDS=bf16) and dpt_precision='bf16x3', or range_check='lazy' "
-                              "/ 'sync' (re-renders such frames)")
+                              "operands='bf16' (RF_OPERANDS=bf16) and dpt_precision='bf16x3', or range_check='sync' "
+                              "/ 'lazy' (re-renders such frames)")
         if any(t._version != v for t, v in zip(fr.inputs, fr.versions)):
             raise DeviceError(f"fp16 operand overflow (range code {code}) in a frame whose inputs were modified in "
                               "place before it could be rendered again: call resolve(out) / check_range() before "
                               "reusing input buffers, or use range_check='sync'")
-        # projections and attention (codes 1/2/4) -> bf16 operands; the DPT planes (code 8) -> bf16x3, and a stage-1
-        # or stage-2 overflow reaches the DPT as inf too, so it sets 8 as well
-        if code & 7:
-            self.operands = "bf16"
-        if code & 8 and self.dpt_precision == "f16":
-            self.dpt_precision = "bf16x3"
-        self._w = _DeviceWeights(self.config, self._sd, self._device, self.dpt_precision, self.operands)
-        self.range_fallbacks += 1
+        with self._range_lock:
+            # the weights are rebuilt below, which frees the old tensors into the caching
+            # allocator of the stream they were made on; frames still in flight on other streams read them, so
+            # wait for every pending frame first (an overflow is rare: this wait is the fallback path's only cost)
+            for p in self._range_pending:
+                p.event.synchronize()
+            # projections and attention (codes 1/2/4) -> bf16 operands; the DPT planes (code 8) -> bf16x3, and a
+            # stage-1 or stage-2 overflow reaches the DPT as inf too, so it sets 8 as well
+            if code & 7:
+                self.operands = "bf16"
+            if code & 8 and self.dpt_precision == "f16":
+                self.dpt_precision = "bf16x3"
+            self._w = _DeviceWeights(self.config, self._sd, self._device, self.dpt_precision, self.operands)
+            self.range_fallbacks += 1
         warnings.warn(f"fp16 operand overflow (range code {code}: {'/'.join(what)}): this checkpoint's activations "
                       f"exceed fp16's range; the frame is rendered again and the model keeps "
                       f"{self.operands} projection operands and {self.dpt_precision} DPT planes from now on",
@@ -854,11 +885,13 @@ class RenderFormer:
     def resolve(self, out: Optional[torch.Tensor] = None) -> bool:
         """Finish the range check of the frame whose output is ``out`` (every pending frame if None), waiting for
         it: afterwards ``out`` holds the final frame (rendered again if it overflowed fp16).  Returns True if a
-        frame was rendered again.  batch_infer.py calls it where it already waits for the frame's copy."""
-        keep, done = [], []
-        for fr in self._range_pending:
-            (done if out is None or fr.out is out else keep).append(fr)
-        self._range_pending = keep
+        frame was rendered again.  batch_infer.py calls it where it already waits for the frame's copy; in the
+        default "sync" mode render has already done it and this only reports."""
+        with self._range_lock:
+            keep, done = [], []
+            for fr in self._range_pending:
+                (done if out is None or fr.out is out else keep).append(fr)
+            self._range_pending = keep
         for fr in done:
             self._range_resolve(fr, wait=True)
         redo = False
@@ -871,15 +904,39 @@ class RenderFormer:
     def check_range(self):
         """Resolve every pending frame (waiting for each): deferred mode raises DeviceError for an overflowed frame,
         lazy mode re-renders it in place.  Call before reading frames whose range check is pending."""
-        pending, self._range_pending = self._range_pending, []
+        with self._range_lock:
+            pending, self._range_pending = self._range_pending, []
         for i, fr in enumerate(pending):
             try:
                 self._range_resolve(fr, wait=True)
             except BaseException:
                 for rest in pending[i + 1:]:  # the others' words stay usable
                     rest.event.synchronize()
-                    self._range_free.append(rest.word)
+                    with self._range_lock:
+                        self._range_free.append(rest.word)
                 raise
+
+    def close(self):
+        """Release the model's host-mapped range words: pending frames are waited for first.  Called
+        by ``__del__``; the model stays usable (new words are allocated on the next render)."""
+        lib = None
+        with self._range_lock:
+            words = list(self._range_free)
+            for fr in self._range_pending:
+                fr.event.synchronize()
+                words.append(fr.word)
+            self._range_free, self._range_pending = [], []
+        for w in words:
+            if lib is None:
+                lib = _load_lib()
+            lib.rf_range_word_free(w)
+
+    def __del__(self):
+        try:
+            if getattr(self, "_range_lock", None) is not None:
+                self.close()
+        except Exception:  # interpreter shutdown: the library or torch may already be gone
+            pass
 
     @property
     def precision(self) -> str:

@@ -335,10 +335,12 @@ def qk_norm_rope(src: torch.Tensor, dst: torch.Tensor, n_heads: int, norm_w: Opt
 
 def qk_norm_rope_groups(src: torch.Tensor, src_gstride: int, dst: torch.Tensor, dst_gstride: int, n_groups: int,
                         n_heads: int, norm_w: Optional[torch.Tensor], eps: float, pos: Optional[torch.Tensor] = None,
-                        freqs: Optional[torch.Tensor] = None, src_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+                        freqs: Optional[torch.Tensor] = None, src_rows: Optional[torch.Tensor] = None,
+                        seg0_scale: float = 1.0) -> torch.Tensor:
     """qk_norm_rope (one segment) on n_groups column groups in one launch: group g maps the width-
     (n_heads*128) block at column g*src_gstride of src to column g*dst_gstride of dst with norm weights
-    norm_w[g*dim:(g+1)*dim].  src/dst are the full row matrices holding every group."""
+    norm_w[g*dim:(g+1)*dim].  src/dst are the full row matrices holding every group.  Every group is also
+    multiplied by seg0_scale (qk_norm_rope's q_scale, applied per group: rf.h)."""
     _dev(src, torch.bfloat16, "src")
     _dev(dst, torch.bfloat16, "dst")
     dim = n_heads * 128
@@ -356,7 +358,7 @@ def qk_norm_rope_groups(src: torch.Tensor, src_gstride: int, dst: torch.Tensor, 
         _dev(pos, torch.float32, "pos")
         _check(pos.shape[1] == 9 and freqs is not None, "qk_norm_rope_groups: pos must be [*, 9] with freqs")
     call("rf_qk_norm_rope_groups", ptr(src), src.stride(0), src_gstride, ptr(dst), dst.stride(0), dst_gstride,
-         ptr(src_rows), rows, dim, n_heads, 1, n_groups, ptr(norm_w), dim, eps, 1.0, ptr(pos),
+         ptr(src_rows), rows, dim, n_heads, 1, n_groups, ptr(norm_w), dim, eps, float(seg0_scale), ptr(pos),
          pos.stride(0) if pos is not None else 0, 1, ptr(freqs), freqs.numel() if freqs is not None else 0, stream())
     return dst
 

@@ -172,6 +172,16 @@ class ShardedRenderer:
         costs = [scene_cost(cfg, int(s["mask"].sum()), int(s["c2w"].shape[1]), res) for s in scenes]
         return assign_units(costs, self.world)
 
+    def _render_resolved(self, scene: dict, res: int, kw: dict) -> torch.Tensor:
+        """One pipeline render whose fp16 range check is finished before the frame is stacked or gathered (VERDICT
+        r5 weak 4): a "lazy" model's re-render happens in place in ``out``, which the gather must not have copied
+        yet.  A "sync" model (the default) has resolved it already; resolve then only reports."""
+        out = self.pipeline(**scene, resolution=res, **kw)
+        resolve = getattr(self.pipeline, "resolve", None)
+        if resolve is not None:
+            resolve(out)
+        return out
+
     def _frame_shape(self, n_views: int, res: int):
         return (n_views, res, res, frame_channels(self.pipeline.config))
 
@@ -185,7 +195,7 @@ class ShardedRenderer:
             raise ValueError("all scenes of one call must have the same view count")
         plan = self.plan(scenes, res)
         mine = plan[self.rank]
-        frames = [self.pipeline(**scenes[i], resolution=res, **kw)[0] for i in mine]  # [V, H, W, C] each
+        frames = [self._render_resolved(scenes[i], res, kw)[0] for i in mine]  # [V, H, W, C] each
         shape = self._frame_shape(views.pop(), res)
         local = (torch.stack(frames) if frames
                  else torch.empty((0,) + shape, dtype=torch.float32, device=self.pipeline.device))
@@ -204,7 +214,7 @@ class ShardedRenderer:
             sub = dict(scene)
             sub["c2w"] = scene["c2w"][:, vr.start:vr.stop].contiguous()
             sub["fov"] = scene["fov"][:, vr.start:vr.stop].contiguous()
-            local = self.pipeline(**sub, resolution=res, **kw)[0]
+            local = self._render_resolved(sub, res, kw)[0]
         else:
             local = torch.empty((0,) + shape, dtype=torch.float32, device=self.pipeline.device)
         if not gather:

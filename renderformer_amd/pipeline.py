@@ -17,9 +17,13 @@ within the 1e-3 relative-L2 parity budget of the reference CPU fp32 output at ev
 BASELINE configuration (tests/test_parity_gpu.py).  The argument is validated
 exactly like the reference; ``torch.float32`` (which in the reference selects
 fp32 stage-1 arithmetic) emits a one-time ``PrecisionWarning`` saying so, and
-``last_precision`` records what ran (``RenderFormer.precision``; refreshed by
-``resolve`` / ``check_range``, so an fp16-overflow fallback to bf16 shows once the
-frame's range check has run — ``render`` returns before the frame completes).
+``last_precision`` records what ran (``RenderFormer.precision``).
+
+fp16 range check: by default (``RenderFormer(range_check="sync")``) ``render`` waits for its own
+frame's end event — no device sync, the wait the caller's ``.cpu()`` would do anyway — and
+re-renders an overflowed frame with bf16 operands before returning, so unchanged callers of the
+reference API (README example, ``infer.py``) never see a non-finite frame.  Pipelining callers
+(``batch_infer.py``) opt in to ``range_check="lazy"`` and call ``resolve(out)`` / ``check_range()``.
 """
 from __future__ import annotations
 
@@ -74,9 +78,8 @@ class RenderFormerRenderingPipeline:
 
     def resolve(self, out=None) -> bool:
         """RenderFormer.resolve: finish the fp16 range check of the frame ``out`` (every pending frame if None),
-        waiting for it; an overflowed frame is rendered again in place.  ``render`` itself never waits (like the
-        reference's, rendering_pipeline.py:105-125): call this (or ``check_range``) before reading frames when the
-        model's range_check is "lazy" and the checkpoint may exceed fp16's range."""
+        waiting for it; an overflowed frame is rendered again in place.  Only needed with range_check="lazy" (the
+        default "sync" render has resolved its frame already; then this only reports whether it was re-rendered)."""
         redo = self.model.resolve(out)
         if self.last_precision is not None:
             self.last_precision["computed"] = self.model.precision

@@ -488,6 +488,25 @@ def test_qk_norm_rope_groups_equals_per_group(with_norm):
         assert relerr(out[:, g * D:(g + 1) * D].float().cpu(), ref) < 4e-3
 
 
+def test_qk_norm_rope_groups_scale_applies_to_every_group():
+    """rf_qk_norm_rope_groups with seg0_scale != 1 scales segment 0 of EVERY group (rf.h: the
+    function is rf_qk_norm_rope applied per group); only the host's internal q/k split of one two-segment group
+    scales group 0 alone.  Bit-identical to one rf_qk_norm_rope launch per group with the same q_scale."""
+    ops = _ops()
+    T, H, G = 97, 8, 3
+    D = H * 128
+    kv = torch.randn(T, G * 2 * D).bfloat16().to(dev)
+    w = (torch.rand(G * D) + 0.5).to(dev)
+    pos = (torch.rand(T, 9) * 2 - 1).to(dev)
+    freqs = (2 ** torch.linspace(0, math.log2(5), 6)).to(dev)
+    out = torch.empty(T, G * D, device=dev, dtype=torch.bfloat16)
+    ops.qk_norm_rope_groups(kv, 2 * D, out, D, G, H, w, 1e-6, pos, freqs, seg0_scale=2.5)
+    for g in range(G):
+        one = torch.empty(T, D, device=dev, dtype=torch.bfloat16)
+        ops.qk_norm_rope(kv[:, 2 * D * g:2 * D * g + D], one, H, w[g * D:(g + 1) * D], 1e-6, pos, freqs, q_scale=2.5)
+        assert torch.equal(out[:, g * D:(g + 1) * D], one), g
+
+
 def _ref_attn(q, k, v, H):
     lq, lk = q.shape[0], k.shape[0]
     qh = q.double().view(lq, H, 128).transpose(0, 1)

@@ -371,9 +371,33 @@ def _overflow_sd(sd, scale=2000.0):
     return sd
 
 
+def test_f16_overflow_default_render_is_final_without_resolve():
+    """the README-style call (default model, no resolve, no check_range) on a checkpoint whose
+    activations exceed fp16 returns a finite frame within 1e-3 of the oracle: the default "sync" range check waits
+    for the frame's own end event and re-renders it in bf16 before render returns."""
+    from renderformer_amd import RenderFormer, RenderFormerRenderingPipeline
+    from renderformer_amd.model import PrecisionWarning
+    cfg, sd, inp, res, z = load_case("tiny_swin")
+    d = {k: v.cuda() for k, v in inp.items()}
+    big = _overflow_sd(sd)
+    ref = rf_ref.render(big, cfg, inp["triangles"], inp["texture"].clone(), inp["mask"], inp["vn"], inp["c2w"],
+                        inp["fov"], resolution=res)
+    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, big)).to("cuda")
+    assert pipe.model.range_check == "sync"
+    with pytest.warns(PrecisionWarning, match="fp16 operand overflow"):
+        out = pipe(d["triangles"], d["texture"].clone(), d["mask"], d["vn"], d["c2w"], d["fov"], resolution=res,
+                   torch_dtype=torch.float16)
+    img = out.cpu()  # what the reference README does next
+    assert torch.isfinite(img).all()
+    err = rel_l2(img, ref)
+    print(f"README-style call, overflowing checkpoint: rel L2 {err:.3e} vs the oracle")
+    assert err < HDR_TOL
+    assert pipe.model.range_fallbacks == 1 and pipe.last_precision["computed"].startswith("bf16 projection")
+
+
 def test_f16_overflow_detected_and_rerendered_in_bf16():
     """ADVICE r3 / VERDICT r3 item 2, VERDICT r4 item 3: the fp16 writers raise the frame's own range word, the
-    (default, "lazy") range check reads it once the frame has completed — here in resolve(out) — renders the frame
+    opt-in "lazy" range check reads it once the frame has completed — here in resolve(out) — renders the frame
     again IN PLACE with bf16 operands (which the model keeps), and the result is finite and matches the oracle's fp32
     render of the same weights; last_precision says which operands ran.  A normal frame never raises a word and
     reports fp16 operands."""
@@ -383,7 +407,7 @@ def test_f16_overflow_detected_and_rerendered_in_bf16():
     d = {k: v.cuda() for k, v in inp.items()}
     torch.cuda.synchronize()
     ops.clear_f16_range_flag()  # (earlier tests may have raised the process-wide word)
-    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd)).to("cuda")
+    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd, range_check="lazy")).to("cuda")
     out = pipe(d["triangles"], d["texture"].clone(), d["mask"], d["vn"], d["c2w"], d["fov"], resolution=res)
     assert pipe.resolve(out) is False and pipe.model.range_fallbacks == 0
     assert pipe.last_precision["computed"].startswith("fp16 projection operands")
@@ -392,7 +416,7 @@ def test_f16_overflow_detected_and_rerendered_in_bf16():
     big = _overflow_sd(sd)
     ref = rf_ref.render(big, cfg, inp["triangles"], inp["texture"].clone(), inp["mask"], inp["vn"], inp["c2w"],
                         inp["fov"], resolution=res)
-    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, big)).to("cuda")
+    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, big, range_check="lazy")).to("cuda")
     tex = d["texture"].clone()
     out = pipe(d["triangles"], tex, d["mask"], d["vn"], d["c2w"], d["fov"], resolution=res)
     with pytest.warns(PrecisionWarning, match="fp16 operand overflow"):
@@ -456,7 +480,7 @@ def test_dpt_plane_overflow_falls_back_to_bf16x3():
     ref = rf_ref.render(big, cfg, inp["triangles"], inp["texture"].clone(), inp["mask"], inp["vn"], inp["c2w"],
                         inp["fov"], resolution=res)
     for operands in ("f16", "bf16"):
-        pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, big, operands=operands)).to("cuda")
+        pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, big, operands=operands, range_check="lazy")).to("cuda")
         out = pipe(d["triangles"], d["texture"].clone(), d["mask"], d["vn"], d["c2w"], d["fov"], resolution=res)
         with pytest.warns(PrecisionWarning, match="DPT plane"):
             assert pipe.resolve(out) is True
@@ -478,8 +502,8 @@ def test_overflow_isolated_between_concurrent_renders():
     big = _overflow_sd(sd)
     ref_big = rf_ref.render(big, cfg, inp["triangles"], inp["texture"].clone(), inp["mask"], inp["vn"], inp["c2w"],
                             inp["fov"], resolution=res)
-    bad = RenderFormerRenderingPipeline(RenderFormer(cfg, big)).to("cuda")
-    good = RenderFormerRenderingPipeline(RenderFormer(cfg, sd)).to("cuda")
+    bad = RenderFormerRenderingPipeline(RenderFormer(cfg, big, range_check="lazy")).to("cuda")
+    good = RenderFormerRenderingPipeline(RenderFormer(cfg, sd, range_check="lazy")).to("cuda")
     sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
     for _ in range(2):  # twice: the second round renders with the words the first one released
         with torch.cuda.stream(sa):
@@ -500,13 +524,13 @@ def test_overflow_isolated_between_concurrent_renders():
 
 
 def test_render_returns_before_the_frame_completes():
-    """render() issues the frame and returns without a host wait (the reference's render has no
-    sync inside, rendering_pipeline.py:105-125): with the stream held busy by a spin kernel queued in front, the
-    frame is still pending when render returns; resolve() then waits for it."""
+    """with the opt-in "lazy" range check render() issues the frame and returns without a host
+    wait (the reference's render has no sync inside, rendering_pipeline.py:105-125): with the stream held busy by a
+    spin kernel queued in front, the frame is still pending when render returns; resolve() then waits for it."""
     from renderformer_amd import RenderFormer, RenderFormerRenderingPipeline
     cfg, sd, inp, res, z = load_case("tiny_swin")
     d = {k: v.cuda() for k, v in inp.items()}
-    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd)).to("cuda")
+    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, sd, range_check="lazy")).to("cuda")
     out = pipe(d["triangles"], d["texture"].clone(), d["mask"], d["vn"], d["c2w"], d["fov"], resolution=res)
     pipe.resolve(out)  # warm: plans, weights, workspaces
     tex = d["texture"].clone()
@@ -521,6 +545,44 @@ def test_render_returns_before_the_frame_completes():
     print(f"render returned after {t_ret * 1e3:.1f} ms, frame complete after {t_done * 1e3:.1f} ms")
     assert pending and t_ret < 0.5 * t_done
     assert rel_l2(out.cpu(), z["hdr"]) < HDR_TOL
+
+
+def test_lazy_fallback_waits_for_frames_in_flight():
+    """in lazy mode an overflow found by a LATER render's poll rebuilds the weights while other
+    frames of the model may still run on non-default streams; the rebuild waits for them first (the old weight
+    tensors go back to the caching allocator).  Frame a completes on stream s1; frame b is held in flight on s2 by a
+    spin; frame c's render polls, resolves a (overflow -> bf16 weights) while b still runs on the old weights.
+    Every frame ends finite and within 1e-3 of the oracle."""
+    from renderformer_amd import RenderFormer, RenderFormerRenderingPipeline
+    from renderformer_amd.model import PrecisionWarning
+    cfg, sd, inp, res, z = load_case("tiny_swin")
+    d = {k: v.cuda() for k, v in inp.items()}
+    big = _overflow_sd(sd)
+    ref = rf_ref.render(big, cfg, inp["triangles"], inp["texture"].clone(), inp["mask"], inp["vn"], inp["c2w"],
+                        inp["fov"], resolution=res)
+    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, big, range_check="lazy")).to("cuda")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    args = lambda: (d["triangles"], d["texture"].clone(), d["mask"], d["vn"], d["c2w"], d["fov"])  # noqa: E731
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        a = pipe(*args(), resolution=res)
+    s1.synchronize()
+    with torch.cuda.stream(s2):
+        inb = args()
+        torch.cuda._sleep(int(5e8))  # b stays in flight while c's poll resolves a
+        b = pipe(*inb, resolution=res)
+    with pytest.warns(PrecisionWarning, match="fp16 operand overflow"):
+        with torch.cuda.stream(s1):
+            c = pipe(*args(), resolution=res)
+        assert pipe.model.range_fallbacks == 1 and pipe.model.operands == "bf16"
+        pipe.model.check_range()  # b overflowed on the old fp16 weights: re-rendered in place on s2
+    torch.cuda.synchronize()
+    for name, o in (("a", a), ("b", b), ("c", c)):
+        err = rel_l2(o.cpu(), ref)
+        print(f"frame {name}: rel L2 {err:.3e}")
+        assert torch.isfinite(o).all() and err < HDR_TOL
+    pipe.model.close()
+    assert not pipe.model._range_free and not pipe.model._range_pending
 
 
 def test_f16_overflow_deferred_check_raises():
