@@ -100,14 +100,27 @@ class StageTimes:
     def timed(self, name, fn, *a, **k):
         if not self.on:
             return fn(*a, **k)
-        t0 = time.perf_counter()
+        t0, c0 = time.perf_counter(), time.thread_time()
         try:
             return fn(*a, **k)
         finally:
             self.add(name, time.perf_counter() - t0)
+            self.add("cpu: " + name, time.thread_time() - c0)  # this thread's CPU seconds in the stage
 
     def summary(self):
         return {k: {"s": round(v, 4), "calls": self.n[k]} for k, v in sorted(self.t.items())}
+
+    def host_budget(self, frames: int, wall: float, proc_cpu: float) -> dict:
+        """CPU seconds per frame of this rank: the whole process (every thread: loader, HDF5 chunk decode pool, main,
+        writers, torch's own), and the main items — what a rank needs of the node's cores at a given frame rate."""
+        g = lambda k: self.t.get(k, 0.0) / max(frames, 1)  # noqa: E731
+        per = {"process_cpu_s": proc_cpu / max(frames, 1), "hdf5_chunk_decode_cpu_s": g("cpu: h5 chunk decode"),
+               "exr_write_cpu_s": g("cpu: write: EXR"), "png_write_cpu_s": g("cpu: write: PNG"),
+               "render_issue_cpu_s": g("cpu: main: render issue (plan + launches)")}
+        fps = frames / wall if wall > 0 else 0.0
+        return {"frames": frames, "wall_s": round(wall, 4), "frames_per_s": round(fps, 2),
+                "per_frame": {k: round(v, 5) for k, v in per.items()},
+                "cores_busy_at_this_rate": round(per["process_cpu_s"] * fps, 2)}
 
 
 STAGES = StageTimes()
@@ -290,6 +303,10 @@ def main(argv=None, pipeline=None):
         pipeline = load_pipeline(args)
     STAGES.add("main: model build (load_pipeline)", time.perf_counter() - t_build)
     t_loop = time.perf_counter()
+    cpu0 = time.process_time()  # every thread of this process (loader, chunk decode pool, main, writers)
+    if STAGES.on:
+        from renderformer_amd import h5io
+        h5io.CPU_HOOK = lambda dt: STAGES.add("cpu: h5 chunk decode", dt)
     cfg = pipeline.config
     if world > 1:
         costs = []
@@ -319,11 +336,15 @@ def main(argv=None, pipeline=None):
         for f in pending:
             STAGES.timed("main: wait for writers", f.result)  # re-raises a writer's error
         writers.shutdown()
-    STAGES.add("main: data path wall (first load -> last file)", time.perf_counter() - t_loop)
+    wall = time.perf_counter() - t_loop
+    STAGES.add("main: data path wall (first load -> last file)", wall)
     print(f"Output saved to: {output_dir} ({n_frames} frames on rank {rank}/{world})")
     if STAGES.on:
         import json
+        from renderformer_amd import h5io
+        h5io.CPU_HOOK = None
         print("stage times:", json.dumps(STAGES.summary()), flush=True)
+        print("host budget:", json.dumps(STAGES.host_budget(n_frames, wall, time.process_time() - cpu0)), flush=True)
     if args.save_video:
         print("video.mp4 not written: no mp4 encoder in this environment (frames are saved as PNG)")
     return 0

@@ -64,7 +64,7 @@ extern "C" {
 #define RF_ERR_UNSUPPORTED 3
 #define RF_ERR_DEVICE 4       /* an earlier launch reported a device-side error (see rf_device_error) */
 
-#define RF_ABI_VERSION 15
+#define RF_ABI_VERSION 16
 
 /* GEMM epilogues */
 #define RF_EPI_BF16 0       /* C(bf16)  = A W^T + bias                                   */
@@ -177,6 +177,31 @@ int rf_gemm_add_prenorm(const void* a, int64_t lda, const void* w, int64_t ldw, 
 int rf_gemm_rownorm(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int m, int n,
                     int k, int epilogue, const float* ss, int norm_dim, float eps, float* seg_ss, int seg_w,
                     int n_seg, int operand_dtype, void* workspace, int64_t ws_bytes, void* stream);
+/* Positional encoding fused into the QK path (ABI 16).  The q/k RMSNorm + rotary encoding of an attention
+ * (attention.py:127-141 q_norm / k_norm then apply_rotary_emb_*cossin, rope.py:106-149) split where each part is
+ * cheapest, with no pass over q:
+ *   - rf_gemm_qk_rope: rf_gemm_rownorm(RF_EPI_BF16) of a projection whose first n_seg segments of seg_w columns
+ *     are q (and k).  Their rows of W must be PERMUTED per 128-wide head so that column 2 m + t holds dimension
+ *     m + 64 t (the rotate-half pairs (m, m + 64) side by side; q and k permuted alike, so q.k is unchanged).  The
+ *     epilogue writes bf16 rope(norm_w * y) (norm_w in the same permuted order, NULL = no norm; segment 0 also
+ *     times q_scale) with angle m = pos[r][m / n_freqs] * freqs[m % n_freqs] for m < 9 n_freqs (else 0), and, when
+ *     norm_w is given, seg_ss[r][seg][RF_PRENORM_SLOTS] = partial sums of y^2 (y before the weight and rotation,
+ *     f32) — the norm's 1 / rms is applied downstream (RoPE and the weight are linear per row).  ss / norm_dim /
+ *     eps: the deferred pre-norm, as rf_gemm_rownorm (ss NULL: none).
+ *   - rf_row_rms_scale: x[r] *= scale / sqrt(sum of ss[r * ld_ss + 0..7] / dim + eps) in place (bf16): the keys.
+ *   - rf_attn_fwd_qn: rf_attn_fwd_dt (bf16 q/k/v) whose q rows are multiplied by q_scale / sqrt(sum of q_ss[r *
+ *     ld_ss + 0..7] / q_dim + eps) as the stream-K kernel loads them (q_scale = softmax_scale * log2 e: the kernel
+ *     runs on exp2 exponents). */
+int rf_gemm_qk_rope(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int m, int n,
+                    int k, const float* ss, int norm_dim, float eps, float* seg_ss, int seg_w, int n_seg,
+                    const float* norm_w, const float* pos, int64_t ld_pos, const float* freqs, int n_freqs,
+                    float q_scale, int operand_dtype, void* workspace, int64_t ws_bytes, void* stream);
+int rf_row_rms_scale(void* x, int64_t ldx, int rows, int dim, const float* ss, int64_t ld_ss, float eps, float scale,
+                     void* stream);
+int rf_attn_fwd_qn(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv, void* o,
+                   int64_t ldo, int o_dtype, const float* q_ss, int64_t ld_ss, int q_dim, float eps, float q_scale,
+                   const int32_t* problems, int n_problems, int n_heads, int head_dim, void* workspace,
+                   const int64_t* bounds, int grid, void* stream);
 /* rf_gemm_bf16 on the HIP engine that does nothing unless *flag != 0 (read on the device when the launch
  * runs); stream-ordered after whatever wrote the flag. */
 int rf_gemm_bf16_if(const int* flag, const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc,
@@ -488,6 +513,10 @@ typedef struct {
     int64_t gemm_ws_bytes;
     void* attn_ws;                              /* rf_attn_workspace_bytes(0, H, 0) bytes, zeroed once */
     int timer_attn;                             /* measurement: rf_ktimer_arm() before every attention launch */
+    int qk_fused;                               /* 1: every layer's w_qkv q/k rows and qk_norm are in rf_gemm_qk_rope's
+                                                   pair-interleaved order and the positional encoding runs fused into
+                                                   the QK path (rf_gemm_qk_rope + rf_row_rms_scale + rf_attn_fwd_qn);
+                                                   0: the standard layout (rf_gemm_rownorm + rf_qk_norm_rope) */
 } rf_encoder_desc;
 
 /* x[rows, dim] (f32 residual stream, row stride ldx) through the encoder stack in place: per layer

@@ -47,6 +47,10 @@ SIGNATURES = {
     "rf_prenorm": [_P, _L, _P, _P, _L, _P, _I, _I, _I, _P],
     "rf_gemm_add_prenorm": [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _P, _L, _P, _I, _P, _L, _P],
     "rf_gemm_rownorm": [_P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _I, _F, _P, _I, _I, _I, _P, _L, _P],
+    "rf_gemm_qk_rope": [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _I, _F, _P, _I, _I, _P, _P, _L, _P, _I, _F, _I, _P,
+                        _L, _P],
+    "rf_row_rms_scale": [_P, _L, _I, _I, _P, _L, _F, _F, _P],
+    "rf_attn_fwd_qn": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _P, _L, _I, _F, _F, _P, _I, _I, _I, _P, _P, _I, _P],
     "rf_qk_norm_rope": [_P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _F, _F, _P, _L, _I, _P, _I, _P],
     "rf_qk_norm_rope_groups": [_P, _L, _L, _P, _L, _L, _P, _I, _I, _I, _I, _I, _P, _L, _F, _F, _P, _L, _I, _P, _I,
                                _P],
@@ -114,7 +118,8 @@ class EncoderDesc(ctypes.Structure):
     _fields_ = [("n_layers", _I), ("rows", _I), ("dim", _I), ("n_heads", _I), ("ffn_dim", _I),
                 ("operand_dtype", _I), ("eps", _F), ("layers", _P), ("pos", _P), ("ld_pos", _L), ("freqs", _P),
                 ("n_freqs", _I), ("problems", _P), ("n_problems", _I), ("bounds", _P), ("grid", _I),
-                ("workspace", _P), ("gemm_ws", _P), ("gemm_ws_bytes", _L), ("attn_ws", _P), ("timer_attn", _I)]
+                ("workspace", _P), ("gemm_ws", _P), ("gemm_ws_bytes", _L), ("attn_ws", _P), ("timer_attn", _I),
+                ("qk_fused", _I)]
 
 
 class DecoderLayer(ctypes.Structure):

@@ -95,6 +95,10 @@ struct AttnArgs {
     const float* qk_w;
     float qk_eps, qk_scale;
     int qk_dim;
+    // stream-K kernel (rf_attn_fwd_qn): q arrives normed-by-weight and rotated (rf_gemm_qk_rope) but not divided by
+    // its rms: row r of q is multiplied by qk_scale / sqrt(sum_{s < 8} qk_ss[r * qk_ld + s] / qk_dim + qk_eps) when
+    // the piece loads it (qk_ss null: q already final)
+    int64_t qk_ld;
 };
 
 // two f32 -> the 16-bit output pair: fp16 (OF16) or bf16, RNE
@@ -806,6 +810,7 @@ constexpr int QB5 = NW5 * 32;
 constexpr int K5 = 0;                  // K ring: 2 x 16 KiB
 constexpr int V5 = 2 * TILE_BYTES;     // V ring: 2 x 16 KiB
 constexpr int Q5 = 4 * TILE_BYTES;     // Q image of a piece: 8 waves x 8 KiB (attn_sk_kernel)
+constexpr int QS5 = Q5 + 8 * 8192;     // the piece's q row sums (rf_attn_fwd_qn): 8 waves x 32 rows x 32 B
 constexpr int SK5_MAX_GRID = 512;
 static_assert(KT == rf::ATTN_KT && QB5 == rf::ATTN_QB && SK5_MAX_GRID == rf::ATTN_MAX_GRID,
               "attn_sched.cpp prices the kernel's geometry");
@@ -843,6 +848,27 @@ RF_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
                                                       0, 0);
     else
         return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// DBG & 2048 (study build, timing only): every v_mfma_f32_32x32x16 of the tile loop replaced by two
+// v_mfma_f32_16x16x32 on the same operand registers into two 4-register slices of its accumulator — the same FLOP
+// and the same VALU / LDS work per tile, issued in the 16x16x32 shape: a probe of that shape's clock and issue cost
+// in this loop (MI355X_MICROARCH "DVFS give-back" item 7) before building the full 16x16x32 kernel.  Garbage results.
+template <bool F16>
+RF_DEV f32x16 mfma16x2(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+    f32x4 lo = {c[0], c[1], c[2], c[3]}, hi = {c[4], c[5], c[6], c[7]};
+    if constexpr (F16) {
+        lo = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), lo, 0, 0,
+                                                   0);
+        hi = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), hi, 0, 0,
+                                                   0);
+    } else {
+        lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, lo, 0, 0, 0);
+        hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, hi, 0, 0, 0);
+    }
+    f32x16 r = c;
+    r[0] = lo[0], r[1] = lo[1], r[2] = lo[2], r[3] = lo[3];
+    r[4] = hi[0], r[5] = hi[1], r[6] = hi[2], r[7] = hi[3];
+    return r;
 }
 // dword w (0..3) of an MFMA bf16x8 operand
 RF_DEV void set_pk(bf16x8& f, int w, uint32_t v) {
@@ -889,7 +915,7 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
     constexpr auto x_blk = [](int x) { return x >> 4; };
     constexpr auto x_sp = [](int x) { return (x >> 3) & 1; };
     // K ring, V ring (2 x 16 KiB each), then the Q image of the next piece (8 waves x 8 KiB)
-    __shared__ __attribute__((aligned(16))) char smem[Q5 + QB5 * HD * 2];  // 128 KiB
+    __shared__ __attribute__((aligned(16))) char smem[QS5 + NW5 * 1024];  // 136 KiB
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1015,6 +1041,11 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
             const uint32_t d0 = __builtin_amdgcn_readfirstlane(lds0 + Q5 + wave * 8192);
 #pragma unroll
             for (int st = 0; st < 8; ++st) dma_piece(src + 16 * st, d0 + 1024 * st);
+            if (p.qk_ss) {  // lane l: 16 B (4 of the 8 slots) of row l >> 1 of the wave's 32 rows, lane-linear in LDS
+                const int srow = q_start + min(q0 + wave * 32 + (opaque(lane) >> 1), q1 - 1);
+                const float* ssrc = p.qk_ss + (int64_t)srow * p.qk_ld + 4 * (lane & 1);
+                dma_piece(reinterpret_cast<const bf16_t*>(ssrc), __builtin_amdgcn_readfirstlane(lds0 + QS5 + wave * 1024));
+            }
         }
         kp = p.k + (int64_t)(k_start + kt0 * KT + d_row) * p.ldk + hoff + 8 * d_ch;
         vp = p.v + (int64_t)(v_start + kt0 * KT + d_row) * p.ldv + hoff + 8 * d_ch;
@@ -1053,6 +1084,20 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
 #pragma unroll
         for (int st = 0; st < 8; ++st)
             qf[st] = *reinterpret_cast<const bf16x8*>(smem + Q5 + wave * 8192 + 1024 * st + 16 * lane);
+        if (p.qk_ss) {  // the q norm's 1 / rms (and the softmax scale) of this lane's query row, folded into its Q
+            const char* sp = smem + QS5 + wave * 1024 + 32 * (lane & 31);
+            const f32x4 a0 = *reinterpret_cast<const f32x4*>(sp), a1 = *reinterpret_cast<const f32x4*>(sp + 16);
+            const float sum = ((a0[0] + a0[1]) + (a0[2] + a0[3])) + ((a1[0] + a1[1]) + (a1[2] + a1[3]));
+            const float f = p.qk_scale / sqrtf(sum / (float)p.qk_dim + p.qk_eps);
+#pragma unroll
+            for (int st = 0; st < 8; ++st) {
+                u32x4 u = __builtin_bit_cast(u32x4, qf[st]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    u[e] = cvt_pk_bf16(__uint_as_float(u[e] << 16) * f, __uint_as_float(u[e] & 0xffff0000u) * f);
+                qf[st] = __builtin_bit_cast(bf16x8, u);
+            }
+        }
         f32x16 o[4];
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
@@ -1185,7 +1230,10 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                     if (st == 0) sn[b] = minit;
                     asm volatile("" : "+v"(kf[j % 3]));
                 } else {
-                    sn[b] = mfma32<IF16>(kf[j % 3], qf[st], st == 0 ? minit : sn[b]);
+                    if constexpr (DBG & 2048)
+                        sn[b] = mfma16x2<IF16>(kf[j % 3], qf[st], st == 0 ? minit : sn[b]);
+                    else
+                        sn[b] = mfma32<IF16>(kf[j % 3], qf[st], st == 0 ? minit : sn[b]);
                 }
                 if (!SPLIT || j < 8) {
                     float e[2];
@@ -1268,7 +1316,10 @@ __global__ __launch_bounds__(NW5 * 64, 1) void attn_sk_kernel(AttnArgs p) {
                 if constexpr (DBG & 4) {
                     asm volatile("" : "+v"(vf[j % 3]), "+v"(pf[b][sp]));
                 } else {
-                    o[dt] = mfma32<IF16>(vf[j % 3], pf[b][sp], o[dt]);
+                    if constexpr (DBG & 2048)
+                        o[dt] = mfma16x2<IF16>(vf[j % 3], pf[b][sp], o[dt]);
+                    else
+                        o[dt] = mfma32<IF16>(vf[j % 3], pf[b][sp], o[dt]);
                 }
                 if (SPLIT && j < 8) {
                     float e[2];
@@ -2035,6 +2086,7 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
 #endif  // RF_STUDY
 
 constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2F = 0.69314718055994530942f;
 
 int cu_count() {  // per-device, queried once
     static int cache[64] = {0};
@@ -2048,10 +2100,17 @@ int cu_count() {  // per-device, queried once
     return cache[dev];
 }
 
+struct QNorm {  // rf_attn_fwd_qn's q row scale (AttnArgs::qk_ss ...)
+    const float* ss = nullptr;
+    int64_t ld = 0;
+    int dim = 0;
+    float eps = 0.f, scale = 1.f;
+};
+
 int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv, void* o,
                    int64_t ldo, const int32_t* problems, int n_problems, int n_heads, float scale, void* workspace,
                    void* stream, const int64_t* bounds = nullptr, int grid = 0, bool o_f16 = false,
-                   bool i_f16 = false) {
+                   bool i_f16 = false, const QNorm* qn = nullptr) {
     RF_REQUIRE(workspace, "rf_attn_fwd: stream-K mode needs the workspace (rf_attn_workspace_bytes(0, H, 0))");
     if (!bounds) {
         grid = cu_count();
@@ -2078,6 +2137,13 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
     a.range = o_f16 ? rf::range_word() : nullptr;
     a.ascend = getenv("RF_SK_ASCEND") && atoi(getenv("RF_SK_ASCEND")) == 1;
     a.bounds = bounds;
+    if (qn && qn->ss) {
+        a.qk_ss = qn->ss;
+        a.qk_ld = qn->ld;
+        a.qk_dim = qn->dim;
+        a.qk_eps = qn->eps;
+        a.qk_scale = qn->scale;
+    }
     if (!bounds) {  // equal split per XCD group, written on the device ahead of the launch (stream-ordered)
         int64_t* eq = (int64_t*)(a.flag + SK5_MAX_GRID);
         RF_LAUNCH(attn_equal_bounds_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a, grid, eq);
@@ -2132,7 +2198,10 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
         case 16: RF_LAUNCH((attn_sk_kernel<true, 16>), g, b, 0, st, a); break;
         case 20: RF_LAUNCH((attn_sk_kernel<true, 20>), g, b, 0, st, a); break;
         case 11: RF_LAUNCH((attn_sk_kernel<true, 11>), g, b, 0, st, a); break;
-        case 32: RF_LAUNCH((attn_sk_kernel<true, 32>), g, b, 0, st, a); break;
+        case 32:  // stamps on the output format asked for (fp16 O: the frame's instantiation)
+            if (o_f16) RF_LAUNCH((attn_sk_kernel<true, 32, true>), g, b, 0, st, a);
+            else RF_LAUNCH((attn_sk_kernel<true, 32>), g, b, 0, st, a);
+            break;
         case 64: RF_LAUNCH((attn_sk_kernel<true, 64>), g, b, 0, st, a); break;
         case 96: RF_LAUNCH((attn_sk_kernel<true, 96>), g, b, 0, st, a); break;
         case 128: RF_LAUNCH((attn_sk_kernel<true, 128>), g, b, 0, st, a); break;
@@ -2141,6 +2210,14 @@ int attn_sk_launch(const void* q, int64_t ldq, const void* k, int64_t ldk, const
         case 288: RF_LAUNCH((attn_sk_kernel<true, 288>), g, b, 0, st, a); break;
         case 384: RF_LAUNCH((attn_sk_kernel<true, 384>), g, b, 0, st, a); break;
         case 512: RF_LAUNCH((attn_sk_kernel<true, 512>), g, b, 0, st, a); break;
+        case 2048:  // the 16x16x32 shape probe (o_f16 as the frame's instantiation)
+            if (o_f16) RF_LAUNCH((attn_sk_kernel<true, 2048, true>), g, b, 0, st, a);
+            else RF_LAUNCH((attn_sk_kernel<true, 2048>), g, b, 0, st, a);
+            break;
+        case 2080:  // the probe with the per-segment stamps and the in-kernel clock (DBG & 32)
+            if (o_f16) RF_LAUNCH((attn_sk_kernel<true, 2080, true>), g, b, 0, st, a);
+            else RF_LAUNCH((attn_sk_kernel<true, 2080>), g, b, 0, st, a);
+            break;
         case 1024:  // (correct results: the per-tile C-operand rebuild, A/B against the default)
             if (o_f16) RF_LAUNCH((attn_sk_kernel<true, 1024, true>), g, b, 0, st, a);
             else RF_LAUNCH((attn_sk_kernel<true, 1024>), g, b, 0, st, a);
@@ -2253,6 +2330,29 @@ extern "C" int rf_attn_fwd_dt(const void* q, int64_t ldq, const void* k, int64_t
     if (n_problems <= 0) return RF_OK;
     return attn_sk_launch(q, ldq, k, ldk, v, ldv, o, ldo, problems, n_problems, n_heads, scale, workspace, stream,
                           bounds, bounds ? grid : 0, o_dtype == RF_DT_F16, qkv_dtype == RF_DT_F16);
+}
+
+extern "C" int rf_attn_fwd_qn(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                              void* o, int64_t ldo, int o_dtype, const float* q_ss, int64_t ld_ss, int q_dim, float eps,
+                              float q_scale, const int32_t* problems, int n_problems, int n_heads, int head_dim,
+                              void* workspace, const int64_t* bounds, int grid, void* stream) {
+    RF_REQUIRE(q && k && v && o && problems && workspace && q_ss, "rf_attn_fwd_qn: null pointer");
+    RF_REQUIRE(head_dim == HD, "rf_attn_fwd_qn: head_dim must be 128 (got %d)", head_dim);
+    RF_REQUIRE(o_dtype == RF_DT_BF16 || o_dtype == RF_DT_F16, "rf_attn_fwd_qn: o_dtype must be RF_DT_BF16/F16");
+    RF_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0, "rf_attn_fwd_qn: strides must be 16-B aligned");
+    RF_REQUIRE(((uintptr_t)q_ss & 15) == 0 && ld_ss >= 8 && ld_ss % 4 == 0 && q_dim > 0,
+               "rf_attn_fwd_qn: q_ss rows of >= 8 partial sums, 16-B aligned");
+    RF_REQUIRE(n_heads >= 1, "rf_attn_fwd_qn: n_heads must be >= 1");
+    if (n_problems <= 0) return RF_OK;
+    QNorm qn;
+    qn.ss = q_ss;
+    qn.ld = ld_ss;
+    qn.dim = q_dim;
+    qn.eps = eps;
+    qn.scale = q_scale;
+    // q_scale carries softmax_scale * log2(e): the kernel runs on exp2 exponents (scale = ln 2)
+    return attn_sk_launch(q, ldq, k, ldk, v, ldv, o, ldo, problems, n_problems, n_heads, LN2F, workspace, stream,
+                          bounds, bounds ? grid : 0, o_dtype == RF_DT_F16, false, &qn);
 }
 
 extern "C" int64_t rf_attn_workspace_bytes(int64_t rows, int n_heads, int n_split) {

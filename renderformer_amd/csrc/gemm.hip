@@ -37,7 +37,10 @@ namespace {
 constexpr int BK = 32;
 constexpr int P_F16 = 2;  // NTERM value of the fp16-operand mode
 
-enum Epi { E_BF16 = RF_EPI_BF16, E_F32 = RF_EPI_F32, E_ADD = RF_EPI_ADD_F32, E_SWIGLU = RF_EPI_SWIGLU, E_CONV = 16 };
+// E_ROPE (rf_gemm_qk_rope): E_BF16 whose q/k column segments get the attention's q/k norm weight and rotary position
+// encoding applied in the epilogue (and per-row partial sums of squares for the norm's 1 / rms, applied downstream)
+enum Epi { E_BF16 = RF_EPI_BF16, E_F32 = RF_EPI_F32, E_ADD = RF_EPI_ADD_F32, E_SWIGLU = RF_EPI_SWIGLU, E_CONV = 16,
+           E_ROPE = 17 };
 
 // Tile configuration: BM x BN block tile, WGM x WGN waves (each (BM/WGM) x (BN/WGN)), S-deep LDS ring of
 // K-steps of KH x 32 (KH = 2: a 64-deep step staged as two 32-deep planes, half the barriers per K).
@@ -117,6 +120,16 @@ struct EngineArgs {
     // values, seg_ss[row][s][slot], slot = (n0 % seg_w) / BN (the segment's first tile zeroes the unused slots)
     float* seg_ss;
     int seg_w, seg_n;
+    // E_ROPE (rf_gemm_qk_rope): the q/k segments' rotary encoding, in the pair-interleaved column order of the
+    // permuted projection rows (per head, column 2 m + t holds dimension m + 64 t): angle of pair m of row r =
+    // rope_pos[r * rope_ld + m / rope_nf] * rope_freqs[m % rope_nf] for m < 9 rope_nf (else 0); rope_g: the
+    // segments' norm weights in the same order (null: no norm, and no sums); segment 0 also times rope_qscale
+    const float* rope_pos;
+    int64_t rope_ld;
+    const float* rope_freqs;
+    int rope_nf;
+    const float* rope_g;
+    float rope_qscale;
 };
 
 constexpr int PN_SLOTS = RF_PRENORM_SLOTS;  // partial sums per row (N <= PN_SLOTS x the narrowest BN, 128)
@@ -453,9 +466,14 @@ RF_DEV void lds_sync() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// E_ROPE's staged positions: [BM][9] floats by 256-B LDS-DMA pieces (one dword a lane), so the area is whole pieces
+template <class C>
+constexpr int ROPE_POS_BYTES = (C::BM * 9 + 63) / 64 * 256;
 template <class C, int EPI>
 constexpr int PN_AREA = EPI == E_ADD      ? C::BN * 4 + C::BM * C::WGN * 4
                         : EPI == E_BF16   ? C::BM * PN_SLOTS * 4 + C::BM * C::WGN * 4
+                        // E_ROPE: + the q/k norm weights of the tile's columns, the tile rows' positions, the frequencies
+                        : EPI == E_ROPE   ? C::BM * PN_SLOTS * 4 + C::BM * C::WGN * 4 + C::BN * 4 + ROPE_POS_BYTES<C> + 64 * 4
                         : EPI == E_SWIGLU ? C::BM * PN_SLOTS * 4
                                           : 0;
 
@@ -467,13 +485,35 @@ RF_DEV void pn_issue(const EngineArgs& p, char* area, int m0, int n0) {
     if constexpr (EPI == E_ADD) {
         if (p.xg && wave == 0 && n0 + 4 * lane < p.n && 4 * lane < C::BN)  // 16 B (4 columns of g) a lane
             __builtin_amdgcn_global_load_lds(GLB_PTR(void, p.norm_g + n0 + 4 * lane), LDS_PTR(void, area), 16, 0, 0);
-    } else if constexpr (EPI == E_BF16 || EPI == E_SWIGLU) {
+    } else if constexpr (EPI == E_BF16 || EPI == E_SWIGLU || EPI == E_ROPE) {
         if (p.rs_part) {
             static_assert(C::BM % 32 == 0, "1-KiB pieces of 32 rows");
             for (int c = wave; c < C::BM / 32; c += C::NWAVE) {  // piece c: rows 32 c .. 32 c + 31, 2 lanes a row
                 const int row = min(m0 + 32 * c + (lane >> 1), p.m - 1);
                 __builtin_amdgcn_global_load_lds(GLB_PTR(void, p.rs_part + (int64_t)row * PN_SLOTS + 4 * (lane & 1)),
                                                  LDS_PTR(void, area + c * 1024), 16, 0, 0);
+            }
+        }
+        if constexpr (EPI == E_ROPE) {
+            if (n0 / p.seg_w < p.seg_n) {  // a q/k tile: its norm weights, the rows' positions, the frequencies
+                char* const gl = area + C::BM * PN_SLOTS * 4 + C::BM * C::WGN * 4;
+                char* const pl = gl + C::BN * 4;
+                char* const fl = pl + ROPE_POS_BYTES<C>;  // (the last pos piece runs past BM * 9 floats)
+                if (wave == 0 && p.rope_g && 4 * lane < C::BN)  // 16 B (4 columns) a lane
+                    __builtin_amdgcn_global_load_lds(GLB_PTR(void, p.rope_g + n0 + 4 * lane), LDS_PTR(void, gl), 16, 0, 0);
+                if (p.rope_pos) {
+                    if (wave == C::NWAVE - 1)
+                        __builtin_amdgcn_global_load_lds(GLB_PTR(void, p.rope_freqs + min(lane, p.rope_nf - 1)),
+                                                         LDS_PTR(void, fl), 4, 0, 0);
+                    // pos[m0 .. m0 + BM)[0..8] as [BM][9] floats, one dword a lane (rows of 9 floats are not 16-B aligned)
+                    for (int c = wave; c * 64 < C::BM * 9; c += C::NWAVE) {
+                        const int e = c * 64 + lane;
+                        const int r = e / 9, col = e - r * 9;
+                        const int row = min(m0 + min(r, C::BM - 1), p.m - 1);
+                        __builtin_amdgcn_global_load_lds(GLB_PTR(void, p.rope_pos + (int64_t)row * p.rope_ld + col),
+                                                         LDS_PTR(void, pl + c * 256), 4, 0, 0);
+                    }
+                }
             }
         }
     }
@@ -502,8 +542,8 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
     // deferred RMSNorm consumer: 1 / rms of each row, one thread per row from its slot sums in slot order (unused
     // slots hold +0, so any producer tiling gives its partials' exact sum), kept in slot 0 of the row's LDS entry;
     // the stores below read it per row (no per-lane array across the epilogue: the 256-row tiles are at 256 VGPRs)
-    const bool rsc = (EPI == E_SWIGLU || EPI == E_BF16) && p.rs_part && area;
-    if constexpr (EPI == E_SWIGLU || EPI == E_BF16) {
+    const bool rsc = (EPI == E_SWIGLU || EPI == E_BF16 || EPI == E_ROPE) && p.rs_part && area;
+    if constexpr (EPI == E_SWIGLU || EPI == E_BF16 || EPI == E_ROPE) {
         if (rsc) {
             lds_sync();  // the staged rows are visible (their DMA was waited for inside the main loop)
             for (int t = threadIdx.x; t < C::BM; t += C::THREADS) {
@@ -715,13 +755,44 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
         // deferred-RMSNorm producer (E_ADD with p.xg): per-lane partial sums of x^2 of the lane's rows
         const bool pre = EPI == E_ADD && p.xg && area;
         // q/k segment sums of the written values (E_BF16 with seg_ss): this tile's segment, if it is one of them
-        const bool segq = EPI == E_BF16 && p.seg_ss && area && n0 / p.seg_w < p.seg_n;
+        // (E_ROPE: of the projection's values before the norm weight and the rotation, in f32)
+        const bool qkseg = EPI == E_ROPE && n0 / p.seg_w < p.seg_n;  // tile-uniform (seg_w is a multiple of BN)
+        const bool segq = (EPI == E_BF16 || (EPI == E_ROPE && qkseg)) && p.seg_ss && area && n0 / p.seg_w < p.seg_n;
         // row-sum scratch: after g of the tile's columns (producer) / after the staged ss rows (consumer)
         char* const red = area + (EPI == E_ADD ? C::BN * 4 : C::BM * PN_SLOTS * 4);
         if (pre) lds_sync();  // g staged (pn_issue) and visible
         float ssr[TI];
 #pragma unroll
         for (int i = 0; i < TI; ++i) ssr[i] = 0.f;
+        // E_ROPE: the rotation's operands were staged in LDS before the main loop (pn_issue: a global load here would
+        // wait behind the stores of earlier fragments, vmcnt counting both in issue order).  Per lane and column
+        // fragment j the 4 columns cq..cq + 3 are rotation pairs m0 = (col % 128) / 2 and m0 + 1: angle = pos[row][pc]
+        // * freq (pc, freq per (j, t) here; the position per row in the loop).
+        const char* const gl = area + C::BM * PN_SLOTS * 4 + C::BM * C::WGN * 4;
+        const float* const pl = reinterpret_cast<const float*>(gl + C::BN * 4);
+        float frq[EPI == E_ROPE ? TJ : 1][2];
+        int pcol[EPI == E_ROPE ? TJ : 1][2];
+        float sscale = 1.f;
+        if constexpr (EPI == E_ROPE) {
+            if (qkseg) {
+                if (!rsc) lds_sync();  // (the staged area is visible: rsc already synchronised)
+                sscale = n0 / p.seg_w == 0 ? p.rope_qscale : 1.f;
+                const int lim = 9 * p.rope_nf;
+                const float* fl = pl + ROPE_POS_BYTES<C> / 4;
+#pragma unroll
+                for (int j = 0; j < TJ; ++j) {
+                    const int col = cbase + j * 16 + cq;
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const int m = ((col & 127) >> 1) + t;
+                        const bool on = p.rope_pos && m < lim;
+                        const int pc = on ? m / p.rope_nf : 0;
+                        frq[j][t] = on ? fl[m - pc * p.rope_nf] : 0.f;
+                        pcol[j][t] = pc;
+                    }
+                }
+            }
+        }
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
             const int row = rbase + i * 16 + rl;
@@ -740,7 +811,25 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
                     v[3] += b.w;
                 }
                 const int64_t o = (int64_t)row * p.ldc + col;
-                if constexpr (EPI == E_BF16) {
+                if constexpr (EPI == E_ROPE) {
+                    if (qkseg) {
+                        if (segq) ssr[i] += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+                        const f32x4 g = p.rope_g ? *reinterpret_cast<const f32x4*>(gl + (col - n0) * 4)
+                                                 : f32x4{1.f, 1.f, 1.f, 1.f};
+                        const float z0 = v[0] * g[0], z1 = v[1] * g[1], z2 = v[2] * g[2], z3 = v[3] * g[3];
+                        const float* prow = pl + (wm * C::MW + i * 16 + rl) * 9;
+                        float s0, c0, s1, c1;
+                        __sincosf(prow[pcol[j][0]] * frq[j][0], &s0, &c0);
+                        __sincosf(prow[pcol[j][1]] * frq[j][1], &s1, &c1);
+                        // rotate_half on the (m, m + 64) pair, stored interleaved (rope.py:106-149)
+                        v[0] = (z0 * c0 - z1 * s0) * sscale;
+                        v[1] = (z1 * c0 + z0 * s0) * sscale;
+                        v[2] = (z2 * c1 - z3 * s1) * sscale;
+                        v[3] = (z3 * c1 + z2 * s1) * sscale;
+                    }
+                    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.c) + o) =
+                        make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+                } else if constexpr (EPI == E_BF16) {
                     amax = amax3(amax3(amax, v[0], v[1]), v[2], v[3]);
                     const uint32_t lo = pack16(p, v[0], v[1]), hi = pack16(p, v[2], v[3]);
                     *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.c) + o) = make_uint2(lo, hi);
@@ -765,7 +854,7 @@ RF_DEV void engine_epilogue(const EngineArgs& p, int m0, int n0, const f32x4 (&a
         }
         if constexpr (EPI == E_BF16)
             if (p.range && !f16_in_range(amax)) report_f16_range(p.range, RF_RANGE_GEMM);
-        if constexpr (EPI == E_ADD || EPI == E_BF16) {
+        if constexpr (EPI == E_ADD || EPI == E_BF16 || EPI == E_ROPE) {
             if (pre && p.xg_f16 && p.range && !f16_in_range(amax)) report_f16_range(p.range, RF_RANGE_RMSNORM);
             if (pre || segq) {
                 // row sums: the 4 lane groups of a row (lanes l, l ^ 16, l ^ 32, l ^ 48), then the WGN waves of
@@ -3384,13 +3473,22 @@ bool persist_on() {
     return on;
 }
 
+// A tile count that is not a whole number of 256-block rounds (the stage-1 SwiGLU W13: 736 tiles) runs one block per
+// tile by default: the persistent kernel's last round is as ragged as the hardware dispatcher's, and its cross-tile
+// prefetch costs registers (phased_sk_kernel spills at 256 VGPRs, phased_kernel<256> does not).  RF_GEMM_PERSIST_RAGGED=1
+// restores the persistent launch there (A/B: profiles/r6_w13_persist_ab.txt).
+bool persist_ragged() {
+    static const bool on = getenv("RF_GEMM_PERSIST_RAGGED") && atoi(getenv("RF_GEMM_PERSIST_RAGGED")) != 0;
+    return on;
+}
+
 template <int EPI, int NTERM, bool GATHER, int BM = 256>
 int launch_phased(EngineArgs a, void* stream, const char* what) {
     const int tiles_m = (a.m + BM - 1) / BM, tiles_n = a.n / 256;
     const int nwg = tiles_n * tiles_m;
     a.group_m = pick_group_m(tiles_m, tiles_n, BM, 256, (nwg + 7) / 8);
     if constexpr (BM == 256 && (NTERM == 1 || NTERM == P_F16) && !GATHER) {
-        if (nwg > 256 && persist_on()) {
+        if (nwg > 256 && persist_on() && (nwg % 256 == 0 || persist_ragged())) {
             a.persist = 1;
             RF_LAUNCH((phased_sk_kernel<EPI, NTERM>), dim3(256), dim3(512), 0, (hipStream_t)stream, a);
             return rf::check_launch(what);
@@ -3809,6 +3907,64 @@ extern "C" int rf_gemm_rownorm(const void* a, int64_t lda, const void* w, int64_
     nio.seg_n = seg_ss ? n_seg : 0;
     return gemm_bf16(a, lda, w, ldw, c, ldc, nullptr, m, n, k, epilogue, workspace, ws_bytes, stream, nullptr,
                      operand_dtype == RF_DT_F16, &nio);
+}
+
+// rf_gemm_qk_rope (rf.h): the q/k/v projection with the attention's q/k norm weight and rotary encoding in the
+// epilogue (E_ROPE) on the engine's 96x256 or 8-wave 128x128 tile (the tiles the cost model picks for these shapes).
+template <class C, int NT>
+static int launch_rope(EngineArgs p, void* stream) {
+    return launch<C, E_ROPE, NT>(p, stream, "rf_gemm_qk_rope");
+}
+
+extern "C" int rf_gemm_qk_rope(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int m,
+                               int n, int k, const float* ss, int norm_dim, float eps, float* seg_ss, int seg_w,
+                               int n_seg, const float* norm_w, const float* pos, int64_t ld_pos, const float* freqs,
+                               int n_freqs, float q_scale, int operand_dtype, void* workspace, int64_t ws_bytes,
+                               void* stream) {
+    (void)workspace;
+    (void)ws_bytes;
+    RF_REQUIRE(a && w && c, "rf_gemm_qk_rope: null pointer");
+    RF_REQUIRE(m > 0 && n > 0 && k > 0, "rf_gemm_qk_rope: empty problem m=%d n=%d k=%d", m, n, k);
+    RF_REQUIRE(operand_dtype == RF_DT_F16 || operand_dtype == RF_DT_BF16, "rf_gemm_qk_rope: operand_dtype");
+    RF_REQUIRE(k % 64 == 0 && n % 128 == 0, "rf_gemm_qk_rope: needs K %% 64 == 0 and N %% 128 == 0");
+    RF_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && lda >= k && ldw >= k && ((uintptr_t)a & 15) == 0 &&
+                   ((uintptr_t)w & 15) == 0, "rf_gemm_qk_rope: operands must be 16-B aligned with lda/ldw >= K");
+    RF_REQUIRE(ldc >= n && ldc % 4 == 0 && ((uintptr_t)c & 7) == 0, "rf_gemm_qk_rope: ldc too small/unaligned");
+    RF_REQUIRE(seg_w > 0 && seg_w % 256 == 0 && seg_w % 128 == 0 && n_seg >= 1 && (int64_t)seg_w * n_seg <= n,
+               "rf_gemm_qk_rope: the q/k segments must be whole 256-column tiles inside N");
+    RF_REQUIRE(!seg_ss || (((uintptr_t)seg_ss & 15) == 0 && seg_w <= PN_SLOTS * 128),
+               "rf_gemm_qk_rope: seg_ss must be 16-B aligned and seg_w <= %d", PN_SLOTS * 128);
+    RF_REQUIRE(!ss || (((uintptr_t)ss & 15) == 0 && norm_dim > 0), "rf_gemm_qk_rope: ss must be 16-B aligned");
+    RF_REQUIRE(!norm_w || ((uintptr_t)norm_w & 15) == 0, "rf_gemm_qk_rope: norm_w must be 16-B aligned");
+    RF_REQUIRE(!pos || (freqs && n_freqs > 0 && 9 * n_freqs <= 64 && ld_pos >= 9),
+               "rf_gemm_qk_rope: pos needs freqs with 9 * n_freqs <= 64 and ld_pos >= 9");
+    EngineArgs p{};
+    p.a = (const bf16_t*)a;
+    p.lda = lda;
+    p.w = (const bf16_t*)w;
+    p.ldw = ldw;
+    p.m = m;
+    p.n = n;
+    p.k = k;
+    p.c = c;
+    p.ldc = ldc;
+    p.rs_part = ss;
+    p.rs_n = (float)norm_dim;
+    p.rs_eps = eps;
+    p.seg_ss = norm_w ? seg_ss : nullptr;  // (no norm: no 1 / rms downstream, no sums)
+    p.seg_w = seg_w;
+    p.seg_n = n_seg;
+    p.rope_pos = pos;
+    p.rope_ld = ld_pos;
+    p.rope_freqs = freqs;
+    p.rope_nf = pos ? n_freqs : 1;
+    p.rope_g = norm_w;
+    p.rope_qscale = q_scale;
+    const bool f16 = operand_dtype == RF_DT_F16;
+    const int cfg = pick_cfg(m, n, k, RF_EPI_BF16);
+    const bool t96 = n % 256 == 0 && (cfg == 962 || cfg != 12884);
+    if (t96) return f16 ? launch_rope<T96x256, P_F16>(p, stream) : launch_rope<T96x256, 1>(p, stream);
+    return f16 ? launch_rope<T128w8k2s4, P_F16>(p, stream) : launch_rope<T128w8k2s4, 1>(p, stream);
 }
 
 extern "C" int rf_gemm_bf16_if(const int* flag, const void* a, int64_t lda, const void* w, int64_t ldw, void* c,

@@ -623,3 +623,51 @@ extern "C" int rf_embed(float* out, int64_t ldo, const int32_t* out_rows, int ro
 #undef RF_EMB
     return rf::check_launch("rf_embed");
 }
+
+// ----------------------------------------------------------------------------- row RMS scale (rf.h)
+// x[r][0:dim] *= scale / sqrt(sum_{s < 8} ss[r * ld_ss + s] / dim + eps), bf16 in place: the keys' 1 / rms after
+// rf_gemm_qk_rope (which applied the norm weight and the rotation in its epilogue and wrote the row's partial sums
+// of squares).  One row per wave, every load of the row issued before any use (one round trip).
+template <int UPL>
+__global__ __launch_bounds__(256) void row_rms_scale_kernel(bf16_t* x, int64_t ldx, int rows, int dim,
+                                                            const float* __restrict__ ss, int64_t ld_ss, float eps,
+                                                            float scale) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    bf16_t* r = x + (int64_t)row * ldx;
+    u32x4 v[UPL];
+#pragma unroll
+    for (int u = 0; u < UPL; ++u)
+        if (8 * (lane + 64 * u) < dim) v[u] = *reinterpret_cast<const u32x4*>(r + 8 * (lane + 64 * u));
+    const float part = lane < 8 ? ss[(int64_t)row * ld_ss + lane] : 0.f;
+    const float f = scale / sqrtf(wave_sum(part) / (float)dim + eps);
+#pragma unroll
+    for (int u = 0; u < UPL; ++u) {
+        if (8 * (lane + 64 * u) < dim) {
+            u32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                o[e] = pack_bf16x2(__uint_as_float(v[u][e] << 16) * f, __uint_as_float(v[u][e] & 0xffff0000u) * f);
+            *reinterpret_cast<u32x4*>(r + 8 * (lane + 64 * u)) = o;
+        }
+    }
+}
+
+extern "C" int rf_row_rms_scale(void* x, int64_t ldx, int rows, int dim, const float* ss, int64_t ld_ss, float eps,
+                                float scale, void* stream) {
+    RF_REQUIRE(x && ss, "rf_row_rms_scale: null pointer");
+    RF_REQUIRE(dim > 0 && dim % 8 == 0 && dim <= 4 * 512 && ldx >= dim && ldx % 8 == 0 && ((uintptr_t)x & 15) == 0,
+               "rf_row_rms_scale: dim must be a multiple of 8 up to 2048 with 16-B aligned rows");
+    RF_REQUIRE(ld_ss >= 8, "rf_row_rms_scale: ld_ss must be >= 8 (RF_PRENORM_SLOTS partial sums a row)");
+    if (rows <= 0) return RF_OK;
+    const int blocks = (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
+    hipStream_t st = (hipStream_t)stream;
+    if (dim <= 512)
+        RF_LAUNCH(row_rms_scale_kernel<1>, dim3(blocks), dim3(256), 0, st, (bf16_t*)x, ldx, rows, dim, ss, ld_ss, eps, scale);
+    else if (dim <= 1024)
+        RF_LAUNCH(row_rms_scale_kernel<2>, dim3(blocks), dim3(256), 0, st, (bf16_t*)x, ldx, rows, dim, ss, ld_ss, eps, scale);
+    else
+        RF_LAUNCH(row_rms_scale_kernel<4>, dim3(blocks), dim3(256), 0, st, (bf16_t*)x, ldx, rows, dim, ss, ld_ss, eps, scale);
+    return rf::check_launch("rf_row_rms_scale");
+}

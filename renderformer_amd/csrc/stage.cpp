@@ -4,7 +4,8 @@
 // AttentionLayer.forward (:484-527): pre-norm multi-head self-attention with full-width q/k RMSNorm and the
 // triangle RoPE (MultiHeadAttention :115-202, rope.py:106-149) and the SwiGLU FFN (:51-57), both residual.  It is
 // host code only: it issues the library's own unit entry points (rf_prenorm, rf_gemm_add_prenorm, rf_gemm_rownorm,
-// rf_gemm_*, rf_qk_norm_rope, rf_attn_fwd_dt) on the caller's stream in exactly the order model.py::_stage1 does,
+// rf_gemm_*, rf_qk_norm_rope, rf_attn_fwd_dt, or with qk_fused rf_gemm_qk_rope, rf_row_rms_scale, rf_attn_fwd_qn) on
+// the caller's stream in exactly the order model.py::_stage1 does,
 // so a stack run through here is bit-identical to the Python-orchestrated one, with one C call instead of 7 per
 // layer from Python.  The pre-norms are deferred (rf.h): no RMSNorm row kernel after layer 0's first one.
 #include <hip/hip_runtime.h>
@@ -20,8 +21,9 @@ int64_t align_up(int64_t b) { return (b + kAlign - 1) / kAlign * kAlign; }
 // activation buffers of the encoder stack, carved from one caller-owned workspace
 struct EncBufs {
     // byte offsets: h [T, D] half (x * g of the deferred RMSNorm), qkv [T, 3D] bf16, att [T, D] half, g [T, F] half,
-    // ss [T, RF_PRENORM_SLOTS] f32 (the norm's partial sums of squares)
-    int64_t h, qkv, att, g, ss, total;
+    // ss [T, RF_PRENORM_SLOTS] f32 (the norm's partial sums of squares), qkss [T, 2, RF_PRENORM_SLOTS] f32 (the
+    // fused QK path's q / k partial sums of squares, rf_gemm_qk_rope)
+    int64_t h, qkv, att, g, ss, qkss, total;
 };
 EncBufs enc_layout(int rows, int dim, int ffn) {
     EncBufs b;
@@ -31,7 +33,8 @@ EncBufs enc_layout(int rows, int dim, int ffn) {
     b.att = b.qkv + align_up(r * 3 * dim * 2);
     b.g = b.att + align_up(r * dim * 2);
     b.ss = b.g + align_up(r * (int64_t)ffn * 2);
-    b.total = b.ss + align_up(r * RF_PRENORM_SLOTS * 4);
+    b.qkss = b.ss + align_up(r * RF_PRENORM_SLOTS * 4);
+    b.total = b.qkss + align_up(r * 2 * RF_PRENORM_SLOTS * 4);
     return b;
 }
 
@@ -81,6 +84,7 @@ extern "C" int rf_encoder_forward(float* x, int64_t ldx, const rf_encoder_desc* 
     void* att = ws + b.att;                           // attention O: the out-projection's A operand
     void* g = ws + b.g;                               // SwiGLU output: W2's A operand
     float* ss = reinterpret_cast<float*>(ws + b.ss);  // the pre-norm's partial sums of squares
+    float* qkss = reinterpret_cast<float*>(ws + b.qkss);  // q / k partial sums of squares (fused QK path)
     auto gemm = f16 ? rf_gemm_f16 : rf_gemm_bf16;
     const int epi_swiglu = f16 ? RF_EPI_SWIGLU_F16 : RF_EPI_SWIGLU;
     const int o_dt = f16 ? RF_DT_F16 : RF_DT_BF16;
@@ -92,13 +96,34 @@ extern "C" int rf_encoder_forward(float* x, int64_t ldx, const rf_encoder_desc* 
     RF_CALL(rf_prenorm(x, ldx, d->layers[0].attn_norm, h, D, ss, T, D, dt, stream));
     for (int i = 0; i < d->n_layers; ++i) {
         const rf_encoder_layer& L = d->layers[i];
-        RF_CALL(rf_gemm_rownorm(h, D, L.w_qkv, D, qkv, 3 * D, T, 3 * D, D, RF_EPI_BF16, ss, D, d->eps, nullptr, 0, 0, dt, gws, gwb,
-                                stream));
-        RF_CALL(rf_qk_norm_rope(qkv, 3 * D, qkv, 3 * D, nullptr, T, D, H, 2, L.qk_norm, d->eps, kQLog2Scale, d->pos,
-                                d->ld_pos, 1, d->freqs, d->pos ? d->n_freqs : 0, stream));
-        if (d->timer_attn) RF_CALL(rf_ktimer_arm());
-        RF_CALL(rf_attn_fwd_dt(qkv, 3 * D, qkv + D, 3 * D, qkv + 2 * D, 3 * D, att, D, RF_DT_BF16, o_dt, d->problems,
-                               d->n_problems, H, 128, kLn2, d->attn_ws, d->bounds, d->bounds ? d->grid : 0, stream));
+        if (d->qk_fused) {
+            // the positional encoding fused into the QK path (rf.h ABI 16): the projection's epilogue applies the
+            // q/k norm weights and the triangle RoPE and writes the rows' sums of squares; k gets its 1 / rms in a
+            // row pass, q as the attention loads it (with no q/k norm, the projection also applies q's softmax scale)
+            const bool qkn = L.qk_norm != nullptr;
+            RF_CALL(rf_gemm_qk_rope(h, D, L.w_qkv, D, qkv, 3 * D, T, 3 * D, D, ss, D, d->eps, qkn ? qkss : nullptr, D, 2,
+                                    L.qk_norm, d->pos, d->ld_pos, d->freqs, d->pos ? d->n_freqs : 0,
+                                    qkn ? 1.0f : kQLog2Scale, dt, gws, gwb, stream));
+            if (qkn) RF_CALL(rf_row_rms_scale(qkv + D, 3 * D, T, D, qkss + RF_PRENORM_SLOTS, 2 * RF_PRENORM_SLOTS, d->eps, 1.0f,
+                                              stream));
+            if (d->timer_attn) RF_CALL(rf_ktimer_arm());
+            if (qkn)
+                RF_CALL(rf_attn_fwd_qn(qkv, 3 * D, qkv + D, 3 * D, qkv + 2 * D, 3 * D, att, D, o_dt, qkss,
+                                       2 * RF_PRENORM_SLOTS, D, d->eps, kQLog2Scale, d->problems, d->n_problems, H, 128,
+                                       d->attn_ws, d->bounds, d->bounds ? d->grid : 0, stream));
+            else
+                RF_CALL(rf_attn_fwd_dt(qkv, 3 * D, qkv + D, 3 * D, qkv + 2 * D, 3 * D, att, D, RF_DT_BF16, o_dt,
+                                       d->problems, d->n_problems, H, 128, kLn2, d->attn_ws, d->bounds,
+                                       d->bounds ? d->grid : 0, stream));
+        } else {
+            RF_CALL(rf_gemm_rownorm(h, D, L.w_qkv, D, qkv, 3 * D, T, 3 * D, D, RF_EPI_BF16, ss, D, d->eps, nullptr, 0, 0, dt,
+                                    gws, gwb, stream));
+            RF_CALL(rf_qk_norm_rope(qkv, 3 * D, qkv, 3 * D, nullptr, T, D, H, 2, L.qk_norm, d->eps, kQLog2Scale, d->pos,
+                                    d->ld_pos, 1, d->freqs, d->pos ? d->n_freqs : 0, stream));
+            if (d->timer_attn) RF_CALL(rf_ktimer_arm());
+            RF_CALL(rf_attn_fwd_dt(qkv, 3 * D, qkv + D, 3 * D, qkv + 2 * D, 3 * D, att, D, RF_DT_BF16, o_dt, d->problems,
+                                   d->n_problems, H, 128, kLn2, d->attn_ws, d->bounds, d->bounds ? d->grid : 0, stream));
+        }
         RF_CALL(rf_gemm_add_prenorm(att, D, L.w_out, D, x, ldx, T, D, D, L.ffn_norm, h, D, ss, dt, gws, gwb, stream));
         RF_CALL(rf_gemm_rownorm(h, D, L.w13, D, g, F, T, 2 * F, D, epi_swiglu, ss, D, d->eps, nullptr, 0, 0, dt, gws, gwb, stream));
         if (i + 1 < d->n_layers)

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import os
 import struct
+import time
 import zlib
 from typing import Dict, List, Optional, Tuple
 
@@ -39,6 +40,8 @@ class H5FormatError(ValueError):
 
 # ----------------------------------------------------------------------------------------- reader
 _POOL = None
+# callable(seconds) given the CPU time of every chunk decode (read + inflate + place), or None (batch_infer profiling)
+CPU_HOOK = None
 
 
 def host_threads() -> int:
@@ -139,6 +142,15 @@ class _Dataset:
             raw, fmask, sl_out, sl_in = job
             raw = self._unfilter(raw, fmask)
             out[sl_out] = np.frombuffer(raw, dtype=self.dtype, count=cn).reshape(cshape)[sl_in]
+        if CPU_HOOK is not None:  # profiling (batch_infer RF_BATCH_PROFILE): CPU seconds of the chunk decode threads
+            plain = place
+
+            def place(j):
+                t0 = time.thread_time()
+                try:
+                    plain(j)
+                finally:
+                    CPU_HOOK(time.thread_time() - t0)
         pool = _decode_pool() if len(jobs) > 1 else None
         if pool is None:
             for j in jobs:

@@ -108,14 +108,24 @@ class _DeviceWeights:
         self.tex_parity = 0
         self.tex_norm = _f32(sd["texture_encoder_norm.weight"], device)
         self.enc_freqs = _f32(sd["transformer.rope_emb.freqs"], device)
+        # stage 1's positional encoding fused into the QK path (rf.h ABI 16; RF_QK_FUSE=0 restores the q/k norm +
+        # RoPE row kernel): the q and k rows of every in-projection (and their norm weights) are stored in
+        # ops.rope_pair_perm order, so the projection's epilogue holds each rotate-half pair in one lane
+        self.qk_fused = os.environ.get("RF_QK_FUSE", "1") != "0"
+        D = cfg.latent_dim
+        perm = ops.rope_pair_perm(D)
+        qk_perm = torch.cat([perm, perm + D, torch.arange(2 * D, 3 * D)]) if self.qk_fused else None
         self.enc = []
         for i in range(cfg.num_layers):
             p = f"transformer.layers.{i}."
             L = _Layer()
-            L.w_in = hw(sd[p + "multihead_attn.in_proj.weight"])
+            w_in = sd[p + "multihead_attn.in_proj.weight"]
+            qn = torch.cat([sd[p + "multihead_attn.q_norm.weight"], sd[p + "multihead_attn.k_norm.weight"]])
+            if self.qk_fused:
+                w_in, qn = w_in[qk_perm], qn[qk_perm[:2 * D]]
+            L.w_in = hw(w_in)
             L.w_out = hw(sd[p + "multihead_attn.out_proj.weight"])
-            L.qk_norm = _f32(torch.cat([sd[p + "multihead_attn.q_norm.weight"], sd[p + "multihead_attn.k_norm.weight"]]),
-                             device)
+            L.qk_norm = _f32(qn, device)
             L.query_norm = _f32(sd[p + "query_norm.weight"], device)
             L.w13 = hw(_interleave_swiglu(sd[p + "ffn.w1.weight"], sd[p + "ffn.w3.weight"]))
             L.w2 = hw(sd[p + "ffn.w2.weight"])
@@ -540,7 +550,7 @@ class RenderFormer:
             if getattr(W, "enc_desc", None) is None:  # host array of the layers' device pointers, built once
                 W.enc_desc = ops.encoder_layers(W.enc, cfg.view_indep_qk_norm)
             ops.encoder_forward(x, W.enc_desc, len(W.enc), H, F, W.half, EPS, pos1, W.enc_freqs, plan.prob1,
-                                schedule=plan.sched1, tag="attn_stage1")
+                                schedule=plan.sched1, tag="attn_stage1", qk_fused=W.qk_fused)
             self._capture_stage1(plan, x)
             return x
         h = torch.empty(T, D, dtype=W.half, device=dev)      # GEMM operands: W.half (fp16 by default)
@@ -553,12 +563,25 @@ class RenderFormer:
         # every pre-norm deferred (rf.h rf_gemm_add_prenorm / rf_gemm_rownorm), as rf_encoder_forward issues them:
         # h holds x * g, ss the row sums of squares, and the projection after the norm applies 1 / rms
         ops.prenorm(x, W.enc[0].query_norm, h, ss)
+        qkn = cfg.view_indep_qk_norm
+        qkss = torch.empty(T, 2, ops.PRENORM_SLOTS, dtype=torch.float32, device=dev) if W.qk_fused and qkn else None
         for li, L in enumerate(W.enc):
-            ops.gemm_rownorm(h, L.w_in, qkv, ss, EPS)
-            ops.qk_norm_rope(qk_pair, qk_pair, H, L.qk_norm if cfg.view_indep_qk_norm else None, EPS, pos1, W.enc_freqs,
-                             n_seg=2, q_scale=ops.Q_LOG2_SCALE)
-            ops.attention(q, k, v, att, plan.prob1, plan.max_s, H, tag="attn_stage1", max_k_len=plan.max_s,
-                          q_prescaled=True, schedule=plan.sched1)
+            if W.qk_fused:  # rf_encoder_forward's qk_fused sequence (stage.cpp), launch for launch
+                ops.gemm_qk_rope(h, L.w_in, qkv, ss, EPS, D, 2, L.qk_norm if qkn else None, qkss, pos1, W.enc_freqs,
+                                 q_scale=1.0 if qkn else ops.Q_LOG2_SCALE)
+                if qkn:
+                    ops.row_rms_scale(k, qkss[:, 1], EPS)
+                    ops.attention(q, k, v, att, plan.prob1, plan.max_s, H, tag="attn_stage1", max_k_len=plan.max_s,
+                                  schedule=plan.sched1, q_ss=qkss[:, 0], q_eps=EPS)
+                else:
+                    ops.attention(q, k, v, att, plan.prob1, plan.max_s, H, tag="attn_stage1", max_k_len=plan.max_s,
+                                  q_prescaled=True, schedule=plan.sched1)
+            else:
+                ops.gemm_rownorm(h, L.w_in, qkv, ss, EPS)
+                ops.qk_norm_rope(qk_pair, qk_pair, H, L.qk_norm if qkn else None, EPS, pos1, W.enc_freqs, n_seg=2,
+                                 q_scale=ops.Q_LOG2_SCALE)
+                ops.attention(q, k, v, att, plan.prob1, plan.max_s, H, tag="attn_stage1", max_k_len=plan.max_s,
+                              q_prescaled=True, schedule=plan.sched1)
             ops.gemm_add_prenorm(att, L.w_out, x, L.ffn_norm, h, ss)
             ops.gemm_rownorm(h, L.w13, g, ss, EPS, ops.EPI_SWIGLU, tag="gemm_w13_stage1")
             if li + 1 < len(W.enc):

@@ -419,10 +419,68 @@ def attn_schedule(problems, n_heads: int, device) -> Optional[torch.Tensor]:
     return torch.from_numpy(attn_schedule_host(problems, n_heads, attn_grid(device))).to(device)
 
 
+def rope_pair_perm(dim: int) -> torch.Tensor:
+    """Row permutation of a q or k projection (dim = heads * 128) for gemm_qk_rope: per head, new row 2 m + t is old
+    row m + 64 t (the rotate-half pairs (m, m + 64) of rope.py side by side, so one lane's 4 output columns hold
+    two whole pairs).  Apply the same permutation to q and k (q.k unchanged) and to their norm weights."""
+    _check(dim % 128 == 0, "rope_pair_perm: dim must be a multiple of 128")
+    m = torch.arange(64)
+    head = torch.stack([m, m + 64], dim=1).reshape(-1)  # [0, 64, 1, 65, ...]
+    return (torch.arange(dim // 128)[:, None] * 128 + head[None, :]).reshape(-1)
+
+
+def gemm_qk_rope(xg: torch.Tensor, w: torch.Tensor, out: torch.Tensor, ss: Optional[torch.Tensor], eps: float,
+                 seg_w: int, n_seg: int, norm_w: Optional[torch.Tensor], seg_ss: Optional[torch.Tensor],
+                 pos: Optional[torch.Tensor], freqs: Optional[torch.Tensor], q_scale: float = 1.0,
+                 tag: Optional[str] = None) -> torch.Tensor:
+    """rf_gemm_qk_rope: out (bf16) = the q/k(/v) projection of the deferred-norm operand xg (1 / rms(x) from ss, as
+    gemm_rownorm) with, on its first n_seg segments of seg_w columns (rows of w permuted by rope_pair_perm),
+    rope(norm_w * y) written (segment 0 also times q_scale) and seg_ss [M, n_seg, 8] = partial sums of y^2 when
+    norm_w is given (the q/k norm's 1 / rms: row_rms_scale for k, attention(q_ss=...) for q)."""
+    _check(xg.dtype in HALF and w.dtype == xg.dtype, "gemm_qk_rope: xg / w must both be bf16 or both fp16")
+    _dev(xg, xg.dtype, "xg")
+    _dev(w, w.dtype, "w")
+    _dev(out, torch.bfloat16, "out")
+    m, k = xg.shape
+    n, k2 = w.shape
+    _check(k == k2 and out.shape[0] == m and out.shape[1] >= n, "gemm_qk_rope: shape mismatch")
+    if ss is not None:
+        _dev(ss, torch.float32, "ss")
+        _check(ss.shape[0] >= m and ss.shape[1] == PRENORM_SLOTS and ss.is_contiguous(), "gemm_qk_rope: ss shape")
+    if norm_w is not None:
+        _dev(norm_w, torch.float32, "norm_w")
+        _check(norm_w.numel() == n_seg * seg_w, "gemm_qk_rope: norm_w size")
+        _dev(seg_ss, torch.float32, "seg_ss")
+        _check(seg_ss.is_contiguous() and seg_ss.shape[0] >= m and seg_ss.shape[1:] == (n_seg, PRENORM_SLOTS),
+               "gemm_qk_rope: seg_ss [M, n_seg, 8]")
+    if pos is not None:
+        _dev(pos, torch.float32, "pos")
+        _check(pos.shape[0] >= m and pos.shape[1] >= 9 and freqs is not None, "gemm_qk_rope: pos [M, 9] with freqs")
+    ws = _gemm_workspace(xg.device)
+    _t0(tag)
+    call("rf_gemm_qk_rope", ptr(xg), xg.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), m, n, k, ptr(ss),
+         k, eps, ptr(seg_ss) if norm_w is not None else None, seg_w, n_seg, ptr(norm_w), ptr(pos),
+         pos.stride(0) if pos is not None else 0, ptr(freqs), freqs.numel() if (pos is not None) else 0,
+         float(q_scale), _dt(xg), ptr(ws), ws.numel(), stream())
+    return out
+
+
+def row_rms_scale(x: torch.Tensor, ss: torch.Tensor, eps: float, scale: float = 1.0) -> torch.Tensor:
+    """rf_row_rms_scale: x (bf16 rows, in place) *= scale / sqrt(sum(ss[r, :8]) / x.shape[1] + eps); ss a float view
+    whose rows hold the 8 partial sums (e.g. seg_ss[:, 1] for the k segment)."""
+    _dev(x, torch.bfloat16, "x")
+    _check(ss.dtype == torch.float32 and ss.device == x.device and ss.shape[0] >= x.shape[0]
+           and ss.shape[-1] == PRENORM_SLOTS and ss.stride(-1) == 1, "row_rms_scale: ss rows of 8 partial sums")
+    call("rf_row_rms_scale", ptr(x), x.stride(0), x.shape[0], x.shape[1], ptr(ss), ss.stride(0), eps, float(scale),
+         stream())
+    return x
+
+
 def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int,
               scale: Optional[float] = None, tag: Optional[str] = None, max_k_len: Optional[int] = None,
               n_split: Optional[int] = None, q_prescaled: bool = False,
-              schedule: Optional[torch.Tensor] = None) -> torch.Tensor:
+              schedule: Optional[torch.Tensor] = None, q_ss: Optional[torch.Tensor] = None,
+              q_eps: float = 0.0) -> torch.Tensor:
     """Varlen attention; problems int32 [P, 5] = (q_start, q_len, k_start, k_len, v_start).
 
     n_split None/0: the stream-K kernel (balanced over the CUs, cut units merged in-kernel), with the
@@ -430,8 +488,26 @@ def attention(q, k, v, out, problems: torch.Tensor, max_q_len: int, n_heads: int
     n_split >= 1: the legacy per-unit kernel with flash-decoding splits + rf_attn_combine.
     q_prescaled: q already carries scale*log2(e) (qk_norm_rope q_scale=Q_LOG2_SCALE).  q/k/v are bf16 or
     all fp16 (rf_attn_fwd_dt: the fp16 operands the reference's default half precision hands flash_attn; the
-    stream-K kernel only)."""
+    stream-K kernel only).  q_ss (rf_attn_fwd_qn; bf16, the stream-K kernel): rows of 8 partial sums of squares of
+    q before its norm (gemm_qk_rope's seg_ss[:, 0]): q rows are scaled by Q_LOG2_SCALE / rms as they load
+    (q_prescaled implied)."""
     _check(q.dtype in HALF, f"attention: q/k/v must be bf16 or fp16, got {q.dtype}")
+    if q_ss is not None:
+        _check(q.dtype == torch.bfloat16 and scale is None and (n_split is None or n_split == 0),
+               "attention: q_ss needs bf16 q/k/v on the stream-K kernel")
+        _check(q_ss.dtype == torch.float32 and q_ss.shape[-1] == PRENORM_SLOTS and q_ss.stride(-1) == 1
+               and q_ss.shape[0] >= q.shape[0], "attention: q_ss rows of 8 partial sums")
+        _dev(problems, torch.int32, "problems")
+        _dev(out, out.dtype, "out")
+        if schedule is not None:
+            _dev(schedule, torch.int64, "schedule")
+        ws = _attn_workspace(out.device)
+        _t0(tag)
+        call("rf_attn_fwd_qn", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out), out.stride(0),
+             DT_F16 if out.dtype == torch.float16 else DT_BF16, ptr(q_ss), q_ss.stride(0), q.shape[1], q_eps,
+             Q_LOG2_SCALE, ptr(problems), problems.shape[0], n_heads, q.shape[1] // n_heads, ptr(ws), ptr(schedule),
+             schedule.numel() - 1 if schedule is not None else 0, stream())
+        return out
     for t, nme in ((q, "q"), (k, "k"), (v, "v")):
         _dev(t, q.dtype, nme)
     _check(out.dtype in HALF, "attention: out must be bf16 or fp16")
@@ -484,9 +560,11 @@ def encoder_layers(layers, qk_norm: bool):
 
 def encoder_forward(x: torch.Tensor, layers, n_layers: int, n_heads: int, ffn_dim: int, operands: torch.dtype,
                     eps: float, pos: Optional[torch.Tensor], freqs: Optional[torch.Tensor], problems: torch.Tensor,
-                    schedule: Optional[torch.Tensor] = None, tag: Optional[str] = None) -> torch.Tensor:
+                    schedule: Optional[torch.Tensor] = None, tag: Optional[str] = None,
+                    qk_fused: bool = False) -> torch.Tensor:
     """x [T, D] f32 through the whole encoder stack in place, one C call (rf_encoder_forward; `layers` from
-    encoder_layers).  Same launches, same order and so the same bits as the per-op sequence of model._stage1."""
+    encoder_layers).  Same launches, same order and so the same bits as the per-op sequence of model._stage1.
+    qk_fused: the layers' q/k weights are in rope_pair_perm order (the fused QK path, rf.h ABI 16)."""
     from ._lib import EncoderDesc
     import ctypes
     _dev(x, torch.float32, "x")
@@ -509,7 +587,7 @@ def encoder_forward(x: torch.Tensor, layers, n_layers: int, n_heads: int, ffn_di
                     n_problems=problems.shape[0], bounds=ptr(schedule),
                     grid=schedule.numel() - 1 if schedule is not None else 0, workspace=ptr(ws), gemm_ws=ptr(gws),
                     gemm_ws_bytes=gws.numel(), attn_ws=ptr(_attn_workspace(x.device)),
-                    timer_attn=int(_timer_takes(tag, n_layers)))
+                    timer_attn=int(_timer_takes(tag, n_layers)), qk_fused=int(qk_fused))
     call("rf_encoder_forward", ptr(x), x.stride(0), ctypes.addressof(d), stream())
     return x
 

@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load(require_device=False)
     for fn in header_functions():
         assert hasattr(lib, fn), fn
-    assert lib.rf_abi_version() == 15
+    assert lib.rf_abi_version() == 16
     # every int-returning entry point has a ctypes signature in the binding
     assert set(_lib.SIGNATURES) == set(header_functions()) - {"rf_last_error", "rf_abi_version", "rf_build_flags",
                                                                "rf_attn_workspace_bytes", "rf_gemm_workspace_bytes",

@@ -550,8 +550,9 @@ def test_render_returns_before_the_frame_completes():
 def test_lazy_fallback_waits_for_frames_in_flight():
     """in lazy mode an overflow found by a LATER render's poll rebuilds the weights while other
     frames of the model may still run on non-default streams; the rebuild waits for them first (the old weight
-    tensors go back to the caching allocator).  Frame a completes on stream s1; frame b is held in flight on s2 by a
-    spin; frame c's render polls, resolves a (overflow -> bf16 weights) while b still runs on the old weights.
+    tensors go back to the caching allocator).  Frame a runs on stream s1 behind a short spin, frame b on s2 behind a
+    long one; once a has completed, frame c's render polls and resolves a (overflow -> bf16 weights) while b still
+    runs on the old weights.
     Every frame ends finite and within 1e-3 of the oracle."""
     from renderformer_amd import RenderFormer, RenderFormerRenderingPipeline
     from renderformer_amd.model import PrecisionWarning
@@ -560,17 +561,26 @@ def test_lazy_fallback_waits_for_frames_in_flight():
     big = _overflow_sd(sd)
     ref = rf_ref.render(big, cfg, inp["triangles"], inp["texture"].clone(), inp["mask"], inp["vn"], inp["c2w"],
                         inp["fov"], resolution=res)
-    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, big, range_check="lazy")).to("cuda")
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     args = lambda: (d["triangles"], d["texture"].clone(), d["mask"], d["vn"], d["c2w"], d["fov"])  # noqa: E731
+    # warm the process (first launches load the kernels' code objects) on a model with the normal weights, so the
+    # spins below dominate the host time between the renders
+    warm = RenderFormerRenderingPipeline(RenderFormer(cfg, sd)).to("cuda")
+    warm(*args(), resolution=res)
+    pipe = RenderFormerRenderingPipeline(RenderFormer(cfg, big, range_check="lazy")).to("cuda")
+    pipe.model.plan_hint(d["mask"], inp["mask"].numpy())  # no mask read-back (a host sync) inside the renders
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     torch.cuda.synchronize()
     with torch.cuda.stream(s1):
-        a = pipe(*args(), resolution=res)
-    s1.synchronize()
+        ina = args()
+        torch.cuda._sleep(int(1e9))  # a is still running when b's render polls
+        a = pipe(*ina, resolution=res)
     with torch.cuda.stream(s2):
         inb = args()
-        torch.cuda._sleep(int(5e8))  # b stays in flight while c's poll resolves a
+        torch.cuda._sleep(int(6e9))  # b stays in flight while c's poll resolves a
         b = pipe(*inb, resolution=res)
+    assert pipe.model.range_fallbacks == 0
+    s1.synchronize()
+    assert not s2.query()
     with pytest.warns(PrecisionWarning, match="fp16 operand overflow"):
         with torch.cuda.stream(s1):
             c = pipe(*args(), resolution=res)
