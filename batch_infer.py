@@ -76,7 +76,7 @@ def collate(items):
     return {k: torch.stack([it[k] for it in items]) for k in keys}
 
 
-LOADERS = 3  # batches decoded ahead (threads)
+LOADERS = int(os.environ.get("RF_BATCH_LOADERS", "3"))  # batches decoded ahead (threads)
 WRITERS = 4  # image encode/write threads
 
 

@@ -184,7 +184,7 @@ int rf_gemm_rownorm(const void* a, int64_t lda, const void* w, int64_t ldw, void
  *     are q (and k).  Their rows of W must be PERMUTED per 128-wide head so that column 2 m + t holds dimension
  *     m + 64 t (the rotate-half pairs (m, m + 64) side by side; q and k permuted alike, so q.k is unchanged).  The
  *     epilogue writes bf16 rope(norm_w * y) (norm_w in the same permuted order, NULL = no norm; segment 0 also
- *     times q_scale) with angle m = pos[r][m / n_freqs] * freqs[m % n_freqs] for m < 9 n_freqs (else 0), and, when
+ *     times q_scale) with angle m = pos[r / pos_div][m / n_freqs] * freqs[m % n_freqs] for m < 9 n_freqs (else 0), and, when
  *     norm_w is given, seg_ss[r][seg][RF_PRENORM_SLOTS] = partial sums of y^2 (y before the weight and rotation,
  *     f32) — the norm's 1 / rms is applied downstream (RoPE and the weight are linear per row).  ss / norm_dim /
  *     eps: the deferred pre-norm, as rf_gemm_rownorm (ss NULL: none).
@@ -194,8 +194,8 @@ int rf_gemm_rownorm(const void* a, int64_t lda, const void* w, int64_t ldw, void
  *     runs on exp2 exponents). */
 int rf_gemm_qk_rope(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int m, int n,
                     int k, const float* ss, int norm_dim, float eps, float* seg_ss, int seg_w, int n_seg,
-                    const float* norm_w, const float* pos, int64_t ld_pos, const float* freqs, int n_freqs,
-                    float q_scale, int operand_dtype, void* workspace, int64_t ws_bytes, void* stream);
+                    const float* norm_w, const float* pos, int64_t ld_pos, int pos_div, const float* freqs,
+                    int n_freqs, float q_scale, int operand_dtype, void* workspace, int64_t ws_bytes, void* stream);
 int rf_row_rms_scale(void* x, int64_t ldx, int rows, int dim, const float* ss, int64_t ld_ss, float eps, float scale,
                      void* stream);
 int rf_attn_fwd_qn(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv, void* o,
@@ -249,6 +249,14 @@ int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t src_gstride,
                            int n_groups, const float* norm_w, int64_t w_gstride, float eps, float seg0_scale,
                            const float* pos, int64_t ld_pos, int pos_div, const float* freqs, int n_freqs,
                            void* stream);
+/* rf_qk_norm_rope_groups on rows in rf_gemm_qk_rope's pair-interleaved column order (ABI 16): per head, column 2 m + t
+ * is dimension m + 64 t, norm_w in the same order; the same angles and arithmetic (the stage-2 keys when the queries'
+ * rotation runs in their projection's epilogue). */
+int rf_qk_norm_rope_groups_ilv(const void* src, int64_t ld_src, int64_t src_gstride, void* dst, int64_t ld_dst,
+                               int64_t dst_gstride, const int32_t* src_rows, int rows, int dim, int n_heads, int n_seg,
+                               int n_groups, const float* norm_w, int64_t w_gstride, float eps, float seg0_scale,
+                               const float* pos, int64_t ld_pos, int pos_div, const float* freqs, int n_freqs,
+                               void* stream);
 
 /* Variable-length multi-head attention, non-causal, head_dim 128, bf16 in/out, f32 softmax.
  * problems: int32[n_problems][5] = {q_start, q_len, k_start, k_len, v_start} (rows); k_len >= 1
@@ -594,6 +602,10 @@ typedef struct {
     int64_t gemm_ws_bytes;
     void* attn_ws;
     int timer_cross;                            /* measurement: rf_ktimer_arm() before every cross-attention launch */
+    int qk_fused;                               /* 1: w_q rows, q_norm, the K rows of w_kv / w_kv_all, k_norm and
+                                                   k_norm_all in rf_gemm_qk_rope's pair-interleaved order: the query
+                                                   rotation runs in the projection's epilogue (rf_gemm_qk_rope), the
+                                                   keys' in rf_qk_norm_rope_groups_ilv, q's 1 / rms in rf_attn_fwd_qn */
 } rf_decoder_desc;
 
 /* x[rows, dim] (f32 ray-token residual stream) through the decoder stack in place; the DPT taps are written as

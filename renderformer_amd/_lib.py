@@ -47,12 +47,14 @@ SIGNATURES = {
     "rf_prenorm": [_P, _L, _P, _P, _L, _P, _I, _I, _I, _P],
     "rf_gemm_add_prenorm": [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _P, _L, _P, _I, _P, _L, _P],
     "rf_gemm_rownorm": [_P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _I, _F, _P, _I, _I, _I, _P, _L, _P],
-    "rf_gemm_qk_rope": [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _I, _F, _P, _I, _I, _P, _P, _L, _P, _I, _F, _I, _P,
-                        _L, _P],
+    "rf_gemm_qk_rope": [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _I, _F, _P, _I, _I, _P, _P, _L, _I, _P, _I, _F, _I,
+                        _P, _L, _P],
     "rf_row_rms_scale": [_P, _L, _I, _I, _P, _L, _F, _F, _P],
     "rf_attn_fwd_qn": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _P, _L, _I, _F, _F, _P, _I, _I, _I, _P, _P, _I, _P],
     "rf_qk_norm_rope": [_P, _L, _P, _L, _P, _I, _I, _I, _I, _P, _F, _F, _P, _L, _I, _P, _I, _P],
     "rf_qk_norm_rope_groups": [_P, _L, _L, _P, _L, _L, _P, _I, _I, _I, _I, _I, _P, _L, _F, _F, _P, _L, _I, _P, _I,
+                               _P],
+    "rf_qk_norm_rope_groups_ilv": [_P, _L, _L, _P, _L, _L, _P, _I, _I, _I, _I, _I, _P, _L, _F, _F, _P, _L, _I, _P, _I,
                                _P],
     "rf_attn_fwd": [_P, _L, _P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _I, _F, _I, _P, _L, _P],
     "rf_attn_fwd_sched": [_P, _L, _P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _F, _P, _P, _I, _P],
@@ -144,7 +146,7 @@ class DecoderDesc(ctypes.Structure):
                 ("n_cross", _I), ("cross_bounds", _P), ("cross_grid", _I), ("swin", _I), ("n_images", _I),
                 ("grid_h", _I), ("grid_w", _I), ("window", _I), ("shift", _I), ("self_problems", _P), ("n_self", _I),
                 ("taps", _P), ("n_taps", _I), ("workspace", _P), ("gemm_ws", _P), ("gemm_ws_bytes", _L),
-                ("attn_ws", _P), ("timer_cross", _I)]
+                ("attn_ws", _P), ("timer_cross", _I), ("qk_fused", _I)]
 
 
 class HipLibraryError(RuntimeError):

@@ -126,6 +126,7 @@ struct EngineArgs {
     // segments' norm weights in the same order (null: no norm, and no sums); segment 0 also times rope_qscale
     const float* rope_pos;
     int64_t rope_ld;
+    int rope_div;  // position row of output row r: r / rope_div (the ray tokens of one view share the view's position)
     const float* rope_freqs;
     int rope_nf;
     const float* rope_g;
@@ -509,7 +510,7 @@ RF_DEV void pn_issue(const EngineArgs& p, char* area, int m0, int n0) {
                     for (int c = wave; c * 64 < C::BM * 9; c += C::NWAVE) {
                         const int e = c * 64 + lane;
                         const int r = e / 9, col = e - r * 9;
-                        const int row = min(m0 + min(r, C::BM - 1), p.m - 1);
+                        const int row = min(m0 + min(r, C::BM - 1), p.m - 1) / p.rope_div;
                         __builtin_amdgcn_global_load_lds(GLB_PTR(void, p.rope_pos + (int64_t)row * p.rope_ld + col),
                                                          LDS_PTR(void, pl + c * 256), 4, 0, 0);
                     }
@@ -3918,9 +3919,9 @@ static int launch_rope(EngineArgs p, void* stream) {
 
 extern "C" int rf_gemm_qk_rope(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int m,
                                int n, int k, const float* ss, int norm_dim, float eps, float* seg_ss, int seg_w,
-                               int n_seg, const float* norm_w, const float* pos, int64_t ld_pos, const float* freqs,
-                               int n_freqs, float q_scale, int operand_dtype, void* workspace, int64_t ws_bytes,
-                               void* stream) {
+                               int n_seg, const float* norm_w, const float* pos, int64_t ld_pos, int pos_div,
+                               const float* freqs, int n_freqs, float q_scale, int operand_dtype, void* workspace,
+                               int64_t ws_bytes, void* stream) {
     (void)workspace;
     (void)ws_bytes;
     RF_REQUIRE(a && w && c, "rf_gemm_qk_rope: null pointer");
@@ -3936,8 +3937,8 @@ extern "C" int rf_gemm_qk_rope(const void* a, int64_t lda, const void* w, int64_
                "rf_gemm_qk_rope: seg_ss must be 16-B aligned and seg_w <= %d", PN_SLOTS * 128);
     RF_REQUIRE(!ss || (((uintptr_t)ss & 15) == 0 && norm_dim > 0), "rf_gemm_qk_rope: ss must be 16-B aligned");
     RF_REQUIRE(!norm_w || ((uintptr_t)norm_w & 15) == 0, "rf_gemm_qk_rope: norm_w must be 16-B aligned");
-    RF_REQUIRE(!pos || (freqs && n_freqs > 0 && 9 * n_freqs <= 64 && ld_pos >= 9),
-               "rf_gemm_qk_rope: pos needs freqs with 9 * n_freqs <= 64 and ld_pos >= 9");
+    RF_REQUIRE(!pos || (freqs && n_freqs > 0 && 9 * n_freqs <= 64 && ld_pos >= 9 && pos_div >= 1),
+               "rf_gemm_qk_rope: pos needs freqs with 9 * n_freqs <= 64, ld_pos >= 9 and pos_div >= 1");
     EngineArgs p{};
     p.a = (const bf16_t*)a;
     p.lda = lda;
@@ -3956,6 +3957,7 @@ extern "C" int rf_gemm_qk_rope(const void* a, int64_t lda, const void* w, int64_
     p.seg_n = n_seg;
     p.rope_pos = pos;
     p.rope_ld = ld_pos;
+    p.rope_div = pos ? pos_div : 1;
     p.rope_freqs = freqs;
     p.rope_nf = pos ? n_freqs : 1;
     p.rope_g = norm_w;

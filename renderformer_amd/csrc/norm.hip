@@ -254,7 +254,10 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(const bf16_t* src, in
 // One row per wave, no row loop (like rmsnorm_v_kernel): the row's q/k chunks are issued first, then the
 // RoPE position and the norm weights, so every load of a wave is in flight in one round trip and the
 // grid holds all rows at once (stage 1: 5,649 rows = 5,652 waves, 5.5 per SIMD).
-template <int UPL>
+// ILV: the pair-interleaved column order of rf_gemm_qk_rope (per head, column 2 m + t = dimension m + 64 t): a unit is
+// 16 consecutive columns (rotation pairs 8 (unit & 7) .. + 7, the same angles as the half-split unit), lo / hi its
+// two 16-B halves, each dword one (x1, x2) pair
+template <int UPL, bool ILV = false>
 __global__ __launch_bounds__(256) void qk_norm_rope_row_kernel(const bf16_t* src, int64_t ld_src, bf16_t* dst,
                                                                int64_t ld_dst, const int32_t* __restrict__ src_rows,
                                                                int rows, int n_heads, int n_seg,
@@ -271,6 +274,7 @@ __global__ __launch_bounds__(256) void qk_norm_rope_row_kernel(const bf16_t* src
     src += blockIdx.y * src_gstride;
     dst += blockIdx.y * dst_gstride;
     if (norm_w) norm_w += blockIdx.y * w_gstride;
+    constexpr int HOFF = ILV ? 8 : 64;  // column of the unit's second 16-B half
     const int upsg = n_heads * 8;
     const int units = n_seg * upsg;
     const int dim = n_heads * 128;
@@ -281,10 +285,10 @@ __global__ __launch_bounds__(256) void qk_norm_rope_row_kernel(const bf16_t* src
 #pragma unroll
     for (int u = 0; u < UPL; ++u) {
         const int unit = lane + 64 * u;
-        col[u] = (unit / upsg) * dim + ((unit % upsg) >> 3) * 128 + 8 * (unit & 7);
+        col[u] = (unit / upsg) * dim + ((unit % upsg) >> 3) * 128 + (ILV ? 16 : 8) * (unit & 7);
         if (unit < units) {
             lo[u] = *reinterpret_cast<const u32x4*>(s + col[u]);
-            hi[u] = *reinterpret_cast<const u32x4*>(s + col[u] + 64);
+            hi[u] = *reinterpret_cast<const u32x4*>(s + col[u] + HOFF);
         }
     }
     float ang = 0.f;
@@ -294,7 +298,7 @@ __global__ __launch_bounds__(256) void qk_norm_rope_row_kernel(const bf16_t* src
     for (int u = 0; u < UPL; ++u) {
         if (norm_w && lane + 64 * u < units) {
             const float4* pl = reinterpret_cast<const float4*>(norm_w + col[u]);
-            const float4* ph = reinterpret_cast<const float4*>(norm_w + col[u] + 64);
+            const float4* ph = reinterpret_cast<const float4*>(norm_w + col[u] + HOFF);
             wl[u][0] = pl[0];
             wl[u][1] = pl[1];
             wh[u][0] = ph[0];
@@ -358,23 +362,40 @@ __global__ __launch_bounds__(256) void qk_norm_rope_row_kernel(const bf16_t* src
             const float whi[8] = {wh[u][0].x, wh[u][0].y, wh[u][0].z, wh[u][0].w,
                                   wh[u][1].x, wh[u][1].y, wh[u][1].z, wh[u][1].w};
             u32x4 olo, ohi;
+            if constexpr (ILV) {  // dword e of lo: pair e, of hi: pair 4 + e, each (x1 low, x2 high)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float ra[2], rb[2];
+                for (int e = 0; e < 4; ++e) {
 #pragma unroll
-                for (int t = 0; t < 2; ++t) {
-                    const int i = 2 * e + t;
-                    const float a = (t ? __uint_as_float(lo[u][e] & 0xffff0000u) : __uint_as_float(lo[u][e] << 16));
-                    const float b = (t ? __uint_as_float(hi[u][e] & 0xffff0000u) : __uint_as_float(hi[u][e] << 16));
-                    const float x0 = a * inv[u] * wlo[i], x1 = b * inv[u] * whi[i];
-                    ra[t] = x0 * cs[i] - x1 * sn[i];  // rotate_half_hf: (-x2, x1)
-                    rb[t] = x1 * cs[i] + x0 * sn[i];
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t wd = h ? hi[u][e] : lo[u][e];
+                        const float* wv = h ? whi : wlo;
+                        const int k = 4 * h + e;
+                        const float x0 = __uint_as_float(wd << 16) * inv[u] * wv[2 * e];
+                        const float x1 = __uint_as_float(wd & 0xffff0000u) * inv[u] * wv[2 * e + 1];
+                        const uint32_t r = pack_bf16x2(x0 * cs[k] - x1 * sn[k], x1 * cs[k] + x0 * sn[k]);
+                        if (h) ohi[e] = r;
+                        else olo[e] = r;
+                    }
                 }
-                olo[e] = pack_bf16x2(ra[0], ra[1]);
-                ohi[e] = pack_bf16x2(rb[0], rb[1]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float ra[2], rb[2];
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const int i = 2 * e + t;
+                        const float a = (t ? __uint_as_float(lo[u][e] & 0xffff0000u) : __uint_as_float(lo[u][e] << 16));
+                        const float b = (t ? __uint_as_float(hi[u][e] & 0xffff0000u) : __uint_as_float(hi[u][e] << 16));
+                        const float x0 = a * inv[u] * wlo[i], x1 = b * inv[u] * whi[i];
+                        ra[t] = x0 * cs[i] - x1 * sn[i];  // rotate_half_hf: (-x2, x1)
+                        rb[t] = x1 * cs[i] + x0 * sn[i];
+                    }
+                    olo[e] = pack_bf16x2(ra[0], ra[1]);
+                    ohi[e] = pack_bf16x2(rb[0], rb[1]);
+                }
             }
             *reinterpret_cast<u32x4*>(d + col[u]) = olo;
-            *reinterpret_cast<u32x4*>(d + col[u] + 64) = ohi;
+            *reinterpret_cast<u32x4*>(d + col[u] + HOFF) = ohi;
         }
     }
 }
@@ -526,11 +547,37 @@ extern "C" int rf_prenorm(const float* x, int64_t ldx, const float* norm_w, void
     return rf::check_launch("rf_prenorm");
 }
 
+static int qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t src_gstride, void* dst, int64_t ld_dst,
+                               int64_t dst_gstride, const int32_t* src_rows, int rows, int dim, int n_heads, int n_seg,
+                               int n_groups, const float* norm_w, int64_t w_gstride, float eps, float seg0_scale,
+                               const float* pos, int64_t ld_pos, int pos_div, const float* freqs, int n_freqs,
+                               void* stream, bool ilv);
+
 extern "C" int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t src_gstride, void* dst, int64_t ld_dst,
                                       int64_t dst_gstride, const int32_t* src_rows, int rows, int dim, int n_heads,
                                       int n_seg, int n_groups, const float* norm_w, int64_t w_gstride, float eps,
                                       float seg0_scale, const float* pos, int64_t ld_pos, int pos_div,
                                       const float* freqs, int n_freqs, void* stream) {
+    return qk_norm_rope_groups(src, ld_src, src_gstride, dst, ld_dst, dst_gstride, src_rows, rows, dim, n_heads, n_seg,
+                               n_groups, norm_w, w_gstride, eps, seg0_scale, pos, ld_pos, pos_div, freqs, n_freqs,
+                               stream, false);
+}
+
+extern "C" int rf_qk_norm_rope_groups_ilv(const void* src, int64_t ld_src, int64_t src_gstride, void* dst,
+                                          int64_t ld_dst, int64_t dst_gstride, const int32_t* src_rows, int rows,
+                                          int dim, int n_heads, int n_seg, int n_groups, const float* norm_w,
+                                          int64_t w_gstride, float eps, float seg0_scale, const float* pos,
+                                          int64_t ld_pos, int pos_div, const float* freqs, int n_freqs, void* stream) {
+    return qk_norm_rope_groups(src, ld_src, src_gstride, dst, ld_dst, dst_gstride, src_rows, rows, dim, n_heads, n_seg,
+                               n_groups, norm_w, w_gstride, eps, seg0_scale, pos, ld_pos, pos_div, freqs, n_freqs,
+                               stream, true);
+}
+
+static int qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t src_gstride, void* dst, int64_t ld_dst,
+                               int64_t dst_gstride, const int32_t* src_rows, int rows, int dim, int n_heads, int n_seg,
+                               int n_groups, const float* norm_w, int64_t w_gstride, float eps, float seg0_scale,
+                               const float* pos, int64_t ld_pos, int pos_div, const float* freqs, int n_freqs,
+                               void* stream, bool ilv) {
     RF_REQUIRE(src && dst, "rf_qk_norm_rope: null pointer");
     RF_REQUIRE(dim == n_heads * 128 && n_seg >= 1 && n_seg * n_heads * 8 <= MAX_UNITS,
                "rf_qk_norm_rope: need head_dim 128 and n_seg*n_heads <= %d", MAX_UNITS / 8);
@@ -546,7 +593,7 @@ extern "C" int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t s
     static const bool loop = getenv("RF_QKN_LOOP") && atoi(getenv("RF_QKN_LOOP"));  // A/B only
     int units = n_seg * n_heads * 8;
     hipStream_t st = (hipStream_t)stream;
-    if (loop) {  // the grid-stride kernel, one launch per group
+    if (loop && !ilv) {  // the grid-stride kernel, one launch per group (standard layout only)
         const dim3 grid(blocks > 2048 ? 2048 : blocks);
         for (int g = 0; g < n_groups; ++g) {
             const bf16_t* s = (const bf16_t*)src + g * src_gstride;
@@ -577,13 +624,22 @@ extern "C" int rf_qk_norm_rope_groups(const void* src, int64_t ld_src, int64_t s
     }
     const dim3 grid(blocks, n_groups);
 #define RF_QKN(U)                                                                                                 \
-    RF_LAUNCH(qk_norm_rope_row_kernel<U>, grid, dim3(256), 0, st, (const bf16_t*)src, ld_src, (bf16_t*)dst, \
-                       ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, seg0_scale, pos, ld_pos, pos_div, freqs, \
-                       n_freqs, src_gstride, dst_gstride, (int)w_gstride, split_qk)
+    if (ilv)                                                                                                      \
+        RF_LAUNCH((qk_norm_rope_row_kernel<U, true>), grid, dim3(256), 0, st, (const bf16_t*)src, ld_src,          \
+                  (bf16_t*)dst, ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, seg0_scale, pos, ld_pos, pos_div, \
+                  freqs, n_freqs, src_gstride, dst_gstride, (int)w_gstride, split_qk);                             \
+    else                                                                                                          \
+        RF_LAUNCH((qk_norm_rope_row_kernel<U, false>), grid, dim3(256), 0, st, (const bf16_t*)src, ld_src,         \
+                  (bf16_t*)dst, ld_dst, src_rows, rows, n_heads, n_seg, norm_w, eps, seg0_scale, pos, ld_pos, pos_div, \
+                  freqs, n_freqs, src_gstride, dst_gstride, (int)w_gstride, split_qk)
     units = n_seg * n_heads * 8;
-    if (units <= 64) RF_QKN(1);
-    else if (units <= 128) RF_QKN(2);
-    else RF_QKN(4);
+    if (units <= 64) {
+        RF_QKN(1);
+    } else if (units <= 128) {
+        RF_QKN(2);
+    } else {
+        RF_QKN(4);
+    }
 #undef RF_QKN
     return rf::check_launch("rf_qk_norm_rope");
 }

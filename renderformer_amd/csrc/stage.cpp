@@ -102,7 +102,7 @@ extern "C" int rf_encoder_forward(float* x, int64_t ldx, const rf_encoder_desc* 
             // row pass, q as the attention loads it (with no q/k norm, the projection also applies q's softmax scale)
             const bool qkn = L.qk_norm != nullptr;
             RF_CALL(rf_gemm_qk_rope(h, D, L.w_qkv, D, qkv, 3 * D, T, 3 * D, D, ss, D, d->eps, qkn ? qkss : nullptr, D, 2,
-                                    L.qk_norm, d->pos, d->ld_pos, d->freqs, d->pos ? d->n_freqs : 0,
+                                    L.qk_norm, d->pos, d->ld_pos, 1, d->freqs, d->pos ? d->n_freqs : 0,
                                     qkn ? 1.0f : kQLog2Scale, dt, gws, gwb, stream));
             if (qkn) RF_CALL(rf_row_rms_scale(qkv + D, 3 * D, T, D, qkss + RF_PRENORM_SLOTS, 2 * RF_PRENORM_SLOTS, d->eps, 1.0f,
                                               stream));
@@ -159,7 +159,8 @@ DecBufs dec_layout(const rf_decoder_desc* d) {
     b.qkv = b.kview + align_up((int64_t)d->kv_rows * (k_batch ? L : 1) * D * 2);
     b.ss = b.qkv + (d->layers && d->n_layers > 0 && d->layers[0].self_norm ? align_up(T2 * 3 * D * 2) : 0);
     b.qkss = b.ss + align_up(T2 * RF_PRENORM_SLOTS * 4);
-    b.total = b.qkss + (d->swin ? align_up(T2 * 2 * RF_PRENORM_SLOTS * 4) : 0);
+    // (Swin's q/k row sums [T2][2][slots]; with qk_fused also the cross-attention q's [T2][1][slots], used earlier)
+    b.total = b.qkss + align_up(T2 * (d->swin ? 2 : 1) * RF_PRENORM_SLOTS * 4);
     return b;
 }
 }  // namespace
@@ -241,17 +242,26 @@ extern "C" int rf_decoder_forward(float* x, int64_t ldx, const rf_decoder_desc* 
         RF_CALL(gemm(hc, d->ctx_dim, d->w_kv_all, d->ctx_dim, kv, ld_kv, nullptr, T1, (int)ld_kv, d->ctx_dim,
                      RF_EPI_BF16, gws, gwb, stream));
     }
+    // the keys' norm + rotation: the standard layout, or (qk_fused) the pair-interleaved order of the permuted weights
+    auto k_rope = d->qk_fused ? rf_qk_norm_rope_groups_ilv : rf_qk_norm_rope_groups;
     if (k_batch)  // every layer's keys normed and rotated per view in one launch
-        RF_CALL(rf_qk_norm_rope_groups(kv, ld_kv, 2 * D, kview, ld_kview, D, d->kv_src_rows, d->kv_rows, D, H, 1, NL,
-                                       d->k_norm_all, D, d->eps, 1.0f, d->kv_pos, d->ld_kv_pos, 1, d->freqs,
-                                       d->kv_pos ? nf : 0, stream));
+        RF_CALL(k_rope(kv, ld_kv, 2 * D, kview, ld_kview, D, d->kv_src_rows, d->kv_rows, D, H, 1, NL, d->k_norm_all, D,
+                       d->eps, 1.0f, d->kv_pos, d->ld_kv_pos, 1, d->freqs, d->kv_pos ? nf : 0, stream));
     int tap = 0;
     // the ray tokens' pre-norms are deferred as in the encoder (rf.h): only layer 0's query norm is a row kernel
     RF_CALL(rf_prenorm(x, ldx, d->layers[0].query_norm, h, D, ss, T2, D, dt, stream));
     for (int i = 0; i < NL; ++i) {
         const rf_decoder_layer& L = d->layers[i];
-        // (i) cross-attention
-        RF_CALL(rf_gemm_rownorm(h, D, L.w_q, D, q2, D, T2, D, D, RF_EPI_BF16, ss, D, d->eps, nullptr, 0, 0, dt, gws, gwb, stream));
+        // (i) cross-attention.  qk_fused: the query's norm weight and ray rotation in its projection's epilogue, its
+        // 1 / rms in the attention's Q load (row sums in qkss, [T2][1][RF_PRENORM_SLOTS]; the Swin sums come later)
+        const bool qf = d->qk_fused != 0, qn = qf && L.q_norm;
+        if (qf)
+            RF_CALL(rf_gemm_qk_rope(h, D, L.w_q, D, q2, D, T2, D, D, ss, D, d->eps, qn ? qkss : nullptr, D, 1, L.q_norm,
+                                    d->ray_pos, d->ld_ray_pos, d->ray_pos ? d->ray_pos_div : 1, d->freqs,
+                                    d->ray_pos ? nf : 0, qn ? 1.0f : kQLog2Scale, dt, gws, gwb, stream));
+        else
+            RF_CALL(rf_gemm_rownorm(h, D, L.w_q, D, q2, D, T2, D, D, RF_EPI_BF16, ss, D, d->eps, nullptr, 0, 0, dt, gws,
+                                    gwb, stream));
         const uint16_t* kvi = kv_batch ? kv + (int64_t)2 * D * i : kv;
         if (!kv_batch) {
             RF_CALL(rmsnorm(d->ctx, d->ld_ctx, L.kv_norm, d->eps, hc, d->ctx_dim, T1, d->ctx_dim, stream));
@@ -259,15 +269,22 @@ extern "C" int rf_decoder_forward(float* x, int64_t ldx, const rf_decoder_desc* 
                          gws, gwb, stream));
         }
         const uint16_t* ki = k_batch ? kview + (int64_t)D * i : kview;
-        RF_CALL(rf_qk_norm_rope(q2, D, q2, D, nullptr, T2, D, H, 1, L.q_norm, d->eps, kQLog2Scale, d->ray_pos,
-                                d->ld_ray_pos, d->ray_pos ? d->ray_pos_div : 1, d->freqs, d->ray_pos ? nf : 0, stream));
+        if (!qf)
+            RF_CALL(rf_qk_norm_rope(q2, D, q2, D, nullptr, T2, D, H, 1, L.q_norm, d->eps, kQLog2Scale, d->ray_pos,
+                                    d->ld_ray_pos, d->ray_pos ? d->ray_pos_div : 1, d->freqs, d->ray_pos ? nf : 0,
+                                    stream));
         if (!k_batch)
-            RF_CALL(rf_qk_norm_rope(kvi, ld_kv, kview, ld_kview, d->kv_src_rows, d->kv_rows, D, H, 1, L.k_norm, d->eps,
-                                    1.0f, d->kv_pos, d->ld_kv_pos, 1, d->freqs, d->kv_pos ? nf : 0, stream));
+            RF_CALL(k_rope(kvi, ld_kv, 0, kview, ld_kview, 0, d->kv_src_rows, d->kv_rows, D, H, 1, 1, L.k_norm, 0, d->eps,
+                           1.0f, d->kv_pos, d->ld_kv_pos, 1, d->freqs, d->kv_pos ? nf : 0, stream));
         if (d->timer_cross) RF_CALL(rf_ktimer_arm());
-        RF_CALL(rf_attn_fwd_dt(q2, D, ki, ld_kview, kvi + D, ld_kv, att, D, RF_DT_BF16, o_dt, d->cross_problems,
-                               d->n_cross, H, 128, kLn2, d->attn_ws, d->cross_bounds,
-                               d->cross_bounds ? d->cross_grid : 0, stream));
+        if (qn)
+            RF_CALL(rf_attn_fwd_qn(q2, D, ki, ld_kview, kvi + D, ld_kv, att, D, o_dt, qkss, RF_PRENORM_SLOTS, D, d->eps,
+                                   kQLog2Scale, d->cross_problems, d->n_cross, H, 128, d->attn_ws, d->cross_bounds,
+                                   d->cross_bounds ? d->cross_grid : 0, stream));
+        else
+            RF_CALL(rf_attn_fwd_dt(q2, D, ki, ld_kview, kvi + D, ld_kv, att, D, RF_DT_BF16, o_dt, d->cross_problems,
+                                   d->n_cross, H, 128, kLn2, d->attn_ws, d->cross_bounds,
+                                   d->cross_bounds ? d->cross_grid : 0, stream));
         RF_CALL(rf_gemm_add_prenorm(att, D, L.w_out, D, x, ldx, T2, D, D, self_attn ? L.self_norm : L.ffn_norm, h, D,
                                     ss, dt, gws, gwb, stream));
         // (ii) self-attention between ray tokens

@@ -137,16 +137,19 @@ class _DeviceWeights:
         self.ray_b = _f32(sd[vt + "ray_map_encoder.bias"], device)
         self.ray_norm = _f32(sd[vt + "ray_map_encoder_norm.weight"], device)
         self.dec_freqs = _f32(sd[vt + "transformer.rope_emb.freqs"], device)
+        dperm = ops.rope_pair_perm(cfg.view_transformer_latent_dim)
+        qk_rows = (lambda t: t[dperm]) if self.qk_fused else (lambda t: t)  # noqa: E731
         self.dec = []
         for i in range(cfg.view_transformer_n_layers):
             p = f"{vt}transformer.layers.{i}."
             a = p + "multihead_attn."
             L = _Layer()
-            L.wq = hw(sd[a + "q_proj.weight"])
-            L.wkv = hw(torch.cat([sd[a + "k_proj.weight"], sd[a + "v_proj.weight"]], 0))
+            # (qk_fused: the cross-attention q and k rows in rope_pair_perm order, as stage 1's)
+            L.wq = hw(qk_rows(sd[a + "q_proj.weight"]))
+            L.wkv = hw(torch.cat([qk_rows(sd[a + "k_proj.weight"]), sd[a + "v_proj.weight"]], 0))
             L.wo = hw(sd[a + "out_proj.weight"])
-            L.q_norm = _f32(sd[a + "q_norm.weight"], device)
-            L.k_norm = _f32(sd[a + "k_norm.weight"], device)
+            L.q_norm = _f32(qk_rows(sd[a + "q_norm.weight"]), device)
+            L.k_norm = _f32(qk_rows(sd[a + "k_norm.weight"]), device)
             L.query_norm = _f32(sd[p + "query_norm.weight"], device)
             L.kv_norm = _f32(sd[p + "kv_norm.weight"], device)
             if cfg.view_transformer_include_self_attn:
@@ -167,11 +170,11 @@ class _DeviceWeights:
         for i in range(cfg.view_transformer_n_layers):
             p = f"{vt}transformer.layers.{i}."
             a = p + "multihead_attn."
-            w = torch.cat([sd[a + "k_proj.weight"], sd[a + "v_proj.weight"]], 0).float()
+            w = torch.cat([qk_rows(sd[a + "k_proj.weight"]), sd[a + "v_proj.weight"]], 0).float()
             wkv_all.append(w * sd[p + "kv_norm.weight"].float()[None, :])
         self.wkv_all = hw(torch.cat(wkv_all, 0))
         # every layer's k_norm weight, for the one-launch key rotation of all layers (ops.qk_norm_rope_groups)
-        self.k_norm_all = _f32(torch.cat([sd[f"{vt}transformer.layers.{i}.multihead_attn.k_norm.weight"]
+        self.k_norm_all = _f32(torch.cat([qk_rows(sd[f"{vt}transformer.layers.{i}.multihead_attn.k_norm.weight"])
                                           for i in range(cfg.view_transformer_n_layers)]), device)
         self.ctx_unit = torch.ones(self.wkv_all.shape[1], dtype=torch.float32, device=device)
         self.dpt = DPTHead(sd, vt + "out_dpt", device, precision=dpt_precision)
@@ -626,7 +629,7 @@ class RenderFormer:
             kv = dict(ctx_norm=W.ctx_unit if kv_batch else None, w_kv_all=W.wkv_all if kv_batch else None,
                       k_batch=k_batch, k_norm_all=W.k_norm_all if qk else None, kv_src_rows=plan.kv_src_rows,
                       kv_pos=pos2, freqs=W.dec_freqs)
-            cross = dict(ray_pos=ray_pos, ray_pos_div=R, problems=plan.prob2, schedule=plan.sched2)
+            cross = dict(ray_pos=ray_pos, ray_pos_div=R, problems=plan.prob2, schedule=plan.sched2, qk_fused=W.qk_fused)
             sa = dict(swin=swin, n_images=P, grid_h=plan.hp, grid_w=plan.wp, window=SWIN_WINDOW, shift=SWIN_SHIFT,
                       problems=None if swin else plan.prob_self)
             ops.decoder_forward(x, W.dec_desc, n_dec, H, F, W.half, EPS, ctx, kv, cross, sa,
@@ -649,7 +652,7 @@ class RenderFormer:
             # its rotated copy the D columns at D*i of kview_all
             kview_all = torch.empty(plan.T_kv, n_dec * D, dtype=torch.bfloat16, device=dev)
             ops.qk_norm_rope_groups(kv_all, 2 * D, kview_all, D, n_dec, H, W.k_norm_all if qk else None, EPS, pos2,
-                                    W.dec_freqs, src_rows=plan.kv_src_rows)
+                                    W.dec_freqs, src_rows=plan.kv_src_rows, ilv=W.qk_fused)
         else:
             kview = torch.empty(plan.T_kv, D, dtype=torch.bfloat16, device=dev)
         qkv = torch.empty(T2, 3 * D, dtype=torch.bfloat16, device=dev) if cfg.view_transformer_include_self_attn else None
@@ -674,6 +677,9 @@ class RenderFormer:
         defer = not fp8
         ss = torch.empty(T2, ops.PRENORM_SLOTS, dtype=torch.float32, device=dev) if defer else None
         qkss = torch.empty(T2, 2, ops.PRENORM_SLOTS, dtype=torch.float32, device=dev) if defer and swin and qk else None
+        # the cross-attention query's rotation in its projection's epilogue (rf_decoder_forward's qk_fused sequence)
+        qfuse = W.qk_fused and defer
+        q2ss = torch.empty(T2, 1, ops.PRENORM_SLOTS, dtype=torch.float32, device=dev) if qfuse and qk else None
 
         def norm_proj(norm_w, w_half, w_fp8, out, epi=ops.EPI_BF16, tag=None, name=""):
             """out (epi)= rmsnorm(x) @ w.T: from the deferred operands, or row kernel + proj in the fp8 mode"""
@@ -694,7 +700,11 @@ class RenderFormer:
             ops.prenorm(x, W.dec[0].query_norm, h, ss)
         for i, L in enumerate(W.dec):
             # (i) cross-attention: K/V projections once per scene, K rotated per view
-            norm_proj(L.query_norm, L.wq, getattr(L, "wq8", None), q2, name="q")
+            if qfuse:
+                ops.gemm_qk_rope(h, L.wq, q2, ss, EPS, D, 1, L.q_norm if qk else None, q2ss, ray_pos, W.dec_freqs,
+                                 q_scale=1.0 if qk else ops.Q_LOG2_SCALE, pos_div=R)
+            else:
+                norm_proj(L.query_norm, L.wq, getattr(L, "wq8", None), q2, name="q")
             if kv_batch:
                 kv = kv_all[:, 2 * D * i:2 * D * (i + 1)]
             else:
@@ -702,13 +712,18 @@ class RenderFormer:
                 ops.gemm(hc, L.wkv, kv)
             if k_batch:
                 kview = kview_all[:, D * i:D * (i + 1)]
-            ops.qk_norm_rope(q2, q2, H, L.q_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R,
-                             q_scale=ops.Q_LOG2_SCALE)
+            if not qfuse:
+                ops.qk_norm_rope(q2, q2, H, L.q_norm if qk else None, EPS, ray_pos, W.dec_freqs, pos_div=R,
+                                 q_scale=ops.Q_LOG2_SCALE, ilv=W.qk_fused)
             if not k_batch:
-                ops.qk_norm_rope(kv[:, :D], kview, H, L.k_norm if qk else None, EPS, pos2, W.dec_freqs,
-                                 src_rows=plan.kv_src_rows)
-            ops.attention(q2, kview, kv[:, D:], att, plan.prob2, R, H, tag="attn_cross", max_k_len=plan.max_s,
-                          q_prescaled=True, schedule=plan.sched2)
+                ops.qk_norm_rope_groups(kv[:, :D], 0, kview, 0, 1, H, L.k_norm if qk else None, EPS, pos2, W.dec_freqs,
+                                        src_rows=plan.kv_src_rows, ilv=W.qk_fused)
+            if q2ss is not None:
+                ops.attention(q2, kview, kv[:, D:], att, plan.prob2, R, H, tag="attn_cross", max_k_len=plan.max_s,
+                              schedule=plan.sched2, q_ss=q2ss[:, 0], q_eps=EPS)
+            else:
+                ops.attention(q2, kview, kv[:, D:], att, plan.prob2, R, H, tag="attn_cross", max_k_len=plan.max_s,
+                              q_prescaled=True, schedule=plan.sched2)
             add_proj(att, L.wo, getattr(L, "wo8", None), L.self_norm if qkv is not None else L.ffn_norm, name="out")
             # (ii) self-attention between ray tokens
             if qkv is not None:

@@ -309,10 +309,12 @@ def gemm_rownorm(xg: torch.Tensor, w: torch.Tensor, out: torch.Tensor, ss: torch
 
 def qk_norm_rope(src: torch.Tensor, dst: torch.Tensor, n_heads: int, norm_w: Optional[torch.Tensor], eps: float,
                  pos: Optional[torch.Tensor] = None, freqs: Optional[torch.Tensor] = None, pos_div: int = 1,
-                 src_rows: Optional[torch.Tensor] = None, n_seg: int = 1, q_scale: float = 1.0) -> torch.Tensor:
+                 src_rows: Optional[torch.Tensor] = None, n_seg: int = 1, q_scale: float = 1.0,
+                 ilv: bool = False) -> torch.Tensor:
     """dst[r] = rope(rmsnorm(src[src_rows[r]])) over the full width (attention.py:127-141), for n_seg
     consecutive width-(n_heads*128) segments (q and k of a qkv row) with weights norm_w [n_seg*dim].
-    Segment 0 is also multiplied by q_scale (Q_LOG2_SCALE pre-scales q for attention(scale=LN2))."""
+    Segment 0 is also multiplied by q_scale (Q_LOG2_SCALE pre-scales q for attention(scale=LN2)).
+    ilv: rows (and norm_w) in rope_pair_perm's pair-interleaved order (rf_qk_norm_rope_groups_ilv)."""
     _dev(src, torch.bfloat16, "src")
     _dev(dst, torch.bfloat16, "dst")
     rows, width = dst.shape
@@ -327,6 +329,11 @@ def qk_norm_rope(src: torch.Tensor, dst: torch.Tensor, n_heads: int, norm_w: Opt
     if pos is not None:
         _dev(pos, torch.float32, "pos")
         _check(pos.shape[1] == 9 and freqs is not None, "qk_norm_rope: pos must be [*, 9] with freqs")
+    if ilv:  # one group of n_seg segments
+        call("rf_qk_norm_rope_groups_ilv", ptr(src), src.stride(0), 0, ptr(dst), dst.stride(0), 0, ptr(src_rows), rows,
+             dim, n_heads, n_seg, 1, ptr(norm_w), 0, eps, q_scale, ptr(pos), pos.stride(0) if pos is not None else 0,
+             pos_div, ptr(freqs), freqs.numel() if freqs is not None else 0, stream())
+        return dst
     call("rf_qk_norm_rope", ptr(src), src.stride(0), ptr(dst), dst.stride(0), ptr(src_rows), rows, dim, n_heads,
          n_seg, ptr(norm_w), eps, q_scale, ptr(pos), pos.stride(0) if pos is not None else 0, pos_div, ptr(freqs),
          freqs.numel() if freqs is not None else 0, stream())
@@ -336,7 +343,7 @@ def qk_norm_rope(src: torch.Tensor, dst: torch.Tensor, n_heads: int, norm_w: Opt
 def qk_norm_rope_groups(src: torch.Tensor, src_gstride: int, dst: torch.Tensor, dst_gstride: int, n_groups: int,
                         n_heads: int, norm_w: Optional[torch.Tensor], eps: float, pos: Optional[torch.Tensor] = None,
                         freqs: Optional[torch.Tensor] = None, src_rows: Optional[torch.Tensor] = None,
-                        seg0_scale: float = 1.0) -> torch.Tensor:
+                        seg0_scale: float = 1.0, ilv: bool = False) -> torch.Tensor:
     """qk_norm_rope (one segment) on n_groups column groups in one launch: group g maps the width-
     (n_heads*128) block at column g*src_gstride of src to column g*dst_gstride of dst with norm weights
     norm_w[g*dim:(g+1)*dim].  src/dst are the full row matrices holding every group.  Every group is also
@@ -357,7 +364,8 @@ def qk_norm_rope_groups(src: torch.Tensor, src_gstride: int, dst: torch.Tensor, 
     if pos is not None:
         _dev(pos, torch.float32, "pos")
         _check(pos.shape[1] == 9 and freqs is not None, "qk_norm_rope_groups: pos must be [*, 9] with freqs")
-    call("rf_qk_norm_rope_groups", ptr(src), src.stride(0), src_gstride, ptr(dst), dst.stride(0), dst_gstride,
+    call("rf_qk_norm_rope_groups_ilv" if ilv else "rf_qk_norm_rope_groups", ptr(src), src.stride(0), src_gstride,
+         ptr(dst), dst.stride(0), dst_gstride,
          ptr(src_rows), rows, dim, n_heads, 1, n_groups, ptr(norm_w), dim, eps, float(seg0_scale), ptr(pos),
          pos.stride(0) if pos is not None else 0, 1, ptr(freqs), freqs.numel() if freqs is not None else 0, stream())
     return dst
@@ -432,7 +440,7 @@ def rope_pair_perm(dim: int) -> torch.Tensor:
 def gemm_qk_rope(xg: torch.Tensor, w: torch.Tensor, out: torch.Tensor, ss: Optional[torch.Tensor], eps: float,
                  seg_w: int, n_seg: int, norm_w: Optional[torch.Tensor], seg_ss: Optional[torch.Tensor],
                  pos: Optional[torch.Tensor], freqs: Optional[torch.Tensor], q_scale: float = 1.0,
-                 tag: Optional[str] = None) -> torch.Tensor:
+                 tag: Optional[str] = None, pos_div: int = 1) -> torch.Tensor:
     """rf_gemm_qk_rope: out (bf16) = the q/k(/v) projection of the deferred-norm operand xg (1 / rms(x) from ss, as
     gemm_rownorm) with, on its first n_seg segments of seg_w columns (rows of w permuted by rope_pair_perm),
     rope(norm_w * y) written (segment 0 also times q_scale) and seg_ss [M, n_seg, 8] = partial sums of y^2 when
@@ -455,12 +463,13 @@ def gemm_qk_rope(xg: torch.Tensor, w: torch.Tensor, out: torch.Tensor, ss: Optio
                "gemm_qk_rope: seg_ss [M, n_seg, 8]")
     if pos is not None:
         _dev(pos, torch.float32, "pos")
-        _check(pos.shape[0] >= m and pos.shape[1] >= 9 and freqs is not None, "gemm_qk_rope: pos [M, 9] with freqs")
+        _check(pos.shape[0] >= (m + pos_div - 1) // pos_div and pos.shape[1] >= 9 and freqs is not None,
+               "gemm_qk_rope: pos [M / pos_div, 9] with freqs")
     ws = _gemm_workspace(xg.device)
     _t0(tag)
     call("rf_gemm_qk_rope", ptr(xg), xg.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), m, n, k, ptr(ss),
          k, eps, ptr(seg_ss) if norm_w is not None else None, seg_w, n_seg, ptr(norm_w), ptr(pos),
-         pos.stride(0) if pos is not None else 0, ptr(freqs), freqs.numel() if (pos is not None) else 0,
+         pos.stride(0) if pos is not None else 0, pos_div, ptr(freqs), freqs.numel() if (pos is not None) else 0,
          float(q_scale), _dt(xg), ptr(ws), ws.numel(), stream())
     return out
 
@@ -613,7 +622,8 @@ def decoder_forward(x: torch.Tensor, layers, n_layers: int, n_heads: int, ffn_di
                     tag: Optional[str] = None) -> torch.Tensor:
     """x [T2, D] f32 through the whole decoder stack in place, one C call (rf_decoder_forward; `layers` from
     decoder_layers).  kv: ctx_norm, w_kv_all (None = per-layer K/V), k_batch, k_norm_all, kv_src_rows, kv_pos,
-    freqs; cross: ray_pos, ray_pos_div, problems, schedule; self_attn: swin, n_images, grid_h, grid_w, window, shift,
+    freqs; cross: ray_pos, ray_pos_div, problems, schedule, qk_fused (the q/k weights in rope_pair_perm order: the
+    query rotation in its projection's epilogue); self_attn: swin, n_images, grid_h, grid_w, window, shift,
     problems; taps: (layer, planes_hi, planes_lo or None, ld) in layer order."""
     from ._lib import DecoderDesc, DecoderTap
     import ctypes
@@ -658,6 +668,7 @@ def decoder_forward(x: torch.Tensor, layers, n_layers: int, n_heads: int, ffn_di
     ws = torch.empty(int(lib.rf_decoder_workspace_bytes(ctypes.addressof(d))), dtype=torch.uint8, device=x.device)
     d.workspace = ptr(ws)
     d.timer_cross = int(_timer_takes(tag, n_layers))
+    d.qk_fused = int(bool(cross.get("qk_fused")))
     call("rf_decoder_forward", ptr(x), x.stride(0), ctypes.addressof(d), stream())
     return x
 

@@ -135,6 +135,36 @@ def test_attention_q_ss_equals_prescaled_q():
     assert err < 2e-3
 
 
+@pytest.mark.parametrize("n_groups,with_norm", [(3, True), (1, False), (10, True)])
+def test_qk_norm_rope_groups_ilv_equals_standard_layout(n_groups, with_norm):
+    """rf_qk_norm_rope_groups_ilv on rows in the pair-interleaved order (the stage-2 keys when the queries are rotated
+    in their projection's epilogue) equals rf_qk_norm_rope_groups on the standard layout, permuted the same way (up to
+    the order of the row's sum of squares)."""
+    ops = _ops()
+    T, H = 211, 8
+    D = H * 128
+    g = torch.Generator().manual_seed(n_groups)
+    kv = torch.randn(T, n_groups * 2 * D, generator=g).bfloat16()
+    w = torch.rand(n_groups * D, generator=g) + 0.5
+    rows = torch.tensor(list(range(T)) + list(range(0, T, 3)), dtype=torch.int32)
+    pos = torch.rand(rows.numel(), 9, generator=g) * 2 - 1
+    freqs = 2 ** torch.linspace(0, math.log2(5), 6)
+    perm = ops.rope_pair_perm(D)
+    cperm = torch.cat([torch.cat([perm + 2 * D * i, torch.arange(D, 2 * D) + 2 * D * i]) for i in range(n_groups)])
+    wperm = torch.cat([perm + D * i for i in range(n_groups)])
+    std = torch.empty(rows.numel(), n_groups * D, dtype=torch.bfloat16, device=dev)
+    ilv = torch.empty_like(std)
+    ops.qk_norm_rope_groups(kv.to(dev), 2 * D, std, D, n_groups, H, w.to(dev) if with_norm else None, 1e-6,
+                            pos.to(dev), freqs.to(dev), src_rows=rows.to(dev))
+    ops.qk_norm_rope_groups(kv[:, cperm].contiguous().to(dev), 2 * D, ilv, D, n_groups, H,
+                            w[wperm].to(dev) if with_norm else None, 1e-6, pos.to(dev), freqs.to(dev),
+                            src_rows=rows.to(dev), ilv=True)
+    a, b = ilv.float().cpu(), std.float().cpu()[:, wperm]
+    e = float((a - b).norm() / b.norm())
+    print(f"ilv vs standard: rel L2 {e:.2e}, max |diff| {float((a - b).abs().max()):.2e}")
+    assert e < 1e-3
+
+
 def _stage1_rows(fuse, monkeypatch, name="large_cbox_r512"):
     from renderformer_amd import RenderFormer, RenderFormerRenderingPipeline
     monkeypatch.setenv("RF_QK_FUSE", "1" if fuse else "0")
@@ -146,9 +176,10 @@ def _stage1_rows(fuse, monkeypatch, name="large_cbox_r512"):
     return out.cpu(), z
 
 
-def test_stage1_fused_matches_unfused_and_reference(monkeypatch):
-    """The whole frame at config 2's size with the fused QK path (default) and the row-kernel path: both inside the
-    1e-3 bar of the reference fixture and within 2e-4 of each other (different rounding points, same arithmetic)."""
+def test_qk_fused_matches_unfused_and_reference(monkeypatch):
+    """The whole frame at config 2's size with the fused QK path (default: stage 1 and the cross-attention queries) and
+    the row-kernel path: both inside the 1e-3 bar of the reference fixture and within 2e-4 of each other (different
+    rounding points, same arithmetic)."""
     from golden_util import reference_hdr
     a, z = _stage1_rows(True, monkeypatch)
     b, _ = _stage1_rows(False, monkeypatch)

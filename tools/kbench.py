@@ -314,6 +314,39 @@ def coldgemm():
         torch.cuda.empty_cache()
 
 
+def mx8():
+    """The MX fp8 GEMM (rf_gemm_mx8) against the engine on fp16 operands at config 5's stage-2 shapes (24 views at
+    1024^2 have 393,216 ray rows; KB_MX8_ROWS rows here, default 98,304 = 6 views), operands resident (the fp8 study:
+    what bounds rf_gemm_mx8).  KB_MX8_ONLY=1 runs only the fp8 legs (for counter passes)."""
+    m = int(os.environ.get("KB_MX8_ROWS", "98304"))
+    only = os.environ.get("KB_MX8_ONLY") == "1"
+    for name, n, k, epi in (("s2 w2", D, F, ops.EPI_ADD_F32), ("s2 q", D, D, ops.EPI_BF16),
+                            ("s2 w13", 2 * F, D, ops.EPI_SWIGLU)):
+        a = torch.randn(m, k, device=dev).bfloat16()
+        w = (torch.randn(n, k, device=dev) / math.sqrt(k)).bfloat16()
+        ncol = n // 2 if epi == ops.EPI_SWIGLU else n
+        odt = torch.float32 if epi == ops.EPI_ADD_F32 else torch.bfloat16
+        c8 = torch.zeros(m, ncol, device=dev, dtype=odt)
+        aq, wq = ops.quant_mx8(a), ops.MX8(*ops.mx8_quant_ref(w))
+        fl = 2 * m * n * k
+        ms = timeit(lambda: ops.gemm_mx8(aq, wq, c8, None, epi), reps=10)
+        print(f"mx8  {name:7s} {m}x{n}x{k}: {ms*1e3:9.1f} us  {fl/ms/1e9:7.1f} TF  ({fl/ms/1e9/5000:.3f} of 5 PF fp8)",
+              flush=True)
+        if not only:
+            msq = timeit(lambda: ops.quant_mx8(a, aq), reps=10)
+            print(f"quant {name:7s} {m}x{k}: {msq*1e3:9.1f} us", flush=True)
+            ah, wh = a.half(), w.half()
+            ch = torch.zeros(m, ncol, device=dev, dtype=torch.float32 if epi == ops.EPI_ADD_F32 else torch.float16)
+            msh = timeit(lambda: ops.gemm(ah, wh, ch, None, epi), reps=10)
+            print(f"f16  {name:7s} {m}x{n}x{k}: {msh*1e3:9.1f} us  {fl/msh/1e9:7.1f} TF  ({fl/msh/1e9/2500:.3f} of 2.5 PF)",
+                  flush=True)
+        del a, w, c8, aq, wq
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "mx8":
+    mx8()
+
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "coldgemm":
     coldgemm()
 
