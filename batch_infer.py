@@ -78,6 +78,15 @@ def collate(items):
 
 LOADERS = int(os.environ.get("RF_BATCH_LOADERS", "3"))  # batches decoded ahead (threads)
 WRITERS = 4  # image encode/write threads
+DEPTH = max(1, int(os.environ.get("RF_BATCH_DEPTH", "2")))  # batches in flight behind the one being issued
+
+
+def _one_omp_thread():
+    """Pool-thread initializer: the loader / writer threads' own torch CPU ops run single-threaded.  Every thread that
+    enters an OpenMP region gets its own team of workers (libgomp), which spin after each region: 3 loaders + 4 writers
+    on a 16-thread host made ~100 extra threads that burned ~0.1 CPU-s per frame (profiles/r6_host_budget.txt),
+    the cores the HDF5 inflate pool needs."""
+    torch.set_num_threads(1)
 
 
 class StageTimes:
@@ -124,6 +133,71 @@ class StageTimes:
 
 
 STAGES = StageTimes()
+
+
+class ThreadCpu:
+    """Profiling only (RF_BATCH_PROFILE): CPU seconds of every OS thread of this process over the data path, from
+    /proc/self/task/<tid>/stat sampled every 0.2 s (a thread that exits between samples loses at most one period),
+    labelled by the Python thread's name (pool suffix dropped) or, for threads Python did not start (torch's
+    OpenMP workers, the HIP runtime's), by the kernel's comm name -- where the host budget's cores go."""
+
+    def __init__(self):
+        import threading
+        self._tick = os.sysconf("SC_CLK_TCK")
+        self._first, self._last, self._label, self._wchan = {}, {}, {}, {}
+        self._stop = threading.Event()
+        self._started = False
+        self._sample()  # threads alive now count from here; threads born later from zero
+        self._started = True
+        self._t = threading.Thread(target=self._run, name="rf_cpu_sampler", daemon=True)
+        self._t.start()
+
+    def _sample(self):
+        import re
+        import threading
+        names = {t.native_id: re.sub(r"_\d+$", "", t.name) for t in threading.enumerate()}
+        try:
+            tids = os.listdir("/proc/self/task")
+        except OSError:
+            return
+        for tid in tids:
+            try:
+                with open(f"/proc/self/task/{tid}/stat") as f:
+                    st = f.read()
+            except OSError:
+                continue
+            comm = st[st.index("(") + 1:st.rindex(")")]
+            fields = st[st.rindex(")") + 2:].split()
+            cpu = (int(fields[11]) + int(fields[12])) / self._tick  # utime + stime
+            t = int(tid)
+            self._first.setdefault(t, cpu if not self._started else 0.0)
+            self._last[t] = cpu
+            self._label.setdefault(t, names.get(t) or "os:" + comm)
+            if self._label[t].startswith("os:"):  # where a foreign thread sleeps ("0": running), most frequent wins
+                try:
+                    with open(f"/proc/self/task/{tid}/wchan") as f:
+                        w = f.read().strip() or "0"
+                except OSError:
+                    w = "?"
+                c = self._wchan.setdefault(t, {})
+                c[w] = c.get(w, 0) + 1
+
+    def _run(self):
+        while not self._stop.wait(0.2):
+            self._sample()
+
+    def stop(self) -> dict:
+        self._stop.set()
+        self._t.join()
+        self._sample()
+        out = {}
+        for t, c in self._last.items():
+            lab = self._label[t]
+            if t in self._wchan:
+                lab += "@" + max(self._wchan[t].items(), key=lambda x: x[1])[0]
+            n, s = out.get(lab, (0, 0.0))
+            out[lab] = (n + 1, s + c - self._first[t])
+        return {k: {"threads": n, "cpu_s": round(s, 3)} for k, (n, s) in sorted(out.items(), key=lambda x: -x[1][1])}
 
 
 def _load_batch(files, idx, padding_length, pin):
@@ -215,7 +289,7 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
             yield items, imgs.cpu()
         return
     # HDF5 decode (zlib releases the GIL) runs LOADERS batches ahead on a thread pool, consumed in order
-    pool = ThreadPoolExecutor(max_workers=LOADERS)
+    pool = ThreadPoolExecutor(max_workers=LOADERS, thread_name_prefix="rf_loader", initializer=_one_omp_thread)
     ahead = [pool.submit(_load_batch, files, idx, args.padding_length, True) for idx in batches[:LOADERS]]
     nxt_batch = len(ahead)
 
@@ -238,7 +312,9 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
     h2d = torch.cuda.Stream(device=dev)
     d2h = torch.cuda.Stream(device=dev)
     compute = torch.cuda.current_stream(dev)
-    pending = None  # (items, pinned host images, their copy event, pinned inputs) of the previous batch
+    # (items, pinned host images, their copy event, pinned inputs, device images) of the batches in flight: batch i is
+    # handed out once batch i + DEPTH is issued, so a late loader or a slow issue does not drain the GPU's queue
+    pending = []
     while True:
         got = loaded.get()
         if isinstance(got, BaseException):
@@ -263,8 +339,10 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
                 copied.record(d2h)
             imgs.record_stream(d2h)
             nxt = (items, out, copied, host, imgs)  # `host` (pinned inputs) lives until this batch is yielded
-        if pending is not None:  # batch i is handed out while batch i+1 renders
-            p_items, p_out, p_copied, _, p_imgs = pending
+        if nxt is not None:
+            pending.append(nxt)
+        while pending and (len(pending) > DEPTH or nxt is None):  # batch i is handed out while i+1.. render
+            p_items, p_out, p_copied, _, p_imgs = pending.pop(0)
             STAGES.timed("main: wait for frame + D2H", p_copied.synchronize)
             # the frame is complete: its fp16 range check reads a host word (no wait); a frame that overflowed is
             # rendered again in place, and copied back again
@@ -275,7 +353,6 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
             STAGES.add("main: consumer (writer submission)", time.perf_counter() - t_y)
         if nxt is None:
             return
-        pending = nxt
 
 
 def main(argv=None, pipeline=None):
@@ -304,9 +381,11 @@ def main(argv=None, pipeline=None):
     STAGES.add("main: model build (load_pipeline)", time.perf_counter() - t_build)
     t_loop = time.perf_counter()
     cpu0 = time.process_time()  # every thread of this process (loader, chunk decode pool, main, writers)
+    threads = None
     if STAGES.on:
         from renderformer_amd import h5io
         h5io.CPU_HOOK = lambda dt: STAGES.add("cpu: h5 chunk decode", dt)
+        threads = ThreadCpu()
     cfg = pipeline.config
     if world > 1:
         costs = []
@@ -322,7 +401,8 @@ def main(argv=None, pipeline=None):
     batches = [mine[b0:b0 + args.batch_size] for b0 in range(0, len(mine), args.batch_size)]
     n_frames = 0
     inline = os.environ.get("RF_BATCH_INLINE", "0") != "0"
-    writers = None if inline else ThreadPoolExecutor(max_workers=WRITERS)
+    writers = None if inline else ThreadPoolExecutor(max_workers=WRITERS, thread_name_prefix="rf_writer",
+                                                    initializer=_one_omp_thread)
     pending = []
     for items, imgs in render_batches(pipeline, files, batches, args, pipelined=not inline):
         for i, it in enumerate(items):
@@ -345,6 +425,7 @@ def main(argv=None, pipeline=None):
         h5io.CPU_HOOK = None
         print("stage times:", json.dumps(STAGES.summary()), flush=True)
         print("host budget:", json.dumps(STAGES.host_budget(n_frames, wall, time.process_time() - cpu0)), flush=True)
+        print("thread cpu:", json.dumps(threads.stop()), flush=True)
     if args.save_video:
         print("video.mp4 not written: no mp4 encoder in this environment (frames are saved as PNG)")
     return 0

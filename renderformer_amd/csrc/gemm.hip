@@ -101,6 +101,7 @@ struct EngineArgs {
     const uint8_t* sw;
     int ld_sa, ld_sw;
     int persist;  // phased_sk_kernel: whole tiles strided over the grid, next tile's first K-tiles prefetched
+    int l2pf;     // phased3 loop: L2 run-ahead distance in K-tiles (0: off; RF_GEMM_L2PF)
     int out_f16;  // E_BF16 / E_SWIGLU: 16-bit output as fp16 instead of bf16 (rf_gemm_f16's RF_EPI_*_F16)
     int* range;   // fp16 outputs (out_f16, fp16 conv planes): the mapped range flag, raised on |x| > 65504
     // Deferred RMSNorm (rf_gemm_add_prenorm / rf_gemm_rownorm, rf.h).  Producer (E_ADD, xg set): besides the
@@ -1178,7 +1179,7 @@ RF_DEV void phased_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int
 // Same stagger (waves 4-7 one section behind), same one counted vmcnt per K-tile.
 template <int BM, int NTERM, bool INITC>
 RF_DEV void phased3_mainloop(const EngineArgs& p, char* smem, int m0, int n0, int kbeg, int kend,
-                             f32x4 (&acc)[BM / 32][4]) {
+                             f32x4 (&acc)[BM / 32][4], char* touch_lds = nullptr) {
     using namespace ph;
     using G = Cfg<BM>;
     static_assert(BM <= 128, "three-buffer loop: short tiles");
@@ -1219,6 +1220,23 @@ RF_DEV void phased3_mainloop(const EngineArgs& p, char* smem, int m0, int n0, in
                 __builtin_amdgcn_global_load_lds(GLB_PTR(void, src[r] + k0 + ch * 8), LDS_PTR(void, dst), 16, 0, 0);
             }
         }
+    };
+    // L2 run-ahead (study build, p.l2pf = P > 0, RF_GEMM_L2PF): after K-tile kt's LDS-DMA every lane issues one 4-B
+    // LDS-DMA "touch" of one 128-B line of K-tile kt + P (thread t: A row t, then the 256 W rows; the rest repeat W
+    // rows) into a dummy LDS word, so the tile's lines are in L2 when its real DMA issues P K-tiles later.  One more
+    // vector-memory op per K-tile per wave: the counted waits below include it.  Measured 29-32 % SLOWER at every
+    // P = 1..4 (profiles/r6_gemm_l2_runahead.txt): a 64-row touch costs the CU's address path about what two
+    // operand pieces do, and the pieces' intake did not rise; production passes no touch area (l2pf = 0).
+    const int l2pf = touch_lds ? p.l2pf : 0;
+    const bf16_t* tsrc;
+    {
+        const int t = threadIdx.x;
+        tsrc = t < BM ? p.a + (int64_t)min(m0 + t, p.m - 1) * p.lda
+                      : p.w + (int64_t)(n0 + (t - BM) % 256) * p.ldw;
+    }
+    auto touch = [&](int kt) {
+        const int kk = min(kt + l2pf, nk - 1);
+        __builtin_amdgcn_global_load_lds(GLB_PTR(void, tsrc + (kbeg + kk) * BK2), LDS_PTR(void, touch_lds), 4, 0, 0);
     };
     if (INITC && kbeg == 0) {
         load_c_acc<BM / 32, 4>(p, m0 + wr * (BM / 2), n0 + wc * 64, acc);
@@ -1274,10 +1292,17 @@ RF_DEV void phased3_mainloop(const EngineArgs& p, char* smem, int m0, int n0, in
     };
     // prologue: tiles 0 and 1 in flight, wait for tile 0 (this wave's 6 LDS-DMA per tile, 4 without RA)
     issue_tile(0);
+    if (l2pf) touch(0);
     if (nk > 1) {
         issue_tile(1);
-        if (has_a) wait_vm<6>();
-        else wait_vm<4>();
+        if (l2pf) {
+            touch(1);
+            if (has_a) wait_vm<8>();
+            else wait_vm<6>();
+        } else {
+            if (has_a) wait_vm<6>();
+            else wait_vm<4>();
+        }
     } else {
         wait_vm<0>();
     }
@@ -1291,15 +1316,23 @@ RF_DEV void phased3_mainloop(const EngineArgs& p, char* smem, int m0, int n0, in
         // phase 0: A + B(n0); tile t+2 into the buffer tile t-1 used
         read_b(buf, 0, fb0);
         read_a(buf);
-        if (t + 2 < nk) issue_tile(t + 2);
+        if (t + 2 < nk) {
+            issue_tile(t + 2);
+            if (l2pf) touch(t + 2);
+        }
         sync_in();
         mma(0, fb0);
         sync_out();
         // phase 1: B(n1); publish tile t+1 (tile t+2 stays in flight)
         read_b(buf, 1, fb1);
         if (t + 2 < nk) {
-            if (has_a) wait_vm<6>();
-            else wait_vm<4>();
+            if (l2pf) {
+                if (has_a) wait_vm<8>();
+                else wait_vm<6>();
+            } else {
+                if (has_a) wait_vm<6>();
+                else wait_vm<4>();
+            }
         } else {
             wait_vm<0>();
         }
@@ -1313,7 +1346,11 @@ RF_DEV void phased3_mainloop(const EngineArgs& p, char* smem, int m0, int n0, in
 template <int BM, int EPI, int NTERM = 1>
 __global__ __launch_bounds__(512, 1) void phased3_kernel(EngineArgs p) {
     using TE = Tile<BM, 256, 2, 4, 4>;  // the epilogue's view of the block
+#ifdef RF_STUDY
+    __shared__ __attribute__((aligned(16))) char smem[3 * ph::Cfg<BM>::TILE + PN_AREA<TE, EPI> + 256];
+#else
     __shared__ __attribute__((aligned(16))) char smem[3 * ph::Cfg<BM>::TILE + PN_AREA<TE, EPI>];
+#endif
     if (gated_off(p)) return;
     const int tiles_m = (p.m + BM - 1) / BM;
     const int nwg = gridDim.x;
@@ -1325,7 +1362,12 @@ __global__ __launch_bounds__(512, 1) void phased3_kernel(EngineArgs p) {
     f32x4 acc[BM / 32][4];
     char* const area = smem + 3 * ph::Cfg<BM>::TILE;
     pn_issue<TE, EPI>(p, area, tm * BM, tn * ph::BN);
-    phased3_mainloop<BM, NTERM, EPI == E_ADD>(p, smem, tm * BM, tn * ph::BN, 0, p.k / ph::BK2, acc);
+#ifdef RF_STUDY  // the L2 run-ahead study (RF_GEMM_L2PF; profiles/r6_gemm_l2_runahead.txt): study build only
+    char* const touch = area + PN_AREA<TE, EPI>;
+#else
+    char* const touch = nullptr;
+#endif
+    phased3_mainloop<BM, NTERM, EPI == E_ADD>(p, smem, tm * BM, tn * ph::BN, 0, p.k / ph::BK2, acc, touch);
     engine_epilogue<TE, EPI>(p, tm * BM, tn * ph::BN, acc, area);
 }
 
@@ -2983,8 +3025,15 @@ using T64x256w4k2 = Tile<64, 256, 1, 4, 3, 2>;
 using T64c = Tile<64, 64, 2, 2, 8>;
 using T64x128c = Tile<64, 128, 2, 2, 6>;
 
-int pick_group_m(int tiles_m, int tiles_n, int bm, int bn, int64_t per_xcd) {
+// a_bytes: the A operand's bytes.  Past 192 MiB (3/4 of the 256 MiB Infinity Cache; config 5's W2 / larger views) A
+// streams from HBM and the square
+// raster below has an XCD's 32 co-running blocks on 32 different m-tiles of one n column, so every A panel is fetched
+// once per n-tile; with few n-tiles (N <= 2,048) the co-running blocks instead take 32 / tiles_n m-tiles x every n
+// column, and each A panel is fetched once per XCD (rf_gemm_mx8 W2 at 98,304 rows: 845 -> 748 us, the f16 engine
+// 814 -> 762: profiles/r6_mx8_raster.txt)
+int pick_group_m(int tiles_m, int tiles_n, int bm, int bn, int64_t per_xcd, int64_t a_bytes = 0) {
     if (const char* env = getenv("RF_GEMM_GROUP_M")) return std::max(1, std::min(tiles_m, atoi(env)));
+    if (a_bytes > (192ll << 20) && tiles_n <= 8) return std::max(1, std::min(tiles_m, 32 / tiles_n));
     const double g = std::sqrt((double)per_xcd * bn / bm);
     int gm = (int)(g + 0.5);
     gm = std::max(1, std::min(gm, tiles_m));
@@ -2996,7 +3045,7 @@ template <class C, int EPI, int NTERM, bool GATHER = false>
 int launch(EngineArgs a, void* stream, const char* what) {
     const int tiles_m = (a.m + C::BM - 1) / C::BM, tiles_n = a.n / C::BN;
     const int nwg = tiles_n * tiles_m;
-    a.group_m = pick_group_m(tiles_m, tiles_n, C::BM, C::BN, (nwg + 7) / 8);
+    a.group_m = pick_group_m(tiles_m, tiles_n, C::BM, C::BN, (nwg + 7) / 8, GATHER ? 0 : (int64_t)a.m * a.k * 2);
     RF_LAUNCH((engine_kernel<C, EPI, NTERM, GATHER, false>), dim3(nwg), dim3(C::THREADS), 0, (hipStream_t)stream,
                        a);
     return rf::check_launch(what);
@@ -3487,7 +3536,7 @@ template <int EPI, int NTERM, bool GATHER, int BM = 256>
 int launch_phased(EngineArgs a, void* stream, const char* what) {
     const int tiles_m = (a.m + BM - 1) / BM, tiles_n = a.n / 256;
     const int nwg = tiles_n * tiles_m;
-    a.group_m = pick_group_m(tiles_m, tiles_n, BM, 256, (nwg + 7) / 8);
+    a.group_m = pick_group_m(tiles_m, tiles_n, BM, 256, (nwg + 7) / 8, GATHER ? 0 : (int64_t)a.m * a.k * 2);
     if constexpr (BM == 256 && (NTERM == 1 || NTERM == P_F16) && !GATHER) {
         if (nwg > 256 && persist_on() && (nwg % 256 == 0 || persist_ragged())) {
             a.persist = 1;
@@ -3499,11 +3548,22 @@ int launch_phased(EngineArgs a, void* stream, const char* what) {
     return rf::check_launch(what);
 }
 
+#ifdef RF_STUDY
+// phased3 loop's L2 run-ahead distance (K-tiles; 0 = off): RF_GEMM_L2PF (study build)
+int l2pf_dist() {
+    const char* env = getenv("RF_GEMM_L2PF");
+    return env ? std::max(0, std::min(8, atoi(env))) : 0;
+}
+#endif
+
 template <int EPI, int BM, int NT = 1>
 int launch_phased3(EngineArgs a, void* stream, const char* what) {
+#ifdef RF_STUDY
+    a.l2pf = l2pf_dist();
+#endif
     const int tiles_m = (a.m + BM - 1) / BM, tiles_n = a.n / 256;
     const int nwg = tiles_n * tiles_m;
-    a.group_m = pick_group_m(tiles_m, tiles_n, BM, 256, (nwg + 7) / 8);
+    a.group_m = pick_group_m(tiles_m, tiles_n, BM, 256, (nwg + 7) / 8, (int64_t)a.m * a.k * 2);
     RF_LAUNCH((phased3_kernel<BM, EPI, NT>), dim3(nwg), dim3(512), 0, (hipStream_t)stream, a);
     return rf::check_launch(what);
 }
@@ -4009,7 +4069,7 @@ extern "C" int rf_gemm_mx8(const void* a, int64_t lda, const void* sa, int64_t l
     if (!plain) {
         const int tiles_m = (m + 127) / 128, tiles_n = n / 256;
         const int nwg = tiles_m * tiles_n;
-        p.group_m = pick_group_m(tiles_m, tiles_n, 128, 256, (nwg + 7) / 8);
+        p.group_m = pick_group_m(tiles_m, tiles_n, 128, 256, (nwg + 7) / 8, (int64_t)m * k);
         const dim3 g(nwg), b(512);
         switch (epilogue) {
             case RF_EPI_BF16: RF_LAUNCH((mx8_p3_kernel<E_BF16>), g, b, 0, st, p); break;
@@ -4021,7 +4081,7 @@ extern "C" int rf_gemm_mx8(const void* a, int64_t lda, const void* sa, int64_t l
     }
     const int tiles_m = (m + 255) / 256, tiles_n = n / 256;
     const int nwg = tiles_m * tiles_n;
-    p.group_m = pick_group_m(tiles_m, tiles_n, 256, 256, (nwg + 7) / 8);
+    p.group_m = pick_group_m(tiles_m, tiles_n, 256, 256, (nwg + 7) / 8, (int64_t)m * k);
     const dim3 g(nwg), b(512);
     switch (epilogue) {
         case RF_EPI_BF16: RF_LAUNCH((mx8_kernel<E_BF16>), g, b, 0, st, p); break;

@@ -22,8 +22,11 @@ files written by libhdf5 itself where such files exist on the machine (tests/tes
 """
 from __future__ import annotations
 
+import ctypes
+import ctypes.util
 import os
 import struct
+import threading
 import time
 import zlib
 from typing import Dict, List, Optional, Tuple
@@ -65,6 +68,48 @@ def _decode_pool():
         n = int(os.environ.get("RF_H5_THREADS", "0")) or min(16, host_threads())
         _POOL = ThreadPoolExecutor(max_workers=n, thread_name_prefix="h5inflate") if n > 1 else False
     return _POOL or None
+
+
+_DEFLATE = None  # (libdeflate CDLL, per-thread decompressors) or False
+
+
+def _libdeflate():
+    """The system's libdeflate (ctypes; releases the GIL in the call), or None: inflates the scene texture's
+    deflate chunks ~2-3x faster than zlib, straight into the destination array (no intermediate bytes).
+    RF_H5_LIBDEFLATE=0 keeps zlib."""
+    global _DEFLATE
+    if _DEFLATE is None:
+        _DEFLATE = False
+        if os.environ.get("RF_H5_LIBDEFLATE", "1") != "0":
+            try:
+                lib = ctypes.CDLL(ctypes.util.find_library("deflate") or "libdeflate.so.0")
+                lib.libdeflate_alloc_decompressor.restype = ctypes.c_void_p
+                lib.libdeflate_alloc_decompressor.argtypes = []
+                lib.libdeflate_zlib_decompress.restype = ctypes.c_int
+                lib.libdeflate_zlib_decompress.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t,
+                                                           ctypes.c_void_p, ctypes.c_size_t,
+                                                           ctypes.POINTER(ctypes.c_size_t)]
+                _DEFLATE = (lib, threading.local())
+            except (OSError, AttributeError):
+                pass
+    return _DEFLATE or None
+
+
+def _inflate_into(raw: bytes, dst: np.ndarray) -> bool:
+    """zlib-wrapped deflate stream `raw` decoded into the C-contiguous array `dst`, which it must fill exactly;
+    False (nothing promised about dst) when libdeflate is absent or the stream does not decode to dst's size."""
+    d = _libdeflate()
+    if d is None:
+        return False
+    lib, tls = d
+    h = getattr(tls, "h", None)
+    if h is None:
+        h = tls.h = lib.libdeflate_alloc_decompressor()
+        if not h:
+            return False
+    got = ctypes.c_size_t(0)
+    rc = lib.libdeflate_zlib_decompress(h, raw, len(raw), dst.ctypes.data, dst.nbytes, ctypes.byref(got))
+    return rc == 0 and got.value == dst.nbytes
 
 
 class _Dataset:
@@ -138,8 +183,22 @@ class _Dataset:
             out[...] = 0
         cn = int(np.prod(cshape))
 
+        # deflate alone (the reference's gzip scene files): libdeflate straight into the chunk's slab of `out` when
+        # the chunk is a whole C-contiguous piece of it, else into a chunk-sized scratch array
+        inflate_only = [f[0] for f in self._filters] == [1]
+
         def place(job):
             raw, fmask, sl_out, sl_in = job
+            if inflate_only and not fmask & 1:
+                dst = out[sl_out]
+                if dst.shape == cshape and dst.flags.c_contiguous:
+                    if _inflate_into(raw, dst):
+                        return
+                else:
+                    tmp = np.empty(cshape, dtype=self.dtype)
+                    if _inflate_into(raw, tmp):
+                        dst[...] = tmp[sl_in]
+                        return
             raw = self._unfilter(raw, fmask)
             out[sl_out] = np.frombuffer(raw, dtype=self.dtype, count=cn).reshape(cshape)[sl_in]
         if CPU_HOOK is not None:  # profiling (batch_infer RF_BATCH_PROFILE): CPU seconds of the chunk decode threads

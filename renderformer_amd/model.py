@@ -876,18 +876,19 @@ class RenderFormer:
                               "place before it could be rendered again: call resolve(out) / check_range() before "
                               "reusing input buffers, or use range_check='sync'")
         with self._range_lock:
-            # the weights are rebuilt below, which frees the old tensors into the caching
-            # allocator of the stream they were made on; frames still in flight on other streams read them, so
-            # wait for every pending frame first (an overflow is rare: this wait is the fallback path's only cost)
-            for p in self._range_pending:
-                p.event.synchronize()
             # projections and attention (codes 1/2/4) -> bf16 operands; the DPT planes (code 8) -> bf16x3, and a
             # stage-1 or stage-2 overflow reaches the DPT as inf too, so it sets 8 as well
-            if code & 7:
-                self.operands = "bf16"
-            if code & 8 and self.dpt_precision == "f16":
-                self.dpt_precision = "bf16x3"
-            self._w = _DeviceWeights(self.config, self._sd, self._device, self.dpt_precision, self.operands)
+            operands = "bf16" if code & 7 else self.operands
+            dpt = "bf16x3" if code & 8 and self.dpt_precision == "f16" else self.dpt_precision
+            if (operands, dpt) != (self.operands, self.dpt_precision):  # (a frame that ran before an earlier
+                # fallback only needs its re-render) ADVICE r5 (medium): the weights are rebuilt below, which frees
+                # the old tensors into the caching allocator of the stream they were made on; frames still in flight
+                # on other streams read them, so wait for every pending frame first (an overflow is rare: this wait
+                # is the fallback path's only cost)
+                for p in self._range_pending:
+                    p.event.synchronize()
+                self.operands, self.dpt_precision = operands, dpt
+                self._w = _DeviceWeights(self.config, self._sd, self._device, self.dpt_precision, self.operands)
             self.range_fallbacks += 1
         warnings.warn(f"fp16 operand overflow (range code {code}: {'/'.join(what)}): this checkpoint's activations "
                       f"exceed fp16's range; the frame is rendered again and the model keeps "

@@ -83,3 +83,22 @@ def test_reader_on_libhdf5_files():
                 np.array(f[k])
             except (h5io.H5FormatError, KeyError):
                 pass
+
+
+@pytest.mark.skipif(h5io._libdeflate() is None, reason="no libdeflate on this machine")
+@pytest.mark.parametrize("shape", [(101, 13, 32, 32), (37, 5, 3)])  # 101 rows: a ragged last chunk
+def test_libdeflate_matches_zlib(tmp_path, monkeypatch, shape):
+    """The libdeflate chunk path (whole chunks inflated into `out`, ragged tail chunks through scratch) reads the
+    same bits as zlib, into a fresh array and into read(out=)."""
+    rng = np.random.default_rng(1)
+    a = (rng.standard_normal(shape) * (rng.random(shape) < 0.3)).astype(np.float16)  # compressible, like textures
+    path = str(tmp_path / "t.h5")
+    h5io.write_datasets(path, {"t": a}, max_chunk_bytes=1 << 16, compression_level=9)
+    got = np.array(h5io.File(path)["t"])
+    out = np.full(shape, np.float16(7.0))
+    h5io.File(path)["t"].read(out=out)
+    monkeypatch.setattr(h5io, "_DEFLATE", False)  # zlib only
+    ref = np.array(h5io.File(path)["t"])
+    assert np.array_equal(ref.view(np.uint16), a.view(np.uint16))
+    assert np.array_equal(got.view(np.uint16), ref.view(np.uint16))
+    assert np.array_equal(out.view(np.uint16), ref.view(np.uint16))

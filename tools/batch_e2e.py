@@ -34,7 +34,7 @@ print(f"model build (synthetic 483.9M-parameter weights + upload): {time.perf_co
 batch_infer.main(args + ["--output_dir", os.path.join(root, "warm")], pipeline=pipe)  # first-touch allocations
 res = {}
 os.environ["RF_BATCH_PROFILE"] = "1"  # batch_infer.StageTimes: per-stage host time, printed by each run
-for mode in ("0", "1", "0"):
+for mode in os.environ.get("RF_E2E_MODES", "0,1,0").split(","):  # 0 pipelined, 1 inline
     batch_infer.STAGES.t.clear()
     batch_infer.STAGES.n.clear()
     batch_infer.STAGES.on = True
