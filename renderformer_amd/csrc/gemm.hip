@@ -3033,7 +3033,8 @@ using T64x128c = Tile<64, 128, 2, 2, 6>;
 // 814 -> 762: profiles/r6_mx8_raster.txt)
 int pick_group_m(int tiles_m, int tiles_n, int bm, int bn, int64_t per_xcd, int64_t a_bytes = 0) {
     if (const char* env = getenv("RF_GEMM_GROUP_M")) return std::max(1, std::min(tiles_m, atoi(env)));
-    if (a_bytes > (192ll << 20) && tiles_n <= 8) return std::max(1, std::min(tiles_m, 32 / tiles_n));
+    static const bool stream_raster = !getenv("RF_GEMM_STREAM_RASTER") || atoi(getenv("RF_GEMM_STREAM_RASTER")) != 0;
+    if (stream_raster && a_bytes > (192ll << 20) && tiles_n <= 8) return std::max(1, std::min(tiles_m, 32 / tiles_n));
     const double g = std::sqrt((double)per_xcd * bn / bm);
     int gm = (int)(g + 0.5);
     gm = std::max(1, std::min(gm, tiles_m));

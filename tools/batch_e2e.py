@@ -40,9 +40,16 @@ for mode in os.environ.get("RF_E2E_MODES", "0,1,0").split(","):  # 0 pipelined, 
     batch_infer.STAGES.on = True
     os.environ["RF_BATCH_INLINE"] = mode
     out = os.path.join(root, "out" + mode)
+    import torch
+    keys = ("num_device_alloc", "num_device_free", "num_alloc_retries", "num_sync_all_streams")
+    d0, h0 = torch.cuda.memory_stats(), torch.cuda.host_memory_stats()
     t0 = time.perf_counter()
     batch_infer.main(args + ["--output_dir", out], pipeline=pipe)  # the data path: the model is built once
     dt = time.perf_counter() - t0
+    d1, h1 = torch.cuda.memory_stats(), torch.cuda.host_memory_stats()
+    print("allocator events in the pass:", json.dumps({**{k: d1.get(k, 0) - d0.get(k, 0) for k in keys},
+          **{"host_" + k: h1[k] - h0.get(k, 0) for k in h1 if ("alloc" in k or "free" in k) and "bytes" not in k
+             and isinstance(h1[k], (int, float))}}), flush=True)
     key = "inline" if mode == "1" else "pipelined"
     res[key] = max(res.get(key, 0.0), n / dt)
     print(f"{key}: {n / dt:.2f} frames/s end to end ({dt:.2f} s for {n} scenes, batch_size {bs}; model built once "

@@ -4,6 +4,7 @@
 #   check            GPU test suite + default bench (20 steps)
 #   round            round evidence: tests, bench (+ CPU baseline), smoke, kernel-trace stats, HBM traffic
 #                    (FETCH_SIZE / WRITE_SIZE, one --pmc pass each), attention MFMA counters and in-kernel clock
+#   roundnt          the same without the GPU test suite (run `check` or the suite on its own first)
 #   prof [bench args]  rocprofv3 kernel-trace stats of a short bench run
 #   trace            kernel + HIP API + memory-copy trace of a 2-frame bench run (no counters)
 #   attn             attention GPU tests, ablation timings, per-segment stamps
@@ -49,8 +50,8 @@ case $TASK in
 check)
     timeout -k 10 900 $T tests -m gpu > $O/tests.log 2>&1
     timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err ;;
-round)
-    timeout -k 10 900 $T tests -m gpu > $O/tests.log 2>&1
+round|roundnt)
+    if [ $TASK = round ]; then timeout -k 10 900 $T tests -m gpu > $O/tests.log 2>&1; fi
     timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
     prof_run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --profile --steps 5 --warmup 2 > $O/prof.log 2>&1
