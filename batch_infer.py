@@ -261,6 +261,51 @@ def _load_batch_pinned(files, idx, padding_length, pinned: bool = True):
     return items, host
 
 
+_COPY_STREAMS = {}
+
+
+def _runs_beside(s, compute) -> bool:
+    """Does work on stream `s` start while `compute` is busy?  HIP maps streams onto a few hardware queues
+    (GPU_MAX_HW_QUEUES, 4 here) round robin; two streams on one queue run in submission order, so a copy stream that
+    shares the compute stream's queue serializes every H2D with the frames' kernels.  Probe: a ~10 ms spin on `compute`,
+    then an event on the idle `s`, which completes at once unless it is queued behind the spin."""
+    with torch.cuda.stream(compute):
+        torch.cuda._sleep(int(2e7))
+    ev = torch.cuda.Event()
+    ev.record(s)
+    t0 = time.perf_counter()
+    ok = False
+    while time.perf_counter() - t0 < 0.004:
+        if ev.query():
+            ok = True
+            break
+    compute.synchronize()
+    return ok
+
+
+def _copy_streams(dev):
+    """The side streams of the H2D / D2H copies, made once per (device, compute stream): pool streams that the probe
+    finds on a hardware queue of their own (profiles/r6_batch_e2e.txt: a copy stream on the compute stream's queue
+    cost 10-15 % end to end, in every other batch_infer call as the pool's round robin came back to that queue).
+    RF_BATCH_COPY_STREAMS=perpass: two new pool streams per call, unprobed (the round-5 behaviour)."""
+    if os.environ.get("RF_BATCH_COPY_STREAMS", "probed") == "perpass":
+        return torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    compute = torch.cuda.current_stream(dev)
+    key = (str(dev), compute.cuda_stream)
+    if key not in _COPY_STREAMS:
+        got = []
+        for _ in range(16):  # the pool hands its streams out round robin over the queues
+            s = torch.cuda.Stream(device=dev)
+            if _runs_beside(s, compute):
+                got.append(s)
+                if len(got) == 2:
+                    break
+        while len(got) < 2:  # no free queue found: keep whatever the pool gives (correct, only slower)
+            got.append(torch.cuda.Stream(device=dev))
+        _COPY_STREAMS[key] = tuple(got)
+    return _COPY_STREAMS[key]
+
+
 def render_batches(pipeline, files, batches, args, pipelined=True):
     """Yield (items, hdr images on the host) per batch, in order.  Pipelined: loader thread -> pinned batch
     -> side-stream H2D -> render on the current stream -> side-stream D2H into pinned memory; batch i is
@@ -309,8 +354,7 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
                 return e
 
     loaded = _Loaded()
-    h2d = torch.cuda.Stream(device=dev)
-    d2h = torch.cuda.Stream(device=dev)
+    h2d, d2h = _copy_streams(dev)
     compute = torch.cuda.current_stream(dev)
     # (items, pinned host images, their copy event, pinned inputs, device images) of the batches in flight: batch i is
     # handed out once batch i + DEPTH is issued, so a late loader or a slow issue does not drain the GPU's queue

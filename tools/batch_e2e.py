@@ -34,12 +34,14 @@ print(f"model build (synthetic 483.9M-parameter weights + upload): {time.perf_co
 batch_infer.main(args + ["--output_dir", os.path.join(root, "warm")], pipeline=pipe)  # first-touch allocations
 res = {}
 os.environ["RF_BATCH_PROFILE"] = "1"  # batch_infer.StageTimes: per-stage host time, printed by each run
-for mode in os.environ.get("RF_E2E_MODES", "0,1,0").split(","):  # 0 pipelined, 1 inline
+out_root = tempfile.mkdtemp(prefix="rf_e2e_out_", dir=os.environ.get("RF_E2E_OUTROOT") or root)  # e.g. /dev/shm
+for i_pass, mode in enumerate(os.environ.get("RF_E2E_MODES", "0,1,0").split(",")):  # 0 pipelined, 1 inline
     batch_infer.STAGES.t.clear()
     batch_infer.STAGES.n.clear()
     batch_infer.STAGES.on = True
     os.environ["RF_BATCH_INLINE"] = mode
-    out = os.path.join(root, "out" + mode)
+    # RF_E2E_DISTINCT=1: every pass writes new files (a directory of its own) instead of overwriting the last pass's
+    out = os.path.join(out_root, "out" + mode + (f"_{i_pass}" if os.environ.get("RF_E2E_DISTINCT") == "1" else ""))
     import torch
     keys = ("num_device_alloc", "num_device_free", "num_alloc_retries", "num_sync_all_streams")
     d0, h0 = torch.cuda.memory_stats(), torch.cuda.host_memory_stats()
@@ -57,4 +59,5 @@ for mode in os.environ.get("RF_E2E_MODES", "0,1,0").split(","):  # 0 pipelined, 
 print(json.dumps({"batch_infer_e2e_frames_per_s": res, "scenes": n, "batch_size": int(bs), "res": 512,
                   "data": "the reference's 16 example scenes converted to HDF5 (gzip 9), cycled",
                   "host_threads": __import__("renderformer_amd.h5io", fromlist=["host_threads"]).host_threads()}))
+shutil.rmtree(out_root, ignore_errors=True)
 shutil.rmtree(root, ignore_errors=True)
