@@ -85,6 +85,8 @@ def _libdeflate():
                 lib = ctypes.CDLL(ctypes.util.find_library("deflate") or "libdeflate.so.0")
                 lib.libdeflate_alloc_decompressor.restype = ctypes.c_void_p
                 lib.libdeflate_alloc_decompressor.argtypes = []
+                lib.libdeflate_free_decompressor.restype = None
+                lib.libdeflate_free_decompressor.argtypes = [ctypes.c_void_p]
                 lib.libdeflate_zlib_decompress.restype = ctypes.c_int
                 lib.libdeflate_zlib_decompress.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t,
                                                            ctypes.c_void_p, ctypes.c_size_t,
@@ -95,6 +97,18 @@ def _libdeflate():
     return _DEFLATE or None
 
 
+class _Decompressor:
+    """One thread's libdeflate decompressor (not thread-safe), freed with the thread's local storage."""
+
+    def __init__(self, lib):
+        self.lib, self.h = lib, lib.libdeflate_alloc_decompressor()
+
+    def __del__(self):
+        if self.h:
+            self.lib.libdeflate_free_decompressor(self.h)
+            self.h = None
+
+
 def _inflate_into(raw: bytes, dst: np.ndarray) -> bool:
     """zlib-wrapped deflate stream `raw` decoded into the C-contiguous array `dst`, which it must fill exactly;
     False (nothing promised about dst) when libdeflate is absent or the stream does not decode to dst's size."""
@@ -102,11 +116,12 @@ def _inflate_into(raw: bytes, dst: np.ndarray) -> bool:
     if d is None:
         return False
     lib, tls = d
-    h = getattr(tls, "h", None)
-    if h is None:
-        h = tls.h = lib.libdeflate_alloc_decompressor()
-        if not h:
-            return False
+    dec = getattr(tls, "dec", None)
+    if dec is None:
+        dec = tls.dec = _Decompressor(lib)
+    h = dec.h
+    if not h:
+        return False
     got = ctypes.c_size_t(0)
     rc = lib.libdeflate_zlib_decompress(h, raw, len(raw), dst.ctypes.data, dst.nbytes, ctypes.byref(got))
     return rc == 0 and got.value == dst.nbytes
