@@ -359,18 +359,32 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
     # (items, pinned host images, their copy event, pinned inputs, device images) of the batches in flight: batch i is
     # handed out once batch i + DEPTH is issued, so a late loader or a slow issue does not drain the GPU's queue
     pending = []
-    while True:
+
+    def upload():
+        """The next loaded batch (waiting for the loader if it is late) copied to the device on the H2D stream."""
         got = loaded.get()
         if isinstance(got, BaseException):
             raise got
+        if got is None:
+            return None
+        items, host = got
+        t_h = time.perf_counter()
+        with torch.cuda.stream(h2d):
+            batch = {k: v.to(dev, non_blocking=True) for k, v in host.items()}
+            copied_in = torch.cuda.Event()
+            copied_in.record(h2d)
+        STAGES.add("main: H2D issue", time.perf_counter() - t_h)
+        return items, host, batch, copied_in
+
+    # batch i + 1's H2D is issued right after batch i's kernels, so the ~150-300 MB texture copy runs under batch i's
+    # frame instead of in front of batch i + 1's (profiles/r6_batch_e2e.txt: the GPU idled behind the copy otherwise)
+    staged = upload()
+    while True:
         nxt = None
-        if got is not None:
-            items, host = got
-            t_h = time.perf_counter()
-            with torch.cuda.stream(h2d):
-                batch = {k: v.to(dev, non_blocking=True) for k, v in host.items()}
-            STAGES.add("main: H2D issue", time.perf_counter() - t_h)
-            compute.wait_stream(h2d)
+        cur, staged = staged, None
+        if cur is not None:
+            items, host, batch, copied_in = cur
+            compute.wait_event(copied_in)
             for v in batch.values():  # allocated on the copy stream, used on the compute stream
                 v.record_stream(compute)
             imgs = STAGES.timed("main: render issue (plan + launches)", render, batch, host)
@@ -383,6 +397,7 @@ def render_batches(pipeline, files, batches, args, pipelined=True):
                 copied.record(d2h)
             imgs.record_stream(d2h)
             nxt = (items, out, copied, host, imgs)  # `host` (pinned inputs) lives until this batch is yielded
+            staged = upload()
         if nxt is not None:
             pending.append(nxt)
         while pending and (len(pending) > DEPTH or nxt is None):  # batch i is handed out while i+1.. render
